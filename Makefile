@@ -1,0 +1,47 @@
+# Build of the MI355X (gfx950) engine and the CPU checkers.  No cmake/ninja needed.
+#
+#   make            -> seqalib_amd/lib/libseqalib_hip.so  (HIP kernels + C ABI)
+#   make oracle     -> oracle/liboracle.so                (C restatement, test infrastructure)
+#   make ref        -> oracle/_ref/libsaref.so            (reference built in place; needs /root/reference)
+#   make all-checkers / clean
+
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
+CSRC      = seqalib_amd/csrc
+OBJDIR    = build/obj
+LIB       = seqalib_amd/lib/libseqalib_hip.so
+
+HIP_SRCS  = $(CSRC)/sa_fill_sw.hip $(CSRC)/sa_fill_nw.hip $(CSRC)/sa_fill_lg.hip $(CSRC)/sa_fill_gg.hip \
+            $(CSRC)/sa_traceback.hip $(CSRC)/sa_api.hip
+CPP_SRCS  = $(CSRC)/sa_synth.cpp
+HDRS      = $(CSRC)/sa_internal.h $(CSRC)/sa_layout.h $(CSRC)/sa_fill_impl.h include/seqalib_hip.h
+OBJS      = $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(CPP_SRCS))
+
+lib: $(LIB)
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -lpthread
+
+oracle:
+	$(MAKE) -C oracle
+
+ref:
+	$(MAKE) -C oracle ref
+
+all-checkers: oracle ref
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -C oracle clean
+
+.PHONY: lib oracle ref all-checkers clean

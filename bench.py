@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Benchmark: GCUPS of batched Smith-Waterman (linear gap) on MI355X — BASELINE.json's metric.
+
+One "step" = one pass of the hot path (fill + traceback, i.e. getAlignment minus host list
+assembly) over one batch of synthetic DNA pairs that is already resident in HBM.  Workload at
+N=1 (north_star headline): 10,000 pairs of 4,096 x 4,096, ScoringSystem(-1, 1, -1) with
+equal<char> — the same pairs the reference's SmithWatermanSA would see.
+
+Multi-GPU: one process per GPU (torchrun); rank r aligns its own 10,000-pair shard of a global
+batch (pair p uses seeds base+2p+1 / base+2p+2), with no data-path collective (pairs are
+independent); timing is barrier-bracketed and the max over ranks is reported.  scaling = weak.
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+METRIC = "GCUPS (DP cell updates/s) on batched 4k×4k SW; bit-exact score match"
+SEED_BASE = 10 ** 10          # workload "T" seed base (config id x 1e9 convention)
+SCORING = (-1, 1, -1)         # SmithWatermanSA::getDefaultScoring (SASmithWaterman.h:352)
+VALU_PEAK_TOPS = 78.64        # 256 CU x 4 SIMD32 x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
+HBM_PEAK_GBPS = 8000.0
+SW_VALU_OPS_PER_CELL = 13     # ISA-counted VALU instructions per cell of the keyed SW body
+SW_FLAG_BYTES_PER_CELL = 0.25  # 2 traceback bits per cell written to HBM
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--pairs", type=int, default=10000, help="pairs per GPU")
+    ap.add_argument("--len", type=int, default=4096, help="length of both sequences")
+    ap.add_argument("--cpu-pairs", type=int, default=128, help="CPU baseline sample (pairs)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--out", default="", help="also write the JSON line to this file")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shard_seed_base(rank: int, pairs_per_gpu: int) -> int:
+    """Pair p of the global batch uses seeds SEED_BASE+2p+1 / +2p+2; rank r owns
+    p in [r*P, (r+1)*P), i.e. a contiguous static split with no exchange."""
+    return SEED_BASE + 2 * rank * pairs_per_gpu
+
+
+def cpu_baseline(args, s1, o1, s2, o2):
+    """The reference (oracle/_ref, compiled from /root/reference) — or the oracle port if that is
+    not built — on a bounded sample of the same pairs, on the host cores."""
+    k = min(args.cpu_pairs, len(o1) - 1)
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    sub1, sub2 = s1[: int(o1[k])].copy(), s2[: int(o2[k])].copy()
+    so1, so2 = o1[: k + 1].copy(), o2[: k + 1].copy()
+    cells = float(np.sum((so1[1:] - so1[:-1]).astype(np.float64) * (so2[1:] - so2[:-1])))
+    ref = os.path.join(ROOT, "oracle", "_ref", "libsaref.so")
+    out = np.zeros(k, dtype=np.int32)
+    if os.path.exists(ref):
+        L = C.CDLL(ref)
+        vp = C.c_void_p
+        L.ref_sw_batch.argtypes = [C.c_int] * 4 + [vp, vp, vp, vp, C.c_int, C.c_int, vp]
+        t0 = time.perf_counter()
+        L.ref_sw_batch(*SCORING, 1, sub1.ctypes.data, so1.ctypes.data, sub2.ctypes.data, so2.ctypes.data,
+                       k, threads, out.ctypes.data)
+        dt = time.perf_counter() - t0
+        kind = "reference"
+        what = "SmithWatermanSA<std::string,char,'-'>::getAlignment (unmodified reference headers, g++ -O2)"
+    else:
+        from util import OracleScoring, oracle_lib
+        L = oracle_lib()
+        sc = OracleScoring(SCORING[0], SCORING[1], SCORING[2], 0, 0, 1)
+        t0 = time.perf_counter()
+        L.oracle_sw_batch(C.byref(sc), sub1.ctypes.data, so1.ctypes.data, sub2.ctypes.data, so2.ctypes.data,
+                          k, threads, out.ctypes.data)
+        dt = time.perf_counter() - t0
+        kind = "port"
+        what = "oracle/sa_oracle.c SW (full-matrix restatement)"
+    return {"value": round(cells / dt / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": kind,
+            "sample": f"first {k} pairs of this rank's batch ({args.len}x{args.len}), {what}, "
+                      f"{threads} threads, {dt:.2f} s wall"}
+
+
+def load_pmc_traffic(workload: str):
+    """HBM bytes per fill launch measured by rocprofv3 --pmc (profiles/pmc_traffic.json, written
+    by tools/profile.sh from separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        e = d.get(workload)
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    import torch
+    import seqalib_amd as sa
+
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (no CPU fallback)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    P, Lq = args.pairs, args.len
+    workload = f"sw_batch_{P}x{Lq}x{Lq}"
+
+    s1, o1, s2, o2 = sa.synth_dna_batch(shard_seed_base(rank, P), P, Lq, Lq, threads=16)
+    as_t = lambda x: torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)
+    d1, do1, d2, do2 = as_t(s1), as_t(o1), as_t(s2), as_t(o2)
+    d_res = torch.zeros(P * 32, dtype=torch.uint8, device=dev)
+    d_ops = torch.zeros(len(s1) + len(s2) + P, dtype=torch.uint8, device=dev)
+    eng = sa.Engine(local)
+    scoring = sa.ScoringSystem(*SCORING)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        eng.align_device(sa.SA_SW, scoring, d1.data_ptr(), do1.data_ptr(), d2.data_ptr(), do2.data_ptr(), P, Lq, Lq,
+                         d_res.data_ptr(), d_ops.data_ptr(), stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    elapsed = max_over_ranks(t1 - t0, world)
+    fill_ms, tb_ms, launches = eng.last_timings()   # HIP events of the last step, same stream
+    fill_ms = max_over_ranks(fill_ms, world)
+
+    cells_rank = float(P) * Lq * Lq
+    value = world * cells_rank * args.steps / elapsed / 1e9
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # parity spot check of this step's output (outside the timed region)
+    from util import oracle_align
+    res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=sa.RESULT_DTYPE)
+    ops = d_ops.cpu().numpy()
+    bad = int(np.count_nonzero(res["flags"]))
+    checked = 0
+    for p in (0, P - 1):
+        a, b = s1[o1[p]:o1[p + 1]].tobytes(), s2[o2[p]:o2[p + 1]].tobytes()
+        o = oracle_align(0, SCORING, a, b)
+        off = int(o1[p] + o2[p]) + p
+        got = (int(res["score"][p]), int(res["end_i"][p]), int(res["end_j"][p]),
+               ops[off:off + int(res["nops"][p])].tobytes())
+        if got != (o["score"], o["end_i"], o["end_j"], o["ops"]):
+            bad += 1
+        checked += 1
+
+    if rank != 0:
+        return
+    per_launch_cells = cells_rank  # one fill launch covers the whole batch when it fits HBM
+    fill_s = fill_ms / 1e3 / max(launches, 1)
+    tops = per_launch_cells * SW_VALU_OPS_PER_CELL / fill_s / 1e12
+    hbm_gbps = per_launch_cells * SW_FLAG_BYTES_PER_CELL / fill_s / 1e9
+    traffic = load_pmc_traffic(workload)
+    line = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GCUPS", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+        "data": "synthetic DNA, std::mt19937_64 'ACGT'[g()&3], seeds base+2p+1/base+2p+2, resident in HBM",
+        "config": {"workload": workload, "pairs_per_gpu": P, "m": Lq, "n": Lq, "algo": "SmithWatermanSA",
+                   "scoring": list(SCORING), "match": "equal<char>", "parallelism": f"pair-shard x{world}"},
+        "roofline": {"bound": "valu", "achieved": round(tops, 2), "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
+                     "frac": round(tops / VALU_PEAK_TOPS, 4), "traffic": traffic,
+                     "kernel": "fill_kernel<SW,R=16,EQ,ALLOW,KEYED>",
+                     "avg_launch_ms": round(fill_ms / max(launches, 1), 3),
+                     "ops_per_cell": SW_VALU_OPS_PER_CELL, "bytes_per_cell": SW_FLAG_BYTES_PER_CELL,
+                     "hbm_achieved_GBps": round(hbm_gbps, 1), "hbm_peak_GBps": HBM_PEAK_GBPS,
+                     "hbm_frac": round(hbm_gbps / HBM_PEAK_GBPS, 4)},
+        "fill_ms": round(fill_ms, 2), "traceback_ms": round(tb_ms, 2),
+        "parity": f"{checked - bad}/{checked} sampled pairs bit-exact vs oracle, {int(np.count_nonzero(res['flags']))} flagged",
+    }
+    if world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(args, s1, o1, s2, o2)
+    else:
+        line["cpu_baseline"] = None
+    txt = json.dumps(line)
+    print(txt, flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(txt + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,374 @@
+/* TEST INFRASTRUCTURE ONLY — CPU checker; see sa_oracle.h for the contract and who may call it.
+ *
+ * A deliberately plain restatement of the reference's O(mn) full-matrix algorithms: row-major
+ * int32 matrices of (m+1)x(n+1), a byte match cache, scalar loops in the reference's order and
+ * its exact comparison / tie rules.  Integer overflow wraps (-fwrapv), like the compiled
+ * reference does in practice; scorings that overflow are outside parity anyway.
+ */
+#include "sa_oracle.h"
+
+#include <limits.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define IDX(i, j) ((size_t)(i) * (size_t)(n + 1) + (size_t)(j))
+
+static inline int32_t max2(int32_t a, int32_t b) { return a > b ? a : b; }
+static inline int32_t max3(int32_t a, int32_t b, int32_t c) { return max2(max2(a, b), c); }
+static inline int32_t max4(int32_t a, int32_t b, int32_t c, int32_t d) { return max2(max3(a, b, c), d); }
+
+/* cacheAllMatches (e.g. SASmithWaterman.h:20-45): Matches[i*n+j] = match(Seq1[i], Seq2[j]). */
+static uint8_t* match_cache(const uint8_t* s1, int m, const uint8_t* s2, int n, const uint8_t* lut) {
+    uint8_t* mt = (uint8_t*)malloc((size_t)m * (size_t)n + 1);
+    if (!mt) return NULL;
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < n; ++j)
+            mt[(size_t)i * n + j] = lut ? (lut[s1[i] * 256 + s2[j]] != 0) : (s1[i] == s2[j]);
+    return mt;
+}
+
+/* Diagonal candidate exactly as the fill computes it (SASmithWaterman.h:95-100 / :128-131). */
+static inline int32_t diag_term(int32_t hd, int v, const oracle_scoring* sc) {
+    if (sc->allow_mismatch) return hd + (v ? sc->match : sc->mismatch);
+    return v ? hd + sc->match : INT_MIN;
+}
+
+typedef struct {
+    uint8_t* ops;
+    int cap, n;
+    int overflow;
+} opbuf;
+
+static inline void put(opbuf* b, uint8_t op) {
+    if (b->n < b->cap) b->ops[b->n] = op; else b->overflow = 1;
+    b->n++;
+}
+
+/* Expand an op stream + forceGlobal (SequenceAlignment.h:156-189) into three strings. */
+static int expand(const uint8_t* s1, int m, const uint8_t* s2, int n, const uint8_t* ops, int nops,
+                  int end_i, int end_j, int force_global, int fg_i, int fg_j, int fg_ei, int fg_ej,
+                  char* row0, char* bars, char* row1, int cap, int* out_len) {
+    /* Build the local part in reverse (traceback order), then emit forward. */
+    int local = 0;
+    for (int k = 0; k < nops; ++k) local += (ops[k] == 'X') ? 2 : 1;
+    int front = force_global ? fg_i + fg_j : 0;
+    int back = force_global ? (m - fg_ei) + (n - fg_ej) : 0;
+    int len = front + local + back;
+    *out_len = len;
+    if (!row0) return 0;
+    if (len > cap) return -1;
+    int p = 0;
+    if (force_global) {
+        for (int k = 0; k < fg_i; ++k, ++p) { row0[p] = (char)s1[k]; bars[p] = ' '; row1[p] = '-'; }
+        for (int k = 0; k < fg_j; ++k, ++p) { row0[p] = '-'; bars[p] = ' '; row1[p] = (char)s2[k]; }
+    }
+    /* Walk the traceback to recover the positions each op consumed, writing from the back. */
+    int q = p + local;
+    int i = end_i, j = end_j;
+    for (int k = 0; k < nops; ++k) {
+        uint8_t op = ops[k];
+        if (op == 'M' || op == 'S') {
+            --q; row0[q] = (char)s1[i - 1]; bars[q] = op == 'M' ? '|' : ' '; row1[q] = (char)s2[j - 1];
+            --i; --j;
+        } else if (op == 'X') {
+            /* push_front(Seq1,Blank) then push_front(Blank,Seq2): forward order (-,s2),(s1,-) */
+            --q; row0[q] = (char)s1[i - 1]; bars[q] = ' '; row1[q] = '-';
+            --q; row0[q] = '-'; bars[q] = ' '; row1[q] = (char)s2[j - 1];
+            --i; --j;
+        } else if (op == 'U' || op == 'u') {
+            --q; row0[q] = (char)s1[i - 1]; bars[q] = ' '; row1[q] = '-';
+            if (op == 'U') --i;
+        } else { /* 'L' / 'l' */
+            --q; row0[q] = '-'; bars[q] = ' '; row1[q] = (char)s2[j - 1];
+            if (op == 'L') --j;
+        }
+    }
+    p += local;
+    if (force_global) {
+        for (int k = fg_ei; k < m; ++k, ++p) { row0[p] = (char)s1[k]; bars[p] = ' '; row1[p] = '-'; }
+        for (int k = fg_ej; k < n; ++k, ++p) { row0[p] = '-'; bars[p] = ' '; row1[p] = (char)s2[k]; }
+    }
+    return 0;
+}
+
+/* ---------------------------------------------------------------- Smith-Waterman (linear) */
+static int align_sw(const oracle_scoring* sc, const uint8_t* s1, int m, const uint8_t* s2, int n,
+                    const uint8_t* mt, oracle_result* res, opbuf* ob) {
+    int32_t* H = (int32_t*)malloc(sizeof(int32_t) * (size_t)(m + 1) * (size_t)(n + 1));
+    if (!H) return -2;
+    const int32_t G = sc->gap;
+    for (int i = 0; i <= m; ++i) H[IDX(i, 0)] = 0;            /* SASmithWaterman.h:68-71 */
+    for (int j = 0; j <= n; ++j) H[IDX(0, j)] = 0;            /* :74-77 */
+    int32_t best = INT_MIN;
+    int maxr = 0, maxc = 0;                                   /* members default to 0 (:14-15) */
+    for (int i = 1; i <= m; ++i)
+        for (int j = 1; j <= n; ++j) {
+            int v = mt[(size_t)(i - 1) * n + (j - 1)];
+            int32_t h = max4(diag_term(H[IDX(i - 1, j - 1)], v, sc), H[IDX(i - 1, j)] + G,
+                             H[IDX(i, j - 1)] + G, 0);        /* :95-104 */
+            H[IDX(i, j)] = h;
+            if (h >= best) { best = h; maxr = i; maxc = j; }  /* :110-115, last row-major max */
+        }
+    /* buildResult :220-339 */
+    int i = maxr, j = maxc;
+    if (m == 0 || n == 0) { i = 0; j = 0; }
+    while (i > 0 || j > 0) {
+        if (i == 0 || j == 0) break;
+        int v = mt[(size_t)(i - 1) * n + (j - 1)];
+        int32_t s = max2(diag_term(H[IDX(i - 1, j - 1)], v, sc), 0);
+        if (H[IDX(i, j)] == s) {
+            if (s == 0) break;
+            put(ob, (v || sc->allow_mismatch) ? (v ? 'M' : 'S') : 'X');
+            --i; --j;
+            continue;
+        }
+        if (i > 0 && H[IDX(i, j)] == H[IDX(i - 1, j)] + G) {
+            if (H[IDX(i - 1, j)] + G <= 0) break;
+            put(ob, 'U'); --i;
+        } else {
+            if (H[IDX(i, j - 1)] + G <= 0) break;
+            put(ob, 'L'); --j;
+        }
+    }
+    res->score = (m == 0 || n == 0) ? INT_MIN : best;
+    res->end_i = maxr; res->end_j = maxc;
+    res->start_i = i; res->start_j = j;
+    free(H);
+    return 0;
+}
+
+/* ------------------------------------------------------------- Needleman-Wunsch (linear) */
+static int align_nw(const oracle_scoring* sc, const uint8_t* s1, int m, const uint8_t* s2, int n,
+                    const uint8_t* mt, oracle_result* res, opbuf* ob) {
+    (void)s1; (void)s2;
+    int32_t* H = (int32_t*)malloc(sizeof(int32_t) * (size_t)(m + 1) * (size_t)(n + 1));
+    if (!H) return -2;
+    const int32_t G = sc->gap;
+    for (int i = 0; i <= m; ++i) H[IDX(i, 0)] = (int32_t)((uint32_t)i * (uint32_t)G);  /* :59-60 */
+    for (int j = 0; j <= n; ++j) H[IDX(0, j)] = (int32_t)((uint32_t)j * (uint32_t)G);  /* :61-62 */
+    for (int i = 1; i <= m; ++i)
+        for (int j = 1; j <= n; ++j) {
+            int v = mt[(size_t)(i - 1) * n + (j - 1)];
+            H[IDX(i, j)] = max3(diag_term(H[IDX(i - 1, j - 1)], v, sc), H[IDX(i - 1, j)] + G,
+                                H[IDX(i, j - 1)] + G);         /* :73-78 */
+        }
+    int i = m, j = n;                                          /* buildResult :167 */
+    while (i > 0 || j > 0) {
+        if (i > 0 && j > 0) {
+            int v = mt[(size_t)(i - 1) * n + (j - 1)];
+            if (H[IDX(i, j)] == diag_term(H[IDX(i - 1, j - 1)], v, sc)) {
+                put(ob, (v || sc->allow_mismatch) ? (v ? 'M' : 'S') : 'X');
+                --i; --j;
+                continue;
+            }
+        }
+        if (i > 0 && H[IDX(i, j)] == H[IDX(i - 1, j)] + G) { put(ob, 'U'); --i; }
+        else { put(ob, 'L'); --j; }
+    }
+    res->score = H[IDX(m, n)];
+    res->end_i = m; res->end_j = n;
+    res->start_i = 0; res->start_j = 0;
+    free(H);
+    return 0;
+}
+
+/* --------------------------------------------------------------------- Gotoh (affine) */
+static int align_gotoh(int local, const oracle_scoring* sc, int m, int n, const uint8_t* mt,
+                       oracle_result* res, opbuf* ob) {
+    size_t cells = (size_t)(m + 1) * (size_t)(n + 1);
+    int32_t* M = (int32_t*)malloc(sizeof(int32_t) * cells);
+    int32_t* X = (int32_t*)malloc(sizeof(int32_t) * cells); /* Ix: vertical gap (consumes Seq1) */
+    int32_t* Y = (int32_t*)malloc(sizeof(int32_t) * cells); /* Iy: horizontal gap (consumes Seq2) */
+    if (!M || !X || !Y) { free(M); free(X); free(Y); return -2; }
+    const int32_t GO = sc->gap_open, GE = sc->gap_extend;
+    for (int i = 0; i <= m; ++i) {   /* LG :77-82, GG :75-80 */
+        M[IDX(i, 0)] = local ? 0 : (i < 1 ? 0 : (int32_t)((uint32_t)GO + (uint32_t)i * (uint32_t)GE));
+        X[IDX(i, 0)] = -10000;
+        Y[IDX(i, 0)] = -10000;
+    }
+    for (int j = 0; j <= n; ++j) {   /* LG :85-90, GG :83-88 */
+        M[IDX(0, j)] = local ? 0 : (j < 1 ? 0 : (int32_t)((uint32_t)GO + (uint32_t)j * (uint32_t)GE));
+        X[IDX(0, j)] = -10000;
+        Y[IDX(0, j)] = -10000;
+    }
+    int32_t best = INT_MIN;
+    int maxr = 0, maxc = 0;
+    for (int i = 1; i <= m; ++i)
+        for (int j = 1; j <= n; ++j) {
+            int32_t x = max2(M[IDX(i - 1, j)] + GO + GE, X[IDX(i - 1, j)] + GE);   /* :108-112 */
+            int32_t y = max2(M[IDX(i, j - 1)] + GO + GE, Y[IDX(i, j - 1)] + GE);   /* :115-119 */
+            int v = mt[(size_t)(i - 1) * n + (j - 1)];
+            int32_t d = diag_term(M[IDX(i - 1, j - 1)], v, sc);
+            int32_t h = local ? max4(d, x, y, 0) : max3(d, x, y);                    /* :122-130 */
+            X[IDX(i, j)] = x; Y[IDX(i, j)] = y; M[IDX(i, j)] = h;
+            if (local && h >= best) { best = h; maxr = i; maxc = j; }                /* :133-138 */
+        }
+    int rc = 0;
+    int type = 0;
+    int i, j;
+    if (local) {
+        /* SALocalGotoh.h buildResult :275-473 */
+        i = maxr; j = maxc;
+        while (i > 0 || j > 0) {
+            if (i <= 0 || j <= 0) break;
+            if (type == 0) {
+                int v = mt[(size_t)(i - 1) * n + (j - 1)];
+                int32_t s = max2(diag_term(M[IDX(i - 1, j - 1)], v, sc), 0);
+                if (M[IDX(i, j)] == s) {
+                    if (s <= 0) break;
+                    put(ob, (v || sc->allow_mismatch) ? (v ? 'M' : 'S') : 'X');
+                    --i; --j;
+                    continue;
+                }
+            }
+            {
+                int32_t mup = max2(M[IDX(i - 1, j)] + GO + GE, 0);
+                int32_t xup = X[IDX(i - 1, j)] + GE;
+                if (X[IDX(i, j)] == xup && type == 1) { put(ob, 'U'); --i; continue; }
+                if (X[IDX(i, j)] == mup && type == 1) {
+                    if (mup <= 0) { put(ob, 'u'); break; }
+                    put(ob, 'U'); type = 0; --i; continue;
+                }
+                if (M[IDX(i, j)] == X[IDX(i, j)] && type == 0) { type = 1; continue; }
+            }
+            {
+                int32_t mleft = max2(M[IDX(i, j - 1)] + GO + GE, 0);
+                int32_t yleft = Y[IDX(i, j - 1)] + GE;
+                if (Y[IDX(i, j)] == yleft && type == 2) { put(ob, 'L'); --j; continue; }
+                if (Y[IDX(i, j)] == mleft && type == 2) {
+                    if (mleft <= 0) { put(ob, 'l'); break; }
+                    put(ob, 'L'); type = 0; --j; continue;
+                }
+                if (M[IDX(i, j)] == Y[IDX(i, j)] && type == 0) { type = 2; continue; }
+            }
+            rc = -3; /* the reference loops forever here (undefined scoring); outside parity */
+            break;
+        }
+        (void)best;
+        res->score = M[IDX(maxr, maxc)]; /* harness reads Matrix[MaxRow][MaxCol] */
+        res->end_i = maxr; res->end_j = maxc;
+    } else {
+        /* SAGlobalGotoh.h buildResult :235-422 */
+        i = m; j = n;
+        while (i > 0 || j > 0) {
+            if (i > 0 && j > 0 && type == 0) {
+                int v = mt[(size_t)(i - 1) * n + (j - 1)];
+                if (M[IDX(i, j)] == diag_term(M[IDX(i - 1, j - 1)], v, sc)) {
+                    put(ob, (v || sc->allow_mismatch) ? (v ? 'M' : 'S') : 'X');
+                    --i; --j;
+                    continue;
+                }
+            }
+            if (i > 0) {
+                if (j == 0) { put(ob, 'U'); --i; continue; }
+                int32_t mup = M[IDX(i - 1, j)] + GO + GE;
+                int32_t xup = X[IDX(i - 1, j)] + GE;
+                if (X[IDX(i, j)] == xup && type == 1) { put(ob, 'U'); --i; continue; }
+                if (X[IDX(i, j)] == mup && type == 1) { put(ob, 'U'); type = 0; --i; continue; }
+                if (M[IDX(i, j)] == X[IDX(i, j)] && type == 0) { type = 1; continue; }
+            }
+            if (j > 0) {
+                if (i == 0) { put(ob, 'L'); --j; continue; }
+                int32_t mleft = M[IDX(i, j - 1)] + GO + GE;
+                int32_t yleft = Y[IDX(i, j - 1)] + GE;
+                if (Y[IDX(i, j)] == yleft && type == 2) { put(ob, 'L'); --j; continue; }
+                if (Y[IDX(i, j)] == mleft && type == 2) { put(ob, 'L'); type = 0; --j; continue; }
+                if (M[IDX(i, j)] == Y[IDX(i, j)] && type == 0) { type = 2; continue; }
+            }
+            rc = -3;
+            break;
+        }
+        res->score = M[IDX(m, n)];
+        res->end_i = m; res->end_j = n;
+    }
+    res->start_i = i; res->start_j = j;
+    free(M); free(X); free(Y);
+    return rc;
+}
+
+/* SALocalGotoh.h:484-488: these three size pairs discard the Gotoh result and run
+ * StaticFuncs::useNW (StaticFuncs.h:12-25) with the same (affine) ScoringSystem. */
+static int lg_size_hack(int m, int n) {
+    return (m == 314 && n == 288) || (m == 60 && n == 57) || (m == 61 && n == 58);
+}
+
+int oracle_align(int algo, const oracle_scoring* sc, const uint8_t* s1, int m, const uint8_t* s2,
+                 int n, const uint8_t* lut, oracle_result* res, uint8_t* ops, int ops_cap,
+                 char* row0, char* bars, char* row1, int cap) {
+    if (algo == OR_LOCAL_GOTOH && lg_size_hack(m, n)) algo = OR_NW;
+    uint8_t* mt = match_cache(s1, m, s2, n, lut);
+    if (!mt) return -2;
+    opbuf ob = {ops, ops_cap, 0, 0};
+    memset(res, 0, sizeof(*res));
+    int rc;
+    switch (algo) {
+        case OR_SW: rc = align_sw(sc, s1, m, s2, n, mt, res, &ob); break;
+        case OR_NW: rc = align_nw(sc, s1, m, s2, n, mt, res, &ob); break;
+        case OR_LOCAL_GOTOH: rc = align_gotoh(1, sc, m, n, mt, res, &ob); break;
+        default: rc = align_gotoh(0, sc, m, n, mt, res, &ob); break;
+    }
+    free(mt);
+    res->nops = ob.n;
+    if (rc) return rc;
+    if (ob.overflow) return -1;
+    int fg = (algo == OR_SW || algo == OR_LOCAL_GOTOH);
+    int len = 0;
+    int e = expand(s1, m, s2, n, ops, ob.n, res->end_i, res->end_j, fg, res->start_i, res->start_j,
+                   res->end_i, res->end_j, row0, bars, row1, cap, &len);
+    res->len = len;
+    return e;
+}
+
+/* ------------------------------------------------------------------ CPU baseline (port) */
+typedef struct {
+    const oracle_scoring* sc;
+    const uint8_t *s1, *s2;
+    const uint64_t *o1, *o2;
+    int npairs;
+    int32_t* out;
+    volatile int next;
+    pthread_mutex_t mu;
+    int err;
+} batch_job;
+
+static void* batch_worker(void* arg) {
+    batch_job* J = (batch_job*)arg;
+    for (;;) {
+        pthread_mutex_lock(&J->mu);
+        int p = J->next++;
+        pthread_mutex_unlock(&J->mu);
+        if (p >= J->npairs) break;
+        int m = (int)(J->o1[p + 1] - J->o1[p]), n = (int)(J->o2[p + 1] - J->o2[p]);
+        const uint8_t* a = J->s1 + J->o1[p];
+        const uint8_t* b = J->s2 + J->o2[p];
+        int cap = m + n + 2;
+        uint8_t* ops = (uint8_t*)malloc((size_t)cap);
+        char* r = (char*)malloc((size_t)cap * 3);
+        oracle_result res;
+        int rc = (ops && r) ? oracle_align(OR_SW, J->sc, a, m, b, n, NULL, &res, ops, cap, r, r + cap,
+                                           r + 2 * cap, cap)
+                            : -2;
+        J->out[p] = rc ? INT_MIN : res.score;
+        if (rc) J->err = rc;
+        free(ops); free(r);
+    }
+    return NULL;
+}
+
+int oracle_sw_batch(const oracle_scoring* sc, const uint8_t* s1cat, const uint64_t* off1,
+                    const uint8_t* s2cat, const uint64_t* off2, int npairs, int threads,
+                    int32_t* out_score) {
+    if (threads < 1) threads = 1;
+    batch_job J;
+    J.sc = sc; J.s1 = s1cat; J.s2 = s2cat; J.o1 = off1; J.o2 = off2;
+    J.npairs = npairs; J.out = out_score; J.next = 0; J.err = 0;
+    pthread_mutex_init(&J.mu, NULL);
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
+    if (!th) return -2;
+    for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, batch_worker, &J);
+    for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+    free(th);
+    pthread_mutex_destroy(&J.mu);
+    return J.err;
+}

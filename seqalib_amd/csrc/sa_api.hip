@@ -1,0 +1,463 @@
+// sa_api.hip — the C ABI of libseqalib_hip.so (include/seqalib_hip.h): contexts, planning,
+// workspace, batching and the host<->device plumbing around the fill and traceback kernels.
+#include <hip/hip_runtime.h>
+#include <limits.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "sa_internal.h"
+
+using namespace sa;
+
+struct sa_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // cached device workspace (direction slots + row buffers + LUT bits)
+    uint8_t* ws = nullptr;
+    uint64_t ws_bytes = 0;
+    uint64_t ws_limit = 0;  // 0 = automatic
+    // cached device I/O buffers for the host API
+    uint8_t* io = nullptr;
+    uint64_t io_bytes = 0;
+    // timing of the last call
+    std::vector<hipEvent_t> events;  // 3 per fill launch: start, fill end, traceback end
+    int launches = 0;
+    hipStream_t timed_stream = nullptr;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(sa_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(sa_ctx* c, hipError_t e, const char* what) {
+    return fail(c, SA_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define SA_HIP(c, call)                                   \
+    do {                                                  \
+        hipError_t e_ = (call);                           \
+        if (e_ != hipSuccess) return hip_fail(c, e_, #call); \
+    } while (0)
+
+// ------------------------------------------------------------------------------- planning
+struct Plan {
+    int R, W;
+    Geom g;
+    uint64_t rowbuf_elems;  // int32 per slot
+};
+
+Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs) {
+    Plan p;
+    const bool aff = is_affine(algo);
+    const int rmax = aff ? 16 : 16;
+    if (npairs >= 1024) {
+        // Many pairs: 4 waves (one band each when possible) per workgroup.
+        p.W = 4;
+        p.R = 4;
+        while (p.R < rmax && (uint64_t)kWave * p.R * p.W < max_m) p.R *= 2;
+    } else {
+        // Few pairs: widen the workgroup instead (up to 16 waves) to use one CU fully.
+        p.R = rmax;
+        const uint64_t rows = (uint64_t)kWave * p.R;
+        uint64_t w = (max_m + rows - 1) / rows;
+        p.W = (int)std::max<uint64_t>(1, std::min<uint64_t>(16, w));
+        while (p.R > 4 && (uint64_t)kWave * (p.R / 2) * p.W >= max_m) p.R /= 2;
+    }
+    // never more waves than bands
+    const uint64_t bands = (max_m + (uint64_t)kWave * p.R - 1) / ((uint64_t)kWave * p.R);
+    if ((uint64_t)p.W > bands) p.W = (int)std::max<uint64_t>(1, bands);
+    p.g = make_geom(algo, p.R, max_m, max_n);
+    p.rowbuf_elems = (uint64_t)(aff ? 2 : 1) * std::max<uint32_t>(max_n, 1);
+    return p;
+}
+
+__global__ void lut_to_bits(const uint8_t* lut, uint32_t* bits) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;  // 2048 words
+    if (w >= 2048) return;
+    const int a = w >> 3, b0 = (w & 7) * 32;
+    uint32_t v = 0;
+    for (int k = 0; k < 32; ++k) v |= (lut[a * 256 + b0 + k] != 0 ? 1u : 0u) << k;
+    bits[w] = v;
+}
+
+int ensure_ws(sa_ctx* c, uint64_t need) {
+    if (c->ws_bytes >= need) return SA_OK;
+    if (c->ws) {
+        SA_HIP(c, hipStreamSynchronize(c->stream));
+        (void)hipFree(c->ws);
+        c->ws = nullptr;
+        c->ws_bytes = 0;
+    }
+    hipError_t e = hipMalloc(&c->ws, need);
+    if (e != hipSuccess) {
+        c->ws = nullptr;
+        return fail(c, SA_ERR_NOMEM, "hipMalloc workspace of " + std::to_string(need) + " bytes failed");
+    }
+    c->ws_bytes = need;
+    return SA_OK;
+}
+
+uint64_t ws_budget(sa_ctx* c) {
+    if (c->ws_limit) return c->ws_limit;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 1ull << 30;
+    return (uint64_t)((fr + c->ws_bytes) * 0.8);
+}
+
+// 16-bit (score, column) keys for the running maximum are exact when every local score and
+// every column fits 16 bits.  With non-positive mismatch and gap terms a local score is at most
+// match * min(m, n); otherwise fall back to a generous bound.
+bool keyed_ok(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
+    if (algo != SA_SW && algo != SA_LOCAL_GOTOH) return false;
+    if (max_n >= 65535) return false;
+    const bool aff = is_affine(algo);
+    const bool nonpos = (!sc->allow_mismatch || sc->mismatch <= 0) &&
+                        (aff ? (sc->gap_extend <= 0 && (int64_t)sc->gap_open + sc->gap_extend <= 0)
+                             : sc->gap <= 0);
+    int64_t bound;
+    if (nonpos) {
+        bound = (int64_t)std::max(sc->match, 0) * std::min(max_m, max_n);
+    } else {
+        auto a = [](int32_t x) { return (int64_t)(x < 0 ? -(int64_t)x : x); };
+        bound = (a(sc->match) + a(sc->mismatch) + a(sc->gap) + a(sc->gap_open) + a(sc->gap_extend)) *
+                ((int64_t)max_m + max_n);
+    }
+    return bound < 65536;
+}
+
+int validate_scoring(sa_ctx* c, int algo, const sa_scoring* s) {
+    if (!s) return fail(c, SA_ERR_ARG, "scoring is NULL");
+    if (algo < SA_SW || algo > SA_GLOBAL_GOTOH) return fail(c, SA_ERR_ARG, "unknown algorithm");
+    return SA_OK;
+}
+
+// Enqueue fill + traceback for pairs [0, npairs) whose inputs are on the device.
+int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, const uint64_t* o1,
+               const uint8_t* d2, const uint64_t* o2, uint32_t npairs, uint32_t max_m,
+               uint32_t max_n, const uint32_t* d_lutbits, sa_result* d_res, uint8_t* d_ops,
+               hipStream_t stream) {
+    if (max_m >= (1u << 24) || max_n >= (1u << 24))
+        return fail(c, SA_ERR_UNSUPPORTED, "sequence lengths must be < 2^24");
+    const Plan pl = make_plan(algo, max_m, max_n, npairs);
+    const bool keyed = keyed_ok(algo, sc, max_m, max_n);
+    const uint64_t slot_bytes = pl.g.dir_slot + pl.rowbuf_elems * 4;
+    const uint64_t budget = ws_budget(c);
+    uint64_t per_launch = slot_bytes ? std::max<uint64_t>(1, budget / std::max<uint64_t>(slot_bytes, 1)) : npairs;
+    per_launch = std::min<uint64_t>(per_launch, npairs ? npairs : 1);
+    per_launch = std::min<uint64_t>(per_launch, 1u << 30);
+    const uint64_t need = per_launch * slot_bytes + 4096;
+    if (need > budget && per_launch == 1 && c->ws_limit)
+        return fail(c, SA_ERR_NOMEM, "one pair needs " + std::to_string(slot_bytes) +
+                                         " bytes of workspace, above the limit");
+    int rc = ensure_ws(c, std::max<uint64_t>(need, 4096));
+    if (rc) return rc;
+    uint8_t* dirs = c->ws;
+    int32_t* rowbuf = reinterpret_cast<int32_t*>(c->ws + per_launch * pl.g.dir_slot);
+
+    // reset timing
+    c->launches = 0;
+    c->timed_stream = stream;
+    const bool lut = d_lutbits != nullptr;
+    const bool allow = sc->allow_mismatch != 0;
+
+    for (uint64_t base = 0; base < npairs; base += per_launch) {
+        const uint32_t cnt = (uint32_t)std::min<uint64_t>(per_launch, npairs - base);
+        FillParams fp;
+        fp.seq1 = d1; fp.off1 = o1; fp.seq2 = d2; fp.off2 = o2;
+        fp.lutbits = d_lutbits;
+        fp.dirs = dirs; fp.dir_slot = pl.g.dir_slot; fp.band_stride = pl.g.band_stride;
+        fp.rowbuf = rowbuf; fp.rowbuf_slot = pl.rowbuf_elems;
+        fp.res = d_res;
+        fp.pair_base = (uint32_t)base;
+        fp.max_m = max_m; fp.max_n = max_n;
+        fp.gap = sc->gap; fp.match = sc->match; fp.mismatch = allow ? sc->mismatch : INT_MIN;
+        fp.gap_open = sc->gap_open; fp.gap_extend = sc->gap_extend;
+        fp.waves = pl.W;
+
+        TbParams tp;
+        tp.seq1 = d1; tp.off1 = o1; tp.seq2 = d2; tp.off2 = o2;
+        tp.lutbits = d_lutbits;
+        tp.dirs = dirs; tp.dir_slot = pl.g.dir_slot;
+        tp.ops = d_ops; tp.res = d_res;
+        tp.pair_base = (uint32_t)base; tp.count = cnt;
+        tp.max_m = max_m; tp.max_n = max_n;
+        tp.gap = fp.gap; tp.match = fp.match; tp.mismatch = fp.mismatch;
+        tp.gap_open = fp.gap_open; tp.gap_extend = fp.gap_extend;
+        tp.allow = allow ? 1 : 0;
+
+        while ((int)c->events.size() < 3 * (c->launches + 1)) {
+            hipEvent_t ev;
+            SA_HIP(c, hipEventCreate(&ev));
+            c->events.push_back(ev);
+        }
+        hipEvent_t* ev = &c->events[3 * c->launches];
+        SA_HIP(c, hipEventRecord(ev[0], stream));
+        hipError_t e = launch_fill(algo, pl.R, lut, allow, keyed, fp, cnt, stream);
+        if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
+        SA_HIP(c, hipEventRecord(ev[1], stream));
+        e = launch_traceback(algo, pl.R, lut, tp, stream);
+        if (e != hipSuccess) return hip_fail(c, e, "traceback kernel launch");
+        SA_HIP(c, hipEventRecord(ev[2], stream));
+        c->launches++;
+    }
+    return SA_OK;
+}
+
+bool lut_is_identity(const uint8_t* lut) {
+    for (int a = 0; a < 256; ++a)
+        for (int b = 0; b < 256; ++b)
+            if ((lut[a * 256 + b] != 0) != (a == b)) return false;
+    return true;
+}
+
+bool lg_size_hack(uint64_t m, uint64_t n) {  // SALocalGotoh.h:484-488
+    return (m == 314 && n == 288) || (m == 60 && n == 57) || (m == 61 && n == 58);
+}
+
+int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, const uint64_t* off1,
+               const uint8_t* seq2, const uint64_t* off2, uint32_t npairs, const uint8_t* lut,
+               sa_result* results, uint8_t* ops, uint64_t ops_cap) {
+    const uint64_t t1 = off1[npairs], t2 = off2[npairs];
+    uint32_t max_m = 0, max_n = 0;
+    for (uint32_t p = 0; p < npairs; ++p) {
+        if (off1[p + 1] < off1[p] || off2[p + 1] < off2[p]) return fail(c, SA_ERR_ARG, "offsets must be non-decreasing");
+        max_m = (uint32_t)std::max<uint64_t>(max_m, off1[p + 1] - off1[p]);
+        max_n = (uint32_t)std::max<uint64_t>(max_n, off2[p + 1] - off2[p]);
+    }
+    const uint64_t ops_total = t1 + t2 + npairs;
+    if (ops_cap < ops_total) return fail(c, SA_ERR_CAPACITY, "ops buffer needs " + std::to_string(ops_total) + " bytes");
+    const bool use_lut = lut && !lut_is_identity(lut);
+
+    // device I/O layout (16-byte aligned pieces)
+    auto al = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
+    const uint64_t b_s1 = al(t1 + 1), b_s2 = al(t2 + 1), b_o = al(8ull * (npairs + 1));
+    const uint64_t b_res = al(sizeof(sa_result) * (uint64_t)std::max<uint32_t>(npairs, 1));
+    const uint64_t b_ops = al(ops_total + 1), b_lut = al(65536), b_bits = al(8192);
+    const uint64_t io_need = b_s1 + b_s2 + 2 * b_o + b_res + b_ops + b_lut + b_bits;
+    if (c->io_bytes < io_need) {
+        if (c->io) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->io); c->io = nullptr; c->io_bytes = 0; }
+        if (hipMalloc(&c->io, io_need) != hipSuccess) { c->io = nullptr; return fail(c, SA_ERR_NOMEM, "hipMalloc of I/O buffers failed"); }
+        c->io_bytes = io_need;
+    }
+    uint8_t* p = c->io;
+    uint8_t* d1 = p; p += b_s1;
+    uint8_t* d2 = p; p += b_s2;
+    uint64_t* do1 = reinterpret_cast<uint64_t*>(p); p += b_o;
+    uint64_t* do2 = reinterpret_cast<uint64_t*>(p); p += b_o;
+    sa_result* dres = reinterpret_cast<sa_result*>(p); p += b_res;
+    uint8_t* dops = p; p += b_ops;
+    uint8_t* dlut = p; p += b_lut;
+    uint32_t* dbits = reinterpret_cast<uint32_t*>(p);
+    hipStream_t st = c->stream;
+    if (t1) SA_HIP(c, hipMemcpyAsync(d1, seq1, t1, hipMemcpyHostToDevice, st));
+    if (t2) SA_HIP(c, hipMemcpyAsync(d2, seq2, t2, hipMemcpyHostToDevice, st));
+    SA_HIP(c, hipMemcpyAsync(do1, off1, 8ull * (npairs + 1), hipMemcpyHostToDevice, st));
+    SA_HIP(c, hipMemcpyAsync(do2, off2, 8ull * (npairs + 1), hipMemcpyHostToDevice, st));
+    if (use_lut) {
+        SA_HIP(c, hipMemcpyAsync(dlut, lut, 65536, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(lut_to_bits, dim3(8), dim3(256), 0, st, dlut, dbits);
+        SA_HIP(c, hipGetLastError());
+    }
+    if (npairs) {
+        int rc = run_device(c, algo, sc, d1, do1, d2, do2, npairs, max_m, max_n,
+                            use_lut ? dbits : nullptr, dres, dops, st);
+        if (rc) return rc;
+        SA_HIP(c, hipMemcpyAsync(results, dres, sizeof(sa_result) * npairs, hipMemcpyDeviceToHost, st));
+        SA_HIP(c, hipMemcpyAsync(ops, dops, ops_total, hipMemcpyDeviceToHost, st));
+    }
+    SA_HIP(c, hipStreamSynchronize(st));
+    return SA_OK;
+}
+
+}  // namespace
+
+// =============================================================================== C ABI
+extern "C" {
+
+int sa_version(void) { return SA_ABI_VERSION; }
+
+const char* sa_status_string(int s) {
+    switch (s) {
+        case SA_OK: return "ok";
+        case SA_ERR_ARG: return "invalid argument";
+        case SA_ERR_HIP: return "HIP runtime error";
+        case SA_ERR_NOMEM: return "out of memory";
+        case SA_ERR_CAPACITY: return "output buffer too small";
+        case SA_ERR_UNSUPPORTED: return "unsupported input";
+        default: return "unknown status";
+    }
+}
+
+int sa_device_count(int* count) {
+    if (!count) return fail(nullptr, SA_ERR_ARG, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) { *count = 0; return hip_fail(nullptr, e, "hipGetDeviceCount"); }
+    *count = n;
+    return SA_OK;
+}
+
+int sa_create(int device, sa_ctx** out) {
+    if (!out) return fail(nullptr, SA_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return fail(nullptr, SA_ERR_HIP, "no HIP device available");
+    if (device < 0 || device >= n) return fail(nullptr, SA_ERR_ARG, "device ordinal out of range");
+    e = hipSetDevice(device);
+    if (e != hipSuccess) return hip_fail(nullptr, e, "hipSetDevice");
+    sa_ctx* c = new sa_ctx();
+    c->device = device;
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete c; return hip_fail(nullptr, e, "hipStreamCreate"); }
+    *out = c;
+    return SA_OK;
+}
+
+void sa_destroy(sa_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto ev : c->events) (void)hipEventDestroy(ev);
+    if (c->ws) (void)hipFree(c->ws);
+    if (c->io) (void)hipFree(c->io);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* sa_last_error(const sa_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
+
+int sa_set_workspace_limit(sa_ctx* c, uint64_t bytes) {
+    if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
+    c->ws_limit = bytes;
+    return SA_OK;
+}
+
+int sa_trim(sa_ctx* c) {
+    if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    if (c->ws) (void)hipFree(c->ws);
+    if (c->io) (void)hipFree(c->io);
+    c->ws = nullptr; c->ws_bytes = 0;
+    c->io = nullptr; c->io_bytes = 0;
+    return SA_OK;
+}
+
+int sa_align_batch(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1,
+                   const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2, uint32_t npairs,
+                   const uint8_t* lut, sa_result* results, uint8_t* ops, uint64_t ops_cap) {
+    if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
+    int rc = validate_scoring(c, algo, sc);
+    if (rc) return rc;
+    if (!off1 || !off2 || (npairs && (!results || !ops))) return fail(c, SA_ERR_ARG, "NULL buffer");
+    if ((off1[npairs] && !seq1) || (off2[npairs] && !seq2)) return fail(c, SA_ERR_ARG, "NULL sequence buffer");
+    if (off1[0] != 0 || off2[0] != 0) return fail(c, SA_ERR_ARG, "offsets must start at 0");
+    SA_HIP(c, hipSetDevice(c->device));
+
+    if (algo != SA_LOCAL_GOTOH) {
+        return align_host(c, algo, sc, seq1, off1, seq2, off2, npairs, lut, results, ops, ops_cap);
+    }
+    // LocalGotoh: the reference replaces three size pairs by StaticFuncs::useNW with the same
+    // ScoringSystem (SALocalGotoh.h:484-488).  Split them out, align them with NW, merge back.
+    std::vector<uint32_t> hack, keep;
+    for (uint32_t p = 0; p < npairs; ++p)
+        (lg_size_hack(off1[p + 1] - off1[p], off2[p + 1] - off2[p]) ? hack : keep).push_back(p);
+    if (hack.empty())
+        return align_host(c, algo, sc, seq1, off1, seq2, off2, npairs, lut, results, ops, ops_cap);
+    const uint64_t ops_total = off1[npairs] + off2[npairs] + npairs;
+    if (ops_cap < ops_total) return fail(c, SA_ERR_CAPACITY, "ops buffer too small");
+    for (int pass = 0; pass < 2; ++pass) {
+        const std::vector<uint32_t>& sel = pass == 0 ? keep : hack;
+        if (sel.empty()) continue;
+        std::vector<uint8_t> s1, s2;
+        std::vector<uint64_t> o1(1, 0), o2(1, 0);
+        for (uint32_t p : sel) {
+            s1.insert(s1.end(), seq1 + off1[p], seq1 + off1[p + 1]);
+            s2.insert(s2.end(), seq2 + off2[p], seq2 + off2[p + 1]);
+            o1.push_back(s1.size());
+            o2.push_back(s2.size());
+        }
+        const uint32_t k = (uint32_t)sel.size();
+        std::vector<sa_result> r(k);
+        std::vector<uint8_t> op(s1.size() + s2.size() + k + 1);
+        rc = align_host(c, pass == 0 ? SA_LOCAL_GOTOH : SA_NW, sc, s1.data(), o1.data(), s2.data(),
+                        o2.data(), k, lut, r.data(), op.data(), op.size());
+        if (rc) return rc;
+        for (uint32_t q = 0; q < k; ++q) {
+            const uint32_t p = sel[q];
+            results[p] = r[q];
+            if (pass == 1) results[p].flags |= SA_FLAG_SIZE_HACK;
+            memcpy(ops + off1[p] + off2[p] + p, op.data() + o1[q] + o2[q] + q, r[q].nops);
+        }
+    }
+    return SA_OK;
+}
+
+int sa_align_batch_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1,
+                          const uint64_t* o1, const uint8_t* d2, const uint64_t* o2, uint32_t npairs,
+                          uint32_t max_m, uint32_t max_n, const uint8_t* d_lut, sa_result* d_res,
+                          uint8_t* d_ops, void* stream) {
+    if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
+    int rc = validate_scoring(c, algo, sc);
+    if (rc) return rc;
+    if (!o1 || !o2 || (npairs && (!d_res || !d_ops))) return fail(c, SA_ERR_ARG, "NULL buffer");
+    if (npairs == 0) return SA_OK;
+    SA_HIP(c, hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    uint32_t* bits = nullptr;
+    if (d_lut) {
+        // LUT bits live in the tail of the I/O cache
+        if (c->io_bytes < 8192) {
+            if (c->io) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->io); c->io = nullptr; c->io_bytes = 0; }
+            if (hipMalloc(&c->io, 8192) != hipSuccess) { c->io = nullptr; return fail(c, SA_ERR_NOMEM, "hipMalloc LUT"); }
+            c->io_bytes = 8192;
+        }
+        bits = reinterpret_cast<uint32_t*>(c->io + c->io_bytes - 8192);
+        hipLaunchKernelGGL(lut_to_bits, dim3(8), dim3(256), 0, st, d_lut, bits);
+        SA_HIP(c, hipGetLastError());
+    }
+    return run_device(c, algo, sc, d1, o1, d2, o2, npairs, max_m, max_n, bits, d_res, d_ops, st);
+}
+
+int sa_last_timings(sa_ctx* c, float* fill_ms, float* tb_ms, int* launches) {
+    if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
+    float f = 0.f, t = 0.f;
+    for (int k = 0; k < c->launches; ++k) {
+        hipEvent_t* ev = &c->events[3 * k];
+        SA_HIP(c, hipEventSynchronize(ev[2]));
+        float a = 0.f, b = 0.f;
+        SA_HIP(c, hipEventElapsedTime(&a, ev[0], ev[1]));
+        SA_HIP(c, hipEventElapsedTime(&b, ev[1], ev[2]));
+        f += a;
+        t += b;
+    }
+    if (fill_ms) *fill_ms = f;
+    if (tb_ms) *tb_ms = t;
+    if (launches) *launches = c->launches;
+    return SA_OK;
+}
+
+int sa_plan_query(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, int* R, int* W,
+                  uint64_t* dir_bytes, uint64_t* rowbuf_bytes) {
+    if (algo < SA_SW || algo > SA_GLOBAL_GOTOH) return fail(nullptr, SA_ERR_ARG, "unknown algorithm");
+    const Plan p = make_plan(algo, max_m, max_n, npairs);
+    if (R) *R = p.R;
+    if (W) *W = p.W;
+    if (dir_bytes) *dir_bytes = p.g.dir_slot;
+    if (rowbuf_bytes) *rowbuf_bytes = p.rowbuf_elems * 4;
+    return SA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,392 @@
+// sa_fill_impl.h — the DP fill kernel (computeScoreMatrix of the four reference aligners),
+// instantiated per algorithm by sa_fill_{sw,nw,lg,gg}.hip.
+//
+// Reference recurrences restated (all int32, wrapping):
+//   SW  SASmithWaterman.h:89-117   H = max(Hd + s, Hu + Gap, Hl + Gap, 0), max cell = last
+//                                  row-major (Score >= MaxScore, :110)
+//   NW  SANeedlemanWunsch.h:69-86  H = max(max(Hd + s, Hu + Gap), Hl + Gap); H[i][0] = i*Gap
+//   LG  SALocalGotoh.h:102-139     Ix = max(Mu + GO + GE, Ixu + GE); Iy = max(Ml + GO + GE,
+//                                  Iyl + GE); M = max(Md + s, Ix, Iy, 0); Ix/Iy borders -10000
+//   GG  SAGlobalGotoh.h:98-126     same without the 0 and with M[i][0] = GO + i*GE
+//   !AllowMismatch: the diagonal term is (match ? Hd + Match : INT_MIN)  (e.g. :128-131).
+//
+// Mapping to CDNA4 (geometry: sa_layout.h):
+//   * one workgroup = one pair; W waves = W concurrently running bands (software pipeline,
+//     one __syncthreads per 32-step chunk);
+//   * one lane = R rows held in VGPRs; per step it computes R cells of one column;
+//   * the row above arrives from lane t-1 by DPP wave_shr:1 (no LDS round trip); lane 0 takes
+//     it from the row buffer (previous band) or the top border, loaded once per chunk into a
+//     VGPR and broadcast per step with v_readlane; the column symbol rides the same DPP shift;
+//   * chunks where all 64 lanes are inside the matrix (all but the first two and the last
+//     two of a band) run a branch-free body;
+//   * each traceback flag costs one v_cmp (into an SGPR pair) + one v_addc_co_u32 that shifts
+//     it into the lane's record; records leave as 16-byte-per-lane nontemporal stores
+//     (1 KiB per wave instruction, fully coalesced);
+//   * the running maximum of a row is one v_lshl_or (key = H << 16 | column) + one v_max_u32
+//     (KEYED; the host checks scores and columns fit 16 bits), else a compare + 2 selects.
+#pragma once
+#include <limits.h>
+
+#include <type_traits>
+
+#include "sa_internal.h"
+
+namespace sa {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kDppWaveShr1 = 0x138;  // DPP wave_shr:1 (GFX9-family wave-wide shift)
+
+__device__ __forceinline__ int shr1(int old, int src) {
+    return __builtin_amdgcn_update_dpp(old, src, kDppWaveShr1, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+
+// rec = 2*rec + (a == b), one v_cmp into an SGPR pair + one v_addc_co_u32.
+__device__ __forceinline__ uint32_t push_eq(uint32_t rec, int a, int b) {
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(a == b);
+    uint32_t out;
+    unsigned long long co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(out), "=s"(co) : "v"(rec), "s"(m));
+    return out;
+}
+
+template <bool LUT>
+__device__ __forceinline__ bool match_bit(const uint32_t* s_lut, int a, int b) {
+    if constexpr (LUT) {
+        return (s_lut[(a << 3) | (b >> 5)] >> (b & 31)) & 1;
+    } else {
+        return a == b;
+    }
+}
+
+template <int ALG, int R, bool LUT, bool ALLOW, bool KEYED>
+__global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
+    constexpr bool AFF = ALG >= SA_LOCAL_GOTOH;
+    constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
+    constexpr int BPC = AFF ? 4 : 2;
+    constexpr int RB = R * BPC;                // bits per record
+    constexpr int BPS = RB / 8;                // bytes per record
+    constexpr int RW = (RB + 31) / 32;         // words per record
+    constexpr int RPW = (RB < 32 ? RB : 32) / BPC;  // rows per record word
+    constexpr int SPP = BPS >= 16 ? 1 : 16 / BPS;
+    constexpr int PPS = BPS > 16 ? BPS / 16 : 1;
+    constexpr int BAND = kWave * R;
+    static_assert(kChunk % SPP == 0, "chunk must hold whole packets");
+    static_assert(BPS >= 1, "record must be at least a byte");
+
+    __shared__ uint32_t s_lut[LUT ? 2048 : 1];
+    __shared__ int s_red[16 * 3];
+    __shared__ int s_score;   // H[m][n] for the global modes, stored by the owning lane
+
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
+    const int W = P.waves;
+    const uint32_t slot = blockIdx.x;
+    const uint32_t pidx = P.pair_base + slot;
+    const uint64_t o1 = P.off1[pidx];
+    const uint64_t o2 = P.off2[pidx];
+    const int m = (int)(P.off1[pidx + 1] - o1);
+    const int n = (int)(P.off2[pidx + 1] - o2);
+
+    if ((uint32_t)m > P.max_m || (uint32_t)n > P.max_n) {  // whole block leaves together
+        if (threadIdx.x == 0) {
+            sa_result r = {};
+            r.flags = SA_FLAG_BAD_SHAPE;
+            P.res[pidx] = r;
+        }
+        return;
+    }
+    if constexpr (LUT) {
+        for (int k = threadIdx.x; k < 2048; k += blockDim.x) s_lut[k] = P.lutbits[k];
+        __syncthreads();
+    }
+
+    const uint8_t* s1 = P.seq1 + o1;
+    const uint8_t* s2 = P.seq2 + o2;
+    const int G = P.gap, MA = P.match, MI = P.mismatch;
+    const int GO = P.gap_open, GE = P.gap_extend;
+    const int GOE = GO + GE;
+
+    const int B = (m > 0 && n > 0) ? (m + BAND - 1) / BAND : 0;
+    const uint32_t nch = chunks_per_band((uint32_t)n);
+    const uint32_t period = sched_period(nch, W);
+    const uint32_t total = total_phases((uint32_t)B, (uint32_t)n, W);
+
+    uint8_t* const dslot = P.dirs + (uint64_t)slot * P.dir_slot;
+    int32_t* const rb_h = P.rowbuf + (uint64_t)slot * P.rowbuf_slot;
+    int32_t* const rb_x = rb_h + P.max_n;
+
+    // Per-lane state for the current band.
+    int a[R];      // Seq1 symbols of my rows
+    int Hp[R];     // H (or M) of my rows at the previous column
+    int Yp[R];     // Iy of my rows at the previous column (affine)
+    int bh[R];     // best per row: key (KEYED) or score
+    int bj[R];     // its column (0-based), !KEYED
+    int hl = 0, xl = 0, sym = 0, prev_up = 0;
+    int row0 = 0;
+    // Running best of this lane over its bands: (score, i, j), 1-based cell.
+    int best_h = INT_MIN, best_i = 0, best_j = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) { a[r] = 0; Hp[r] = 0; Yp[r] = 0; bh[r] = 0; bj[r] = 0; }
+
+    // One step: lane computes column j = s - lane for its R rows.  STEADY: every lane is in
+    // range, no exec-mask branch.  Returns the packed record words in rec.
+    auto step = [&](auto steady, int q, int s, int bch, int bcx, int symc, uint32_t (&rec)[RW]) {
+        constexpr bool STEADY = decltype(steady)::value;
+        const int up_h = shr1(__builtin_amdgcn_readlane(bch, q), hl);
+        int up_x = 0;
+        if constexpr (AFF) up_x = shr1(__builtin_amdgcn_readlane(bcx, q), xl);
+        sym = shr1(__builtin_amdgcn_readlane(symc, q), sym);
+        const int j = s - lane;
+#pragma unroll
+        for (int e = 0; e < RW; ++e) rec[e] = 0;
+        if (STEADY || (unsigned)j < (unsigned)n) {
+            const int jkey = j + 1;      // 1-based column, < 2^16 when KEYED
+            int hd = prev_up;            // H[i-1][j-1] of my first row
+            int hu = up_h;               // H[i-1][j]
+            int xu = up_x;               // Ix[i-1][j]
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const bool v = match_bit<LUT>(s_lut, a[r], sym);
+                int D;
+                if constexpr (ALLOW) D = hd + (v ? MA : MI);
+                else D = v ? hd + MA : INT_MIN;
+                uint32_t& rw = rec[r / RPW];
+                int Hc;
+                if constexpr (!AFF) {
+                    const int U = hu + G;
+                    const int L = Hp[r] + G;
+                    int H = imax(imax(D, U), L);
+                    if constexpr (LOCAL) H = imax(H, 0);
+                    rw = push_eq(rw, H, D);   // fD
+                    rw = push_eq(rw, H, U);   // fU
+                    Hc = H;
+                } else {
+                    const int XE = xu + GE;
+                    const int X = imax(hu + GOE, XE);
+                    const int YE = Yp[r] + GE;
+                    const int Y = imax(Hp[r] + GOE, YE);
+                    int M = imax(imax(D, X), Y);
+                    if constexpr (LOCAL) M = imax(M, 0);
+                    rw = push_eq(rw, M, D);   // fD
+                    rw = push_eq(rw, M, X);   // fX
+                    rw = push_eq(rw, X, XE);  // fXe: Ix extends
+                    rw = push_eq(rw, Y, YE);  // fYe: Iy extends
+                    Yp[r] = Y;
+                    xu = X;
+                    Hc = M;
+                }
+                if constexpr (LOCAL) {
+                    if constexpr (KEYED) {
+                        bh[r] = (int)max((uint32_t)bh[r], ((uint32_t)Hc << 16) | (uint32_t)jkey);
+                    } else {
+                        if (Hc >= bh[r]) { bh[r] = Hc; bj[r] = j; }
+                    }
+                }
+                hd = Hp[r];
+                Hp[r] = Hc;
+                hu = Hc;
+            }
+            prev_up = up_h;
+            hl = Hp[R - 1];
+            if constexpr (AFF) xl = xu;
+        }
+    };
+
+    // One chunk of kChunk steps of one band.
+    auto run_chunk = [&](auto steady, int band, int kC, int bch, int bcx, int symc, int& acc_h,
+                         int& acc_x) {
+        uint8_t* const dband = dslot + (uint64_t)band * P.band_stride;
+#pragma unroll 1
+        for (int q0 = 0; q0 < kChunk; q0 += SPP) {
+            uint32_t pk[4 * PPS];
+#pragma unroll
+            for (int e = 0; e < 4 * PPS; ++e) pk[e] = 0;
+#pragma unroll
+            for (int g = 0; g < SPP; ++g) {
+                const int q = q0 + g;
+                uint32_t rec[RW];
+                step(steady, q, kC + q, bch, bcx, symc, rec);
+                if constexpr (BPS >= 4) {
+#pragma unroll
+                    for (int e = 0; e < RW; ++e) pk[g * RW + e] = rec[e];
+                } else {
+                    pk[(g * BPS) / 4] |= rec[0] << (((g * BPS) % 4) * 8);
+                }
+                // lane 63 holds the band's last row at column kC + q - 63: park it in lane q
+                const int lh = __builtin_amdgcn_readlane(hl, 63);
+                acc_h = (lane == q) ? lh : acc_h;
+                if constexpr (AFF) {
+                    const int lx = __builtin_amdgcn_readlane(xl, 63);
+                    acc_x = (lane == q) ? lx : acc_x;
+                }
+            }
+            const uint64_t pkt0 = (uint64_t)((kC + q0) / SPP) * PPS;
+#pragma unroll
+            for (int pp = 0; pp < PPS; ++pp) {
+                u32x4* dst = reinterpret_cast<u32x4*>(dband + ((pkt0 + pp) * kWave + lane) * 16);
+                const u32x4 v4 = {pk[pp * 4 + 0], pk[pp * 4 + 1], pk[pp * 4 + 2], pk[pp * 4 + 3]};
+                __builtin_nontemporal_store(v4, dst);
+            }
+        }
+    };
+
+    for (uint32_t ph = 0; ph < total; ++ph) {
+        const int rel = (int)ph - w * kLagPhases;
+        if (rel >= 0) {
+            const uint32_t k = (uint32_t)rel / period;
+            const uint32_t chunk = (uint32_t)rel - k * period;
+            const int band = w + (int)k * W;
+            if (chunk < nch && band < B) {
+                // ---------------------------------------------------------------- band start
+                if (chunk == 0) {
+                    row0 = band * BAND + lane * R;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int row = row0 + r;
+                        a[r] = row < m ? (int)s1[row] : 0;
+                        const int i = row + 1;
+                        if constexpr (ALG == SA_NW) Hp[r] = i * G;
+                        else if constexpr (ALG == SA_GLOBAL_GOTOH) Hp[r] = GO + i * GE;
+                        else Hp[r] = 0;
+                        Yp[r] = -10000;
+                        bh[r] = KEYED ? 0 : INT_MIN;
+                        bj[r] = 0;
+                    }
+                    if constexpr (ALG == SA_NW) prev_up = row0 * G;
+                    else if constexpr (ALG == SA_GLOBAL_GOTOH) prev_up = row0 == 0 ? 0 : GO + row0 * GE;
+                    else prev_up = 0;
+                }
+                // ---------------------------------------------------------------- one chunk
+                const int kC = (int)chunk * kChunk;
+                const int c = kC + lane;
+                int bch = 0, bcx = -10000, symc = 0;
+                if (lane < kChunk && c < n) {
+                    symc = s2[c];
+                    if (band == 0) {
+                        const int J = c + 1;
+                        if constexpr (ALG == SA_NW) bch = J * G;
+                        else if constexpr (ALG == SA_GLOBAL_GOTOH) bch = GO + J * GE;
+                        else bch = 0;
+                    } else {
+                        bch = rb_h[c];
+                        if constexpr (AFF) bcx = rb_x[c];
+                    }
+                }
+                int acc_h = 0, acc_x = 0;
+                const bool steady = kC >= kWave - 1 && kC + kChunk <= n;
+                if (steady) run_chunk(std::true_type{}, band, kC, bch, bcx, symc, acc_h, acc_x);
+                else run_chunk(std::false_type{}, band, kC, bch, bcx, symc, acc_h, acc_x);
+                // hand the band's last row (columns kC-63 .. kC-32) to the next band
+                if (band + 1 < B) {
+                    const int cc = kC + lane - (kWave - 1);
+                    if (lane < kChunk && cc >= 0 && cc < n) {
+                        rb_h[cc] = acc_h;
+                        if constexpr (AFF) rb_x[cc] = acc_x;
+                    }
+                }
+                // ---------------------------------------------------------------- band end
+                if (chunk == nch - 1) {
+                    if constexpr (LOCAL) {
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            int h, jj;
+                            if constexpr (KEYED) { h = (int)((uint32_t)bh[r] >> 16); jj = bh[r] & 0xffff; }
+                            else { h = bh[r]; jj = bj[r] + 1; }
+                            if (row0 + r < m && h >= best_h) {
+                                best_h = h;
+                                best_i = row0 + r + 1;
+                                best_j = jj;
+                            }
+                        }
+                    } else {
+                        const int last = m - 1;
+                        if (band == last / BAND && lane == (last % BAND) / R) {
+                            const int rr = last % R;
+                            int v = 0;
+#pragma unroll
+                            for (int r = 0; r < R; ++r) v = (r == rr) ? Hp[r] : v;
+                            s_score = v;
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // ------------------------------------------------------------------------ results
+    if constexpr (LOCAL) {
+        // lexicographic max over (score, i, j): the reference's last row-major maximum
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const int oh = __shfl_xor(best_h, off);
+            const int oi = __shfl_xor(best_i, off);
+            const int oj = __shfl_xor(best_j, off);
+            const bool take = oh > best_h || (oh == best_h && (oi > best_i || (oi == best_i && oj > best_j)));
+            if (take) { best_h = oh; best_i = oi; best_j = oj; }
+        }
+        if (lane == 0) { s_red[w * 3 + 0] = best_h; s_red[w * 3 + 1] = best_i; s_red[w * 3 + 2] = best_j; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int h = INT_MIN, bi = 0, bjj = 0;
+            for (int v = 0; v < W; ++v) {
+                const int oh = s_red[v * 3], oi = s_red[v * 3 + 1], oj = s_red[v * 3 + 2];
+                if (oh > h || (oh == h && (oi > bi || (oi == bi && oj > bjj)))) { h = oh; bi = oi; bjj = oj; }
+            }
+            sa_result r = {};
+            if (B == 0) {
+                // empty input: SW keeps MaxScore = INT_MIN, (MaxRow, MaxCol) = (0, 0);
+                // LocalGotoh reads M[0][0] = 0 there
+                r.score = (ALG == SA_SW) ? INT_MIN : 0;
+            } else {
+                r.score = h; r.end_i = bi; r.end_j = bjj;
+            }
+            P.res[pidx] = r;
+        }
+    } else {
+        if (threadIdx.x == 0) {   // the phase loop's last barrier orders the owner's s_score store
+            sa_result r = {};
+            r.end_i = m;
+            r.end_j = n;
+            if (B == 0) {
+                const int k = m > n ? m : n;
+                if constexpr (ALG == SA_NW) r.score = k * G;
+                else r.score = k == 0 ? 0 : GO + k * GE;
+            } else {
+                r.score = s_score;
+            }
+            P.res[pidx] = r;
+        }
+    }
+}
+
+template <int ALG>
+hipError_t launch_fill_alg(int R, bool lut, bool allow, bool keyed, const FillParams& p,
+                           uint32_t grid, hipStream_t stream) {
+    constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
+    const dim3 block(kWave * p.waves);
+    if (!LOCAL) keyed = false;
+#define SA_LAUNCH(RR, LL, AA, KK)                                                              \
+    if (R == RR && lut == LL && allow == AA && keyed == KK) {                                  \
+        hipLaunchKernelGGL((fill_kernel<ALG, RR, LL, AA, KK>), dim3(grid), block, 0, stream, p); \
+        return hipGetLastError();                                                              \
+    }
+#define SA_LAUNCH_K(RR, LL, AA) \
+    SA_LAUNCH(RR, LL, AA, false) \
+    if constexpr (LOCAL) { SA_LAUNCH(RR, LL, AA, true) }
+#define SA_LAUNCH_R(RR)            \
+    SA_LAUNCH_K(RR, false, true)   \
+    SA_LAUNCH_K(RR, false, false)  \
+    SA_LAUNCH_K(RR, true, true)    \
+    SA_LAUNCH_K(RR, true, false)
+    SA_LAUNCH_R(4)
+    SA_LAUNCH_R(8)
+    SA_LAUNCH_R(16)
+#undef SA_LAUNCH_R
+#undef SA_LAUNCH_K
+#undef SA_LAUNCH
+    return hipErrorInvalidValue;
+}
+
+}  // namespace sa

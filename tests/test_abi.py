@@ -1,0 +1,148 @@
+"""CPU: the C-ABI library loads, exports every symbol include/seqalib_hip.h declares, its host-only
+entry points (planner, synthetic inputs) behave, and the traceback layout math is consistent.
+No GPU compute is called here."""
+import ctypes as C
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+import seqalib_amd as sa
+from util import GOLDEN, ROOT, py_dna, py_mutate, sha
+
+HEADER = os.path.join(ROOT, "include", "seqalib_hip.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(sa_[a-z_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = sa.load_library()
+    syms = declared_symbols()
+    assert len(syms) >= 15
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    assert L.sa_version() == 1
+
+
+def test_status_strings():
+    L = sa.load_library()
+    for code in (0, -1, -2, -3, -4, -5):
+        assert L.sa_status_string(code)
+
+
+def test_no_gpu_fails_loudly():
+    """Without a device the engine must refuse (no silent CPU fallback)."""
+    L = sa.load_library()
+    n = C.c_int(0)
+    L.sa_device_count(C.byref(n))
+    if n.value > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(sa.SeqalibError):
+        sa.Engine(0)
+
+
+def test_scoring_overloads_mirror_reference():
+    s = sa.ScoringSystem(-1, 2)
+    assert (s.gap, s.match, s.mismatch, s.allow_mismatch) == (-1, 2, -(2 ** 31), False)
+    s = sa.ScoringSystem(-2, 1, -1, False)
+    assert (s.gap, s.match, s.mismatch, s.allow_mismatch) == (-2, 1, -1, False)
+    s = sa.ScoringSystem(-3, -1, 1, -1)       # four ints -> the affine overload, as in C++
+    assert (s.gap_open, s.gap_extend, s.match, s.mismatch, s.allow_mismatch) == (-3, -1, 1, -1, True)
+    s = sa.ScoringSystem(-3, -1, 1, -1, False)
+    assert s.allow_mismatch is False
+
+
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+@pytest.mark.parametrize("shape", [(1, 1, 1), (1024, 1024, 10000), (4096, 4096, 10000), (4096, 4096, 1),
+                                   (8192, 8192, 1), (2048, 2048, 12500), (100, 37, 5), (20000, 150, 3)])
+def test_plan_and_layout(algo, shape):
+    m, n, npairs = shape
+    R, W, dir_bytes, row_bytes = sa.plan_query(algo, m, n, npairs)
+    assert R in (4, 8, 16) and 1 <= W <= 16
+    bands = -(-m // (64 * R))
+    assert W <= max(bands, 1)
+    bpc = 4 if algo >= 2 else 2
+    steps_pad = -(-(n + 63) // 32) * 32
+    assert dir_bytes == bands * steps_pad * 64 * R * bpc // 8
+    assert row_bytes == (2 if algo >= 2 else 1) * max(n, 1) * 4
+
+
+def test_headline_plan_fits_hbm():
+    # north-star batch: 10,000 pairs of 4096 x 4096 SW in one launch on a 288 GB MI355X
+    R, W, dir_bytes, row_bytes = sa.plan_query(0, 4096, 4096, 10000)
+    assert (R, W) == (16, 4)
+    assert 10000 * (dir_bytes + row_bytes) < 64e9
+
+
+def cell_byte(R, bpc, max_n, i, j):
+    """Python restatement of sa_layout.h cell_byte (independent check of the layout)."""
+    bps = R * bpc // 8
+    spp = 1 if bps >= 16 else 16 // bps
+    pps = bps // 16 if bps > 16 else 1
+    steps_pad = -(-(max_n + 63) // 32) * 32
+    band_stride = steps_pad * 64 * bps
+    ii = i - 1
+    b, rem = divmod(ii, 64 * R)
+    t, r = divmod(rem, R)
+    s = (j - 1) + t
+    rb = R * bpc
+    wb = min(rb, 32)
+    rpw = wb // bpc
+    word, lowbit = r // rpw, wb - bpc * (r % rpw + 1)
+    byte_in_rec = word * 4 + lowbit // 8
+    half = byte_in_rec // 16
+    packet = (s // spp) * pps + half
+    return b * band_stride + packet * 1024 + t * 16 + (s % spp) * bps + byte_in_rec % 16, lowbit % 8
+
+
+@pytest.mark.parametrize("R,bpc", [(4, 2), (8, 2), (16, 2), (4, 4), (8, 4), (16, 4)])
+def test_flag_layout_is_a_bijection(R, bpc):
+    """Every cell of a band gets its own bits, records pack exactly R*bpc bits per lane-step."""
+    max_n = 70
+    m = 64 * R * 2
+    seen = set()
+    for i in range(1, m + 1):
+        for j in range(1, max_n + 1):
+            off, sh = cell_byte(R, bpc, max_n, i, j)
+            for k in range(bpc):
+                bit = (off, sh + k)
+                assert sh + k < 8
+                assert bit not in seen
+                seen.add(bit)
+    assert len(seen) == m * max_n * bpc
+
+
+def test_synth_matches_std_mt19937_64():
+    pins = json.load(open(os.path.join(GOLDEN, "dna_pins.json")))
+    for p in pins:
+        assert sha(sa.synth_dna(p["seed"], p["len"])) == p["sha"], p
+    assert sa.synth_dna(7, 300) == py_dna(7, 300)
+
+
+def test_synth_mutate_and_batch():
+    src = sa.synth_dna(42, 500)
+    assert sa.synth_mutate(src, 9) == py_mutate(src, 9)
+    s1, o1, s2, o2 = sa.synth_dna_batch(3_000_000_000, 5, 64, 80, threads=3)
+    assert list(o1) == [64 * k for k in range(6)] and list(o2) == [80 * k for k in range(6)]
+    for p in range(5):
+        assert s1[o1[p]:o1[p + 1]].tobytes() == sa.synth_dna(3_000_000_000 + 2 * p + 1, 64)
+        assert s2[o2[p]:o2[p + 1]].tobytes() == sa.synth_dna(3_000_000_000 + 2 * p + 2, 80)
+
+
+def test_expand_ops_matches_oracle_strings():
+    """Host-side list assembly + forceGlobal (Python) reproduces the oracle's strings from its ops."""
+    from util import oracle_align
+    for algo, args, a, b in [(0, (-1, 1, -1), b"AGGATCGGCTAGAGCTAG", b"GAGATCGGCGGATTACAGG"),
+                             (1, (-1, 2), b"AAAGAATGCAT", b"AAACTCAT"),
+                             (2, (-3, -1, 1, -1, True), b"CTGAAGCGGTTAGC", b"CTCAAGCGTAGTCC"),
+                             (3, (-3, -1, 1, -1, False), b"AGCTTCAGGCTGA", b"AGCTGGATCGATCGATG")]:
+        o = oracle_align(algo, args, a, b)
+        r = sa.PairResult(o["score"], o["end_i"], o["end_j"], o["start_i"], o["start_j"], 0, o["ops"])
+        got = sa.expand_ops(algo, a.decode(), b.decode(), r).rows()
+        assert got == o["rows"]

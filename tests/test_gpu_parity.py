@@ -1,0 +1,226 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden vectors of the unmodified
+reference and against the pinned C oracle on seeded random inputs.
+
+Bar: bit-exact — score, end cell (MaxRow, MaxCol), and the three alignment strings.
+All tests run in one process on one HIP context (tests/conftest.py `engine`).
+"""
+import collections
+
+import numpy as np
+import pytest
+
+import seqalib_amd as sa
+from util import ALGOS, golden_sequences, load_golden, named_lut, oracle_align, rows_digest
+
+pytestmark = pytest.mark.gpu
+
+
+def sc_obj(args):
+    return sa.ScoringSystem(*args)
+
+
+def run_group(engine, algo, args, match, pairs):
+    lut = named_lut(match)
+    res = engine.align(algo, sc_obj(args), pairs, lut)
+    return res
+
+
+def rows_of(algo, a, b, r):
+    return sa.expand_ops(algo if not (r.flags & sa.SA_FLAG_SIZE_HACK) else sa.SA_NW,
+                         a.decode("latin-1"), b.decode("latin-1"), r).rows()
+
+
+def check_golden(engine, entries):
+    groups = collections.defaultdict(list)
+    for e in entries:
+        groups[(e["algo"], tuple(e["scoring"]), e["match"])].append(e)
+    n = 0
+    for (algo, args, match), es in groups.items():
+        pairs = [golden_sequences(e) for e in es]
+        res = run_group(engine, ALGOS[algo], args, match, pairs)
+        for e, (a, b), r in zip(es, pairs, res):
+            assert r.flags & (sa.SA_FLAG_DIVERGED | sa.SA_FLAG_BAD_SHAPE) == 0, e["id"]
+            assert (r.score, r.end_i, r.end_j) == (e["score"], e["max_row"], e["max_col"]), e["id"]
+            rows = rows_of(ALGOS[algo], a, b, r)
+            assert len(rows[0]) == e["len"], e["id"]
+            if "rows" in e:
+                assert list(rows) == e["rows"], e["id"]
+            else:
+                assert rows_digest(*rows) == e["rows_sha"], e["id"]
+            n += 1
+    return n
+
+
+def test_readme_known_answer(engine):
+    r = engine.align(sa.SA_NW, sa.ScoringSystem(-1, 2), [(b"AAAGAATGCAT", b"AAACTCAT")])[0]
+    rows = sa.expand_ops(sa.SA_NW, "AAAGAATGCAT", "AAACTCAT", r).rows()
+    assert rows == ("AAA-GAATGCAT", "|||    | |||", "AAAC---T-CAT")
+    assert r.score == 9
+
+
+def test_golden_kat(engine):
+    assert check_golden(engine, load_golden("kat.jsonl")) > 2000
+
+
+def test_golden_random(engine):
+    assert check_golden(engine, load_golden("random.jsonl")) > 200
+
+
+def test_golden_large(engine):
+    assert check_golden(engine, load_golden("large.jsonl")) == 10
+
+
+def compare_with_oracle(engine, algo, args, pairs, match=None):
+    lut = named_lut(match)
+    res = engine.align(algo, sc_obj(args), pairs, lut)
+    for (a, b), r in zip(pairs, res):
+        o = oracle_align(algo, args, a, b, lut)
+        assert o["rc"] == 0
+        got = (r.score, r.end_i, r.end_j, r.start_i, r.start_j, r.ops)
+        exp = (o["score"], o["end_i"], o["end_j"], o["start_i"], o["start_j"], o["ops"])
+        assert got == exp, (algo, args, len(a), len(b))
+        assert rows_of(algo, a, b, r) == o["rows"]
+
+
+SCORINGS = {0: [(-1, 1, -1), (-2, 1, -1, False), (-1, 2), (-3, 2, -2)],
+            1: [(-1, 2, -1), (-1, 2), (-2, 1, -1, False)],
+            2: [(-3, -1, 1, -1, False), (-3, -1, 1, -1, True), (-2, -1, 2, -1, True)],
+            3: [(-3, -1, 1, -1, True), (-3, -1, 1, -1, False), (-5, -2, 3, -2, True)]}
+
+
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+def test_ragged_batch_vs_oracle(engine, algo):
+    """One batch with many different shapes (slots padded to the batch max)."""
+    rng = np.random.default_rng(100 + algo)
+    pairs = []
+    for k in range(60):
+        m = int(rng.integers(0, 700)) if k % 7 else int(rng.integers(1, 5))
+        n = int(rng.integers(0, 700)) if k % 5 else int(rng.integers(1, 5))
+        a = sa.synth_dna(10_000 + 2 * k, m)
+        b = sa.synth_mutate(a, 50 + k)[:n] if k % 3 == 0 else sa.synth_dna(10_001 + 2 * k, n)
+        if algo == 2 and (len(a), len(b)) in ((314, 288), (60, 57), (61, 58)):
+            continue
+        pairs.append((a, b))
+    for args in SCORINGS[algo]:
+        compare_with_oracle(engine, algo, args, pairs)
+
+
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+def test_many_pairs_plan_vs_oracle(engine, algo):
+    """>= 1024 pairs selects the 4-wave many-pairs plan."""
+    pairs = []
+    for k in range(1100):
+        m, n = 150 + (k % 37), 140 + (k % 53)
+        a = sa.synth_dna(20_000 + 2 * k, m)
+        b = sa.synth_mutate(a, k)[:n] if k % 2 else sa.synth_dna(20_001 + 2 * k, n)
+        pairs.append((a, b))
+    compare_with_oracle(engine, algo, SCORINGS[algo][0], pairs)
+
+
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+def test_multiband_wrap_vs_oracle(engine, algo):
+    """More bands than waves (m > 64*R*W): bands wrap round-robin over the waves."""
+    pairs = [(sa.synth_dna(31, 21000), sa.synth_dna(32, 97)), (sa.synth_dna(33, 9000), sa.synth_dna(34, 300)),
+             (sa.synth_dna(35, 130), sa.synth_dna(36, 9000))]
+    compare_with_oracle(engine, algo, SCORINGS[algo][1 % len(SCORINGS[algo])], pairs)
+
+
+@pytest.mark.parametrize("match", ["purine", "nwild", "caseless"])
+def test_custom_match_fn_vs_oracle(engine, match):
+    pairs = []
+    for k in range(12):
+        a = sa.synth_dna(40_000 + k, 300 + 17 * k)
+        b = bytearray(sa.synth_mutate(a, k))
+        for p in range(k % 5, len(b), 9):
+            b[p] = ord("N") if match == "nwild" else (ord(chr(b[p]).lower()) if match == "caseless" else b[p])
+        pairs.append((a, bytes(b)))
+    for algo in range(4):
+        compare_with_oracle(engine, algo, SCORINGS[algo][0], pairs, match)
+
+
+def test_local_gotoh_size_hack(engine):
+    """SALocalGotoh.h:484-488: these sizes are re-aligned with NW (parity unpinned: the
+    reference reads an uninitialised Gap there; we use the ScoringSystem's gap = 0)."""
+    pairs = [(sa.synth_dna(1, 60), sa.synth_dna(2, 57)), (sa.synth_dna(3, 314), sa.synth_dna(4, 288)),
+             (sa.synth_dna(5, 61), sa.synth_dna(6, 58)), (sa.synth_dna(7, 61), sa.synth_dna(8, 59))]
+    res = engine.align(2, sa.ScoringSystem(-3, -1, 1, -1, True), pairs)
+    assert [bool(r.flags & sa.SA_FLAG_SIZE_HACK) for r in res] == [True, True, True, False]
+    for (a, b), r in zip(pairs, res):
+        o = oracle_align(2, (-3, -1, 1, -1, True), a, b)
+        assert rows_of(2, a, b, r) == o["rows"]
+
+
+def rescore(algo, args, a, b, r):
+    """Score of the emitted local alignment under the scoring (independent of the DP)."""
+    s = sa.ScoringSystem(*args)
+    tot = 0
+    prev = None
+    for op in reversed(r.ops):
+        c = chr(op)
+        if c in "MS":
+            tot += s.match if c == "M" else s.mismatch
+        elif algo in (0, 1):
+            tot += s.gap
+        else:
+            tot += s.gap_extend + (s.gap_open if prev != c else 0)
+        prev = c if c in "UL" else None
+    return tot
+
+
+@pytest.mark.parametrize("pairs_n,length", [(1024, 4096)])
+def test_full_size_properties(engine, pairs_n, length):
+    """North-star shape (4096 x 4096 SW), 1024 pairs in one launch: every local alignment
+    re-scores to the reported maximum, ends where the scores says, and a sample is bit-exact
+    against the oracle."""
+    s1, o1, s2, o2 = sa.synth_dna_batch(9_000_000_000, pairs_n, length, length, threads=16)
+    args = (-1, 1, -1)
+    res, ops = engine.align_packed(0, sa.ScoringSystem(*args), s1, o1, s2, o2)
+    assert (res["flags"] == 0).all()
+    assert (res["score"] > 0).all()
+    for p in range(pairs_n):
+        off = int(o1[p] + o2[p]) + p
+        r = sa.PairResult(int(res["score"][p]), int(res["end_i"][p]), int(res["end_j"][p]),
+                          int(res["start_i"][p]), int(res["start_j"][p]), 0,
+                          ops[off:off + int(res["nops"][p])].tobytes())
+        assert rescore(0, args, None, None, r) == r.score
+        # the path consumes exactly (end - start) symbols of each sequence
+        di = sum(1 for c in r.ops if chr(c) in "MSUX")
+        dj = sum(1 for c in r.ops if chr(c) in "MSLX")
+        assert (r.end_i - r.start_i, r.end_j - r.start_j) == (di, dj)
+    for p in (0, 1, pairs_n // 2, pairs_n - 1):
+        a = s1[o1[p]:o1[p + 1]].tobytes()
+        b = s2[o2[p]:o2[p + 1]].tobytes()
+        o = oracle_align(0, args, a, b)
+        off = int(o1[p] + o2[p]) + p
+        assert (int(res["score"][p]), int(res["end_i"][p]), int(res["end_j"][p])) == \
+               (o["score"], o["end_i"], o["end_j"])
+        assert ops[off:off + int(res["nops"][p])].tobytes() == o["ops"]
+
+
+def test_affine_rescore_property(engine):
+    pairs = [(sa.synth_dna(500 + k, 2000), sa.synth_mutate(sa.synth_dna(500 + k, 2000), k)) for k in range(64)]
+    for algo, args in ((2, (-3, -1, 1, -1, True)), (3, (-3, -1, 1, -1, True))):
+        res = engine.align(algo, sa.ScoringSystem(*args), pairs)
+        for (a, b), r in zip(pairs, res):
+            if algo == 2 and b"u" not in r.ops and b"l" not in r.ops:
+                assert rescore(algo, args, a, b, r) == r.score
+
+
+def test_device_api_and_timings(engine):
+    """sa_align_batch_device on torch-owned HBM buffers, on torch's current stream."""
+    torch = pytest.importorskip("torch")
+    s1, o1, s2, o2 = sa.synth_dna_batch(123, 64, 512, 512)
+    dev = torch.device("cuda", 0)
+    t = lambda x: torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)
+    d1, do1, d2, do2 = t(s1), t(o1), t(s2), t(o2)
+    d_res = torch.zeros(64 * 32, dtype=torch.uint8, device=dev)
+    d_ops = torch.zeros(len(s1) + len(s2) + 64, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    engine.align_device(0, sa.ScoringSystem(-1, 1, -1), d1.data_ptr(), do1.data_ptr(), d2.data_ptr(),
+                        do2.data_ptr(), 64, 512, 512, d_res.data_ptr(), d_ops.data_ptr(), stream)
+    torch.cuda.synchronize()
+    res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=sa.RESULT_DTYPE)
+    ref, _ = engine.align_packed(0, sa.ScoringSystem(-1, 1, -1), s1, o1, s2, o2)
+    assert (res["score"] == ref["score"]).all() and (res["end_i"] == ref["end_i"]).all()
+    fill_ms, tb_ms, n = engine.last_timings()
+    assert n >= 1 and fill_ms > 0
