@@ -39,8 +39,8 @@ SW_FLAG_BYTES_PER_CELL = 0.25  # 2 traceback bits per cell written to HBM
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pairs", type=int, default=10000, help="pairs per GPU")
     ap.add_argument("--len", type=int, default=4096, help="length of both sequences")
     ap.add_argument("--cpu-pairs", type=int, default=128, help="CPU baseline sample (pairs)")

@@ -67,6 +67,25 @@ def library_path() -> str:
     return os.environ.get("SEQALIB_HIP_LIB", os.path.join(_HERE, "lib", "libseqalib_hip.so"))
 
 
+def _share_hip_runtime_with_torch():
+    """PyTorch-ROCm wheels bundle their own libamdhip64 (same soname as /opt/rocm's).  Two HIP
+    runtimes in one process cannot both own the device, so when torch is installed we bind the
+    engine to torch's copy (loaded RTLD_GLOBAL by path, without importing torch); a later
+    ``import torch`` then maps the very same file.  SEQALIB_HIP_RUNTIME=system disables this."""
+    if os.environ.get("SEQALIB_HIP_RUNTIME", "torch") != "torch":
+        return
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return
+    if spec is None or not spec.submodule_search_locations:
+        return
+    hip = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(hip):
+        C.CDLL(hip, mode=C.RTLD_GLOBAL)
+
+
 def load_library():
     """Load libseqalib_hip.so (built in-tree by ``make`` / ``__graft_entry__.build()``)."""
     global _lib
@@ -75,6 +94,7 @@ def load_library():
     path = library_path()
     if not os.path.exists(path):
         raise SeqalibError(f"HIP engine not built: {path} missing (run `make` or __graft_entry__.build())")
+    _share_hip_runtime_with_torch()
     L = C.CDLL(path)
     vp, u8p, u64p, i32p = C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.POINTER(C.c_int)
     L.sa_version.restype = C.c_int
