@@ -83,10 +83,12 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
-def shard_seed_base(rank: int, pairs_per_gpu: int) -> int:
-    """Pair p of the global batch uses seeds SEED_BASE+2p+1 / +2p+2; rank r owns
-    p in [r*P, (r+1)*P), i.e. a contiguous static split with no exchange."""
-    return SEED_BASE + 2 * rank * pairs_per_gpu
+def shard_seed_base(rank: int, world: int, pairs_per_gpu: int) -> int:
+    """Pair p of the global batch (world x P pairs) uses seeds SEED_BASE+2p+1 / +2p+2; rank r owns
+    the contiguous slice seqalib_amd.multi.shard_range(r, world, world*P) — no exchange."""
+    from seqalib_amd.multi import shard_range
+    start, _ = shard_range(rank, world, world * pairs_per_gpu)
+    return SEED_BASE + 2 * start
 
 
 def cpu_baseline(args, s1, o1, s2, o2):
@@ -149,7 +151,7 @@ def main():
     P, Lq = args.pairs, args.len
     workload = f"sw_batch_{P}x{Lq}x{Lq}"
 
-    s1, o1, s2, o2 = sa.synth_dna_batch(shard_seed_base(rank, P), P, Lq, Lq, threads=16)
+    s1, o1, s2, o2 = sa.synth_dna_batch(shard_seed_base(rank, world, P), P, Lq, Lq, threads=16)
     as_t = lambda x: torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)
     d1, do1, d2, do2 = as_t(s1), as_t(o1), as_t(s2), as_t(o2)
     d_res = torch.zeros(P * 32, dtype=torch.uint8, device=dev)

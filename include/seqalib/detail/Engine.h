@@ -1,0 +1,135 @@
+// seqalib/detail/Engine.h — glue between the reference-shaped C++ templates and the C ABI
+// (include/seqalib_hip.h): per-thread device context, symbol coding for arbitrary Ty, the match
+// table built from the user's MatchFnTy, and op-stream -> AlignedSequence assembly.
+#pragma once
+
+#include <climits>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "../../seqalib_hip.h"
+
+namespace seqalib {
+namespace detail {
+
+// One HIP context per host thread (the reference's aligners are not reentrant either; separate
+// instances on separate threads are independent).  Device: $SEQALIB_DEVICE or 0.
+struct ThreadContext {
+    sa_ctx* h = nullptr;
+    ~ThreadContext() {
+        if (h) sa_destroy(h);
+    }
+};
+
+inline sa_ctx* context() {
+    thread_local ThreadContext c;
+    if (!c.h) {
+        const char* env = std::getenv("SEQALIB_DEVICE");
+        const int dev = env ? std::atoi(env) : 0;
+        const int rc = sa_create(dev, &c.h);
+        if (rc != SA_OK) {
+            c.h = nullptr;
+            throw std::runtime_error(std::string("seqalib: cannot open HIP device: ") + sa_last_error(nullptr));
+        }
+    }
+    return c.h;
+}
+
+inline void check(int rc, const char* what) {
+    if (rc != SA_OK)
+        throw std::runtime_error(std::string("seqalib: ") + what + ": " + sa_status_string(rc) + " (" +
+                                 sa_last_error(context()) + ")");
+}
+
+// Maps symbols of type Ty onto byte codes.  Single-byte integral types are their own code; other
+// types get codes in order of first appearance (at most 256 distinct symbols per batch).
+template <typename Ty, bool Direct = (std::is_integral<Ty>::value && sizeof(Ty) == 1)>
+struct SymbolCoder {
+    std::vector<Ty> values;
+    uint8_t code(const Ty& v) {
+        for (size_t k = 0; k < values.size(); ++k)
+            if (values[k] == v) return (uint8_t)k;
+        if (values.size() == 256)
+            throw std::runtime_error("seqalib: more than 256 distinct symbols in one batch");
+        values.push_back(v);
+        return (uint8_t)(values.size() - 1);
+    }
+    size_t size() const { return values.size(); }
+    const Ty& value(size_t k) const { return values[k]; }
+    bool identity_on_equal() const { return true; }   // distinct values -> distinct codes
+};
+
+template <typename Ty>
+struct SymbolCoder<Ty, true> {
+    bool seen[256] = {};
+    uint8_t code(const Ty& v) {
+        const uint8_t c = (uint8_t)v;
+        seen[c] = true;
+        return c;
+    }
+    size_t size() const { return 256; }
+    Ty value(size_t k) const { return (Ty)(uint8_t)k; }
+    bool used(size_t k) const { return seen[k]; }
+};
+
+template <typename Ty, typename MatchFnTy, bool Direct>
+std::vector<uint8_t> build_lut(SymbolCoder<Ty, Direct>& coder, MatchFnTy& fn) {
+    std::vector<uint8_t> lut(65536, 0);
+    const size_t k = Direct ? 256 : coder.size();
+    for (size_t a = 0; a < k; ++a) {
+        if constexpr (Direct) {
+            if (!coder.used(a)) continue;
+        }
+        for (size_t b = 0; b < k; ++b) {
+            if constexpr (Direct) {
+                if (!coder.used(b)) continue;
+            }
+            lut[a * 256 + b] = fn(coder.value(a), coder.value(b)) ? 1 : 0;
+        }
+    }
+    return lut;
+}
+
+// Aligns a batch of (Seq1, Seq2) pairs on the GPU.  Returns the per-pair results and the op
+// streams (traceback order).  has_fn = false means the reference's nullptr match fn (equality).
+template <typename Ty, typename ContainerType, typename MatchFnTy>
+void align(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
+           const std::vector<std::pair<ContainerType*, ContainerType*>>& pairs,
+           std::vector<sa_result>& res, std::vector<uint8_t>& ops, std::vector<uint64_t>& ops_off) {
+    SymbolCoder<Ty> coder;
+    std::vector<uint8_t> s1, s2;
+    std::vector<uint64_t> o1(1, 0), o2(1, 0);
+    for (auto& p : pairs) {
+        ContainerType& a = *p.first;
+        ContainerType& b = *p.second;
+        for (size_t k = 0; k < (size_t)a.size(); ++k) s1.push_back(coder.code(a[k]));
+        for (size_t k = 0; k < (size_t)b.size(); ++k) s2.push_back(coder.code(b[k]));
+        o1.push_back(s1.size());
+        o2.push_back(s2.size());
+    }
+    std::vector<uint8_t> lut;
+    if (has_fn) lut = build_lut(coder, fn);
+    const uint32_t n = (uint32_t)pairs.size();
+    res.assign(n, sa_result{});
+    const uint64_t cap = s1.size() + s2.size() + n + 1;
+    ops.assign(cap, 0);
+    ops_off.resize(n);
+    for (uint32_t p = 0; p < n; ++p) ops_off[p] = o1[p] + o2[p] + p;
+    s1.push_back(0);   // never hand a NULL pointer for an empty batch
+    s2.push_back(0);
+    check(sa_align_batch(context(), algo, &sc, s1.data(), o1.data(), s2.data(), o2.data(), n,
+                         has_fn ? lut.data() : nullptr, res.data(), ops.data(), cap),
+          "sa_align_batch");
+    for (auto& r : res)
+        if (r.flags & SA_FLAG_DIVERGED)
+            throw std::runtime_error("seqalib: the reference traceback does not terminate for this scoring");
+}
+
+}  // namespace detail
+}  // namespace seqalib

@@ -224,3 +224,15 @@ def test_device_api_and_timings(engine):
     assert (res["score"] == ref["score"]).all() and (res["end_i"] == ref["end_i"]).all()
     fill_ms, tb_ms, n = engine.last_timings()
     assert n >= 1 and fill_ms > 0
+
+
+def test_multi_gpu_threads_match_single(engine):
+    """align_multi_gpu (one host thread + context per device; here two contexts on GPU 0) returns
+    exactly what one sa_align_batch returns."""
+    from seqalib_amd.multi import align_multi_gpu
+    pairs = [(sa.synth_dna(700 + k, 200 + 31 * k), sa.synth_dna(900 + k, 150 + 17 * k)) for k in range(40)]
+    s1, o1, s2, o2 = sa.pack_pairs(pairs)
+    ref, ref_ops = engine.align_packed(0, sa.ScoringSystem(-1, 1, -1), s1, o1, s2, o2)
+    res, ops = align_multi_gpu(0, sa.ScoringSystem(-1, 1, -1), s1, o1, s2, o2, devices=[0, 0])
+    assert (res == ref).all()
+    assert ops[: len(ref_ops) - 1].tobytes() == ref_ops[: len(ref_ops) - 1].tobytes()
