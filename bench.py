@@ -30,9 +30,12 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 METRIC = "GCUPS (DP cell updates/s) on batched 4k×4k SW; bit-exact score match"
 SEED_BASE = 10 ** 10          # workload "T" seed base (config id x 1e9 convention)
 SCORING = (-1, 1, -1)         # SmithWatermanSA::getDefaultScoring (SASmithWaterman.h:352)
-VALU_PEAK_TOPS = 78.64        # 256 CU x 4 SIMD32 x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md)
+# gfx950 int32 VALU issue ceiling: one wave64 instruction per 4 cycles per SIMD for max/min/
+# compare/carry/shift-left/3-input ops (profiles/microbench_valu_issue_r01.txt) =
+# 256 CU x 4 SIMD x 16 lanes/cycle x 2.4 GHz.  (FP32 add/fma and bitwise ops issue ~1.8x faster.)
+VALU_PEAK_TOPS = 39.32
 HBM_PEAK_GBPS = 8000.0
-SW_VALU_OPS_PER_CELL = 13     # ISA-counted VALU instructions per cell of the keyed SW body
+SW_VALU_OPS_PER_CELL = 13     # VALU instructions per cell of the keyed SW body (PMC SQ_INSTS_VALU*64/cells)
 SW_FLAG_BYTES_PER_CELL = 0.25  # 2 traceback bits per cell written to HBM
 
 

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <limits.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -73,6 +74,14 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs) {
         uint64_t w = (max_m + rows - 1) / rows;
         p.W = (int)std::max<uint64_t>(1, std::min<uint64_t>(16, w));
         while (p.R > 4 && (uint64_t)kWave * (p.R / 2) * p.W >= max_m) p.R /= 2;
+    }
+    // tuning override: SEQALIB_PLAN="R,W"
+    if (const char* ov = getenv("SEQALIB_PLAN")) {
+        int r = 0, w = 0;
+        if (sscanf(ov, "%d,%d", &r, &w) == 2 && (r == 4 || r == 8 || r == 16) && w >= 1 && w <= 16) {
+            p.R = r;
+            p.W = w;
+        }
     }
     // never more waves than bands
     const uint64_t bands = (max_m + (uint64_t)kWave * p.R - 1) / ((uint64_t)kWave * p.R);
@@ -184,6 +193,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         fp.gap = sc->gap; fp.match = sc->match; fp.mismatch = allow ? sc->mismatch : INT_MIN;
         fp.gap_open = sc->gap_open; fp.gap_extend = sc->gap_extend;
         fp.waves = pl.W;
+        fp.stage_seq2 = max_n <= kMaxStagedSeq2 ? 1 : 0;
 
         TbParams tp;
         tp.seq1 = d1; tp.off1 = o1; tp.seq2 = d2; tp.off2 = o2;

@@ -74,7 +74,9 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
     static_assert(kChunk % SPP == 0, "chunk must hold whole packets");
     static_assert(BPS >= 1, "record must be at least a byte");
 
-    __shared__ uint32_t s_lut[LUT ? 2048 : 1];
+    // Dynamic LDS (sizes from lds_layout(), host and device agree):
+    //   [match bits: 2048 words, LUT only][hand-off rings: W x kRing x (1|2) ints][Seq2 bytes, staged]
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     __shared__ int s_red[16 * 3];
     __shared__ int s_score;   // H[m][n] for the global modes, stored by the owning lane
 
@@ -96,13 +98,19 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
         }
         return;
     }
-    if constexpr (LUT) {
-        for (int k = threadIdx.x; k < 2048; k += blockDim.x) s_lut[k] = P.lutbits[k];
-        __syncthreads();
-    }
-
+    const LdsLayout lay = lds_layout(LUT, AFF, W, P.stage_seq2 ? P.max_n : 0);
+    uint32_t* const s_lut = smem;
+    int32_t* const s_ring = reinterpret_cast<int32_t*>(smem + lay.ring_off / 4);
+    uint8_t* const s_seq2 = reinterpret_cast<uint8_t*>(smem) + lay.seq_off;
     const uint8_t* s1 = P.seq1 + o1;
     const uint8_t* s2 = P.seq2 + o2;
+    if constexpr (LUT) {
+        for (int k = threadIdx.x; k < 2048; k += blockDim.x) s_lut[k] = P.lutbits[k];
+    }
+    if (P.stage_seq2) {
+        for (int k = threadIdx.x; k < n; k += blockDim.x) s_seq2[k] = s2[k];
+    }
+    __syncthreads();
     const int G = P.gap, MA = P.match, MI = P.mismatch;
     const int GO = P.gap_open, GE = P.gap_extend;
     const int GOE = GO + GE;
@@ -231,6 +239,35 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
         }
     };
 
+    // Band -> band hand-off.  The last row of band b (H and, affine, Ix) goes to band b+1 through
+    // an LDS ring of kRing columns owned by wave (b+1) % W — unless b+1 wraps round to wave 0
+    // (more bands than waves), which uses the per-pair global row buffer.  Everything a steady
+    // chunk reads is in LDS, so the only memory traffic of the chunk loop is the fire-and-forget
+    // flag stores (no s_waitcnt vmcnt behind them).
+    auto ring = [&](int wave, int comp) -> int32_t* {
+        return s_ring + (wave * (AFF ? 2 : 1) + comp) * kRing;
+    };
+    // Lane q < kChunk of the returned registers holds column c0 + q: the row-above value for
+    // lane 0 (top border, or the previous band's last row) and Seq2[c].
+    auto load_chunk = [&](int band, int c0, int& vh, int& vx, int& vs) {
+        const int c = c0 + lane;
+        vh = 0; vx = -10000; vs = 0;
+        if (lane < kChunk && c < n) {
+            vs = P.stage_seq2 ? (int)s_seq2[c] : (int)s2[c];
+            if (band == 0) {
+                const int J = c + 1;
+                if constexpr (ALG == SA_NW) vh = J * G;
+                else if constexpr (ALG == SA_GLOBAL_GOTOH) vh = GO + J * GE;
+            } else if (band % W != 0) {
+                vh = ring(band % W, 0)[c % kRing];
+                if constexpr (AFF) vx = ring(band % W, 1)[c % kRing];
+            } else {
+                vh = rb_h[c];
+                if constexpr (AFF) vx = rb_x[c];
+            }
+        }
+    };
+
     for (uint32_t ph = 0; ph < total; ++ph) {
         const int rel = (int)ph - w * kLagPhases;
         if (rel >= 0) {
@@ -259,20 +296,8 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
                 }
                 // ---------------------------------------------------------------- one chunk
                 const int kC = (int)chunk * kChunk;
-                const int c = kC + lane;
-                int bch = 0, bcx = -10000, symc = 0;
-                if (lane < kChunk && c < n) {
-                    symc = s2[c];
-                    if (band == 0) {
-                        const int J = c + 1;
-                        if constexpr (ALG == SA_NW) bch = J * G;
-                        else if constexpr (ALG == SA_GLOBAL_GOTOH) bch = GO + J * GE;
-                        else bch = 0;
-                    } else {
-                        bch = rb_h[c];
-                        if constexpr (AFF) bcx = rb_x[c];
-                    }
-                }
+                int bch, bcx, symc;
+                load_chunk(band, kC, bch, bcx, symc);
                 int acc_h = 0, acc_x = 0;
                 const bool steady = kC >= kWave - 1 && kC + kChunk <= n;
                 if (steady) run_chunk(std::true_type{}, band, kC, bch, bcx, symc, acc_h, acc_x);
@@ -281,8 +306,14 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
                 if (band + 1 < B) {
                     const int cc = kC + lane - (kWave - 1);
                     if (lane < kChunk && cc >= 0 && cc < n) {
-                        rb_h[cc] = acc_h;
-                        if constexpr (AFF) rb_x[cc] = acc_x;
+                        const int nw = (band + 1) % W;
+                        if (nw != 0) {
+                            ring(nw, 0)[cc % kRing] = acc_h;
+                            if constexpr (AFF) ring(nw, 1)[cc % kRing] = acc_x;
+                        } else {
+                            rb_h[cc] = acc_h;
+                            if constexpr (AFF) rb_x[cc] = acc_x;
+                        }
                     }
                 }
                 // ---------------------------------------------------------------- band end
@@ -366,10 +397,11 @@ hipError_t launch_fill_alg(int R, bool lut, bool allow, bool keyed, const FillPa
                            uint32_t grid, hipStream_t stream) {
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
     const dim3 block(kWave * p.waves);
+    const size_t lds = lds_layout(lut, is_affine(ALG), p.waves, p.stage_seq2 ? p.max_n : 0).total;
     if (!LOCAL) keyed = false;
 #define SA_LAUNCH(RR, LL, AA, KK)                                                              \
     if (R == RR && lut == LL && allow == AA && keyed == KK) {                                  \
-        hipLaunchKernelGGL((fill_kernel<ALG, RR, LL, AA, KK>), dim3(grid), block, 0, stream, p); \
+        hipLaunchKernelGGL((fill_kernel<ALG, RR, LL, AA, KK>), dim3(grid), block, lds, stream, p); \
         return hipGetLastError();                                                              \
     }
 #define SA_LAUNCH_K(RR, LL, AA) \

@@ -24,6 +24,7 @@ struct FillParams {
     uint32_t max_m, max_n;
     int32_t gap, match, mismatch, gap_open, gap_extend;
     int waves;                 // waves per workgroup (blockDim.x / 64)
+    int stage_seq2;            // 1: Seq2 of the pair is copied to LDS (max_n <= kMaxStagedSeq2)
 };
 
 struct TbParams {

@@ -34,10 +34,30 @@ namespace sa {
 
 constexpr int kWave = 64;   // CDNA wavefront
 constexpr int kChunk = 32;  // steps between workgroup barriers
-// Phases a band lags its producer band: its chunk k reads columns [kC, kC+C) of the row
-// buffer, which the producer wrote at the END of its chunk floor((c+63)/C) (lane 63 reaches
-// column c at step c+63) -> floor((C+62)/C) chunks later, +1 for the barrier.
+// Phases a band lags its producer band: its chunk k reads columns [kC, kC+C) of the hand-off,
+// which the producer wrote at the END of its chunk floor((c+63)/C) (lane 63 reaches column c at
+// step c+63) -> floor((C+62)/C) chunks later, +1 for the barrier.
 constexpr int kLagPhases = (kChunk + 62) / kChunk + 1;
+// LDS hand-off ring (columns).  Within one phase the producer writes columns [kC-63, kC-31) while
+// its consumer reads [kC-96, kC-64): disjoint and 64 apart; a slot is rewritten (column c+kRing)
+// at producer chunk floor((c+kRing+63)/C) >= floor(c/C) + 5 > the consumer's read phase
+// floor(c/C) + kLagPhases, so 128 columns never alias a pending read.
+constexpr int kRing = 128;
+static_assert(kLagPhases == 3 && kRing >= 4 * kChunk, "re-derive the ring bound");
+
+// Dynamic LDS of the fill kernel: [match bits (LUT)][hand-off rings][staged Seq2].
+struct LdsLayout {
+    uint32_t ring_off, seq_off, total;
+};
+SA_HD LdsLayout lds_layout(bool lut, bool affine, int W, uint32_t staged_n) {
+    LdsLayout L;
+    L.ring_off = lut ? 2048 * 4 : 0;
+    L.seq_off = L.ring_off + (uint32_t)W * (affine ? 2 : 1) * kRing * 4;
+    L.total = L.seq_off + ((staged_n + 15) / 16) * 16;
+    return L;
+}
+// Seq2 is staged in LDS when it fits this budget (else read from global per chunk).
+constexpr uint32_t kMaxStagedSeq2 = 48 * 1024;
 
 SA_HD constexpr bool is_affine(int algo) { return algo >= 2; }
 SA_HD constexpr int bits_per_cell(int algo) { return is_affine(algo) ? 4 : 2; }
