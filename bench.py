@@ -30,12 +30,11 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 METRIC = "GCUPS (DP cell updates/s) on batched 4k×4k SW; bit-exact score match"
 SEED_BASE = 10 ** 10          # workload "T" seed base (config id x 1e9 convention)
 SCORING = (-1, 1, -1)         # SmithWatermanSA::getDefaultScoring (SASmithWaterman.h:352)
-# gfx950 int32 VALU issue ceiling: one wave64 instruction per 4 cycles per SIMD for max/min/
-# compare/carry/shift-left/3-input ops (profiles/microbench_valu_issue_r01.txt) =
-# 256 CU x 4 SIMD x 16 lanes/cycle x 2.4 GHz.  (FP32 add/fma and bitwise ops issue ~1.8x faster.)
-VALU_PEAK_TOPS = 39.32
+# The fill kernel is VALU-issue bound.  Its roofline peak is the issue ceiling of the steady
+# loop's own instruction mix, every opcode priced at its measured gfx950 issue rate
+# (tools/issue_model.py -> ISSUE_MODEL, rates from profiles/microbench_valu_issue_r01.txt).
+ISSUE_MODEL = os.path.join(ROOT, "profiles", "issue_model_r02.json")
 HBM_PEAK_GBPS = 8000.0
-SW_VALU_OPS_PER_CELL = 13     # VALU instructions per cell of the keyed SW body (PMC SQ_INSTS_VALU*64/cells)
 SW_FLAG_BYTES_PER_CELL = 0.25  # 2 traceback bits per cell written to HBM
 
 
@@ -141,6 +140,13 @@ def load_pmc_traffic(workload: str):
         return None
 
 
+def issue_model(label: str):
+    try:
+        return json.load(open(ISSUE_MODEL))["kernels"][label]
+    except Exception:
+        return None
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
@@ -183,6 +189,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = max_over_ranks(t1 - t0, world)
     fill_ms, tb_ms, launches = eng.last_timings()   # HIP events of the last step, same stream
+    kernel, plan_R, plan_W = eng.last_plan()
     fill_ms = max_over_ranks(fill_ms, world)
 
     cells_rank = float(P) * Lq * Lq
@@ -209,23 +216,37 @@ def main():
         return
     per_launch_cells = cells_rank  # one fill launch covers the whole batch when it fits HBM
     fill_s = fill_ms / 1e3 / max(launches, 1)
-    tops = per_launch_cells * SW_VALU_OPS_PER_CELL / fill_s / 1e12
+    t16 = kernel == sa.SA_KERNEL_T16
+    label = f"sw_{'t16' if t16 else 'int32'}_r{plan_R}"
+    model = issue_model(label)
+    fill_gcups = per_launch_cells / fill_s / 1e9
     hbm_gbps = per_launch_cells * SW_FLAG_BYTES_PER_CELL / fill_s / 1e9
     traffic = load_pmc_traffic(workload)
+    kname = (f"fill_kernel<SW,R={plan_R},W={plan_W}," + ("T16 tagged int16 profile" if t16 else "int32 flags")
+             + ",KEYED>")
+    if model:
+        vpc = model["valu_per_cell"]
+        roof = {"bound": "valu", "achieved": round(fill_gcups * vpc / 1e3, 2),
+                "peak": round(model["peak_gcups"] * vpc / 1e3, 2), "unit": "Tops/s",
+                "frac": round(fill_gcups / model["peak_gcups"], 4)}
+    else:
+        vpc = None
+        roof = {"bound": "valu", "achieved": None, "peak": None, "unit": "Tops/s", "frac": None}
+    roof.update({"traffic": traffic, "kernel": kname, "avg_launch_ms": round(fill_ms / max(launches, 1), 3),
+                 "fill_gcups": round(fill_gcups, 1),
+                 "issue_ceiling_gcups": model["peak_gcups"] if model else None, "valu_per_cell": vpc,
+                 "peak_basis": "steady-loop VALU mix x measured per-opcode issue rates (tools/issue_model.py, "
+                               "profiles/issue_model_r02.json)",
+                 "bytes_per_cell": SW_FLAG_BYTES_PER_CELL, "hbm_achieved_GBps": round(hbm_gbps, 1),
+                 "hbm_peak_GBps": HBM_PEAK_GBPS, "hbm_frac": round(hbm_gbps / HBM_PEAK_GBPS, 4)})
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GCUPS", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+        "scaling": "weak", "vs_baseline": None, "dtype": "int16" if t16 else "int32",
         "data": "synthetic DNA, std::mt19937_64 'ACGT'[g()&3], seeds base+2p+1/base+2p+2, resident in HBM",
         "config": {"workload": workload, "pairs_per_gpu": P, "m": Lq, "n": Lq, "algo": "SmithWatermanSA",
                    "scoring": list(SCORING), "match": "equal<char>", "parallelism": f"pair-shard x{world}"},
-        "roofline": {"bound": "valu", "achieved": round(tops, 2), "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
-                     "frac": round(tops / VALU_PEAK_TOPS, 4), "traffic": traffic,
-                     "kernel": "fill_kernel<SW,R=16,EQ,ALLOW,KEYED>",
-                     "avg_launch_ms": round(fill_ms / max(launches, 1), 3),
-                     "ops_per_cell": SW_VALU_OPS_PER_CELL, "bytes_per_cell": SW_FLAG_BYTES_PER_CELL,
-                     "hbm_achieved_GBps": round(hbm_gbps, 1), "hbm_peak_GBps": HBM_PEAK_GBPS,
-                     "hbm_frac": round(hbm_gbps / HBM_PEAK_GBPS, 4)},
+        "roofline": roof,
         "fill_ms": round(fill_ms, 2), "traceback_ms": round(tb_ms, 2),
         "parity": f"{checked - bad}/{checked} sampled pairs bit-exact vs oracle, {int(np.count_nonzero(res['flags']))} flagged",
     }

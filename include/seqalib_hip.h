@@ -134,6 +134,14 @@ int sa_align_batch_device(sa_ctx* ctx, int algo, const sa_scoring* scoring,
  * number of fill launches.  Waits for those events. */
 int sa_last_timings(sa_ctx* ctx, float* fill_ms, float* traceback_ms, int* fill_launches);
 
+/* Fill kernel of the last sa_align_batch[_device] call: SA_KERNEL_INT32 (int32 scores, equality
+ * flags; any alphabet, LUT, scoring) or SA_KERNEL_T16 (tagged 16-bit profile kernel: SW/NW with
+ * allow-mismatch, <= 4 distinct symbols in the batch, scores proven to fit).  Also R and W.
+ * Environment: SEQALIB_T16=0 forces the int32 kernel. */
+#define SA_KERNEL_INT32 0
+#define SA_KERNEL_T16 1
+int sa_last_plan(sa_ctx* ctx, int* kernel, int* rows_per_lane, int* waves);
+
 /* Kernel plan the engine would use for a batch (host-only query, no device needed):
  * rows per lane R, waves per workgroup W, direction bytes per pair, row-buffer bytes per pair. */
 int sa_plan_query(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs,

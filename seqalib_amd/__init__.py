@@ -36,6 +36,7 @@ __all__ = [
 SA_SW, SA_NW, SA_LOCAL_GOTOH, SA_GLOBAL_GOTOH = 0, 1, 2, 3
 ALGO_NAMES = {SA_SW: "sw", SA_NW: "nw", SA_LOCAL_GOTOH: "local_gotoh", SA_GLOBAL_GOTOH: "global_gotoh"}
 SA_FLAG_DIVERGED, SA_FLAG_BAD_SHAPE, SA_FLAG_SIZE_HACK = 1, 2, 4
+SA_KERNEL_INT32, SA_KERNEL_T16 = 0, 1
 INT32_MIN = -(2 ** 31)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -114,11 +115,12 @@ def load_library():
                                         C.c_uint32, C.c_uint32, vp, vp, vp, vp]
     L.sa_last_timings.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_float), i32p]
     L.sa_plan_query.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, i32p, i32p, u64p, u64p]
+    L.sa_last_plan.argtypes = [vp, i32p, i32p, i32p]
     L.sa_synth_dna.argtypes = [C.c_uint64, C.c_uint32, vp]
     L.sa_synth_mutate.argtypes = [vp, C.c_uint32, C.c_uint64, vp, C.c_uint32, C.POINTER(C.c_uint32)]
     L.sa_synth_dna_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_int]
     for fn in ("sa_set_workspace_limit", "sa_trim", "sa_align_batch", "sa_align_batch_device",
-               "sa_last_timings", "sa_plan_query", "sa_synth_dna", "sa_synth_mutate", "sa_synth_dna_batch",
+               "sa_last_timings", "sa_last_plan", "sa_plan_query", "sa_synth_dna", "sa_synth_mutate", "sa_synth_dna_batch",
                "sa_create", "sa_device_count"):
         getattr(L, fn).restype = C.c_int
     if L.sa_version() != 1:
@@ -378,6 +380,13 @@ class Engine:
         f, t, n = C.c_float(), C.c_float(), C.c_int()
         self._check(self.L.sa_last_timings(self.h, C.byref(f), C.byref(t), C.byref(n)), "sa_last_timings")
         return f.value, t.value, n.value
+
+
+    def last_plan(self) -> Tuple[int, int, int]:
+        """(kernel, R, W) of the last call: kernel is SA_KERNEL_INT32 or SA_KERNEL_T16."""
+        k, R, W = C.c_int(), C.c_int(), C.c_int()
+        self._check(self.L.sa_last_plan(self.h, C.byref(k), C.byref(R), C.byref(W)), "sa_last_plan")
+        return k.value, R.value, W.value
 
 
 def plan_query(algo: int, max_m: int, max_n: int, npairs: int):

@@ -1,0 +1,89 @@
+// sa_alphabet.hip — batch alphabet scan and the substitution profile of the T16 fill kernel.
+//
+// The T16 kernel (sa_fill_impl.h) codes symbols 0..3 and reads the substitution term of a cell
+// from a per-row byte profile, so it applies when the whole batch uses at most four distinct
+// byte values (DNA).  The host learns that from a 256-bit presence bitmap of every byte of both
+// sequence sets (one streaming pass, ~HBM speed) before it plans the launch.
+#include "sa_internal.h"
+
+namespace sa {
+
+typedef unsigned int u32x4a __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void mark(uint32_t (&bm)[8], uint32_t b) {
+    const uint32_t bit = 1u << (b & 31u), w = b >> 5;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) bm[k] |= (w == (uint32_t)k) ? bit : 0u;
+}
+__device__ __forceinline__ void mark4(uint32_t (&bm)[8], uint32_t v) {
+    mark(bm, v & 255u); mark(bm, (v >> 8) & 255u); mark(bm, (v >> 16) & 255u); mark(bm, v >> 24);
+}
+
+__global__ __launch_bounds__(256) void alphabet_scan(const uint8_t* d1, const uint64_t* o1,
+                                                     const uint8_t* d2, const uint64_t* o2,
+                                                     uint32_t npairs, uint32_t* bitmap) {
+    __shared__ uint32_t sb[8];
+    if (threadIdx.x < 8) sb[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t bm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+    for (int set = 0; set < 2; ++set) {
+        const uint8_t* d = set ? d2 : d1;
+        const uint64_t* o = set ? o2 : o1;
+        const uint64_t b0 = o[0], b1 = o[npairs];
+        if (b1 <= b0) continue;
+        const uint8_t* p0 = d + b0;
+        const uint8_t* p1 = d + b1;
+        // 16-byte aligned body, bytes before and after it
+        const uint8_t* a0 = reinterpret_cast<const uint8_t*>((reinterpret_cast<uintptr_t>(p0) + 15) & ~(uintptr_t)15);
+        const uint8_t* a1 = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p1) & ~(uintptr_t)15);
+        if (a0 >= a1) { a0 = p1; a1 = p1; }
+        const uint64_t head = (uint64_t)(a0 - p0), tail = (uint64_t)(p1 - a1);
+        for (uint64_t k = tid; k < head; k += nth) mark(bm, p0[k]);
+        for (uint64_t k = tid; k < tail; k += nth) mark(bm, a1[k]);
+        const u32x4a* v = reinterpret_cast<const u32x4a*>(a0);
+        const uint64_t nv = (uint64_t)(a1 - a0) / 16;
+        for (uint64_t k = tid; k < nv; k += nth) {
+            const u32x4a x = __builtin_nontemporal_load(v + k);
+            mark4(bm, x.x); mark4(bm, x.y); mark4(bm, x.z); mark4(bm, x.w);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (bm[k]) atomicOr(&sb[k], bm[k]);
+    __syncthreads();
+    if (threadIdx.x < 8 && sb[threadIdx.x]) atomicOr(&bitmap[threadIdx.x], sb[threadIdx.x]);
+}
+
+// prof[c] byte c' = (int8)(4 * s(sym c, sym c') + 3), s = match ? match : mismatch.
+__global__ void build_profile(const uint32_t* lutbits, uint32_t sym_pack, int match, int mismatch,
+                              uint32_t* prof) {
+    const int c = threadIdx.x;
+    if (c >= 4) return;
+    const uint32_t a = (sym_pack >> (8 * c)) & 255u;
+    uint32_t w = 0;
+    for (int c2 = 0; c2 < 4; ++c2) {
+        const uint32_t b = (sym_pack >> (8 * c2)) & 255u;
+        const bool v = lutbits ? ((lutbits[(a << 3) | (b >> 5)] >> (b & 31u)) & 1u) : (a == b);
+        const int t = 4 * (v ? match : mismatch) + 3;
+        w |= ((uint32_t)t & 255u) << (8 * c2);
+    }
+    prof[c] = w;
+}
+
+hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uint8_t* d2,
+                                const uint64_t* o2, uint32_t npairs, uint32_t* bitmap, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(bitmap, 0, 32, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(alphabet_scan, dim3(2048), dim3(256), 0, s, d1, o1, d2, o2, npairs, bitmap);
+    return hipGetLastError();
+}
+
+hipError_t launch_build_profile(const uint32_t* lutbits, uint32_t sym_pack, int match, int mismatch,
+                                uint32_t* prof, hipStream_t s) {
+    hipLaunchKernelGGL(build_profile, dim3(1), dim3(64), 0, s, lutbits, sym_pack, match, mismatch, prof);
+    return hipGetLastError();
+}
+
+}  // namespace sa

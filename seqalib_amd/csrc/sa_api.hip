@@ -29,6 +29,9 @@ struct sa_ctx {
     std::vector<hipEvent_t> events;  // 3 per fill launch: start, fill end, traceback end
     int launches = 0;
     hipStream_t timed_stream = nullptr;
+    // alphabet bitmap (8 words) + T16 profile (4 words)
+    uint32_t* aux = nullptr;
+    int last_kernel = SA_KERNEL_INT32, last_R = 0, last_W = 0;
 };
 
 namespace {
@@ -58,7 +61,7 @@ struct Plan {
     uint64_t rowbuf_elems;  // int32 per slot
 };
 
-Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs) {
+Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t16 = false) {
     Plan p;
     const bool aff = is_affine(algo);
     const int rmax = aff ? 16 : 16;
@@ -86,7 +89,7 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs) {
     // never more waves than bands
     const uint64_t bands = (max_m + (uint64_t)kWave * p.R - 1) / ((uint64_t)kWave * p.R);
     if ((uint64_t)p.W > bands) p.W = (int)std::max<uint64_t>(1, bands);
-    p.g = make_geom(algo, p.R, max_m, max_n);
+    p.g = make_geom(algo, p.R, max_m, max_n, t16);
     p.rowbuf_elems = (uint64_t)(aff ? 2 : 1) * std::max<uint32_t>(max_n, 1);
     return p;
 }
@@ -145,6 +148,30 @@ bool keyed_ok(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
     return bound < 65536;
 }
 
+// T16 kernel (sa_fill_impl.h) preconditions on the scoring and shapes: it keeps 4*H + tag in
+// int16, so every value a cell can take, and every candidate, must stay inside int16 after the
+// scaling; the profile bytes hold 4*s + 3 as int8.  Bounds (allow-mismatch, gap <= 0,
+// mismatch <= match):
+//   SW: 0 <= H <= max(match, 0) * min(m, n)
+//   NW: H[i][j] <= max(match, 0) * min(i, j); H[i][j] >= min(i,j)*mismatch + |i-j|*gap (the
+//       all-diagonal-then-straight path), minimised over the grid at its corner points.
+bool t16_ok(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
+    if (algo != SA_SW && algo != SA_NW) return false;
+    if (!sc->allow_mismatch) return false;
+    const int64_t MA = sc->match, MI = sc->mismatch, G = sc->gap;
+    if (MA < -32 || MA > 31 || MI < -32 || MI > 31) return false;
+    if (G > 0 || MI > MA || G < -4096) return false;
+    const int64_t m = max_m, n = max_n, k = std::min(m, n);
+    const int64_t hi = std::max<int64_t>(MA, 0) * k;
+    int64_t lo = 0;
+    if (algo == SA_NW) {
+        auto A = [&](int64_t i, int64_t j) { return std::min(i, j) * MI + (i > j ? i - j : j - i) * G; };
+        lo = std::min({A(0, n), A(m, 0), A(k, n), A(m, k), A(k, k), A(m, n), (int64_t)0});
+    }
+    const int64_t cand_lo = 4 * (lo + std::min<int64_t>(std::min(MI, G), 0));
+    return 4 * hi + 3 <= 32767 && cand_lo >= -32768 && max_n < 65535;
+}
+
 int validate_scoring(sa_ctx* c, int algo, const sa_scoring* s) {
     if (!s) return fail(c, SA_ERR_ARG, "scoring is NULL");
     if (algo < SA_SW || algo > SA_GLOBAL_GOTOH) return fail(c, SA_ERR_ARG, "unknown algorithm");
@@ -158,8 +185,43 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                hipStream_t stream) {
     if (max_m >= (1u << 24) || max_n >= (1u << 24))
         return fail(c, SA_ERR_UNSUPPORTED, "sequence lengths must be < 2^24");
-    const Plan pl = make_plan(algo, max_m, max_n, npairs);
     const bool keyed = keyed_ok(algo, sc, max_m, max_n);
+    const bool allow = sc->allow_mismatch != 0;
+    const bool lut = d_lutbits != nullptr;
+    // T16 eligibility: scoring/shape bounds on the host, then the batch alphabet from the device
+    bool t16 = t16_ok(algo, sc, max_m, max_n) && (algo == SA_NW || keyed);
+    if (const char* e16 = getenv("SEQALIB_T16")) if (e16[0] == '0') t16 = false;
+    uint32_t sym_pack = 0;
+    if (!c->aux) SA_HIP(c, hipMalloc(&c->aux, 256));
+    if (t16) {
+        SA_HIP(c, launch_alphabet_scan(d1, o1, d2, o2, npairs, c->aux, stream));
+        uint32_t bm[8];
+        SA_HIP(c, hipMemcpyAsync(bm, c->aux, 32, hipMemcpyDeviceToHost, stream));
+        SA_HIP(c, hipStreamSynchronize(stream));
+        int nsym = 0;
+        uint8_t syms[4];
+        for (int b = 0; b < 256; ++b)
+            if ((bm[b >> 5] >> (b & 31)) & 1u) {
+                if (nsym < 4) syms[nsym] = (uint8_t)b;
+                ++nsym;
+            }
+        if (nsym > 4) {
+            t16 = false;
+        } else {
+            // pad with byte values absent from the batch so codes stay distinct
+            for (int b = 0; nsym < 4 && b < 256; ++b) {
+                bool used = false;
+                for (int q = 0; q < nsym; ++q) used |= syms[q] == b;
+                if (!used) syms[nsym++] = (uint8_t)b;
+            }
+            sym_pack = syms[0] | (uint32_t)syms[1] << 8 | (uint32_t)syms[2] << 16 | (uint32_t)syms[3] << 24;
+            SA_HIP(c, launch_build_profile(d_lutbits, sym_pack, sc->match, sc->mismatch, c->aux + 8, stream));
+        }
+    }
+    const Plan pl = make_plan(algo, max_m, max_n, npairs, t16);
+    c->last_kernel = t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
+    c->last_R = pl.R;
+    c->last_W = pl.W;
     const uint64_t slot_bytes = pl.g.dir_slot + pl.rowbuf_elems * 4;
     const uint64_t budget = ws_budget(c);
     uint64_t per_launch = slot_bytes ? std::max<uint64_t>(1, budget / std::max<uint64_t>(slot_bytes, 1)) : npairs;
@@ -177,8 +239,6 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     // reset timing
     c->launches = 0;
     c->timed_stream = stream;
-    const bool lut = d_lutbits != nullptr;
-    const bool allow = sc->allow_mismatch != 0;
 
     for (uint64_t base = 0; base < npairs; base += per_launch) {
         const uint32_t cnt = (uint32_t)std::min<uint64_t>(per_launch, npairs - base);
@@ -194,6 +254,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         fp.gap_open = sc->gap_open; fp.gap_extend = sc->gap_extend;
         fp.waves = pl.W;
         fp.stage_seq2 = max_n <= kMaxStagedSeq2 ? 1 : 0;
+        fp.prof = c->aux + 8;
+        fp.sym_pack = sym_pack;
 
         TbParams tp;
         tp.seq1 = d1; tp.off1 = o1; tp.seq2 = d2; tp.off2 = o2;
@@ -205,6 +267,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         tp.gap = fp.gap; tp.match = fp.match; tp.mismatch = fp.mismatch;
         tp.gap_open = fp.gap_open; tp.gap_extend = fp.gap_extend;
         tp.allow = allow ? 1 : 0;
+        tp.tagged = t16 ? 1 : 0;
 
         while ((int)c->events.size() < 3 * (c->launches + 1)) {
             hipEvent_t ev;
@@ -213,7 +276,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         }
         hipEvent_t* ev = &c->events[3 * c->launches];
         SA_HIP(c, hipEventRecord(ev[0], stream));
-        hipError_t e = launch_fill(algo, pl.R, lut, allow, keyed, fp, cnt, stream);
+        const FillVariant fv = {pl.R, lut, allow, keyed, t16};
+        hipError_t e = launch_fill(algo, fv, fp, cnt, stream);
         if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
         SA_HIP(c, hipEventRecord(ev[1], stream));
         e = launch_traceback(algo, pl.R, lut, tp, stream);
@@ -342,6 +406,7 @@ void sa_destroy(sa_ctx* c) {
     for (auto ev : c->events) (void)hipEventDestroy(ev);
     if (c->ws) (void)hipFree(c->ws);
     if (c->io) (void)hipFree(c->io);
+    if (c->aux) (void)hipFree(c->aux);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -456,6 +521,14 @@ int sa_last_timings(sa_ctx* c, float* fill_ms, float* tb_ms, int* launches) {
     if (fill_ms) *fill_ms = f;
     if (tb_ms) *tb_ms = t;
     if (launches) *launches = c->launches;
+    return SA_OK;
+}
+
+int sa_last_plan(sa_ctx* c, int* kernel, int* R, int* W) {
+    if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
+    if (kernel) *kernel = c->last_kernel;
+    if (R) *R = c->last_R;
+    if (W) *W = c->last_W;
     return SA_OK;
 }
 

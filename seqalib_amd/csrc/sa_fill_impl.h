@@ -24,6 +24,19 @@
 //     (1 KiB per wave instruction, fully coalesced);
 //   * the running maximum of a row is one v_lshl_or (key = H << 16 | column) + one v_max_u32
 //     (KEYED; the host checks scores and columns fit 16 bits), else a compare + 2 selects.
+//
+// T16 (tagged 16-bit profile kernel; SW and NW with allow-mismatch, batch alphabet <= 4 symbols,
+// host-proven |4H| < 2^15).  gfx950 issues 16-bit VOP2 add/max and 32-bit bitwise ops at about
+// twice the rate of 32-bit max/compare/carry ops (profiles/microbench_valu_issue_r01.txt), so:
+//   * scores are kept as 4*H; every candidate carries its move tag in the two low bits
+//     (diag 4D+3, up 4U+2, left 4L+1, clamp 0), so ONE v_max_i16 chain yields both the cell
+//     value and the winning move with the reference's tie order (diag, then up, then left:
+//     SASmithWaterman.h:274-312, SANeedlemanWunsch.h:181-214);
+//   * the substitution term comes from a per-row byte profile with one v_bfe_i32 (offset =
+//     8 * symbol code of the column) instead of a compare + select;
+//   * the tag is pushed into the record with one v_alignbit_b32 (rec = rec >> 2 | T << 30) and
+//     stripped from the value with one v_and_b32.
+// Cell = bfe + 3 add_u16 + 2-3 max_i16 + and + alignbit (+ lshl_or + max_u32 for the key).
 #pragma once
 #include <limits.h>
 
@@ -40,6 +53,8 @@ __device__ __forceinline__ int shr1(int old, int src) {
     return __builtin_amdgcn_update_dpp(old, src, kDppWaveShr1, 0xf, 0xf, false);
 }
 __device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+// v_writelane_b32 through the LLVM intrinsic (the compiler routes the lane select via m0).
+extern "C" __device__ int sa_writelane(int value, int lane, int old) __asm("llvm.amdgcn.writelane");
 
 // rec = 2*rec + (a == b), one v_cmp into an SGPR pair + one v_addc_co_u32.
 __device__ __forceinline__ uint32_t push_eq(uint32_t rec, int a, int b) {
@@ -48,6 +63,12 @@ __device__ __forceinline__ uint32_t push_eq(uint32_t rec, int a, int b) {
     unsigned long long co;
     asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(out), "=s"(co) : "v"(rec), "s"(m));
     return out;
+}
+
+// 8 * code of symbol b in the T16 alphabet (bytes of sym_pack are distinct; code 0 = byte 0).
+__device__ __forceinline__ uint32_t t16_code8(uint32_t sp, uint32_t b) {
+    return (b == ((sp >> 8) & 255u) ? 8u : 0u) | (b == ((sp >> 16) & 255u) ? 16u : 0u) |
+           (b == (sp >> 24) ? 24u : 0u);
 }
 
 template <bool LUT>
@@ -59,7 +80,7 @@ __device__ __forceinline__ bool match_bit(const uint32_t* s_lut, int a, int b) {
     }
 }
 
-template <int ALG, int R, bool LUT, bool ALLOW, bool KEYED>
+template <int ALG, int R, bool LUT, bool ALLOW, bool KEYED, bool T16>
 __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
     constexpr bool AFF = ALG >= SA_LOCAL_GOTOH;
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
@@ -73,6 +94,9 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
     constexpr int BAND = kWave * R;
     static_assert(kChunk % SPP == 0, "chunk must hold whole packets");
     static_assert(BPS >= 1, "record must be at least a byte");
+    static_assert(!T16 || (!AFF && ALLOW && !LUT && RB <= 32), "T16: linear, allow-mismatch, profile");
+    static_assert(!T16 || !LOCAL || KEYED, "T16 local mode tracks its maximum with keys");
+    constexpr int SC = T16 ? 4 : 1;            // score scale of the register values
 
     // Dynamic LDS (sizes from lds_layout(), host and device agree):
     //   [match bits: 2048 words, LUT only][hand-off rings: W x kRing x (1|2) ints][Seq2 bytes, staged]
@@ -108,12 +132,14 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
         for (int k = threadIdx.x; k < 2048; k += blockDim.x) s_lut[k] = P.lutbits[k];
     }
     if (P.stage_seq2) {
-        for (int k = threadIdx.x; k < n; k += blockDim.x) s_seq2[k] = s2[k];
+        for (int k = threadIdx.x; k < n; k += blockDim.x)
+            s_seq2[k] = T16 ? (uint8_t)t16_code8(P.sym_pack, s2[k]) : s2[k];
     }
     __syncthreads();
     const int G = P.gap, MA = P.match, MI = P.mismatch;
     const int GO = P.gap_open, GE = P.gap_extend;
     const int GOE = GO + GE;
+    const uint32_t CU = (uint32_t)(4 * G + 2), CL = (uint32_t)(4 * G + 1);   // T16 tagged gaps
 
     const int B = (m > 0 && n > 0) ? (m + BAND - 1) / BAND : 0;
     const uint32_t nch = chunks_per_band((uint32_t)n);
@@ -139,8 +165,11 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
 
     // One step: lane computes column j = s - lane for its R rows.  STEADY: every lane is in
     // range, no exec-mask branch.  Returns the packed record words in rec.
-    auto step = [&](auto steady, int q, int s, int bch, int bcx, int symc, uint32_t (&rec)[RW]) {
+    uint32_t kprev[R];   // T16 steady chunks: the previous step's keys, merged pairwise by v_max3
+    auto step = [&](auto steady, int q, int s, int bch, int bcx, int symc, uint32_t (&rec)[RW],
+                    auto odd) {
         constexpr bool STEADY = decltype(steady)::value;
+        constexpr bool ODD = decltype(odd)::value;
         const int up_h = shr1(__builtin_amdgcn_readlane(bch, q), hl);
         int up_x = 0;
         if constexpr (AFF) up_x = shr1(__builtin_amdgcn_readlane(bcx, q), xl);
@@ -153,14 +182,68 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
             int hd = prev_up;            // H[i-1][j-1] of my first row
             int hu = up_h;               // H[i-1][j]
             int xu = up_x;               // Ix[i-1][j]
+            uint32_t dcur = 0;           // T16: tagged diagonal candidate of the current row
+            if constexpr (T16) {
+                asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0"
+                    : "=&v"(dcur) : "v"(a[0]), "v"(sym), "v"(hd));
+            }
 #pragma unroll
             for (int r = 0; r < R; ++r) {
+                uint32_t& rw = rec[r / RPW];
+                int Hc;
+                if constexpr (T16) {
+                    // One asm block per cell (plain VALU->VALU dependences need no wait
+                    // states; the compiler pads s_nop between separate asm statements).  The
+                    // block also forms the NEXT row's diagonal candidate from Hp[r] before
+                    // updating Hp[r] in place, so no register copies are needed.
+                    uint32_t t0, t1;
+#define SA_T16_HEAD                                                                          \
+    "v_add_u16 %[t1], %[cu], %[hu]\n\t"                                                      \
+    "v_max_i16 %[t0], %[dr], %[t1]\n\t"                                                      \
+    "v_add_u16 %[t1], %[cl], %[hp]\n\t"                                                      \
+    "v_max_i16 %[t0], %[t1], %[t0]\n\t"
+#define SA_T16_TAIL                                                                          \
+    "v_and_b32 %[hp], -4, %[t0]\n\t"                                                         \
+    "v_alignbit_b32 %[rec], %[t0], %[rec], 2"
+#define SA_T16_NEXT                                                                          \
+    "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\t"                                                \
+    "v_add_u16 %[dn], %[hp], %[dn]\n\t"
+#define SA_T16_CLAMP "v_max_i16 %[t0], 0, %[t0]\n\t"
+                    if (r + 1 < R) {
+                        uint32_t dn;
+                        if constexpr (LOCAL)
+                            asm(SA_T16_HEAD SA_T16_CLAMP SA_T16_NEXT SA_T16_TAIL
+                                : [t0] "=&v"(t0), [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r]),
+                                  [rec] "+v"(rw)
+                                : [dr] "v"(dcur), [hu] "v"(hu), [tabn] "v"(a[r + 1 < R ? r + 1 : r]),
+                                  [sym] "v"(sym), [cu] "s"(CU), [cl] "s"(CL));
+                        else
+                            asm(SA_T16_HEAD SA_T16_NEXT SA_T16_TAIL
+                                : [t0] "=&v"(t0), [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r]),
+                                  [rec] "+v"(rw)
+                                : [dr] "v"(dcur), [hu] "v"(hu), [tabn] "v"(a[r + 1 < R ? r + 1 : r]),
+                                  [sym] "v"(sym), [cu] "s"(CU), [cl] "s"(CL));
+                        dcur = dn;
+                    } else {
+                        if constexpr (LOCAL)
+                            asm(SA_T16_HEAD SA_T16_CLAMP SA_T16_TAIL
+                                : [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r]), [rec] "+v"(rw)
+                                : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL));
+                        else
+                            asm(SA_T16_HEAD SA_T16_TAIL
+                                : [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r]), [rec] "+v"(rw)
+                                : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL));
+                    }
+#undef SA_T16_HEAD
+#undef SA_T16_TAIL
+#undef SA_T16_NEXT
+#undef SA_T16_CLAMP
+                    Hc = Hp[r];
+                } else {
                 const bool v = match_bit<LUT>(s_lut, a[r], sym);
                 int D;
                 if constexpr (ALLOW) D = hd + (v ? MA : MI);
                 else D = v ? hd + MA : INT_MIN;
-                uint32_t& rw = rec[r / RPW];
-                int Hc;
                 if constexpr (!AFF) {
                     const int U = hu + G;
                     const int L = Hp[r] + G;
@@ -184,20 +267,30 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
                     xu = X;
                     Hc = M;
                 }
+                }
                 if constexpr (LOCAL) {
-                    if constexpr (KEYED) {
-                        bh[r] = (int)max((uint32_t)bh[r], ((uint32_t)Hc << 16) | (uint32_t)jkey);
+                    if constexpr (T16 && STEADY) {
+                        // Hc = 4H with clear tag bits, so Hc << 14 == H << 16.  Two steps' keys
+                        // per v_max3, in place (lets the compiler keep bh[] in fixed registers).
+                        const uint32_t k = ((uint32_t)Hc << 14) | (uint32_t)jkey;
+                        if constexpr (!ODD) kprev[r] = k;
+                        else asm("v_max3_u32 %0, %0, %1, %2" : "+v"(bh[r]) : "v"(kprev[r]), "v"(k));
+                    } else if constexpr (KEYED) {
+                        bh[r] = (int)max((uint32_t)bh[r], ((uint32_t)Hc << (T16 ? 14 : 16)) | (uint32_t)jkey);
                     } else {
                         if (Hc >= bh[r]) { bh[r] = Hc; bj[r] = j; }
                     }
                 }
-                hd = Hp[r];
-                Hp[r] = Hc;
+                if constexpr (!T16) {
+                    hd = Hp[r];
+                    Hp[r] = Hc;
+                }
                 hu = Hc;
             }
             prev_up = up_h;
             hl = Hp[R - 1];
             if constexpr (AFF) xl = xu;
+            if constexpr (T16 && RB < 32) rec[0] >>= (32 - RB);   // alignbit filled from the top
         }
     };
 
@@ -210,11 +303,13 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
             uint32_t pk[4 * PPS];
 #pragma unroll
             for (int e = 0; e < 4 * PPS; ++e) pk[e] = 0;
+            static_assert(SPP % 2 == 0, "steps pair up for the key max3");
 #pragma unroll
             for (int g = 0; g < SPP; ++g) {
                 const int q = q0 + g;
                 uint32_t rec[RW];
-                step(steady, q, kC + q, bch, bcx, symc, rec);
+                if (g & 1) step(steady, q, kC + q, bch, bcx, symc, rec, std::true_type{});
+                else step(steady, q, kC + q, bch, bcx, symc, rec, std::false_type{});
                 if constexpr (BPS >= 4) {
 #pragma unroll
                     for (int e = 0; e < RW; ++e) pk[g * RW + e] = rec[e];
@@ -223,7 +318,7 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
                 }
                 // lane 63 holds the band's last row at column kC + q - 63: park it in lane q
                 const int lh = __builtin_amdgcn_readlane(hl, 63);
-                acc_h = (lane == q) ? lh : acc_h;
+                acc_h = sa_writelane(lh, q, acc_h);
                 if constexpr (AFF) {
                     const int lx = __builtin_amdgcn_readlane(xl, 63);
                     acc_x = (lane == q) ? lx : acc_x;
@@ -253,10 +348,11 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
         const int c = c0 + lane;
         vh = 0; vx = -10000; vs = 0;
         if (lane < kChunk && c < n) {
-            vs = P.stage_seq2 ? (int)s_seq2[c] : (int)s2[c];
+            if (P.stage_seq2) vs = (int)s_seq2[c];
+            else vs = T16 ? (int)t16_code8(P.sym_pack, s2[c]) : (int)s2[c];
             if (band == 0) {
                 const int J = c + 1;
-                if constexpr (ALG == SA_NW) vh = J * G;
+                if constexpr (ALG == SA_NW) vh = SC * J * G;
                 else if constexpr (ALG == SA_GLOBAL_GOTOH) vh = GO + J * GE;
             } else if (band % W != 0) {
                 vh = ring(band % W, 0)[c % kRing];
@@ -281,16 +377,17 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
                         const int row = row0 + r;
-                        a[r] = row < m ? (int)s1[row] : 0;
+                        if constexpr (T16) a[r] = row < m ? (int)P.prof[t16_code8(P.sym_pack, s1[row]) >> 3] : 0;
+                        else a[r] = row < m ? (int)s1[row] : 0;
                         const int i = row + 1;
-                        if constexpr (ALG == SA_NW) Hp[r] = i * G;
+                        if constexpr (ALG == SA_NW) Hp[r] = SC * i * G;
                         else if constexpr (ALG == SA_GLOBAL_GOTOH) Hp[r] = GO + i * GE;
                         else Hp[r] = 0;
                         Yp[r] = -10000;
                         bh[r] = KEYED ? 0 : INT_MIN;
                         bj[r] = 0;
                     }
-                    if constexpr (ALG == SA_NW) prev_up = row0 * G;
+                    if constexpr (ALG == SA_NW) prev_up = SC * row0 * G;
                     else if constexpr (ALG == SA_GLOBAL_GOTOH) prev_up = row0 == 0 ? 0 : GO + row0 * GE;
                     else prev_up = 0;
                 }
@@ -337,7 +434,7 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
                             int v = 0;
 #pragma unroll
                             for (int r = 0; r < R; ++r) v = (r == rr) ? Hp[r] : v;
-                            s_score = v;
+                            s_score = T16 ? ((int)(int16_t)(v & 0xffff)) / 4 : v;
                         }
                     }
                 }
@@ -393,15 +490,33 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
 }
 
 template <int ALG>
-hipError_t launch_fill_alg(int R, bool lut, bool allow, bool keyed, const FillParams& p,
-                           uint32_t grid, hipStream_t stream) {
+hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream) {
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
+    const int R = v.R;
+    const bool lut = v.t16 ? false : v.lut, allow = v.allow;
+    const bool keyed = LOCAL && v.keyed;
     const dim3 block(kWave * p.waves);
     const size_t lds = lds_layout(lut, is_affine(ALG), p.waves, p.stage_seq2 ? p.max_n : 0).total;
-    if (!LOCAL) keyed = false;
+    if constexpr (ALG == SA_SW || ALG == SA_NW) {
+        if (v.t16) {
+            if (!allow || (LOCAL && !keyed)) return hipErrorInvalidValue;
+#define SA_LAUNCH16(RR)                                                                              \
+    if (R == RR) {                                                                                   \
+        hipLaunchKernelGGL((fill_kernel<ALG, RR, false, true, LOCAL, true>), dim3(grid), block, lds, \
+                           stream, p);                                                               \
+        return hipGetLastError();                                                                    \
+    }
+            SA_LAUNCH16(4)
+            SA_LAUNCH16(8)
+            SA_LAUNCH16(16)
+#undef SA_LAUNCH16
+            return hipErrorInvalidValue;
+        }
+    }
+    if (v.t16) return hipErrorInvalidValue;
 #define SA_LAUNCH(RR, LL, AA, KK)                                                              \
     if (R == RR && lut == LL && allow == AA && keyed == KK) {                                  \
-        hipLaunchKernelGGL((fill_kernel<ALG, RR, LL, AA, KK>), dim3(grid), block, lds, stream, p); \
+        hipLaunchKernelGGL((fill_kernel<ALG, RR, LL, AA, KK, false>), dim3(grid), block, lds, stream, p); \
         return hipGetLastError();                                                              \
     }
 #define SA_LAUNCH_K(RR, LL, AA) \

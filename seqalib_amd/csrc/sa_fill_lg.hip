@@ -2,7 +2,7 @@
 #include "sa_fill_impl.h"
 
 namespace sa {
-hipError_t launch_fill_lg(int R, bool lut, bool allow, bool keyed, const FillParams& p, uint32_t grid, hipStream_t s) {
-    return launch_fill_alg<SA_LOCAL_GOTOH>(R, lut, allow, keyed, p, grid, s);
+hipError_t launch_fill_lg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s) {
+    return launch_fill_alg<SA_LOCAL_GOTOH>(v, p, grid, s);
 }
 }  // namespace sa

@@ -25,6 +25,10 @@ struct FillParams {
     int32_t gap, match, mismatch, gap_open, gap_extend;
     int waves;                 // waves per workgroup (blockDim.x / 64)
     int stage_seq2;            // 1: Seq2 of the pair is copied to LDS (max_n <= kMaxStagedSeq2)
+    // T16 kernel only: the batch alphabet is <= 4 symbols (bytes of sym_pack = code 0..3) and
+    // prof[c] holds, in byte c', the tagged substitution term 4*s(sym c, sym c') + 3 as int8.
+    const uint32_t* prof;
+    uint32_t sym_pack;
 };
 
 struct TbParams {
@@ -41,16 +45,27 @@ struct TbParams {
     uint32_t max_m, max_n;
     int32_t gap, match, mismatch, gap_open, gap_extend;
     int allow;
+    int tagged;                // records hold T16 max tags (sa_layout.h)
 };
 
-// R in {4, 8, 16}; keyed: 16-bit (score, column) max keys (local modes only).
+// R in {4, 8, 16}; keyed: 16-bit (score, column) max keys (local modes only); t16: the tagged
+// 16-bit profile kernel (SW/NW with allow-mismatch, see sa_fill_impl.h).
 // Returns hipSuccess or the launch error.
-hipError_t launch_fill(int algo, int R, bool lut, bool allow, bool keyed, const FillParams& p,
-                       uint32_t grid, hipStream_t stream);
-hipError_t launch_fill_sw(int R, bool lut, bool allow, bool keyed, const FillParams& p, uint32_t grid, hipStream_t s);
-hipError_t launch_fill_nw(int R, bool lut, bool allow, bool keyed, const FillParams& p, uint32_t grid, hipStream_t s);
-hipError_t launch_fill_lg(int R, bool lut, bool allow, bool keyed, const FillParams& p, uint32_t grid, hipStream_t s);
-hipError_t launch_fill_gg(int R, bool lut, bool allow, bool keyed, const FillParams& p, uint32_t grid, hipStream_t s);
+struct FillVariant {
+    int R;
+    bool lut, allow, keyed, t16;
+};
+hipError_t launch_fill(int algo, const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream);
+hipError_t launch_fill_sw(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
+hipError_t launch_fill_nw(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
+hipError_t launch_fill_lg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
+hipError_t launch_fill_gg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
+// Batch alphabet scan (presence bitmap of every byte of both sequence sets, 8 words) and the
+// T16 substitution profile.
+hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uint8_t* d2,
+                                const uint64_t* o2, uint32_t npairs, uint32_t* bitmap, hipStream_t s);
+hipError_t launch_build_profile(const uint32_t* lutbits, uint32_t sym_pack, int match, int mismatch,
+                                uint32_t* prof, hipStream_t s);
 hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
 
 }  // namespace sa

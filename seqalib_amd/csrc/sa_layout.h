@@ -13,12 +13,14 @@
 //   linear (SW/NW), BPC = 2:  fD = (H == diag term), fU = (H == up term)
 //   affine (Gotoh), BPC = 4:  fD = (M == diag term), fX = (M == Ix),
 //                             fXe = (Ix == Ix_up + GE), fYe = (Iy == Iy_left + GE)
+// or, for the tagged 16-bit linear kernel (TAGGED records, BPC = 2), the 2-bit tag that won the
+// cell's max: 3 = diag, 2 = up, 1 = left, 0 = zero clamp (sa_fill_impl.h, "T16").
 // The traceback re-derives the cell scores along its path from the end score (every move is an
 // exact equality), so zero tests and gap-open clamps need no stored bits.
 //
-// Per band, per step, per lane a record of R*BPC bits is built by shifting flags in (first flag
-// of row 0 ends up most significant); records are grouped into 16-byte packets so every store is
-// one coalesced 1 KiB wave instruction:
+// Per band, per step, per lane a record of R*BPC bits is built by shifting flags in (flags: first
+// flag of row 0 ends up most significant; tags: row r lands at bits 2r); records are grouped into
+// 16-byte packets so every store is one coalesced 1 KiB wave instruction:
 //   packet(b, s, half) = b*band_stride + ((s / SPP) * PPS + half) * 1024, lane t at +16*t,
 //   step s at +(s % SPP)*BPS inside the lane's 16 bytes.
 #pragma once
@@ -72,13 +74,15 @@ struct Geom {
     uint32_t bands;     // bands for max_m
     uint64_t band_stride;  // bytes per band
     uint64_t dir_slot;     // bytes per pair
+    bool tagged;           // 2-bit max tags (T16 kernel) instead of equality flags
 };
 
 SA_HD uint32_t round_up(uint32_t x, uint32_t a) { return (x + a - 1) / a * a; }
 
-SA_HD Geom make_geom(int algo, int R, uint32_t max_m, uint32_t max_n) {
+SA_HD Geom make_geom(int algo, int R, uint32_t max_m, uint32_t max_n, bool tagged = false) {
     Geom g;
     g.R = R;
+    g.tagged = tagged;
     g.bpc = bits_per_cell(algo);
     g.bps = R * g.bpc / 8;
     g.spp = g.bps >= 16 ? 1 : 16 / g.bps;
@@ -90,14 +94,15 @@ SA_HD Geom make_geom(int algo, int R, uint32_t max_m, uint32_t max_n) {
     return g;
 }
 
-// Bit index, inside its 32-bit record word, of the LAST-pushed (least significant) flag of row r.
-// Rows are pushed r = 0..R-1, BPC flags each, into words of min(32, R*BPC) bits.
-SA_HD void cell_word_bit(int R, int bpc, int r, int* word, int* lowbit) {
+// Bit index, inside its 32-bit record word, of the least significant bit of row r's group.
+// Flags: rows are pushed r = 0..R-1, BPC flags each, into words of min(32, R*BPC) bits, first row
+// most significant.  Tags: v_alignbit pushes each row in at the top, so row r ends at bits 2r.
+SA_HD void cell_word_bit(int R, int bpc, int r, int* word, int* lowbit, bool tagged = false) {
     const int rb = R * bpc;
     const int wb = rb < 32 ? rb : 32;
     const int rpw = wb / bpc;
     *word = r / rpw;
-    *lowbit = wb - bpc * ((r % rpw) + 1);
+    *lowbit = tagged ? bpc * (r % rpw) : wb - bpc * ((r % rpw) + 1);
 }
 
 // Byte offset (inside a pair's slot) and bit shift of the flag group of cell (i, j), 1-based.
@@ -110,7 +115,7 @@ SA_HD uint64_t cell_byte(const Geom& g, uint32_t i, uint32_t j, int* shift) {
     const int r = (int)(rem - t * g.R);
     const uint32_t s = (j - 1) + t;
     int word, lowbit;
-    cell_word_bit(g.R, g.bpc, r, &word, &lowbit);
+    cell_word_bit(g.R, g.bpc, r, &word, &lowbit, g.tagged);
     const uint32_t byte_in_rec = (uint32_t)word * 4 + (uint32_t)lowbit / 8;
     *shift = lowbit % 8;
     const uint32_t half = byte_in_rec / 16;

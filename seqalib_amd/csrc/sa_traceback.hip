@@ -36,7 +36,8 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
     const int n = (int)(P.off2[pidx + 1] - o2);
     const uint8_t* s1 = P.seq1 + o1;
     const uint8_t* s2 = P.seq2 + o2;
-    const Geom g = make_geom(ALG, R, P.max_m, P.max_n);
+    const bool tagged = P.tagged != 0;
+    const Geom g = make_geom(ALG, R, P.max_m, P.max_n, tagged);
     const uint8_t* dir = P.dirs + (uint64_t)slot * P.dir_slot;
     uint8_t* ops = P.ops + o1 + o2 + pidx;
     const bool allow = P.allow != 0;
@@ -49,6 +50,12 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
         int sh;
         const uint64_t off = cell_byte(g, (uint32_t)i, (uint32_t)j, &sh);
         return (uint32_t)(dir[off] >> sh);
+    };
+    // linear modes: flags fD (bit 1) / fU (bit 0); a T16 max tag (3 diag, 2 up, 1 left, 0 clamp)
+    // says the same thing: diag wins iff H == D, else up iff H == U.
+    auto lin = [&](int i, int j) -> uint32_t {
+        const uint32_t f = cell(i, j) & 3u;
+        return tagged ? (f == 3u ? 2u : (f == 2u ? 1u : 0u)) : f;
     };
     // diagonal move: emits the op and returns the substitution term that was added
     auto diag = [&](int i, int j) -> int {
@@ -65,7 +72,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
         if (m == 0 || n == 0) { i = 0; j = 0; }
         while (i > 0 && j > 0) {
             if (H == 0) break;        // diag test max(D,0) == H == 0 -> end of the local path
-            const uint32_t f = cell(i, j);
+            const uint32_t f = lin(i, j);
             if (f & 2u) { H -= diag(i, j); --i; --j; }
             else if (f & 1u) { ops[k++] = 'U'; H -= G; --i; }
             else { ops[k++] = 'L'; H -= G; --j; }
@@ -74,7 +81,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
         i = m; j = n;
         while (i > 0 || j > 0) {
             if (i > 0 && j > 0) {
-                const uint32_t f = cell(i, j);
+                const uint32_t f = lin(i, j);
                 if (f & 2u) { diag(i, j); --i; --j; }
                 else if (f & 1u) { ops[k++] = 'U'; --i; }
                 else { ops[k++] = 'L'; --j; }
@@ -152,13 +159,13 @@ hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStr
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_fill(int algo, int R, bool lut, bool allow, bool keyed, const FillParams& p,
-                       uint32_t grid, hipStream_t stream) {
+hipError_t launch_fill(int algo, const FillVariant& v, const FillParams& p, uint32_t grid,
+                       hipStream_t stream) {
     switch (algo) {
-        case SA_SW: return launch_fill_sw(R, lut, allow, keyed, p, grid, stream);
-        case SA_NW: return launch_fill_nw(R, lut, allow, keyed, p, grid, stream);
-        case SA_LOCAL_GOTOH: return launch_fill_lg(R, lut, allow, keyed, p, grid, stream);
-        case SA_GLOBAL_GOTOH: return launch_fill_gg(R, lut, allow, keyed, p, grid, stream);
+        case SA_SW: return launch_fill_sw(v, p, grid, stream);
+        case SA_NW: return launch_fill_nw(v, p, grid, stream);
+        case SA_LOCAL_GOTOH: return launch_fill_lg(v, p, grid, stream);
+        case SA_GLOBAL_GOTOH: return launch_fill_gg(v, p, grid, stream);
         default: return hipErrorInvalidValue;
     }
 }

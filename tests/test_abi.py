@@ -80,7 +80,7 @@ def test_headline_plan_fits_hbm():
     assert 10000 * (dir_bytes + row_bytes) < 64e9
 
 
-def cell_byte(R, bpc, max_n, i, j):
+def cell_byte(R, bpc, max_n, i, j, tagged=False):
     """Python restatement of sa_layout.h cell_byte (independent check of the layout)."""
     bps = R * bpc // 8
     spp = 1 if bps >= 16 else 16 // bps
@@ -94,22 +94,25 @@ def cell_byte(R, bpc, max_n, i, j):
     rb = R * bpc
     wb = min(rb, 32)
     rpw = wb // bpc
-    word, lowbit = r // rpw, wb - bpc * (r % rpw + 1)
+    word = r // rpw
+    lowbit = bpc * (r % rpw) if tagged else wb - bpc * (r % rpw + 1)
     byte_in_rec = word * 4 + lowbit // 8
     half = byte_in_rec // 16
     packet = (s // spp) * pps + half
     return b * band_stride + packet * 1024 + t * 16 + (s % spp) * bps + byte_in_rec % 16, lowbit % 8
 
 
-@pytest.mark.parametrize("R,bpc", [(4, 2), (8, 2), (16, 2), (4, 4), (8, 4), (16, 4)])
-def test_flag_layout_is_a_bijection(R, bpc):
+@pytest.mark.parametrize("R,bpc,tagged", [(4, 2, False), (8, 2, False), (16, 2, False), (4, 4, False),
+                                          (8, 4, False), (16, 4, False), (4, 2, True), (8, 2, True),
+                                          (16, 2, True)])
+def test_flag_layout_is_a_bijection(R, bpc, tagged):
     """Every cell of a band gets its own bits, records pack exactly R*bpc bits per lane-step."""
     max_n = 70
     m = 64 * R * 2
     seen = set()
     for i in range(1, m + 1):
         for j in range(1, max_n + 1):
-            off, sh = cell_byte(R, bpc, max_n, i, j)
+            off, sh = cell_byte(R, bpc, max_n, i, j, tagged)
             for k in range(bpc):
                 bit = (off, sh + k)
                 assert sh + k < 8

@@ -125,6 +125,55 @@ def test_multiband_wrap_vs_oracle(engine, algo):
     compare_with_oracle(engine, algo, SCORINGS[algo][1 % len(SCORINGS[algo])], pairs)
 
 
+def dna_pairs(seed, count, maxlen):
+    rng = np.random.default_rng(seed)
+    pairs = []
+    for k in range(count):
+        m, n = int(rng.integers(0, maxlen)), int(rng.integers(0, maxlen))
+        a = sa.synth_dna(seed * 1000 + 2 * k, m)
+        b = sa.synth_mutate(a, k)[:n] if k % 2 else sa.synth_dna(seed * 1000 + 2 * k + 1, n)
+        pairs.append((a, b))
+    return pairs
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_t16_and_int32_kernels_both_exact(engine, algo, monkeypatch):
+    """DNA SW/NW with allow-mismatch run on the tagged 16-bit kernel; SEQALIB_T16=0 forces the
+    int32 kernel.  Both must equal the oracle."""
+    pairs = dna_pairs(7 + algo, 40, 900)
+    allow_scorings = [a for a in SCORINGS[algo] if len(a) == 3 or (len(a) == 4 and a[3])]
+    for args in allow_scorings:
+        compare_with_oracle(engine, algo, args, pairs)
+        assert engine.last_plan()[0] == sa.SA_KERNEL_T16, args
+    monkeypatch.setenv("SEQALIB_T16", "0")
+    for args in allow_scorings:
+        compare_with_oracle(engine, algo, args, pairs)
+        assert engine.last_plan()[0] == sa.SA_KERNEL_INT32, args
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_t16_eligibility(engine, algo):
+    """Kernel choice follows the preconditions: <= 4 symbols, int16 headroom, allow-mismatch."""
+    dna = dna_pairs(21 + algo, 6, 400)
+    # fewer than four symbols (codes padded with absent bytes)
+    two = [(bytes(b"AC"[x & 1] for x in a), bytes(b"CA"[x % 3 == 0] for x in b)) for a, b in dna]
+    compare_with_oracle(engine, algo, (-1, 2, -1), two)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    # a fifth symbol -> int32 kernel
+    five = dna[:-1] + [(dna[-1][0] + b"N", dna[-1][1])]
+    compare_with_oracle(engine, algo, (-1, 2, -1), five)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
+    # scores that would overflow 4*H in int16 -> int32 kernel
+    big = [(sa.synth_dna(77, 3000), sa.synth_dna(77, 3000))]
+    compare_with_oracle(engine, algo, (-1, 3, -1), big)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
+    compare_with_oracle(engine, algo, (-1, 2, -1), big)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    # !allowMismatch -> int32 kernel
+    compare_with_oracle(engine, algo, (-2, 1, -1, False), dna)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
+
+
 @pytest.mark.parametrize("match", ["purine", "nwild", "caseless"])
 def test_custom_match_fn_vs_oracle(engine, match):
     pairs = []

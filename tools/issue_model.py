@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""VALU issue-bound model of a fill kernel's steady loop (the roofline "peak" of bench.py).
+
+The fill kernel is bound by VALU instruction issue, not HBM (0.25 B/cell) and not MFMA (no
+matrix work).  gfx950 issues different opcodes at different rates (profiles/
+microbench_valu_issue_r01.txt: 16-bit add/max, mov, f32 add/fma ~0.41 wave-instr/cycle/SIMD;
+32-bit max/min/cmp/carry/shift-or/bfe/alignbit ~0.22-0.23), so the ceiling depends on the mix.
+
+This script compiles the fill TU for gfx950, takes the largest basic block of the requested
+kernel (the branch-free steady chunk loop: SPP steps x R rows per lane), prices every VALU
+instruction at its measured issue rate and reports
+    cycles_per_lane_cell = sum(count / rate) / cells_per_lane_in_block   [SIMD cycles / 64 cells]
+    peak_gcups = SIMDs * clock * 64 / cycles_per_lane_cell / 1e9
+Scalar and memory instructions issue on other units and are not charged.
+    python3 tools/issue_model.py [--out profiles/issue_model_r02.json]
+"""
+import argparse, collections, json, os, re, subprocess, sys, tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RATES_FILE = os.path.join(ROOT, "profiles", "microbench_valu_issue_r01.txt")
+SIMDS, CLOCK = 256 * 4, 2.4e9
+
+ALIAS = {"v_mov_b32_dpp": "v_mov_b32_dpp_shr", "v_readlane_b32": "readlane", "v_writelane_b32": "readlane",
+         "v_mov_b32": "mov_b32", "v_max_i16": "max_i16", "v_add_u16": "add_u16", "v_alignbit_b32": "alignbit_b32",
+         "v_bfe_i32": "v_bfe_u32", "v_addc_co_u32": "addc_only", "v_cndmask_b32": "cndmask_e64_sgpr",
+         "v_cmp_eq_u32": "cmp_only", "v_cmp_gt_u32": "cmp_only", "v_cmp_le_u32": "cmp_only",
+         "v_lshl_add_u64": "v_lshl_add_u32", "v_max3_i32": "v_max3_i32", "v_add_co_u32": "add_co_e64"}
+
+KERNELS = {  # label -> (TU, mangled name, cells per lane in one steady block = SPP * R)
+    "sw_t16_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELb0ELb1ELb1ELb1EEEvNS_10FillParamsE", 64),
+    "sw_int32_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELb0ELb1ELb1ELb0EEEvNS_10FillParamsE", 64),
+    "nw_t16_r16": ("sa_fill_nw.hip", "_ZN2sa11fill_kernelILi1ELi16ELb0ELb1ELb0ELb1EEEvNS_10FillParamsE", 64),
+    "lg_int32_r16": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi16ELb0ELb1ELb1ELb0EEEvNS_10FillParamsE", 32),
+}
+
+
+def rates():
+    r = {}
+    for line in open(RATES_FILE):
+        m = re.match(r"^(\S+)\s+[\d.]+ ms\s+([\d.]+) wave-instr", line)
+        if m:
+            r[m.group(1)] = float(m.group(2))
+    return r
+
+
+def rate_of(op, R):
+    base = re.sub(r"_e(32|64)$", "", op)
+    for k in (op, base, ALIAS.get(op), ALIAS.get(base)):
+        if k and k in R:
+            return R[k]
+    return None
+
+
+def steady_block(asm, name):
+    st = asm.find(name + ":")
+    en = asm.find("s_endpgm", st)
+    blocks, cur = [], []
+    for line in asm[st:en].split("\n"):
+        if re.match(r"^\.LBB|^_Z|^; %bb\.", line):
+            blocks.append(cur)
+            cur = []
+        else:
+            t = line.strip()
+            if t and not t.startswith(";") and not t.startswith("."):
+                cur.append(t.split()[0])
+    blocks.append(cur)
+    return max(blocks, key=len)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out")
+    ap.add_argument("--kernels", default=",".join(KERNELS))
+    a = ap.parse_args()
+    R = rates()
+    out = {"rates_file": os.path.relpath(RATES_FILE, ROOT), "simds": SIMDS, "clock_hz": CLOCK, "kernels": {}}
+    cache = {}
+    with tempfile.TemporaryDirectory() as td:
+        for label in a.kernels.split(","):
+            tu, name, cells = KERNELS[label]
+            if tu not in cache:
+                subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-c",
+                                os.path.join(ROOT, "seqalib_amd", "csrc", tu), "-o", os.path.join(td, "x.o"),
+                                "-save-temps"], cwd=td, check=True, capture_output=True)
+                s = [f for f in os.listdir(td) if f.endswith("gfx950.s") and f.startswith(tu[:-4])][0]
+                cache[tu] = open(os.path.join(td, s)).read()
+            blk = steady_block(cache[tu], name)
+            cnt = collections.Counter(blk)
+            cyc, valu, unknown = 0.0, 0, {}
+            for op, c in cnt.items():
+                if not op.startswith("v_"):
+                    continue
+                valu += c
+                r = rate_of(op, R)
+                if r is None:
+                    unknown[op] = c
+                    r = 0.22
+                cyc += c / r
+            cpc = cyc / cells
+            out["kernels"][label] = {
+                "kernel": name, "cells_per_lane_in_block": cells, "valu_per_cell": round(valu / cells, 3),
+                "cycles_per_lane_cell": round(cpc, 3),
+                "peak_gcups": round(SIMDS * CLOCK * 64 / cpc / 1e9, 1),
+                "mix": dict(sorted(((k, v) for k, v in cnt.items() if k.startswith("v_")), key=lambda x: -x[1])),
+                "unpriced_at_slow_rate": unknown}
+            print(f"{label:14s} VALU/cell {valu / cells:6.2f}  cycles/lane-cell {cpc:6.2f}  "
+                  f"issue ceiling {SIMDS * CLOCK * 64 / cpc / 1e9:8.1f} GCUPS  unpriced {unknown}")
+    if a.out:
+        json.dump(out, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
