@@ -12,6 +12,14 @@
 //   LG  SALocalGotoh.h:285-470      3-state machine; stops on M == 0 / gap-open <= 0 / edge
 //   GG  SAGlobalGotoh.h:245-421     3-state machine; j == 0 -> up, i == 0 -> left
 // Ops are written in traceback order (include/seqalib_hip.h); forceGlobal is host work.
+//
+// Memory: a walk is a chain of dependent reads, one cell per move, and a 4k x 4k local path is
+// ~5k moves long, so per-move HBM latency would dominate.  Each lane therefore keeps private LDS
+// windows that one batch of independent loads refills:
+//   flags: lanes {t, t-1} x step groups {G .. G-7} of its band (16-byte packets, sa_layout.h)
+//          -- a walk only moves to smaller steps s = j-1+t and smaller lanes t;
+//   Seq1 / Seq2: the 32 bytes below the current row / column.
+// and refills are batched across the wave (see the round loop at the end of the kernel).
 #include <limits.h>
 
 #include "sa_internal.h"
@@ -24,8 +32,19 @@ __device__ __forceinline__ bool tb_match(const uint32_t* lut, uint8_t a, uint8_t
     else return a == b;
 }
 
+constexpr int kTbLanes = 2;                   // lanes {t, t-1} per flag window
+constexpr int kTbGroups = 8;                  // step groups {G .. G-7} per flag window
+constexpr int kTbSeqWin = 32;                 // bytes per sequence window
+constexpr int kTbFlagBytes = kTbLanes * kTbGroups * 16;
+constexpr int kTbLaneWords = (kTbFlagBytes + 2 * kTbSeqWin) / 4 + 1;   // odd: conflict-free LDS
+static_assert(kTbLaneWords % 2 == 1, "per-lane LDS stride must be odd in words");
+
 template <int ALG, int R, bool LUT>
 __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
+    __shared__ uint32_t s_win[64 * kTbLaneWords];
+    uint8_t* const win = reinterpret_cast<uint8_t*>(s_win + threadIdx.x * kTbLaneWords);
+    uint8_t* const win1 = win + kTbFlagBytes;
+    uint8_t* const win2 = win1 + kTbSeqWin;
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     if (slot >= P.count) return;
     const uint32_t pidx = P.pair_base + slot;
@@ -38,6 +57,8 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
     const uint8_t* s2 = P.seq2 + o2;
     const bool tagged = P.tagged != 0;
     const Geom g = make_geom(ALG, R, P.max_m, P.max_n, tagged);
+    constexpr int BPC = bits_per_cell(ALG), BPS = R * BPC / 8, SPP = 16 / BPS;
+    static_assert(BPS <= 16 && (SPP & (SPP - 1)) == 0, "one packet per step record");
     const uint8_t* dir = P.dirs + (uint64_t)slot * P.dir_slot;
     uint8_t* ops = P.ops + o1 + o2 + pidx;
     const bool allow = P.allow != 0;
@@ -46,42 +67,105 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
     uint32_t k = 0;
     uint32_t flags = res.flags;
 
-    auto cell = [&](int i, int j) -> uint32_t {
-        int sh;
-        const uint64_t off = cell_byte(g, (uint32_t)i, (uint32_t)j, &sh);
-        return (uint32_t)(dir[off] >> sh);
+    // ---------------------------------------------------------------- windows
+    const uint32_t band_rows = (uint32_t)kWave * R;
+    int wb = -1, wt = 0, wg = 0;             // flag window: band, top lane, top step group
+    int w1 = -kTbSeqWin, w2 = -kTbSeqWin;    // sequence windows cover [w, w + kTbSeqWin)
+    int cb = 0, ct = 0, cgrp = 0, csub = 0, cr = 0;   // cell (i, j) decomposed by ready()
+    auto locate = [&](int i, int j) {
+        const uint32_t ii = (uint32_t)i - 1;
+        cb = (int)(ii / band_rows);
+        const uint32_t rem = ii - (uint32_t)cb * band_rows;
+        ct = (int)(rem / R);
+        cr = (int)(rem - (uint32_t)ct * R);
+        const int s = j - 1 + ct;
+        cgrp = s / SPP;               // s >= 0 whenever i, j > 0
+        csub = s % SPP;
+    };
+    // true when everything a move at (i, j) may read is in the windows
+    auto ready = [&](int i, int j) -> bool {
+        if (!(i > 0 && j > 0)) return true;
+        locate(i, j);
+        return cb == wb && (unsigned)(wt - ct) < (unsigned)kTbLanes && (unsigned)(wg - cgrp) < (unsigned)kTbGroups &&
+               (unsigned)(i - 1 - w1) < (unsigned)kTbSeqWin && (unsigned)(j - 1 - w2) < (unsigned)kTbSeqWin;
+    };
+    // one batch of independent loads re-anchors all three windows at (i, j)
+    auto refill = [&](int i, int j) {
+        if (!(i > 0 && j > 0)) return;       // edge moves read nothing (and (i-1) would wrap)
+        locate(i, j);
+        wb = cb; wt = ct; wg = cgrp;
+        w1 = (i - kTbSeqWin) < 0 ? 0 : i - kTbSeqWin;
+        w2 = (j - kTbSeqWin) < 0 ? 0 : j - kTbSeqWin;
+        const uint8_t* base = dir + (uint64_t)cb * g.band_stride;
+        // every load of the refill is issued before the first LDS store: one memory latency
+        uint4 v[kTbLanes][kTbGroups];
+#pragma unroll
+        for (int dl = 0; dl < kTbLanes; ++dl)
+#pragma unroll
+            for (int dg = 0; dg < kTbGroups; ++dg) {
+                const int lane = ct - dl, gg = cgrp - dg;
+                v[dl][dg] = (lane >= 0 && gg >= 0)
+                                ? *reinterpret_cast<const uint4*>(base + ((uint64_t)gg * kWave + lane) * 16)
+                                : make_uint4(0, 0, 0, 0);
+            }
+        uint8_t b1[kTbSeqWin], b2[kTbSeqWin];
+#pragma unroll
+        for (int q = 0; q < kTbSeqWin; ++q) {
+            b1[q] = (w1 + q < m) ? s1[w1 + q] : 0;
+            b2[q] = (w2 + q < n) ? s2[w2 + q] : 0;
+        }
+#pragma unroll
+        for (int dl = 0; dl < kTbLanes; ++dl)
+#pragma unroll
+            for (int dg = 0; dg < kTbGroups; ++dg) {
+                uint32_t* w = reinterpret_cast<uint32_t*>(win + (dl * kTbGroups + dg) * 16);
+                w[0] = v[dl][dg].x; w[1] = v[dl][dg].y; w[2] = v[dl][dg].z; w[3] = v[dl][dg].w;
+            }
+#pragma unroll
+        for (int q = 0; q < kTbSeqWin; ++q) { win1[q] = b1[q]; win2[q] = b2[q]; }
+    };
+    // flags of the cell located by the last ready() (which returned true)
+    auto cell = [&]() -> uint32_t {
+        int word, lowbit;
+        cell_word_bit(R, BPC, cr, &word, &lowbit, tagged);
+        const int byte = ((wt - ct) * kTbGroups + (wg - cgrp)) * 16 + csub * BPS + word * 4 + lowbit / 8;
+        return (uint32_t)(win[byte] >> (lowbit % 8));
     };
     // linear modes: flags fD (bit 1) / fU (bit 0); a T16 max tag (3 diag, 2 up, 1 left, 0 clamp)
     // says the same thing: diag wins iff H == D, else up iff H == U.
-    auto lin = [&](int i, int j) -> uint32_t {
-        const uint32_t f = cell(i, j) & 3u;
+    auto lin = [&]() -> uint32_t {
+        const uint32_t f = cell() & 3u;
         return tagged ? (f == 3u ? 2u : (f == 2u ? 1u : 0u)) : f;
     };
     // diagonal move: emits the op and returns the substitution term that was added
     auto diag = [&](int i, int j) -> int {
-        const bool v = tb_match<LUT>(P.lutbits, s1[i - 1], s2[j - 1]);
+        const bool v = tb_match<LUT>(P.lutbits, win1[i - 1 - w1], win2[j - 1 - w2]);
         ops[k++] = v ? 'M' : (allow ? 'S' : 'X');
         return v ? MA : MI;
     };
 
-    int i, j;
-    if constexpr (ALG == SA_SW) {
-        // flags: bit1 = fD (H == diag term), bit0 = fU (H == up term)
-        i = res.end_i; j = res.end_j;
-        int H = res.score;
-        if (m == 0 || n == 0) { i = 0; j = 0; }
-        while (i > 0 && j > 0) {
-            if (H == 0) break;        // diag test max(D,0) == H == 0 -> end of the local path
-            const uint32_t f = lin(i, j);
-            if (f & 2u) { H -= diag(i, j); --i; --j; }
-            else if (f & 1u) { ops[k++] = 'U'; H -= G; --i; }
-            else { ops[k++] = 'L'; H -= G; --j; }
-        }
-    } else if constexpr (ALG == SA_NW) {
+    // ---------------------------------------------------------------- walk state
+    int i, j, st = 0;
+    int V = 0;          // SW: H; LG: M, Ix or Iy of the current cell, by state
+    bool fin = false;
+    if constexpr (ALG == SA_SW || ALG == SA_LOCAL_GOTOH) {
+        i = res.end_i; j = res.end_j; V = res.score;
+        if (ALG == SA_SW && (m == 0 || n == 0)) { i = 0; j = 0; }
+    } else {
         i = m; j = n;
-        while (i > 0 || j > 0) {
+    }
+    // One iteration of the reference's traceback loop (sets fin when it would leave the loop).
+    auto move = [&]() {
+        if constexpr (ALG == SA_SW) {
+            if (!(i > 0 && j > 0) || V == 0) { fin = true; return; }   // H == 0: end of local path
+            const uint32_t f = lin();
+            if (f & 2u) { V -= diag(i, j); --i; --j; }
+            else if (f & 1u) { ops[k++] = 'U'; V -= G; --i; }
+            else { ops[k++] = 'L'; V -= G; --j; }
+        } else if constexpr (ALG == SA_NW) {
+            if (!(i > 0 || j > 0)) { fin = true; return; }
             if (i > 0 && j > 0) {
-                const uint32_t f = lin(i, j);
+                const uint32_t f = lin();
                 if (f & 2u) { diag(i, j); --i; --j; }
                 else if (f & 1u) { ops[k++] = 'U'; --i; }
                 else { ops[k++] = 'L'; --j; }
@@ -90,37 +174,30 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
             } else {
                 ops[k++] = 'L'; --j;
             }
-        }
-    } else if constexpr (ALG == SA_LOCAL_GOTOH) {
-        // flags: bit3 = fD (M == diag), bit2 = fX (M == Ix), bit1 = Ix extends, bit0 = Iy extends
-        i = res.end_i; j = res.end_j;
-        int st = 0;
-        int V = res.score;            // M, Ix or Iy of the current cell, by state
-        while (i > 0 && j > 0) {
-            const uint32_t f = cell(i, j);
+        } else if constexpr (ALG == SA_LOCAL_GOTOH) {
+            // flags: bit3 = fD (M == diag), bit2 = fX (M == Ix), bit1 = Ix extends, bit0 = Iy extends
+            if (!(i > 0 && j > 0)) { fin = true; return; }
+            const uint32_t f = cell();
             if (st == 0) {
-                if (V <= 0) break;    // M == max(D, 0) <= 0
+                if (V <= 0) { fin = true; return; }    // M == max(D, 0) <= 0
                 if (f & 8u) { V -= diag(i, j); --i; --j; }
-                else st = (f & 4u) ? 1 : 2;   // M == Ix, else M == Iy (same value)
+                else st = (f & 4u) ? 1 : 2;              // M == Ix, else M == Iy (same value)
             } else if (st == 1) {
                 if (f & 2u) { ops[k++] = 'U'; V -= GE; --i; }
                 else if (V > 0) { ops[k++] = 'U'; V -= GOE; --i; st = 0; }
-                else if (V == 0) { ops[k++] = 'u'; break; }
-                else { flags |= SA_FLAG_DIVERGED; break; }
+                else if (V == 0) { ops[k++] = 'u'; fin = true; }
+                else { flags |= SA_FLAG_DIVERGED; fin = true; }
             } else {
                 if (f & 1u) { ops[k++] = 'L'; V -= GE; --j; }
                 else if (V > 0) { ops[k++] = 'L'; V -= GOE; --j; st = 0; }
-                else if (V == 0) { ops[k++] = 'l'; break; }
-                else { flags |= SA_FLAG_DIVERGED; break; }
+                else if (V == 0) { ops[k++] = 'l'; fin = true; }
+                else { flags |= SA_FLAG_DIVERGED; fin = true; }
             }
-        }
-    } else {  // SA_GLOBAL_GOTOH
-        i = m; j = n;
-        int st = 0;
-        while (i > 0 || j > 0) {
-            if (j == 0) { ops[k++] = 'U'; --i; continue; }   // edge rules hold in any state
-            if (i == 0) { ops[k++] = 'L'; --j; continue; }
-            const uint32_t f = cell(i, j);
+        } else {  // SA_GLOBAL_GOTOH
+            if (!(i > 0 || j > 0)) { fin = true; return; }
+            if (j == 0) { ops[k++] = 'U'; --i; return; }   // edge rules hold in any state
+            if (i == 0) { ops[k++] = 'L'; --j; return; }
+            const uint32_t f = cell();
             if (st == 0) {
                 if (f & 8u) { diag(i, j); --i; --j; }
                 else st = (f & 4u) ? 1 : 2;
@@ -131,6 +208,21 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
                 ops[k++] = 'L'; --j;
                 if (!(f & 1u)) st = 0;
             }
+        }
+    };
+
+    // The 64 lanes of the wave walk 64 different pairs.  A lane whose next move would leave its
+    // windows parks; once every unfinished lane is parked they all refill together, so the wave
+    // pays one memory latency per round of ~kTbGroups*spp moves instead of one per move.
+    bool parked = true;
+    for (;;) {
+        if (__builtin_amdgcn_ballot_w64(!fin && !parked) == 0) {
+            if (__builtin_amdgcn_ballot_w64(!fin) == 0) break;
+            if (!fin) { refill(i, j); parked = false; }
+        }
+        if (!fin && !parked) {
+            if (ready(i, j)) move();
+            else parked = true;
         }
     }
     res.start_i = i;
