@@ -65,7 +65,13 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t
     Plan p;
     const bool aff = is_affine(algo);
     const int rmax = aff ? 16 : 16;
-    if (npairs >= 1024) {
+    if (npairs >= 1024 && t16) {
+        // Many pairs, T16: one wave per workgroup running its bands back to back (no pipeline
+        // skew between bands; hand-off through the row buffer), R up to 32 rows per lane.
+        p.W = 1;
+        p.R = 4;
+        while (p.R < 32 && (uint64_t)kWave * p.R < max_m) p.R *= 2;
+    } else if (npairs >= 1024) {
         // Many pairs: 4 waves (one band each when possible) per workgroup.
         p.W = 4;
         p.R = 4;
@@ -81,11 +87,13 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t
     // tuning override: SEQALIB_PLAN="R,W"
     if (const char* ov = getenv("SEQALIB_PLAN")) {
         int r = 0, w = 0;
-        if (sscanf(ov, "%d,%d", &r, &w) == 2 && (r == 4 || r == 8 || r == 16) && w >= 1 && w <= 16) {
+        if (sscanf(ov, "%d,%d", &r, &w) == 2 && (r == 4 || r == 8 || r == 16 || ((r == 32 || r == 64) && t16)) &&
+            w >= 1 && w <= 16) {
             p.R = r;
             p.W = w;
         }
     }
+    if (p.R >= 32 && p.W > 4) p.W = 4;   // fill_max_threads<32>
     // never more waves than bands
     const uint64_t bands = (max_m + (uint64_t)kWave * p.R - 1) / ((uint64_t)kWave * p.R);
     if ((uint64_t)p.W > bands) p.W = (int)std::max<uint64_t>(1, bands);

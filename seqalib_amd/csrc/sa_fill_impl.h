@@ -80,8 +80,12 @@ __device__ __forceinline__ bool match_bit(const uint32_t* s_lut, int a, int b) {
     }
 }
 
+// Max workgroup size: 16 waves, except R = 32 (T16 only) which needs > 128 VGPRs per lane.
+template <int R>
+constexpr int fill_max_threads() { return R >= 32 ? 256 : 1024; }
+
 template <int ALG, int R, bool LUT, bool ALLOW, bool KEYED, bool T16>
-__global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
+__global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams P) {
     constexpr bool AFF = ALG >= SA_LOCAL_GOTOH;
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
     constexpr int BPC = AFF ? 4 : 2;
@@ -94,7 +98,8 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
     constexpr int BAND = kWave * R;
     static_assert(kChunk % SPP == 0, "chunk must hold whole packets");
     static_assert(BPS >= 1, "record must be at least a byte");
-    static_assert(!T16 || (!AFF && ALLOW && !LUT && RB <= 32), "T16: linear, allow-mismatch, profile");
+    static_assert(!T16 || (!AFF && ALLOW && !LUT && (RB <= 32 || RB % 32 == 0)),
+                  "T16: linear, allow-mismatch, profile");
     static_assert(!T16 || !LOCAL || KEYED, "T16 local mode tracks its maximum with keys");
     constexpr int SC = T16 ? 4 : 1;            // score scale of the register values
 
@@ -197,47 +202,59 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
                     // block also forms the NEXT row's diagonal candidate from Hp[r] before
                     // updating Hp[r] in place, so no register copies are needed.
                     uint32_t t0, t1;
+                    // R >= 32: the row-max key update (lshl_or + max_u32, in place) joins the
+                    // block -- separate statements would cost s_nops and register renaming.
+                    constexpr bool KIN = LOCAL && R >= 32;
+                    const uint32_t jk = (uint32_t)jkey;
 #define SA_T16_HEAD                                                                          \
     "v_add_u16 %[t1], %[cu], %[hu]\n\t"                                                      \
     "v_max_i16 %[t0], %[dr], %[t1]\n\t"                                                      \
     "v_add_u16 %[t1], %[cl], %[hp]\n\t"                                                      \
     "v_max_i16 %[t0], %[t1], %[t0]\n\t"
-#define SA_T16_TAIL                                                                          \
-    "v_and_b32 %[hp], -4, %[t0]\n\t"                                                         \
-    "v_alignbit_b32 %[rec], %[t0], %[rec], 2"
+#define SA_T16_CLAMP "v_max_i16 %[t0], 0, %[t0]\n\t"
 #define SA_T16_NEXT                                                                          \
     "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\t"                                                \
     "v_add_u16 %[dn], %[hp], %[dn]\n\t"
-#define SA_T16_CLAMP "v_max_i16 %[t0], 0, %[t0]\n\t"
+#define SA_T16_TAIL                                                                          \
+    "v_and_b32 %[hp], -4, %[t0]\n\t"                                                         \
+    "v_alignbit_b32 %[rec], %[t0], %[rec], 2\n\t"
+#define SA_T16_KEY                                                                           \
+    "v_lshl_or_b32 %[t1], %[hp], 14, %[jk]\n\t"                                              \
+    "v_max_u32 %[bh], %[bh], %[t1]\n\t"
+#define SA_T16_OUT [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r]), [rec] "+v"(rw)
+#define SA_T16_IN [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL)
                     if (r + 1 < R) {
                         uint32_t dn;
-                        if constexpr (LOCAL)
+                        const uint32_t tabn = (uint32_t)a[r + 1 < R ? r + 1 : r];
+                        if constexpr (KIN)
+                            asm(SA_T16_HEAD SA_T16_CLAMP SA_T16_NEXT SA_T16_TAIL SA_T16_KEY
+                                : SA_T16_OUT, [dn] "=&v"(dn), [bh] "+v"(bh[r])
+                                : SA_T16_IN, [tabn] "v"(tabn), [sym] "v"(sym), [jk] "v"(jk));
+                        else if constexpr (LOCAL)
                             asm(SA_T16_HEAD SA_T16_CLAMP SA_T16_NEXT SA_T16_TAIL
-                                : [t0] "=&v"(t0), [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r]),
-                                  [rec] "+v"(rw)
-                                : [dr] "v"(dcur), [hu] "v"(hu), [tabn] "v"(a[r + 1 < R ? r + 1 : r]),
-                                  [sym] "v"(sym), [cu] "s"(CU), [cl] "s"(CL));
+                                : SA_T16_OUT, [dn] "=&v"(dn)
+                                : SA_T16_IN, [tabn] "v"(tabn), [sym] "v"(sym));
                         else
                             asm(SA_T16_HEAD SA_T16_NEXT SA_T16_TAIL
-                                : [t0] "=&v"(t0), [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r]),
-                                  [rec] "+v"(rw)
-                                : [dr] "v"(dcur), [hu] "v"(hu), [tabn] "v"(a[r + 1 < R ? r + 1 : r]),
-                                  [sym] "v"(sym), [cu] "s"(CU), [cl] "s"(CL));
+                                : SA_T16_OUT, [dn] "=&v"(dn)
+                                : SA_T16_IN, [tabn] "v"(tabn), [sym] "v"(sym));
                         dcur = dn;
                     } else {
-                        if constexpr (LOCAL)
-                            asm(SA_T16_HEAD SA_T16_CLAMP SA_T16_TAIL
-                                : [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r]), [rec] "+v"(rw)
-                                : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL));
+                        if constexpr (KIN)
+                            asm(SA_T16_HEAD SA_T16_CLAMP SA_T16_TAIL SA_T16_KEY
+                                : SA_T16_OUT, [bh] "+v"(bh[r]) : SA_T16_IN, [jk] "v"(jk));
+                        else if constexpr (LOCAL)
+                            asm(SA_T16_HEAD SA_T16_CLAMP SA_T16_TAIL : SA_T16_OUT : SA_T16_IN);
                         else
-                            asm(SA_T16_HEAD SA_T16_TAIL
-                                : [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r]), [rec] "+v"(rw)
-                                : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL));
+                            asm(SA_T16_HEAD SA_T16_TAIL : SA_T16_OUT : SA_T16_IN);
                     }
 #undef SA_T16_HEAD
 #undef SA_T16_TAIL
 #undef SA_T16_NEXT
 #undef SA_T16_CLAMP
+#undef SA_T16_KEY
+#undef SA_T16_OUT
+#undef SA_T16_IN
                     Hc = Hp[r];
                 } else {
                 const bool v = match_bit<LUT>(s_lut, a[r], sym);
@@ -269,7 +286,9 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
                 }
                 }
                 if constexpr (LOCAL) {
-                    if constexpr (T16 && STEADY) {
+                    if constexpr (T16 && R >= 32) {
+                        // key already folded in by the cell's asm block
+                    } else if constexpr (T16 && STEADY) {
                         // Hc = 4H with clear tag bits, so Hc << 14 == H << 16.  Two steps' keys
                         // per v_max3, in place (lets the compiler keep bh[] in fixed registers).
                         const uint32_t k = ((uint32_t)Hc << 14) | (uint32_t)jkey;
@@ -303,7 +322,7 @@ __global__ __launch_bounds__(1024) void fill_kernel(FillParams P) {
             uint32_t pk[4 * PPS];
 #pragma unroll
             for (int e = 0; e < 4 * PPS; ++e) pk[e] = 0;
-            static_assert(SPP % 2 == 0, "steps pair up for the key max3");
+            static_assert(SPP % 2 == 0 || !T16 || R >= 32, "steps pair up for the key max3");
 #pragma unroll
             for (int g = 0; g < SPP; ++g) {
                 const int q = q0 + g;
@@ -500,6 +519,8 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
     if constexpr (ALG == SA_SW || ALG == SA_NW) {
         if (v.t16) {
             if (!allow || (LOCAL && !keyed)) return hipErrorInvalidValue;
+            if ((int)block.x > (R >= 32 ? fill_max_threads<32>() : fill_max_threads<16>()))
+                return hipErrorInvalidConfiguration;
 #define SA_LAUNCH16(RR)                                                                              \
     if (R == RR) {                                                                                   \
         hipLaunchKernelGGL((fill_kernel<ALG, RR, false, true, LOCAL, true>), dim3(grid), block, lds, \
@@ -509,6 +530,8 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
             SA_LAUNCH16(4)
             SA_LAUNCH16(8)
             SA_LAUNCH16(16)
+            SA_LAUNCH16(32)
+            SA_LAUNCH16(64)
 #undef SA_LAUNCH16
             return hipErrorInvalidValue;
         }

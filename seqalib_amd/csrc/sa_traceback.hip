@@ -16,8 +16,8 @@
 // Memory: a walk is a chain of dependent reads, one cell per move, and a 4k x 4k local path is
 // ~5k moves long, so per-move HBM latency would dominate.  Each lane therefore keeps private LDS
 // windows that one batch of independent loads refills:
-//   flags: lanes {t, t-1} x step groups {G .. G-7} of its band (16-byte packets, sa_layout.h)
-//          -- a walk only moves to smaller steps s = j-1+t and smaller lanes t;
+//   flags: ~32 rows x 32 steps: lanes {t, t-1, ..} x step groups {G, G-1, ..} of its band
+//          (16-byte packets, sa_layout.h) -- a walk only moves to smaller s = j-1+t and t;
 //   Seq1 / Seq2: the 32 bytes below the current row / column.
 // and refills are batched across the wave (see the round loop at the end of the kernel).
 #include <limits.h>
@@ -32,15 +32,20 @@ __device__ __forceinline__ bool tb_match(const uint32_t* lut, uint8_t a, uint8_t
     else return a == b;
 }
 
-constexpr int kTbLanes = 2;                   // lanes {t, t-1} per flag window
-constexpr int kTbGroups = 8;                  // step groups {G .. G-7} per flag window
+// Flag window ~32 rows x 32 steps whatever the geometry: max(1, 32/R) lanes x 32/SPP groups.
 constexpr int kTbSeqWin = 32;                 // bytes per sequence window
-constexpr int kTbFlagBytes = kTbLanes * kTbGroups * 16;
-constexpr int kTbLaneWords = (kTbFlagBytes + 2 * kTbSeqWin) / 4 + 1;   // odd: conflict-free LDS
+constexpr int kTbMaxFlagBytes = 512;          // 128 * bits per cell
+constexpr int kTbLaneWords = (kTbMaxFlagBytes + 2 * kTbSeqWin) / 4 + 1;   // odd: conflict-free LDS
 static_assert(kTbLaneWords % 2 == 1, "per-lane LDS stride must be odd in words");
 
 template <int ALG, int R, bool LUT>
 __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
+    constexpr int BPC = bits_per_cell(ALG), BPS = R * BPC / 8, SPP = 16 / BPS;
+    static_assert(BPS <= 16 && (SPP & (SPP - 1)) == 0, "one packet per step record");
+    constexpr int kTbLanes = R >= 32 ? 1 : 32 / R;
+    constexpr int kTbGroups = 32 / SPP;
+    constexpr int kTbFlagBytes = kTbLanes * kTbGroups * 16;
+    static_assert(kTbFlagBytes <= kTbMaxFlagBytes, "flag window");
     __shared__ uint32_t s_win[64 * kTbLaneWords];
     uint8_t* const win = reinterpret_cast<uint8_t*>(s_win + threadIdx.x * kTbLaneWords);
     uint8_t* const win1 = win + kTbFlagBytes;
@@ -57,8 +62,6 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
     const uint8_t* s2 = P.seq2 + o2;
     const bool tagged = P.tagged != 0;
     const Geom g = make_geom(ALG, R, P.max_m, P.max_n, tagged);
-    constexpr int BPC = bits_per_cell(ALG), BPS = R * BPC / 8, SPP = 16 / BPS;
-    static_assert(BPS <= 16 && (SPP & (SPP - 1)) == 0, "one packet per step record");
     const uint8_t* dir = P.dirs + (uint64_t)slot * P.dir_slot;
     uint8_t* ops = P.ops + o1 + o2 + pidx;
     const bool allow = P.allow != 0;
@@ -244,6 +247,8 @@ hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStr
                     SA_TB(AA, 4, true) SA_TB(AA, 8, true) SA_TB(AA, 16, true)
     SA_TB_A(SA_SW)
     SA_TB_A(SA_NW)
+    SA_TB(SA_SW, 32, false) SA_TB(SA_SW, 32, true) SA_TB(SA_NW, 32, false) SA_TB(SA_NW, 32, true)
+    SA_TB(SA_SW, 64, false) SA_TB(SA_SW, 64, true) SA_TB(SA_NW, 64, false) SA_TB(SA_NW, 64, true)
     SA_TB_A(SA_LOCAL_GOTOH)
     SA_TB_A(SA_GLOBAL_GOTOH)
 #undef SA_TB_A
