@@ -216,14 +216,15 @@ def main():
         return
     per_launch_cells = cells_rank  # one fill launch covers the whole batch when it fits HBM
     fill_s = fill_ms / 1e3 / max(launches, 1)
-    t16 = kernel == sa.SA_KERNEL_T16
-    label = f"sw_{'t16' if t16 else 'int32'}_r{plan_R}"
+    t16 = kernel in (sa.SA_KERNEL_T16, sa.SA_KERNEL_T16_ENDCELL)
+    endcell = kernel == sa.SA_KERNEL_T16_ENDCELL
+    label = f"sw_{'t16c' if endcell else 't16' if t16 else 'int32'}_r{plan_R}"
     model = issue_model(label)
     fill_gcups = per_launch_cells / fill_s / 1e9
     hbm_gbps = per_launch_cells * SW_FLAG_BYTES_PER_CELL / fill_s / 1e9
     traffic = load_pmc_traffic(workload)
     kname = (f"fill_kernel<SW,R={plan_R},W={plan_W}," + ("T16 tagged int16 profile" if t16 else "int32 flags")
-             + ",KEYED>")
+             + (",chunk-max end cell>" if endcell else ",KEYED>"))
     if model:
         vpc = model["valu_per_cell"]
         roof = {"bound": "valu", "achieved": round(fill_gcups * vpc / 1e3, 2),

@@ -140,6 +140,7 @@ int sa_last_timings(sa_ctx* ctx, float* fill_ms, float* traceback_ms, int* fill_
  * Environment: SEQALIB_T16=0 forces the int32 kernel. */
 #define SA_KERNEL_INT32 0
 #define SA_KERNEL_T16 1
+#define SA_KERNEL_T16_ENDCELL 2   /* T16 SW with per-chunk maxima + end-cell replay */
 int sa_last_plan(sa_ctx* ctx, int* kernel, int* rows_per_lane, int* waves);
 
 /* Kernel plan the engine would use for a batch (host-only query, no device needed):

@@ -36,7 +36,7 @@ __all__ = [
 SA_SW, SA_NW, SA_LOCAL_GOTOH, SA_GLOBAL_GOTOH = 0, 1, 2, 3
 ALGO_NAMES = {SA_SW: "sw", SA_NW: "nw", SA_LOCAL_GOTOH: "local_gotoh", SA_GLOBAL_GOTOH: "global_gotoh"}
 SA_FLAG_DIVERGED, SA_FLAG_BAD_SHAPE, SA_FLAG_SIZE_HACK = 1, 2, 4
-SA_KERNEL_INT32, SA_KERNEL_T16 = 0, 1
+SA_KERNEL_INT32, SA_KERNEL_T16, SA_KERNEL_T16_ENDCELL = 0, 1, 2
 INT32_MIN = -(2 ** 31)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))

@@ -226,11 +226,22 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             SA_HIP(c, launch_build_profile(d_lutbits, sym_pack, sc->match, sc->mismatch, c->aux + 8, stream));
         }
     }
-    const Plan pl = make_plan(algo, max_m, max_n, npairs, t16);
-    c->last_kernel = t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
+    Plan pl = make_plan(algo, max_m, max_n, npairs, t16);
+    // CMAX end-cell tracking (sa_fill_impl.h / sa_endcell.hip): T16 SW on one-wave plans
+    bool cmax = t16 && algo == SA_SW && pl.W == 1 && pl.R >= 4;
+    if (const char* ec = getenv("SEQALIB_CMAX")) if (ec[0] == '0') cmax = false;
+    uint32_t snap_nch = 0;
+    uint64_t snap_h_slot = 0, snap_p_slot = 0;
+    if (cmax) {
+        snap_nch = chunks_per_band(max_n);
+        snap_p_slot = (uint64_t)pl.g.bands * snap_nch * kWave;
+        snap_h_slot = snap_p_slot * (pl.R / 2);
+        pl.rowbuf_elems = (uint64_t)pl.g.bands * std::max<uint32_t>(max_n, 1);
+    }
+    c->last_kernel = cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
     c->last_R = pl.R;
     c->last_W = pl.W;
-    const uint64_t slot_bytes = pl.g.dir_slot + pl.rowbuf_elems * 4;
+    const uint64_t slot_bytes = pl.g.dir_slot + pl.rowbuf_elems * 4 + (snap_h_slot + snap_p_slot) * 4;
     const uint64_t budget = ws_budget(c);
     uint64_t per_launch = slot_bytes ? std::max<uint64_t>(1, budget / std::max<uint64_t>(slot_bytes, 1)) : npairs;
     per_launch = std::min<uint64_t>(per_launch, npairs ? npairs : 1);
@@ -243,6 +254,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     if (rc) return rc;
     uint8_t* dirs = c->ws;
     int32_t* rowbuf = reinterpret_cast<int32_t*>(c->ws + per_launch * pl.g.dir_slot);
+    uint32_t* snap_h = reinterpret_cast<uint32_t*>(rowbuf + per_launch * pl.rowbuf_elems);
+    int32_t* snap_p = reinterpret_cast<int32_t*>(snap_h + per_launch * snap_h_slot);
 
     // reset timing
     c->launches = 0;
@@ -264,6 +277,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         fp.stage_seq2 = max_n <= kMaxStagedSeq2 ? 1 : 0;
         fp.prof = c->aux + 8;
         fp.sym_pack = sym_pack;
+        fp.snap_h = snap_h; fp.snap_p = snap_p;
+        fp.snap_h_slot = snap_h_slot; fp.snap_p_slot = snap_p_slot; fp.snap_nch = snap_nch;
 
         TbParams tp;
         tp.seq1 = d1; tp.off1 = o1; tp.seq2 = d2; tp.off2 = o2;
@@ -284,9 +299,21 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         }
         hipEvent_t* ev = &c->events[3 * c->launches];
         SA_HIP(c, hipEventRecord(ev[0], stream));
-        const FillVariant fv = {pl.R, lut, allow, keyed, t16};
+        const FillVariant fv = {pl.R, lut, allow, keyed, t16, cmax};
         hipError_t e = launch_fill(algo, fv, fp, cnt, stream);
         if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
+        if (cmax) {
+            EndcellParams ep;
+            ep.seq1 = d1; ep.off1 = o1; ep.seq2 = d2; ep.off2 = o2;
+            ep.prof = fp.prof; ep.sym_pack = sym_pack;
+            ep.snap_h = snap_h; ep.snap_p = snap_p;
+            ep.snap_h_slot = snap_h_slot; ep.snap_p_slot = snap_p_slot; ep.snap_nch = snap_nch;
+            ep.rowbuf = rowbuf; ep.rowbuf_slot = pl.rowbuf_elems; ep.max_n = max_n;
+            ep.res = d_res; ep.pair_base = (uint32_t)base; ep.count = cnt;
+            ep.gap = sc->gap;
+            e = launch_endcell(pl.R, ep, stream);
+            if (e != hipSuccess) return hip_fail(c, e, "end-cell kernel launch");
+        }
         SA_HIP(c, hipEventRecord(ev[1], stream));
         e = launch_traceback(algo, pl.R, lut, tp, stream);
         if (e != hipSuccess) return hip_fail(c, e, "traceback kernel launch");

@@ -1,0 +1,113 @@
+// sa_endcell.hip — exact end cell (MaxRow, MaxCol) after a CMAX fill (sa_fill_impl.h).
+//
+// The reference keeps the LAST row-major maximum of the score matrix (SASmithWaterman.h:110:
+// Score >= MaxScore inside the i-then-j loops).  A CMAX fill reports, per pair, the maximum
+// score S, the largest row i holding it, and the last 32-step chunk c of i's band in which row i
+// reached S.  This kernel replays that one chunk of that band from the snapshot the fill stored
+// at the end of chunk c-1 (every lane's R row values and its diagonal input; the band's top row
+// comes from the per-band row buffer) and keeps the last column of row i whose value equals S.
+// The replay repeats the fill's recurrence and its wavefront order exactly (lane t computes
+// column s - t at step s; the row above comes from lane t-1's previous step), in int32 on the
+// unscaled scores, so it yields the same cell values the fill produced.
+//
+// One wave per pair; 32 steps x R rows per lane: ~0.05% of the fill's work at 4096 x 4096.
+#include "sa_internal.h"
+
+namespace sa {
+
+__device__ __forceinline__ uint32_t ec_code8(uint32_t sp, uint32_t b) {
+    return (b == ((sp >> 8) & 255u) ? 8u : 0u) | (b == ((sp >> 16) & 255u) ? 16u : 0u) |
+           (b == (sp >> 24) ? 24u : 0u);
+}
+
+template <int R>
+__global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
+    const int lane = threadIdx.x;
+    const uint32_t slot = blockIdx.x;
+    if (slot >= P.count) return;
+    const uint32_t pidx = P.pair_base + slot;
+    sa_result res = P.res[pidx];
+    if (res.reserved == 0 || (res.flags & SA_FLAG_BAD_SHAPE)) return;   // uniform over the wave
+    const int c = (int)res.reserved - 1;
+    const int S = res.score;
+    const int iend = res.end_i;
+    const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
+    const int m = (int)(P.off1[pidx + 1] - o1);
+    const int n = (int)(P.off2[pidx + 1] - o2);
+    const uint8_t* s1 = P.seq1 + o1;
+    const uint8_t* s2 = P.seq2 + o2;
+    constexpr int BAND = kWave * R;
+    const int b = (iend - 1) / BAND;
+    const int tstar = ((iend - 1) % BAND) / R;
+    const int rstar = (iend - 1) % R;
+    const int row0 = b * BAND + lane * R;
+    const int G = P.gap;
+
+    uint32_t tab[R];
+    int Hp[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int row = row0 + r;
+        tab[r] = row < m ? P.prof[ec_code8(P.sym_pack, s1[row]) >> 3] : 0u;
+        Hp[r] = 0;
+    }
+    int prev_up = 0;
+    if (c > 0) {
+        const uint64_t e = (uint64_t)b * P.snap_nch + (c - 1);
+        const uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + (e * kWave + lane) * (R / 2);
+#pragma unroll
+        for (int q = 0; q < R / 2; ++q) {
+            const uint32_t w = sh[q];
+            Hp[2 * q] = (int)(w & 0xffffu) >> 2;        // stored as 4H (non-negative)
+            Hp[2 * q + 1] = (int)(w >> 16) >> 2;
+        }
+        prev_up = P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] >> 2;
+    }
+    int hl = Hp[R - 1];
+    const int32_t* top = b > 0 ? P.rowbuf + (uint64_t)slot * P.rowbuf_slot + (uint64_t)(b - 1) * P.max_n : nullptr;
+    int jbest = -1;
+    for (int q = 0; q < kChunk; ++q) {
+        const int s = c * kChunk + q;
+        const int j0 = s - lane;
+        int up_h = __shfl_up(hl, 1);
+        if (lane == 0) up_h = (top && s < n) ? (top[s] >> 2) : 0;
+        if (j0 >= 0 && j0 < n) {
+            const uint32_t sym = ec_code8(P.sym_pack, s2[j0]);
+            int hd = prev_up, hu = up_h;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                // profile byte = 4s+3 (signed); the builtin returns unsigned: shift as int
+                const int sub = ((int)__builtin_amdgcn_sbfe(tab[r], sym, 8) - 3) >> 2;
+                int H = hd + sub;
+                H = max(H, hu + G);
+                H = max(H, Hp[r] + G);
+                H = max(H, 0);
+                hd = Hp[r];
+                Hp[r] = H;
+                hu = H;
+                if (lane == tstar && r == rstar && H == S) jbest = j0;
+            }
+            prev_up = up_h;
+            hl = Hp[R - 1];
+        }
+    }
+    if (lane == tstar) {
+        res.end_j = jbest + 1;   // 1-based; jbest >= 0 whenever the fill's report is consistent
+        res.reserved = 0;
+        P.res[pidx] = res;
+    }
+}
+
+hipError_t launch_endcell(int R, const EndcellParams& p, hipStream_t stream) {
+    const dim3 grid(p.count), block(64);
+    switch (R) {
+        case 4: hipLaunchKernelGGL(endcell_kernel<4>, grid, block, 0, stream, p); break;
+        case 8: hipLaunchKernelGGL(endcell_kernel<8>, grid, block, 0, stream, p); break;
+        case 16: hipLaunchKernelGGL(endcell_kernel<16>, grid, block, 0, stream, p); break;
+        case 32: hipLaunchKernelGGL(endcell_kernel<32>, grid, block, 0, stream, p); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace sa

@@ -37,6 +37,12 @@
 //   * the tag is pushed into the record with one v_alignbit_b32 (rec = rec >> 2 | T << 30) and
 //     stripped from the value with one v_and_b32.
 // Cell = bfe + 3 add_u16 + 2-3 max_i16 + and + alignbit (+ lshl_or + max_u32 for the key).
+//
+// CMAX (T16 SW, one-wave plans): instead of a (score, column) key per cell, each row keeps its
+// maximum over the current 32-step chunk with one more v_max_i16 (fast class); at the chunk end
+// the row's (max, chunk) pair joins its key and the lane stores a snapshot of its state (R
+// 16-bit values + the diagonal input), and each band's top row is kept.  The fill then reports
+// (score, row, chunk) and sa_endcell.hip replays that one chunk to find the exact column.
 #pragma once
 #include <limits.h>
 
@@ -84,7 +90,7 @@ __device__ __forceinline__ bool match_bit(const uint32_t* s_lut, int a, int b) {
 template <int R>
 constexpr int fill_max_threads() { return R >= 32 ? 256 : 1024; }
 
-template <int ALG, int R, bool LUT, bool ALLOW, bool KEYED, bool T16>
+template <int ALG, int R, bool LUT, bool ALLOW, bool KEYED, bool T16, bool CMAX>
 __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams P) {
     constexpr bool AFF = ALG >= SA_LOCAL_GOTOH;
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
@@ -102,6 +108,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                   "T16: linear, allow-mismatch, profile");
     static_assert(!T16 || !LOCAL || KEYED, "T16 local mode tracks its maximum with keys");
     constexpr int SC = T16 ? 4 : 1;            // score scale of the register values
+    static_assert(!CMAX || (T16 && ALG == SA_SW && R % 2 == 0), "CMAX: T16 Smith-Waterman");
 
     // Dynamic LDS (sizes from lds_layout(), host and device agree):
     //   [match bits: 2048 words, LUT only][hand-off rings: W x kRing x (1|2) ints][Seq2 bytes, staged]
@@ -154,6 +161,8 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     uint8_t* const dslot = P.dirs + (uint64_t)slot * P.dir_slot;
     int32_t* const rb_h = P.rowbuf + (uint64_t)slot * P.rowbuf_slot;
     int32_t* const rb_x = rb_h + P.max_n;
+    // CMAX keeps every band's top row (row buffer = bands x max_n); otherwise one row is reused
+    const uint64_t rbs = CMAX ? P.max_n : 0;
 
     // Per-lane state for the current band.
     int a[R];      // Seq1 symbols of my rows
@@ -161,12 +170,13 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     int Yp[R];     // Iy of my rows at the previous column (affine)
     int bh[R];     // best per row: key (KEYED) or score
     int bj[R];     // its column (0-based), !KEYED
+    uint32_t cm[R];  // CMAX: per-row max over the current chunk (int16, 0x8000 = none)
     int hl = 0, xl = 0, sym = 0, prev_up = 0;
     int row0 = 0;
     // Running best of this lane over its bands: (score, i, j), 1-based cell.
     int best_h = INT_MIN, best_i = 0, best_j = 0;
 #pragma unroll
-    for (int r = 0; r < R; ++r) { a[r] = 0; Hp[r] = 0; Yp[r] = 0; bh[r] = 0; bj[r] = 0; }
+    for (int r = 0; r < R; ++r) { a[r] = 0; Hp[r] = 0; Yp[r] = 0; bh[r] = 0; bj[r] = 0; cm[r] = 0x8000u; }
 
     // One step: lane computes column j = s - lane for its R rows.  STEADY: every lane is in
     // range, no exec-mask branch.  Returns the packed record words in rec.
@@ -204,7 +214,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                     uint32_t t0, t1;
                     // R >= 32: the row-max key update (lshl_or + max_u32, in place) joins the
                     // block -- separate statements would cost s_nops and register renaming.
-                    constexpr bool KIN = LOCAL && R >= 32;
+                    constexpr bool KIN = LOCAL && R >= 32 && !CMAX;
                     const uint32_t jk = (uint32_t)jkey;
 #define SA_T16_HEAD                                                                          \
     "v_add_u16 %[t1], %[cu], %[hu]\n\t"                                                      \
@@ -223,10 +233,15 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     "v_max_u32 %[bh], %[bh], %[t1]\n\t"
 #define SA_T16_OUT [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r]), [rec] "+v"(rw)
 #define SA_T16_IN [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL)
+#define SA_T16_CM "v_max_i16 %[cm], %[cm], %[hp]\n\t"
                     if (r + 1 < R) {
                         uint32_t dn;
                         const uint32_t tabn = (uint32_t)a[r + 1 < R ? r + 1 : r];
-                        if constexpr (KIN)
+                        if constexpr (CMAX)
+                            asm(SA_T16_HEAD SA_T16_CLAMP SA_T16_NEXT SA_T16_TAIL SA_T16_CM
+                                : SA_T16_OUT, [dn] "=&v"(dn), [cm] "+v"(cm[r])
+                                : SA_T16_IN, [tabn] "v"(tabn), [sym] "v"(sym));
+                        else if constexpr (KIN)
                             asm(SA_T16_HEAD SA_T16_CLAMP SA_T16_NEXT SA_T16_TAIL SA_T16_KEY
                                 : SA_T16_OUT, [dn] "=&v"(dn), [bh] "+v"(bh[r])
                                 : SA_T16_IN, [tabn] "v"(tabn), [sym] "v"(sym), [jk] "v"(jk));
@@ -240,7 +255,10 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                                 : SA_T16_IN, [tabn] "v"(tabn), [sym] "v"(sym));
                         dcur = dn;
                     } else {
-                        if constexpr (KIN)
+                        if constexpr (CMAX)
+                            asm(SA_T16_HEAD SA_T16_CLAMP SA_T16_TAIL SA_T16_CM
+                                : SA_T16_OUT, [cm] "+v"(cm[r]) : SA_T16_IN);
+                        else if constexpr (KIN)
                             asm(SA_T16_HEAD SA_T16_CLAMP SA_T16_TAIL SA_T16_KEY
                                 : SA_T16_OUT, [bh] "+v"(bh[r]) : SA_T16_IN, [jk] "v"(jk));
                         else if constexpr (LOCAL)
@@ -248,6 +266,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                         else
                             asm(SA_T16_HEAD SA_T16_TAIL : SA_T16_OUT : SA_T16_IN);
                     }
+#undef SA_T16_CM
 #undef SA_T16_HEAD
 #undef SA_T16_TAIL
 #undef SA_T16_NEXT
@@ -286,8 +305,8 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 }
                 }
                 if constexpr (LOCAL) {
-                    if constexpr (T16 && R >= 32) {
-                        // key already folded in by the cell's asm block
+                    if constexpr (CMAX || (T16 && R >= 32)) {
+                        // chunk max / key already updated by the cell's asm block
                     } else if constexpr (T16 && STEADY) {
                         // Hc = 4H with clear tag bits, so Hc << 14 == H << 16.  Two steps' keys
                         // per v_max3, in place (lets the compiler keep bh[] in fixed registers).
@@ -377,7 +396,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 vh = ring(band % W, 0)[c % kRing];
                 if constexpr (AFF) vx = ring(band % W, 1)[c % kRing];
             } else {
-                vh = rb_h[c];
+                vh = rb_h[(uint64_t)(band - 1) * rbs + c];
                 if constexpr (AFF) vx = rb_x[c];
             }
         }
@@ -404,6 +423,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                         else Hp[r] = 0;
                         Yp[r] = -10000;
                         bh[r] = KEYED ? 0 : INT_MIN;
+                        cm[r] = 0x8000u;
                         bj[r] = 0;
                     }
                     if constexpr (ALG == SA_NW) prev_up = SC * row0 * G;
@@ -427,9 +447,27 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                             ring(nw, 0)[cc % kRing] = acc_h;
                             if constexpr (AFF) ring(nw, 1)[cc % kRing] = acc_x;
                         } else {
-                            rb_h[cc] = acc_h;
+                            rb_h[(uint64_t)band * rbs + cc] = acc_h;
                             if constexpr (AFF) rb_x[cc] = acc_x;
                         }
+                    }
+                }
+                // ------------------------------------------------ CMAX: chunk maxima, snapshot
+                if constexpr (CMAX) {
+                    const uint32_t ck = chunk + 1;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int v = (int)(int16_t)(cm[r] & 0xffffu);   // 4H, or -32768 = none
+                        if (v >= 0) bh[r] = (int)max((uint32_t)bh[r], ((uint32_t)v << 14) | ck);
+                        cm[r] = 0x8000u;
+                    }
+                    if (chunk + 1 < nch) {   // state entering chunk + 1, for the end-cell replay
+                        const uint64_t e = (uint64_t)band * P.snap_nch + chunk;
+                        uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + (e * kWave + lane) * (R / 2);
+#pragma unroll
+                        for (int q = 0; q < R / 2; ++q)
+                            sh[q] = ((uint32_t)Hp[2 * q] & 0xffffu) | ((uint32_t)Hp[2 * q + 1] << 16);
+                        P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = prev_up;
                     }
                 }
                 // ---------------------------------------------------------------- band end
@@ -438,7 +476,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
 #pragma unroll
                         for (int r = 0; r < R; ++r) {
                             int h, jj;
-                            if constexpr (KEYED) { h = (int)((uint32_t)bh[r] >> 16); jj = bh[r] & 0xffff; }
+                            if constexpr (KEYED || CMAX) { h = (int)((uint32_t)bh[r] >> 16); jj = bh[r] & 0xffff; }
                             else { h = bh[r]; jj = bj[r] + 1; }
                             if (row0 + r < m && h >= best_h) {
                                 best_h = h;
@@ -486,6 +524,9 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 // empty input: SW keeps MaxScore = INT_MIN, (MaxRow, MaxCol) = (0, 0);
                 // LocalGotoh reads M[0][0] = 0 there
                 r.score = (ALG == SA_SW) ? INT_MIN : 0;
+            } else if constexpr (CMAX) {
+                r.score = h; r.end_i = bi; r.end_j = 0;
+                r.reserved = (uint32_t)bjj;   // chunk + 1: sa_endcell.hip resolves the column
             } else {
                 r.score = h; r.end_i = bi; r.end_j = bjj;
             }
@@ -523,8 +564,15 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
                 return hipErrorInvalidConfiguration;
 #define SA_LAUNCH16(RR)                                                                              \
     if (R == RR) {                                                                                   \
-        hipLaunchKernelGGL((fill_kernel<ALG, RR, false, true, LOCAL, true>), dim3(grid), block, lds, \
-                           stream, p);                                                               \
+        if constexpr (ALG == SA_SW) {                                                                \
+            if (v.cmax) {                                                                            \
+                hipLaunchKernelGGL((fill_kernel<ALG, RR, false, true, LOCAL, true, true>), dim3(grid), \
+                                   block, lds, stream, p);                                           \
+                return hipGetLastError();                                                            \
+            }                                                                                        \
+        }                                                                                            \
+        hipLaunchKernelGGL((fill_kernel<ALG, RR, false, true, LOCAL, true, false>), dim3(grid), block, \
+                           lds, stream, p);                                                          \
         return hipGetLastError();                                                                    \
     }
             SA_LAUNCH16(4)
@@ -536,10 +584,10 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
             return hipErrorInvalidValue;
         }
     }
-    if (v.t16) return hipErrorInvalidValue;
+    if (v.t16 || v.cmax) return hipErrorInvalidValue;
 #define SA_LAUNCH(RR, LL, AA, KK)                                                              \
     if (R == RR && lut == LL && allow == AA && keyed == KK) {                                  \
-        hipLaunchKernelGGL((fill_kernel<ALG, RR, LL, AA, KK, false>), dim3(grid), block, lds, stream, p); \
+        hipLaunchKernelGGL((fill_kernel<ALG, RR, LL, AA, KK, false, false>), dim3(grid), block, lds, stream, p); \
         return hipGetLastError();                                                              \
     }
 #define SA_LAUNCH_K(RR, LL, AA) \

@@ -29,6 +29,32 @@ struct FillParams {
     // prof[c] holds, in byte c', the tagged substitution term 4*s(sym c, sym c') + 3 as int8.
     const uint32_t* prof;
     uint32_t sym_pack;
+    // CMAX only (see sa_fill_impl.h): per-slot snapshots [band][chunk][lane] of the R 16-bit row
+    // values (R/2 words) and of the diagonal input (1 word); snap_nch = chunks per band.
+    uint32_t* snap_h;
+    int32_t* snap_p;
+    uint64_t snap_h_slot, snap_p_slot;
+    uint32_t snap_nch;
+};
+
+// End-cell replay (sa_endcell.hip) after a CMAX fill: res.reserved = chunk + 1 of the maximum.
+struct EndcellParams {
+    const uint8_t* seq1;
+    const uint64_t* off1;
+    const uint8_t* seq2;
+    const uint64_t* off2;
+    const uint32_t* prof;
+    uint32_t sym_pack;
+    const uint32_t* snap_h;
+    const int32_t* snap_p;
+    uint64_t snap_h_slot, snap_p_slot;
+    uint32_t snap_nch;
+    const int32_t* rowbuf;
+    uint64_t rowbuf_slot;
+    uint32_t max_n;
+    sa_result* res;
+    uint32_t pair_base, count;
+    int32_t gap;
 };
 
 struct TbParams {
@@ -53,7 +79,7 @@ struct TbParams {
 // Returns hipSuccess or the launch error.
 struct FillVariant {
     int R;
-    bool lut, allow, keyed, t16;
+    bool lut, allow, keyed, t16, cmax;
 };
 hipError_t launch_fill(int algo, const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream);
 hipError_t launch_fill_sw(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
@@ -67,5 +93,6 @@ hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uin
 hipError_t launch_build_profile(const uint32_t* lutbits, uint32_t sym_pack, int match, int mismatch,
                                 uint32_t* prof, hipStream_t s);
 hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
+hipError_t launch_endcell(int R, const EndcellParams& p, hipStream_t stream);
 
 }  // namespace sa

@@ -125,6 +125,9 @@ def test_multiband_wrap_vs_oracle(engine, algo):
     compare_with_oracle(engine, algo, SCORINGS[algo][1 % len(SCORINGS[algo])], pairs)
 
 
+T16_KERNELS = (sa.SA_KERNEL_T16, sa.SA_KERNEL_T16_ENDCELL)
+
+
 def dna_pairs(seed, count, maxlen):
     rng = np.random.default_rng(seed)
     pairs = []
@@ -144,7 +147,7 @@ def test_t16_and_int32_kernels_both_exact(engine, algo, monkeypatch):
     allow_scorings = [a for a in SCORINGS[algo] if len(a) == 3 or (len(a) == 4 and a[3])]
     for args in allow_scorings:
         compare_with_oracle(engine, algo, args, pairs)
-        assert engine.last_plan()[0] == sa.SA_KERNEL_T16, args
+        assert engine.last_plan()[0] in T16_KERNELS, args
     monkeypatch.setenv("SEQALIB_T16", "0")
     for args in allow_scorings:
         compare_with_oracle(engine, algo, args, pairs)
@@ -158,7 +161,7 @@ def test_t16_eligibility(engine, algo):
     # fewer than four symbols (codes padded with absent bytes)
     two = [(bytes(b"AC"[x & 1] for x in a), bytes(b"CA"[x % 3 == 0] for x in b)) for a, b in dna]
     compare_with_oracle(engine, algo, (-1, 2, -1), two)
-    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    assert engine.last_plan()[0] in T16_KERNELS
     # a fifth symbol -> int32 kernel
     five = dna[:-1] + [(dna[-1][0] + b"N", dna[-1][1])]
     compare_with_oracle(engine, algo, (-1, 2, -1), five)
@@ -168,10 +171,38 @@ def test_t16_eligibility(engine, algo):
     compare_with_oracle(engine, algo, (-1, 3, -1), big)
     assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
     compare_with_oracle(engine, algo, (-1, 2, -1), big)
-    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    assert engine.last_plan()[0] in T16_KERNELS
     # !allowMismatch -> int32 kernel
     compare_with_oracle(engine, algo, (-2, 1, -1, False), dna)
     assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
+
+
+def test_endcell_replay_vs_oracle(engine):
+    """>= 1024 DNA SW pairs take the one-wave T16 plan with per-chunk maxima and the end-cell
+    replay (sa_endcell.hip).  Cases: all-zero matrices (end cell = last cell), periodic
+    sequences (many tied maxima across rows and chunks), identical sequences, and multi-band
+    pairs at R = 32 (max_m 4200 -> 3 bands)."""
+    rng = np.random.default_rng(5)
+    pairs = []
+    for k in range(1030):
+        kind = k % 6
+        if kind == 0:
+            a, b = b"A" * (1 + k % 70), b"C" * (1 + k % 50)
+        elif kind == 1:
+            a, b = b"AC" * (5 + k % 40), b"CA" * (3 + k % 45)
+        elif kind == 2:
+            a = sa.synth_dna(k, 1 + k % 97)
+            b = a
+        else:
+            a = sa.synth_dna(50_000 + k, int(rng.integers(1, 300)))
+            b = sa.synth_mutate(a, k)[: int(rng.integers(1, 300))]
+        pairs.append((a, b))
+    pairs[7] = (sa.synth_dna(1, 4200), sa.synth_dna(2, 3100))
+    pairs[11] = (sa.synth_dna(3, 2100), sa.synth_mutate(sa.synth_dna(3, 2100), 9))
+    pairs[13] = (b"ACGT" * 1050, b"ACGT" * 700)
+    for args in [(-1, 1, -1), (-3, 2, -2), (-1, 2, -1)]:
+        compare_with_oracle(engine, 0, args, pairs)
+        assert engine.last_plan()[:2] == (sa.SA_KERNEL_T16_ENDCELL, 32), args
 
 
 @pytest.mark.parametrize("match", ["purine", "nwild", "caseless"])
