@@ -221,7 +221,10 @@ def main():
     label = f"sw_{'t16c' if endcell else 't16' if t16 else 'int32'}_r{plan_R}"
     model = issue_model(label)
     fill_gcups = per_launch_cells / fill_s / 1e9
-    hbm_gbps = per_launch_cells * SW_FLAG_BYTES_PER_CELL / fill_s / 1e9
+    # algorithmic HBM bytes per cell: 2 traceback bits, plus the end-cell snapshots (64 lanes x
+    # (R/2 + 1) words per 32-step chunk of a band = (R/2+1)*4 / (32*R) B per cell)
+    bytes_per_cell = SW_FLAG_BYTES_PER_CELL + ((plan_R // 2 + 1) * 4 / (32 * plan_R) if endcell else 0.0)
+    hbm_gbps = per_launch_cells * bytes_per_cell / fill_s / 1e9
     traffic = load_pmc_traffic(workload)
     kname = (f"fill_kernel<SW,R={plan_R},W={plan_W}," + ("T16 tagged int16 profile" if t16 else "int32 flags")
              + (",chunk-max end cell>" if endcell else ",KEYED>"))
@@ -238,7 +241,7 @@ def main():
                  "issue_ceiling_gcups": model["peak_gcups"] if model else None, "valu_per_cell": vpc,
                  "peak_basis": "steady-loop VALU mix x measured per-opcode issue rates (tools/issue_model.py, "
                                "profiles/issue_model_r02.json)",
-                 "bytes_per_cell": SW_FLAG_BYTES_PER_CELL, "hbm_achieved_GBps": round(hbm_gbps, 1),
+                 "bytes_per_cell": round(bytes_per_cell, 4), "hbm_achieved_GBps": round(hbm_gbps, 1),
                  "hbm_peak_GBps": HBM_PEAK_GBPS, "hbm_frac": round(hbm_gbps / HBM_PEAK_GBPS, 4)})
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GCUPS", "n_gpus": world, "steps": args.steps,

@@ -95,7 +95,7 @@ def main():
     if traffic is not None:
         cells = bench["config"]["pairs_per_gpu"] * bench["config"]["m"] * bench["config"]["n"]
         lines += [f"fill kernel: {traffic / cells:.4f} HBM bytes per cell measured vs "
-                  f"{bench['roofline']['bytes_per_cell']} algorithmic (2 flag bits / cell)", ""]
+                  f"{bench['roofline']['bytes_per_cell']} algorithmic (2 traceback bits / cell + end-cell snapshots)", ""]
         if fill_avg_ns:
             lines.append(f"fill kernel average duration (rocprofv3): {fill_avg_ns / 1e6:.3f} ms; "
                          f"HBM rate {traffic / (fill_avg_ns * 1e-9) / 1e9:.1f} GB/s")
