@@ -45,6 +45,7 @@ using SW = SmithWatermanSA<std::string, char, '-'>;
 using NW = NeedlemanWunschSA<std::string, char, '-'>;
 using LG = LocalGotohSA<std::string, char, '-'>;
 using GG = GlobalGotohSA<std::string, char, '-'>;
+using HB = HirschbergSA<std::string, char, '-'>;
 
 bool equal_char(char a, char b) { return a == b; }
 
@@ -129,6 +130,23 @@ int ref_align(int algo, int nargs, int a0, int a1, int a2, int a3, int allow, in
         out->max_col = (int)a.MaxCol;
         a.buildResult(q, t, res);
         a.clearAll();
+    } else if (algo == 4) {
+        // HirschbergSA::getAlignment (SAHirschberg.h:172-184) exposes no score: report H[m][n] of
+        // NW with the same scoring (every Hirschberg alignment is an optimal NW alignment).
+        NW s(sc, fn);
+        s.cacheAllMatches(q, t);
+        s.computeScoreMatrix(q, t);
+        out->score = s.Matrix[(size_t)m * (n + 1) + n];
+        s.clearAll();
+        out->max_row = m;
+        out->max_col = n;
+        HB a(sc, fn);
+        // copy-initialise: AlignedSequence::operator= does not compile (SequenceAlignment.h:62-66)
+        AlignedSequence<char, '-'> hres = a.getAlignment(q, t);
+        int len = 0;
+        emit<int>(hres, row0, bars, row1, cap, &len);
+        out->len = len;
+        return len <= cap ? 0 : -1;
     } else {
         GG a(sc, fn);
         a.cacheAllMatches(q, t);

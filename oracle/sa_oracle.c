@@ -287,6 +287,101 @@ static int align_gotoh(int local, const oracle_scoring* sc, int m, int n, const 
     return rc;
 }
 
+/* ------------------------------------------------------- Hirschberg (SAHirschberg.h) */
+typedef struct {
+    const oracle_scoring* sc;
+    const uint8_t *s1, *s2, *lut;
+    int32_t *F, *A, *C;      /* FinalScore, ScoreAux, ScoreCache (n+1 each), :174-178 */
+    uint8_t* fwd;            /* forward-order op list of the whole alignment */
+    int nf;
+    int err;
+} hb_ctx;
+
+static inline int hb_match(const hb_ctx* h, uint8_t a, uint8_t b) {
+    return h->lut ? h->lut[a * 256 + b] != 0 : a == b;
+}
+
+/* NWScore (:11-100): last row of NW over a[0..alen) x b[0..blen), each read forwards or (rev)
+ * backwards, into h->F[0..blen]. */
+static void hb_nwscore(hb_ctx* h, const uint8_t* a, int alen, int arev, const uint8_t* b, int blen,
+                       int brev) {
+    const int32_t G = h->sc->gap, MA = h->sc->match;
+    const int allow = h->sc->allow_mismatch;
+    const int32_t MI = allow ? h->sc->mismatch : INT_MIN;
+    int32_t *F = h->F, *A = h->A;
+    F[0] = 0;
+    for (int j = 1; j <= blen; ++j) F[j] = F[j - 1] + G;
+    for (int i = 1; i <= alen; ++i) {
+        const uint8_t ai = arev ? a[alen - i] : a[i - 1];
+        A[0] = F[0] + G;
+        for (int j = 1; j <= blen; ++j) {
+            const uint8_t bj = brev ? b[blen - j] : b[j - 1];
+            const int v = hb_match(h, ai, bj);
+            const int32_t sub = allow ? F[j - 1] + (v ? MA : MI) : (v ? F[j - 1] + MA : MI);
+            A[j] = max3(sub, F[j] + G, A[j - 1] + G);
+        }
+        int32_t* t = F; F = A; A = t;
+    }
+    h->F = F; h->A = A;
+}
+
+static void hb_put(hb_ctx* h, uint8_t op) { h->fwd[h->nf++] = op; }
+
+/* HirschbergRec (:102-163) over s1[a0..a0+alen) x s2[b0..b0+blen); appends forward ops. */
+static void hb_rec(hb_ctx* h, int a0, int alen, int b0, int blen) {
+    if (h->err) return;
+    if (alen == 0) {
+        for (int k = 0; k < blen; ++k) hb_put(h, 'L');   /* Entry(Blank, Char) */
+    } else if (blen == 0) {
+        for (int k = 0; k < alen; ++k) hb_put(h, 'U');   /* Entry(Char, Blank) */
+    } else if (alen == 1 || blen == 1) {
+        /* NeedlemanWunschSA::getAlignment on the two views, spliced at the end (:119-126) */
+        uint8_t* mt = match_cache(h->s1 + a0, alen, h->s2 + b0, blen, h->lut);
+        uint8_t* tb = (uint8_t*)malloc((size_t)(alen + blen) + 1);
+        if (!mt || !tb) { free(mt); free(tb); h->err = -2; return; }
+        opbuf ob = {tb, alen + blen + 1, 0, 0};
+        oracle_result r;
+        if (align_nw(h->sc, h->s1 + a0, alen, h->s2 + b0, blen, mt, &r, &ob)) h->err = -2;
+        for (int k = ob.n - 1; k >= 0; --k) hb_put(h, tb[k]);   /* traceback order -> forward */
+        free(mt); free(tb);
+    } else {
+        const int mid = alen / 2;
+        hb_nwscore(h, h->s1 + a0, mid, 0, h->s2 + b0, blen, 0);
+        memcpy(h->C, h->F, sizeof(int32_t) * (size_t)(blen + 1));          /* swap into ScoreCache */
+        hb_nwscore(h, h->s1 + a0 + mid, alen - mid, 1, h->s2 + b0, blen, 1);
+        int mid2 = 0;
+        int32_t best = INT_MIN;
+        for (int i = 0; i < blen; ++i) {                                  /* :138-149, i < size */
+            const int32_t sc = h->C[i] + h->F[blen - i];
+            if (sc >= best) { best = sc; mid2 = i; }
+        }
+        hb_rec(h, a0, mid, b0, mid2);
+        hb_rec(h, a0 + mid, alen - mid, b0 + mid2, blen - mid2);
+    }
+}
+
+static int align_hirschberg(const oracle_scoring* sc, const uint8_t* s1, int m, const uint8_t* s2,
+                            int n, const uint8_t* lut, oracle_result* res, opbuf* ob) {
+    hb_ctx h;
+    memset(&h, 0, sizeof(h));
+    h.sc = sc; h.s1 = s1; h.s2 = s2; h.lut = lut;
+    h.F = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n + 1) * 3);
+    h.fwd = (uint8_t*)malloc((size_t)(m + n) + 1);
+    if (!h.F || !h.fwd) { free(h.F); free(h.fwd); return -2; }
+    h.A = h.F + (n + 1);
+    h.C = h.A + (n + 1);
+    int32_t* base = h.F;
+    hb_nwscore(&h, s1, m, 0, s2, n, 0);                 /* score: NW H[m][n] */
+    res->score = h.F[n];
+    hb_rec(&h, 0, m, 0, n);
+    for (int k = h.nf - 1; k >= 0; --k) put(ob, h.fwd[k]);   /* back to traceback order */
+    res->end_i = m; res->end_j = n;
+    res->start_i = 0; res->start_j = 0;
+    free(base);
+    free(h.fwd);
+    return h.err;
+}
+
 /* SALocalGotoh.h:484-488: these three size pairs discard the Gotoh result and run
  * StaticFuncs::useNW (StaticFuncs.h:12-25) with the same (affine) ScoringSystem. */
 static int lg_size_hack(int m, int n) {
@@ -297,6 +392,18 @@ int oracle_align(int algo, const oracle_scoring* sc, const uint8_t* s1, int m, c
                  int n, const uint8_t* lut, oracle_result* res, uint8_t* ops, int ops_cap,
                  char* row0, char* bars, char* row1, int cap) {
     if (algo == OR_LOCAL_GOTOH && lg_size_hack(m, n)) algo = OR_NW;
+    if (algo == OR_HIRSCHBERG) {
+        opbuf hb = {ops, ops_cap, 0, 0};
+        memset(res, 0, sizeof(*res));
+        int rc = align_hirschberg(sc, s1, m, s2, n, lut, res, &hb);
+        res->nops = hb.n;
+        if (rc) return rc;
+        if (hb.overflow) return -1;
+        int len = 0;
+        int e = expand(s1, m, s2, n, ops, hb.n, m, n, 0, 0, 0, m, n, row0, bars, row1, cap, &len);
+        res->len = len;
+        return e;
+    }
     uint8_t* mt = match_cache(s1, m, s2, n, lut);
     if (!mt) return -2;
     opbuf ob = {ops, ops_cap, 0, 0};

@@ -81,7 +81,7 @@ def ref_align(algo: int, args, match: str, s1: bytes, s2: bytes):
                                            r1.raw[:k].decode("latin-1"))
 
 
-ALGO = {"sw": 0, "nw": 1, "lg": 2, "gg": 3}
+ALGO = {"sw": 0, "nw": 1, "lg": 2, "gg": 3, "hb": 4}
 LINEAR = [(-1, 2), (-1, 1, -1), (-1, 2, -1), (-2, 1, -1, False), (-3, 2, -2), (-1, 1, -1, False)]
 AFFINE = [(-3, -1, 1, -1, False), (-3, -1, 1, -1, True), (-2, -1, 2, -1, True), (-5, -2, 3, -2, True),
           (0, -1, 1, -1, True), (-4, -1, 2, -3, False)]
@@ -156,11 +156,44 @@ def lg_hack(m, n):
     return (m, n) in ((314, 288), (60, 57), (61, 58))
 
 
+def hirschberg_vectors():
+    """HirschbergSA (SAHirschberg.h) vectors: KAT pairs x linear scorings x match fns, random and
+    mutated DNA up to 2k, empty and length-1 edges (the NW base case :119-126)."""
+    hb = []
+    for pi, (a, b) in enumerate(TEST_CPP_PAIRS):
+        for sc in LINEAR:
+            for mt in ("equal", "null", "purine"):
+                record(hb, f"testcpp{pi}", "hb", sc, mt, a, b)
+                if a != b:
+                    record(hb, f"testcpp{pi}r", "hb", sc, mt, b, a)
+    for a, b in (("", "ACGT"), ("ACGT", ""), ("", ""), ("A", "ACGTTGCA"), ("ACGTTGCA", "A"), ("A", "C"),
+                 ("AC", "CA"), ("ACGT" * 8, "TGCA" * 8)):
+        for sc in ((-1, 2), (-1, 2, -1), (-2, 1, -1, False)):
+            record(hb, "edge", "hb", sc, "equal", a, b)
+    for k, (m, n) in enumerate(((17, 23), (64, 64), (65, 63), (128, 97), (255, 300), (513, 511), (1000, 1024),
+                                (2048, 2048))):
+        s1 = {"kind": "dna", "seed": 3_000_000_001 + 2 * k, "len": m}
+        s2 = {"kind": "dna", "seed": 3_000_000_002 + 2 * k, "len": n}
+        for sc in ((-1, 2, -1), (-1, 1, -1), (-2, 1, -1, False)):
+            record(hb, f"rnd{m}x{n}", "hb", sc, "equal", s1, s2)
+        src = {"kind": "dna", "seed": 3_100_000_000 + k, "len": m}
+        record(hb, f"mut{m}", "hb", (-1, 2, -1), "equal", src, {"kind": "mut", "src": src, "seed": 11 + k})
+        record(hb, f"mutP{m}", "hb", (-1, 2, -1), "purine", src, {"kind": "mut", "src": src, "seed": 11 + k})
+    return hb
+
+
 def main():
     global L
     if not os.path.exists(REF_SO):
         sys.exit("oracle/_ref/libsaref.so missing: run `make ref` (needs /root/reference)")
     L = ref_lib()
+    if "--only-hirschberg" in sys.argv:
+        rows = hirschberg_vectors()
+        with open(os.path.join(HERE, "hirschberg.jsonl"), "w") as f:
+            for e in rows:
+                f.write(json.dumps(e, separators=(",", ":")) + "\n")
+        print(f"hirschberg.jsonl: {len(rows)} vectors")
+        return
     # pin the pure-Python generators to std::mt19937_64 before using them
     for seed, n in ((1, 1000), (2, 333), (1_000_000_001, 64)):
         assert py_dna(seed, n) == ref_dna(seed, n), "MT64 restatement disagrees with std::mt19937_64"
@@ -238,7 +271,8 @@ def main():
     record(big, "mut4096", "sw", (-1, 1, -1), "equal", src, {"kind": "mut", "src": src, "seed": 5})
     record(big, "mut4096", "lg", (-3, -1, 1, -1, True), "equal", src, {"kind": "mut", "src": src, "seed": 5})
 
-    for name, rows in (("kat.jsonl", kat), ("random.jsonl", rnd), ("large.jsonl", big)):
+    for name, rows in (("kat.jsonl", kat), ("random.jsonl", rnd), ("large.jsonl", big),
+                       ("hirschberg.jsonl", hirschberg_vectors())):
         with open(os.path.join(HERE, name), "w") as f:
             for e in rows:
                 f.write(json.dumps(e, separators=(",", ":")) + "\n")

@@ -10,6 +10,7 @@ from util import ALGOS, golden_sequences, load_golden, named_lut, oracle_align, 
 KAT = load_golden("kat.jsonl")
 RND = load_golden("random.jsonl")
 BIG = load_golden("large.jsonl")
+HB = load_golden("hirschberg.jsonl")
 
 
 def check(e):
@@ -38,6 +39,13 @@ def test_readme_known_answer():
 @pytest.mark.parametrize("chunk", range(8))
 def test_oracle_kat(chunk):
     for e in KAT[chunk::8]:
+        check(e)
+
+
+def test_oracle_hirschberg():
+    """HirschbergSA restatement (SAHirschberg.h) vs the reference's own output."""
+    assert len(HB) > 500
+    for e in HB:
         check(e)
 
 
