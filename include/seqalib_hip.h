@@ -33,7 +33,10 @@ enum {
     SA_SW = 0,            /* SmithWatermanSA   — linear gap, local  (SASmithWaterman.h)   */
     SA_NW = 1,            /* NeedlemanWunschSA — linear gap, global (SANeedlemanWunsch.h) */
     SA_LOCAL_GOTOH = 2,   /* LocalGotohSA      — affine gap, local  (SALocalGotoh.h)      */
-    SA_GLOBAL_GOTOH = 3   /* GlobalGotohSA     — affine gap, global (SAGlobalGotoh.h)     */
+    SA_GLOBAL_GOTOH = 3,  /* GlobalGotohSA     — affine gap, global (SAGlobalGotoh.h)     */
+    SA_HIRSCHBERG = 4     /* HirschbergSA      — linear gap, global, linear space (SAHirschberg.h):
+                             the reference's own split/tie rules, not just an optimal alignment;
+                             score = NW H[m][n]; ops in traceback order like NW */
 };
 
 /* Status codes. */

@@ -33,8 +33,9 @@ __all__ = [
     "SA_FLAG_DIVERGED", "SA_FLAG_BAD_SHAPE", "SA_FLAG_SIZE_HACK",
 ]
 
-SA_SW, SA_NW, SA_LOCAL_GOTOH, SA_GLOBAL_GOTOH = 0, 1, 2, 3
-ALGO_NAMES = {SA_SW: "sw", SA_NW: "nw", SA_LOCAL_GOTOH: "local_gotoh", SA_GLOBAL_GOTOH: "global_gotoh"}
+SA_SW, SA_NW, SA_LOCAL_GOTOH, SA_GLOBAL_GOTOH, SA_HIRSCHBERG = 0, 1, 2, 3, 4
+ALGO_NAMES = {SA_SW: "sw", SA_NW: "nw", SA_LOCAL_GOTOH: "local_gotoh", SA_GLOBAL_GOTOH: "global_gotoh",
+              SA_HIRSCHBERG: "hirschberg"}
 SA_FLAG_DIVERGED, SA_FLAG_BAD_SHAPE, SA_FLAG_SIZE_HACK = 1, 2, 4
 SA_KERNEL_INT32, SA_KERNEL_T16, SA_KERNEL_T16_ENDCELL = 0, 1, 2
 INT32_MIN = -(2 ** 31)
@@ -261,7 +262,7 @@ def expand_ops(algo: int, s1: Sequence, s2: Sequence, r: PairResult, blank="-",
         else:
             raise SeqalibError(f"bad op {op!r}")
     local.reverse()   # push_front order -> forward order
-    if r.flags & SA_FLAG_SIZE_HACK or algo in (SA_NW, SA_GLOBAL_GOTOH):
+    if r.flags & SA_FLAG_SIZE_HACK or algo in (SA_NW, SA_GLOBAL_GOTOH, SA_HIRSCHBERG):
         return AlignedSequence(local, blank)
     idx1, idx2, end1, end2 = r.start_i, r.start_j, r.end_i, r.end_j
     front = [Entry(s1[k], blank, False) for k in range(idx1)] + [Entry(blank, s2[k], False) for k in range(idx2)]
@@ -501,6 +502,12 @@ class NeedlemanWunschSA(_Aligner):
 
 class LocalGotohSA(_Aligner):
     ALGO = SA_LOCAL_GOTOH
+
+
+class HirschbergSA(_Aligner):
+    """HirschbergSA (SAHirschberg.h): linear-space NW with the reference's own split/tie rules.
+    Default scoring is NeedlemanWunschSA's (-1, 2, -1) (:166-167)."""
+    ALGO = SA_HIRSCHBERG
 
 
 class GlobalGotohSA(_Aligner):

@@ -1,0 +1,455 @@
+// sa_hirschberg.hip — HirschbergSA::getAlignment (SAHirschberg.h:102-184) on the GPU, batched over
+// pairs: linear-space global alignment whose result is exactly the reference's (its own split
+// tie rule and NW base case), not merely an optimal alignment.
+//
+// The recursion is run breadth-first over all pairs at once:
+//   * device levels: every subproblem with more than kHbLeafRows rows of Seq1 and >= 2 columns
+//     is split.  Its two NWScore sweeps (:131 forward over the top half, :136 over the reversed
+//     bottom half and reversed Seq2) become two rows of one batched launch of hb_sweep_kernel
+//     (score-only NW, one wave per sweep, anti-diagonal wavefront as in the fill kernel, the
+//     last DP row written out); hb_split_kernel then takes, per subproblem, the LAST i in
+//     [0, |Seq2|) maximising Fwd[i] + Rev[|Seq2|-i] (:138-149; i never reaches |Seq2|) and the
+//     host forms the two children (:151-161).
+//   * leaves: everything smaller (and every base case) is finished by hb_leaf_kernel, one
+//     thread per subproblem running the same recursion iteratively (explicit stack, left child
+//     first), including the NW base case of :119-126 with the reference's NW traceback rules.
+//   * assembly: a pair's leaves cover disjoint, increasing ranges of Seq1, so its alignment is
+//     the concatenation of its leaves' forward op lists in Seq1 order; the host reverses it into
+//     the engine's traceback-order op stream (include/seqalib_hip.h).
+// Score reported: NW H[m][n] (the reference exposes none): max over i in [0, n] of the level-0
+// split sums, or the leaf's own full NWScore.
+#include <hip/hip_runtime.h>
+#include <limits.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "sa_internal.h"
+
+namespace sa {
+
+constexpr int kHbLeafRows = 64;   // subproblems with <= this many Seq1 rows are leaves
+
+struct HbSweep {       // NWScore over A (alen) x B (blen) -> rows[out .. out+blen]
+    uint64_t a, b;     // index of A[0] / B[0] in seq1 / seq2 (rev: of the LAST element read first)
+    int32_t alen, blen;
+    int32_t rev;       // 1: A and B are both read backwards
+    int32_t pad;
+    uint64_t out;      // int32 index into the row buffer
+};
+
+struct HbSplit {
+    uint64_t fwd, rev; // row indices of the forward / reverse last rows (blen + 1 each)
+    int32_t n, top;    // |Seq2| of the subproblem; top: also report the NW score
+};
+
+struct HbLeaf {
+    uint64_t a0, b0;   // Seq1 / Seq2 start (indices into seq1 / seq2)
+    int32_t alen, blen;
+    uint64_t scratch;  // int32 index into the leaf scratch
+    uint64_t out;      // byte index into the leaf op buffer (capacity alen + blen)
+    int32_t top, pad;
+};
+
+struct HbScore {
+    int32_t gap, match, mismatch, allow;
+};
+
+__device__ __forceinline__ bool hb_match(const uint32_t* lut, uint32_t a, uint32_t b) {
+    return lut ? ((lut[(a << 3) | (b >> 5)] >> (b & 31)) & 1) : a == b;
+}
+
+// NW cell as NWScore computes it (:40-44 / :56-59).
+__device__ __forceinline__ int32_t hb_cell(int32_t hd, int32_t hu, int32_t hl, bool v, const HbScore& s) {
+    const int32_t sub = s.allow ? hd + (v ? s.match : s.mismatch) : (v ? hd + s.match : INT_MIN);
+    return max(max(sub, hu + s.gap), hl + s.gap);
+}
+
+// ------------------------------------------------------------------ batched NWScore sweeps
+template <int R>
+__global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const uint8_t* s2, const HbSweep* sweeps,
+                                                      int32_t* rows, const uint32_t* lutbits, HbScore sc) {
+    __shared__ uint32_t s_lut[2048];
+    const int lane = threadIdx.x;
+    const HbSweep d = sweeps[blockIdx.x];
+    if (lutbits) {
+        for (int k = lane; k < 2048; k += 64) s_lut[k] = lutbits[k];
+        __syncthreads();
+    }
+    const uint32_t* lut = lutbits ? s_lut : nullptr;
+    int32_t* out = rows + d.out;
+    const int m = d.alen, n = d.blen, G = sc.gap;
+    auto symA = [&](int k) -> uint32_t { return d.rev ? s1[d.a - k] : s1[d.a + k]; };
+    auto symB = [&](int k) -> uint32_t { return d.rev ? s2[d.b - k] : s2[d.b + k]; };
+    constexpr int BAND = 64 * R;
+    const int bands = (m + BAND - 1) / BAND;
+    const int lastb = bands - 1;
+    const int tl = ((m - 1) % BAND) / R, rl = (m - 1) % R;   // owner of row m-1 in the last band
+    int hl = 0;
+    for (int band = 0; band < bands; ++band) {
+        const int row0 = band * BAND + lane * R;
+        uint32_t a[R];
+        int32_t Hp[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            a[r] = row0 + r < m ? symA(row0 + r) : 0u;
+            Hp[r] = (row0 + r + 1) * G;                      // H[i][0] = i * Gap (:37)
+        }
+        int32_t prev_up = row0 * G;                          // H[row0][0]
+        int32_t vup = 0;
+        for (int s = 0; s < n + 63; ++s) {
+            if ((s & 63) == 0) {   // row-above values for lane 0, columns s .. s+63
+                const int j = s + lane;
+                vup = j < n ? (band == 0 ? (j + 1) * G : out[j + 1]) : 0;
+            }
+            int32_t up_h = __shfl_up(hl, 1);
+            if (lane == 0) up_h = __builtin_amdgcn_readlane(vup, s & 63);
+            const int j0 = s - lane;
+            if (j0 >= 0 && j0 < n) {
+                const uint32_t b = symB(j0);
+                int32_t hd = prev_up, hu = up_h;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int32_t h = hb_cell(hd, hu, Hp[r], hb_match(lut, a[r], b), sc);
+                    hd = Hp[r];
+                    Hp[r] = h;
+                    hu = h;
+                }
+                prev_up = up_h;
+                hl = Hp[R - 1];
+                if (band < lastb) {
+                    if (lane == 63) out[j0 + 1] = hl;        // this band's last row, in place
+                } else if (lane == tl) {
+                    int32_t v = 0;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) v = r == rl ? Hp[r] : v;
+                    out[j0 + 1] = v;                         // row m of the sweep
+                }
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+    if (lane == 0) out[0] = m * G;
+}
+
+// ---------------------------------------------------------------------------- split
+__global__ __launch_bounds__(64) void hb_split_kernel(const HbSplit* splits, const int32_t* rows, int32_t* mid2,
+                                                      int32_t* score) {
+    const int lane = threadIdx.x;
+    const HbSplit d = splits[blockIdx.x];
+    const int32_t* F = rows + d.fwd;
+    const int32_t* B = rows + d.rev;
+    const int n = d.n;
+    int32_t best = INT_MIN;
+    int idx = 0;
+    for (int i = lane; i < n; i += 64) {
+        const int32_t s = F[i] + B[n - i];
+        if (s >= best) { best = s; idx = i; }
+    }
+    // lexicographic (sum, i) maximum = the reference's last maximum (S >= MaxScore, :144)
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const int32_t ob = __shfl_xor(best, off);
+        const int oi = __shfl_xor(idx, off);
+        if (ob > best || (ob == best && oi > idx)) { best = ob; idx = oi; }
+    }
+    if (lane == 0) {
+        mid2[blockIdx.x] = idx;
+        if (d.top) score[blockIdx.x] = max(best, F[n] + B[0]);   // NW H[m][n] over i in [0, n]
+    }
+}
+
+// ---------------------------------------------------------------------------- leaves
+__device__ void hb_nwscore(const uint8_t* A, int alen, int arev, const uint8_t* B, int blen, int brev,
+                           const uint32_t* lut, const HbScore& sc, int32_t*& F, int32_t*& X) {
+    F[0] = 0;
+    for (int j = 1; j <= blen; ++j) F[j] = F[j - 1] + sc.gap;
+    for (int i = 1; i <= alen; ++i) {
+        const uint32_t ai = arev ? A[alen - i] : A[i - 1];
+        int32_t left = F[0] + sc.gap, diag = F[0];
+        X[0] = left;
+        for (int j = 1; j <= blen; ++j) {
+            const uint32_t bj = brev ? B[blen - j] : B[j - 1];
+            const int32_t up = F[j];
+            left = hb_cell(diag, up, left, hb_match(lut, ai, bj), sc);
+            X[j] = left;
+            diag = up;
+        }
+        int32_t* t = F; F = X; X = t;
+    }
+}
+
+// NeedlemanWunschSA::getAlignment on a 1 x k or k x 1 view (:119-126): full matrix + the
+// reference NW traceback (SANeedlemanWunsch.h:167-230); writes forward-order ops at out.
+__device__ int hb_nw_small(const uint8_t* A, int m, const uint8_t* B, int n, const uint32_t* lut,
+                           const HbScore& sc, int32_t* H, uint8_t* out) {
+    const int w = n + 1;
+    for (int i = 0; i <= m; ++i) H[i * w] = i * sc.gap;
+    for (int j = 0; j <= n; ++j) H[j] = j * sc.gap;
+    for (int i = 1; i <= m; ++i)
+        for (int j = 1; j <= n; ++j)
+            H[i * w + j] = hb_cell(H[(i - 1) * w + j - 1], H[(i - 1) * w + j], H[i * w + j - 1],
+                                   hb_match(lut, A[i - 1], B[j - 1]), sc);
+    int k = 0, i = m, j = n;
+    while (i > 0 || j > 0) {
+        if (i > 0 && j > 0) {
+            const bool v = hb_match(lut, A[i - 1], B[j - 1]);
+            const int32_t hd = H[(i - 1) * w + j - 1];
+            const int32_t dt = sc.allow ? hd + (v ? sc.match : sc.mismatch) : (v ? hd + sc.match : INT_MIN);
+            if (H[i * w + j] == dt) {
+                out[k++] = (v || sc.allow) ? (v ? 'M' : 'S') : 'X';
+                --i; --j;
+                continue;
+            }
+        }
+        if (i > 0 && H[i * w + j] == H[(i - 1) * w + j] + sc.gap) { out[k++] = 'U'; --i; }
+        else { out[k++] = 'L'; --j; }
+    }
+    for (int p = 0, q = k - 1; p < q; ++p, --q) { const uint8_t t = out[p]; out[p] = out[q]; out[q] = t; }
+    return k;
+}
+
+__global__ __launch_bounds__(64) void hb_leaf_kernel(const uint8_t* s1, const uint8_t* s2, const HbLeaf* leaves,
+                                                     uint32_t nleaves, int32_t* scratch, uint8_t* outops,
+                                                     int32_t* nout, int32_t* score, const uint32_t* lut,
+                                                     HbScore sc) {
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= nleaves) return;
+    const HbLeaf L = leaves[id];
+    const uint8_t* S1 = s1 + L.a0;
+    const uint8_t* S2 = s2 + L.b0;
+    const int mx = max(L.alen, L.blen);
+    int32_t* F = scratch + L.scratch;
+    int32_t* X = F + (L.blen + 1);
+    int32_t* Cc = X + (L.blen + 1);
+    int32_t* Hs = Cc + (L.blen + 1);          // 2 * (mx + 1): base-case matrix
+    uint8_t* out = outops + L.out;
+    if (L.top) {
+        int32_t s;
+        if (L.alen == 0) s = L.blen * sc.gap;
+        else if (L.blen == 0) s = L.alen * sc.gap;
+        else { hb_nwscore(S1, L.alen, 0, S2, L.blen, 0, lut, sc, F, X); s = F[L.blen]; }
+        score[id] = s;
+    }
+    (void)mx;
+    int k = 0;
+    int stk[40][4];   // pending right children; depth <= 2 + log2(alen)
+    int sp = 0;
+    stk[sp][0] = 0; stk[sp][1] = L.alen; stk[sp][2] = 0; stk[sp][3] = L.blen; ++sp;
+    while (sp > 0) {
+        --sp;
+        const int x0 = stk[sp][0], xl = stk[sp][1], y0 = stk[sp][2], yl = stk[sp][3];
+        if (xl == 0) {
+            for (int q = 0; q < yl; ++q) out[k++] = 'L';
+        } else if (yl == 0) {
+            for (int q = 0; q < xl; ++q) out[k++] = 'U';
+        } else if (xl == 1 || yl == 1) {
+            k += hb_nw_small(S1 + x0, xl, S2 + y0, yl, lut, sc, Hs, out + k);
+        } else {
+            const int mid = xl / 2;
+            hb_nwscore(S1 + x0, mid, 0, S2 + y0, yl, 0, lut, sc, F, X);
+            for (int q = 0; q <= yl; ++q) Cc[q] = F[q];
+            hb_nwscore(S1 + x0 + mid, xl - mid, 1, S2 + y0, yl, 1, lut, sc, F, X);
+            int mid2 = 0;
+            int32_t best = INT_MIN;
+            for (int i = 0; i < yl; ++i) {
+                const int32_t s = Cc[i] + F[yl - i];
+                if (s >= best) { best = s; mid2 = i; }
+            }
+            // right child below, left child on top: left is finished first (:155, :161)
+            stk[sp][0] = x0 + mid; stk[sp][1] = xl - mid; stk[sp][2] = y0 + mid2; stk[sp][3] = yl - mid2; ++sp;
+            stk[sp][0] = x0; stk[sp][1] = mid; stk[sp][2] = y0; stk[sp][3] = mid2; ++sp;
+        }
+    }
+    nout[id] = k;
+}
+
+// ---------------------------------------------------------------------------- host driver
+namespace {
+
+struct Sub {
+    uint32_t pair;
+    uint64_t a0, b0;   // absolute indices into seq1 / seq2
+    int32_t m, n;
+    bool top;
+};
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t alloc(size_t count) {
+        if (count <= n && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T));
+        if (e == hipSuccess) n = count;
+        return e;
+    }
+    ~DevBuf() { if (p) (void)hipFree(p); }
+};
+
+#define HB_HIP(call)                                                    \
+    do {                                                                \
+        hipError_t e_ = (call);                                         \
+        if (e_ != hipSuccess) { *err = std::string(#call) + ": " + hipGetErrorString(e_); return -1; } \
+    } while (0)
+
+hipError_t launch_sweeps(int R, uint32_t count, const uint8_t* d1, const uint8_t* d2, const HbSweep* sw,
+                         int32_t* rows, const uint32_t* lut, const HbScore& sc, hipStream_t st) {
+    const dim3 grid(count), block(64);
+    switch (R) {
+        case 2: hipLaunchKernelGGL(hb_sweep_kernel<2>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 4: hipLaunchKernelGGL(hb_sweep_kernel<4>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 8: hipLaunchKernelGGL(hb_sweep_kernel<8>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 16: hipLaunchKernelGGL(hb_sweep_kernel<16>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        default: hipLaunchKernelGGL(hb_sweep_kernel<32>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// Host driver: inputs on the device (offsets too), results and the traceback-order op streams
+// returned in host memory (res[npairs], ops laid out at off1[p] + off2[p] + p).
+int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
+                   const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
+                   std::vector<sa_result>& res, std::vector<uint8_t>& ops, std::string* err) {
+    HbScore sc;
+    sc.gap = scoring->gap;
+    sc.match = scoring->match;
+    sc.allow = scoring->allow_mismatch != 0;
+    sc.mismatch = sc.allow ? scoring->mismatch : INT_MIN;
+    std::vector<uint64_t> o1(npairs + 1), o2(npairs + 1);
+    HB_HIP(hipMemcpyAsync(o1.data(), d_o1, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
+    HB_HIP(hipMemcpyAsync(o2.data(), d_o2, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
+    HB_HIP(hipStreamSynchronize(st));
+    res.assign(npairs, sa_result{});
+    std::vector<Sub> cur, leaves;
+    cur.reserve(npairs);
+    for (uint32_t p = 0; p < npairs; ++p)
+        cur.push_back(Sub{p, o1[p], o2[p], (int32_t)(o1[p + 1] - o1[p]), (int32_t)(o2[p + 1] - o2[p]), true});
+
+    DevBuf<HbSweep> dsw;
+    DevBuf<HbSplit> dsp;
+    DevBuf<int32_t> drows, dmid, dscore;
+    std::vector<HbSweep> sw;
+    std::vector<HbSplit> sp;
+    std::vector<Sub> split, next;
+    std::vector<int32_t> mid2, tops;
+    while (!cur.empty()) {
+        split.clear();
+        for (const Sub& s : cur) (s.m > kHbLeafRows && s.n >= 2 ? split : leaves).push_back(s);
+        if (split.empty()) break;
+        sw.clear();
+        sp.clear();
+        uint64_t rowpos = 0;
+        int maxa = 0;
+        for (const Sub& s : split) {
+            const int mid = s.m / 2;
+            HbSplit d;
+            d.n = s.n;
+            d.top = s.top ? 1 : 0;
+            d.fwd = rowpos;
+            sw.push_back(HbSweep{s.a0, s.b0, mid, s.n, 0, 0, rowpos});
+            rowpos += (uint64_t)s.n + 1;
+            d.rev = rowpos;
+            sw.push_back(HbSweep{s.a0 + (uint64_t)s.m - 1, s.b0 + (uint64_t)s.n - 1, s.m - mid, s.n, 1, 0, rowpos});
+            rowpos += (uint64_t)s.n + 1;
+            sp.push_back(d);
+            maxa = std::max(maxa, s.m - mid);
+        }
+        HB_HIP(dsw.alloc(sw.size()));
+        HB_HIP(dsp.alloc(sp.size()));
+        HB_HIP(drows.alloc(rowpos));
+        HB_HIP(dmid.alloc(sp.size()));
+        HB_HIP(dscore.alloc(sp.size()));
+        HB_HIP(hipMemcpyAsync(dsw.p, sw.data(), sw.size() * sizeof(HbSweep), hipMemcpyHostToDevice, st));
+        HB_HIP(hipMemcpyAsync(dsp.p, sp.data(), sp.size() * sizeof(HbSplit), hipMemcpyHostToDevice, st));
+        int R = 2;
+        while (R < 32 && 64 * R < maxa) R *= 2;
+        HB_HIP(launch_sweeps(R, (uint32_t)sw.size(), d1, d2, dsw.p, drows.p, d_lutbits, sc, st));
+        hipLaunchKernelGGL(hb_split_kernel, dim3((uint32_t)sp.size()), dim3(64), 0, st, dsp.p, drows.p, dmid.p,
+                           dscore.p);
+        HB_HIP(hipGetLastError());
+        mid2.resize(sp.size());
+        tops.resize(sp.size());
+        HB_HIP(hipMemcpyAsync(mid2.data(), dmid.p, sp.size() * 4, hipMemcpyDeviceToHost, st));
+        HB_HIP(hipMemcpyAsync(tops.data(), dscore.p, sp.size() * 4, hipMemcpyDeviceToHost, st));
+        HB_HIP(hipStreamSynchronize(st));
+        next.clear();
+        for (size_t k = 0; k < split.size(); ++k) {
+            const Sub& s = split[k];
+            if (s.top) res[s.pair].score = tops[k];
+            const int mid = s.m / 2, j = mid2[k];
+            next.push_back(Sub{s.pair, s.a0, s.b0, mid, j, false});
+            next.push_back(Sub{s.pair, s.a0 + (uint64_t)mid, s.b0 + (uint64_t)j, s.m - mid, s.n - j, false});
+        }
+        cur.swap(next);
+    }
+
+    // leaves: one thread each
+    std::vector<HbLeaf> lv(leaves.size());
+    uint64_t scr = 0, outpos = 0;
+    for (size_t k = 0; k < leaves.size(); ++k) {
+        const Sub& s = leaves[k];
+        lv[k] = HbLeaf{s.a0, s.b0, s.m, s.n, scr, outpos, s.top ? 1 : 0, 0};
+        scr += 3ull * ((uint64_t)s.n + 1) + 2ull * ((uint64_t)std::max(s.m, s.n) + 1);
+        outpos += (uint64_t)s.m + (uint64_t)s.n;
+    }
+    if (!lv.empty()) {
+        DevBuf<HbLeaf> dlv;
+        DevBuf<int32_t> dscr, dnout, dlscore;
+        DevBuf<uint8_t> dout;
+        HB_HIP(dlv.alloc(lv.size()));
+        HB_HIP(dscr.alloc(scr));
+        HB_HIP(dnout.alloc(lv.size()));
+        HB_HIP(dlscore.alloc(lv.size()));
+        HB_HIP(dout.alloc(outpos));
+        HB_HIP(hipMemcpyAsync(dlv.p, lv.data(), lv.size() * sizeof(HbLeaf), hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(hb_leaf_kernel, dim3((uint32_t)((lv.size() + 63) / 64)), dim3(64), 0, st, d1, d2, dlv.p,
+                           (uint32_t)lv.size(), dscr.p, dout.p, dnout.p, dlscore.p, d_lutbits, sc);
+        HB_HIP(hipGetLastError());
+        std::vector<int32_t> nout(lv.size()), lscore(lv.size());
+        std::vector<uint8_t> lops(outpos);
+        HB_HIP(hipMemcpyAsync(nout.data(), dnout.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
+        HB_HIP(hipMemcpyAsync(lscore.data(), dlscore.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
+        if (outpos) HB_HIP(hipMemcpyAsync(lops.data(), dout.p, outpos, hipMemcpyDeviceToHost, st));
+        HB_HIP(hipStreamSynchronize(st));
+        // assembly: a pair's leaves in Seq1 order, forward ops reversed into traceback order
+        std::vector<uint32_t> order(lv.size());
+        for (uint32_t k = 0; k < order.size(); ++k) order[k] = k;
+        std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+            return leaves[x].pair != leaves[y].pair ? leaves[x].pair < leaves[y].pair : leaves[x].a0 < leaves[y].a0;
+        });
+        ops.assign(o1[npairs] + o2[npairs] + npairs, 0);
+        std::vector<uint32_t> fill(npairs, 0);
+        for (uint32_t p = 0; p < npairs; ++p) {
+            sa_result& r = res[p];
+            r.end_i = (int32_t)(o1[p + 1] - o1[p]);
+            r.end_j = (int32_t)(o2[p + 1] - o2[p]);
+        }
+        // count ops per pair, then write each leaf's ops reversed at the tail of its pair's stream
+        for (uint32_t k : order) fill[leaves[k].pair] += (uint32_t)nout[k];
+        std::vector<uint32_t> wpos(fill);   // forward position of the next leaf's first op (from the end)
+        for (uint32_t k : order) {
+            const Sub& s = leaves[k];
+            if (s.top) res[s.pair].score = lscore[k];
+            uint8_t* dst = ops.data() + o1[s.pair] + o2[s.pair] + s.pair;
+            // forward index f of this leaf's q-th op -> traceback index (total - 1 - f)
+            const uint32_t total = fill[s.pair];
+            const uint32_t f0 = total - wpos[s.pair];
+            for (int32_t q = 0; q < nout[k]; ++q) dst[total - 1 - (f0 + (uint32_t)q)] = lops[lv[k].out + (uint64_t)q];
+            wpos[s.pair] -= (uint32_t)nout[k];
+        }
+        for (uint32_t p = 0; p < npairs; ++p) res[p].nops = fill[p];
+    } else {
+        ops.assign(o1[npairs] + o2[npairs] + npairs, 0);
+    }
+    return 0;
+}
+
+}  // namespace sa

@@ -94,5 +94,14 @@ hipError_t launch_build_profile(const uint32_t* lutbits, uint32_t sym_pack, int 
                                 uint32_t* prof, hipStream_t s);
 hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
 hipError_t launch_endcell(int R, const EndcellParams& p, hipStream_t stream);
+}  // namespace sa
+#include <string>
+#include <vector>
+namespace sa {
+// HirschbergSA driver (sa_hirschberg.hip): device inputs, host outputs (results, op streams at
+// off1[p] + off2[p] + p).  Returns 0 or -1 with *err set.
+int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
+                   const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
+                   std::vector<sa_result>& res, std::vector<uint8_t>& ops, std::string* err);
 
 }  // namespace sa

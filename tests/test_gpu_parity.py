@@ -66,6 +66,29 @@ def test_golden_random(engine):
     assert check_golden(engine, load_golden("random.jsonl")) > 200
 
 
+def test_golden_hirschberg(engine):
+    """HirschbergSA (SAHirschberg.h) vectors of the unmodified reference: device levels (pairs
+    taller than 64 rows), per-thread leaves, NW base cases, empty / length-1 edges."""
+    assert check_golden(engine, load_golden("hirschberg.jsonl")) > 800
+
+
+@pytest.mark.parametrize("args,match", [((-1, 2, -1), None), ((-2, 1, -1, False), None), ((-1, 2), "purine"),
+                                        ((-3, 2, -2), "nwild")])
+def test_hirschberg_batch_vs_oracle(engine, args, match):
+    rng = np.random.default_rng(11)
+    pairs = []
+    for k in range(120):
+        m = int(rng.integers(0, 900)) if k % 4 else int(rng.integers(0, 4))
+        n = int(rng.integers(0, 900)) if k % 5 else int(rng.integers(0, 4))
+        a = sa.synth_dna(70_000 + 2 * k, m)
+        b = sa.synth_mutate(a, k)[:n] if k % 2 else sa.synth_dna(70_001 + 2 * k, n)
+        if match == "nwild":
+            b = bytes(ord("N") if (x % 7 == 3) else c for x, c in enumerate(b))
+        pairs.append((a, b))
+    pairs.append((sa.synth_dna(5, 3000), sa.synth_dna(6, 2500)))
+    compare_with_oracle(engine, sa.SA_HIRSCHBERG, args, pairs, match)
+
+
 def test_golden_large(engine):
     assert check_golden(engine, load_golden("large.jsonl")) == 10
 
