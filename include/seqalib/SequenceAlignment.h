@@ -190,6 +190,7 @@ std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std
 #include "ArrayView.h"
 #include "SANeedlemanWunsch.h"
 #include "StaticFuncs.h"
+#include "SAHirschberg.h"
 #include "SASmithWaterman.h"
 #include "SAGlobalGotoh.h"
 #include "SALocalGotoh.h"

@@ -21,15 +21,20 @@
 #include <hip/hip_runtime.h>
 #include <limits.h>
 
+#include <stdio.h>
+#include <stdlib.h>
+
 #include <algorithm>
+#include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sa_internal.h"
 
 namespace sa {
 
-constexpr int kHbLeafRows = 64;   // subproblems with <= this many Seq1 rows are leaves
+constexpr int kHbLeafRows = 48;   // subproblems with <= this many Seq1 rows are leaves (tuned)
 
 struct HbSweep {       // NWScore over A (alen) x B (blen) -> rows[out .. out+blen]
     uint64_t a, b;     // index of A[0] / B[0] in seq1 / seq2 (rev: of the LAST element read first)
@@ -97,36 +102,49 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
             Hp[r] = (row0 + r + 1) * G;                      // H[i][0] = i * Gap (:37)
         }
         int32_t prev_up = row0 * G;                          // H[row0][0]
-        int32_t vup = 0;
-        for (int s = 0; s < n + 63; ++s) {
-            if ((s & 63) == 0) {   // row-above values for lane 0, columns s .. s+63
-                const int j = s + lane;
-                vup = j < n ? (band == 0 ? (j + 1) * G : out[j + 1]) : 0;
+        // Per 64-step chunk, lane k holds column c0+k's row-above value (for lane 0) and Seq2
+        // symbol, loaded one chunk ahead; both reach their lane by DPP wave_shr:1 like the fill.
+        auto load_chunk = [&](int c0, int32_t& vu, uint32_t& vs) {
+            const int j = c0 + lane;
+            vu = 0;
+            vs = 0;
+            if (j < n) {
+                vu = band == 0 ? (j + 1) * G : out[j + 1];
+                vs = symB(j);
             }
-            int32_t up_h = __shfl_up(hl, 1);
-            if (lane == 0) up_h = __builtin_amdgcn_readlane(vup, s & 63);
-            const int j0 = s - lane;
-            if (j0 >= 0 && j0 < n) {
-                const uint32_t b = symB(j0);
-                int32_t hd = prev_up, hu = up_h;
+        };
+        int32_t vup, nvup;
+        uint32_t vsym, nvsym, sym = 0;
+        load_chunk(0, vup, vsym);
+        for (int c0 = 0; c0 < n + 63; c0 += 64) {
+            load_chunk(c0 + 64, nvup, nvsym);
+            const int steps = min(64, n + 63 - c0);
+            for (int q = 0; q < steps; ++q) {
+                const int s = c0 + q;
+                const int32_t up_h = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vup, q), hl, 0x138, 0xf,
+                                                                 0xf, false);
+                sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vsym, q), sym, 0x138, 0xf, 0xf, false);
+                const int j0 = s - lane;
+                if (j0 >= 0 && j0 < n) {
+                    int32_t hd = prev_up, hu = up_h;
 #pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int32_t h = hb_cell(hd, hu, Hp[r], hb_match(lut, a[r], b), sc);
-                    hd = Hp[r];
-                    Hp[r] = h;
-                    hu = h;
-                }
-                prev_up = up_h;
-                hl = Hp[R - 1];
-                if (band < lastb) {
-                    if (lane == 63) out[j0 + 1] = hl;        // this band's last row, in place
-                } else if (lane == tl) {
-                    int32_t v = 0;
-#pragma unroll
-                    for (int r = 0; r < R; ++r) v = r == rl ? Hp[r] : v;
-                    out[j0 + 1] = v;                         // row m of the sweep
+                    for (int r = 0; r < R; ++r) {
+                        const int32_t h = hb_cell(hd, hu, Hp[r], hb_match(lut, a[r], sym), sc);
+                        hd = Hp[r];
+                        Hp[r] = h;
+                        hu = h;
+                    }
+                    prev_up = up_h;
+                    hl = Hp[R - 1];
+                    if (band < lastb) {
+                        if (lane == 63) out[j0 + 1] = hl;    // this band's last row, in place
+                    } else if (lane == tl) {
+                        out[j0 + 1] = Hp[rl];                // row m of the sweep (uniform index)
+                    }
                 }
             }
+            vup = nvup;
+            vsym = nvsym;
         }
         __threadfence_block();
         __syncthreads();
@@ -162,8 +180,32 @@ __global__ __launch_bounds__(64) void hb_split_kernel(const HbSplit* splits, con
 }
 
 // ---------------------------------------------------------------------------- leaves
-__device__ void hb_nwscore(const uint8_t* A, int alen, int arev, const uint8_t* B, int blen, int brev,
-                           const uint32_t* lut, const HbScore& sc, int32_t*& F, int32_t*& X) {
+// Row / symbol accessors for the leaf solver: global scratch, or LDS laid out item-major
+// (element k of thread t at k * 64 + t: conflict-free when the threads are in step).
+typedef int32_t __attribute__((address_space(3))) hb_lds_i32;
+typedef uint8_t __attribute__((address_space(3))) hb_lds_u8;
+struct GRow {
+    int32_t* p;
+    __device__ int32_t& operator[](int k) const { return p[k]; }
+};
+struct LRow {
+    hb_lds_i32* p;
+    __device__ hb_lds_i32& operator[](int k) const { return p[k * 64]; }
+};
+struct GSeq {
+    const uint8_t* p;
+    __device__ uint32_t operator[](int k) const { return p[k]; }
+    __device__ GSeq shifted(int k) const { return GSeq{p + k}; }
+};
+struct LSeq {
+    const hb_lds_u8* p;
+    __device__ uint32_t operator[](int k) const { return p[k * 64]; }
+    __device__ LSeq shifted(int k) const { return LSeq{p + k * 64}; }
+};
+
+template <typename Row, typename Seq>
+__device__ void hb_nwscore(Seq A, int alen, int arev, Seq B, int blen, int brev,
+                           const uint32_t* lut, const HbScore& sc, Row& F, Row& X) {
     F[0] = 0;
     for (int j = 1; j <= blen; ++j) F[j] = F[j - 1] + sc.gap;
     for (int i = 1; i <= alen; ++i) {
@@ -177,7 +219,7 @@ __device__ void hb_nwscore(const uint8_t* A, int alen, int arev, const uint8_t* 
             X[j] = left;
             diag = up;
         }
-        int32_t* t = F; F = X; X = t;
+        Row t = F; F = X; X = t;
     }
 }
 
@@ -211,33 +253,22 @@ __device__ int hb_nw_small(const uint8_t* A, int m, const uint8_t* B, int n, con
     return k;
 }
 
-__global__ __launch_bounds__(64) void hb_leaf_kernel(const uint8_t* s1, const uint8_t* s2, const HbLeaf* leaves,
-                                                     uint32_t nleaves, int32_t* scratch, uint8_t* outops,
-                                                     int32_t* nout, int32_t* score, const uint32_t* lut,
-                                                     HbScore sc) {
-    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
-    if (id >= nleaves) return;
-    const HbLeaf L = leaves[id];
-    const uint8_t* S1 = s1 + L.a0;
-    const uint8_t* S2 = s2 + L.b0;
-    const int mx = max(L.alen, L.blen);
-    int32_t* F = scratch + L.scratch;
-    int32_t* X = F + (L.blen + 1);
-    int32_t* Cc = X + (L.blen + 1);
-    int32_t* Hs = Cc + (L.blen + 1);          // 2 * (mx + 1): base-case matrix
-    uint8_t* out = outops + L.out;
-    if (L.top) {
+// One leaf: the whole HirschbergRec below it (explicit stack, left child first), forward ops.
+template <typename Row, typename Seq>
+__device__ int hb_leaf_solve(Seq S1, Seq S2, const uint8_t* g1, const uint8_t* g2, int alen, int blen, bool top,
+                             Row F, Row X, Row Cc, int32_t* Hs, uint8_t* out, int32_t* score,
+                             const uint32_t* lut, const HbScore& sc) {
+    if (top) {
         int32_t s;
-        if (L.alen == 0) s = L.blen * sc.gap;
-        else if (L.blen == 0) s = L.alen * sc.gap;
-        else { hb_nwscore(S1, L.alen, 0, S2, L.blen, 0, lut, sc, F, X); s = F[L.blen]; }
-        score[id] = s;
+        if (alen == 0) s = blen * sc.gap;
+        else if (blen == 0) s = alen * sc.gap;
+        else { hb_nwscore(S1, alen, 0, S2, blen, 0, lut, sc, F, X); s = F[blen]; }
+        *score = s;
     }
-    (void)mx;
     int k = 0;
     int stk[40][4];   // pending right children; depth <= 2 + log2(alen)
     int sp = 0;
-    stk[sp][0] = 0; stk[sp][1] = L.alen; stk[sp][2] = 0; stk[sp][3] = L.blen; ++sp;
+    stk[sp][0] = 0; stk[sp][1] = alen; stk[sp][2] = 0; stk[sp][3] = blen; ++sp;
     while (sp > 0) {
         --sp;
         const int x0 = stk[sp][0], xl = stk[sp][1], y0 = stk[sp][2], yl = stk[sp][3];
@@ -246,12 +277,13 @@ __global__ __launch_bounds__(64) void hb_leaf_kernel(const uint8_t* s1, const ui
         } else if (yl == 0) {
             for (int q = 0; q < xl; ++q) out[k++] = 'U';
         } else if (xl == 1 || yl == 1) {
-            k += hb_nw_small(S1 + x0, xl, S2 + y0, yl, lut, sc, Hs, out + k);
+            k += hb_nw_small(g1 + x0, xl, g2 + y0, yl, lut, sc, Hs, out + k);
         } else {
             const int mid = xl / 2;
-            hb_nwscore(S1 + x0, mid, 0, S2 + y0, yl, 0, lut, sc, F, X);
+            const Seq A0 = S1.shifted(x0), B0 = S2.shifted(y0), A1 = S1.shifted(x0 + mid);
+            hb_nwscore(A0, mid, 0, B0, yl, 0, lut, sc, F, X);
             for (int q = 0; q <= yl; ++q) Cc[q] = F[q];
-            hb_nwscore(S1 + x0 + mid, xl - mid, 1, S2 + y0, yl, 1, lut, sc, F, X);
+            hb_nwscore(A1, xl - mid, 1, B0, yl, 1, lut, sc, F, X);
             int mid2 = 0;
             int32_t best = INT_MIN;
             for (int i = 0; i < yl; ++i) {
@@ -262,6 +294,41 @@ __global__ __launch_bounds__(64) void hb_leaf_kernel(const uint8_t* s1, const ui
             stk[sp][0] = x0 + mid; stk[sp][1] = xl - mid; stk[sp][2] = y0 + mid2; stk[sp][3] = yl - mid2; ++sp;
             stk[sp][0] = x0; stk[sp][1] = mid; stk[sp][2] = y0; stk[sp][3] = mid2; ++sp;
         }
+    }
+    return k;
+}
+
+constexpr int kHbLdsCols = 64;   // leaves with |Seq1|, |Seq2| <= this run with LDS rows + symbols
+
+__global__ __launch_bounds__(64) void hb_leaf_kernel(const uint8_t* s1, const uint8_t* s2, const HbLeaf* leaves,
+                                                     uint32_t nleaves, int32_t* scratch, uint8_t* outops,
+                                                     int32_t* nout, int32_t* score, const uint32_t* lut,
+                                                     HbScore sc) {
+    __shared__ int32_t s_rows[3 * (kHbLdsCols + 1) * 64];
+    __shared__ uint8_t s_seq[2 * kHbLdsCols * 64];
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= nleaves) return;
+    const int t = threadIdx.x;
+    const HbLeaf L = leaves[id];
+    const uint8_t* g1 = s1 + L.a0;
+    const uint8_t* g2 = s2 + L.b0;
+    int32_t* Fg = scratch + L.scratch;
+    int32_t* Hs = Fg + 3 * (L.blen + 1);        // 2 * (max(alen, blen) + 1): base-case matrix
+    uint8_t* out = outops + L.out;
+    int k;
+    if (L.alen <= kHbLdsCols && L.blen <= kHbLdsCols) {
+        hb_lds_u8* q1 = (hb_lds_u8*)s_seq + t;
+        hb_lds_u8* q2 = q1 + kHbLdsCols * 64;
+        for (int c = 0; c < L.alen; ++c) q1[c * 64] = g1[c];
+        for (int c = 0; c < L.blen; ++c) q2[c * 64] = g2[c];
+        hb_lds_i32* r0 = (hb_lds_i32*)s_rows + t;
+        const LRow F{r0}, X{r0 + (kHbLdsCols + 1) * 64}, Cc{r0 + 2 * (kHbLdsCols + 1) * 64};
+        k = hb_leaf_solve(LSeq{q1}, LSeq{q2}, g1, g2, L.alen, L.blen, L.top != 0, F, X, Cc, Hs, out, score + id,
+                          lut, sc);
+    } else {
+        const GRow F{Fg}, X{Fg + (L.blen + 1)}, Cc{Fg + 2 * (L.blen + 1)};
+        k = hb_leaf_solve(GSeq{g1}, GSeq{g2}, g1, g2, L.alen, L.blen, L.top != 0, F, X, Cc, Hs, out, score + id,
+                          lut, sc);
     }
     nout[id] = k;
 }
@@ -302,6 +369,7 @@ hipError_t launch_sweeps(int R, uint32_t count, const uint8_t* d1, const uint8_t
                          int32_t* rows, const uint32_t* lut, const HbScore& sc, hipStream_t st) {
     const dim3 grid(count), block(64);
     switch (R) {
+        case 1: hipLaunchKernelGGL(hb_sweep_kernel<1>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
         case 2: hipLaunchKernelGGL(hb_sweep_kernel<2>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
         case 4: hipLaunchKernelGGL(hb_sweep_kernel<4>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
         case 8: hipLaunchKernelGGL(hb_sweep_kernel<8>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
@@ -318,6 +386,17 @@ hipError_t launch_sweeps(int R, uint32_t count, const uint8_t* d1, const uint8_t
 int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
                    const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
                    std::vector<sa_result>& res, std::vector<uint8_t>& ops, std::string* err) {
+    const bool timing = getenv("SEQALIB_HB_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto t_start = now(), t_mark = t_start;
+    auto lap = [&](const char* what) {
+        if (!timing) return;
+        const auto t = now();
+        fprintf(stderr, "[hb] %-28s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_mark).count());
+        t_mark = t;
+    };
+    int leaf_rows = kHbLeafRows;   // tuning override: SEQALIB_HB_LEAF
+    if (const char* lr = getenv("SEQALIB_HB_LEAF")) leaf_rows = std::max(2, atoi(lr));
     HbScore sc;
     sc.gap = scoring->gap;
     sc.match = scoring->match;
@@ -333,16 +412,17 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
     for (uint32_t p = 0; p < npairs; ++p)
         cur.push_back(Sub{p, o1[p], o2[p], (int32_t)(o1[p + 1] - o1[p]), (int32_t)(o2[p + 1] - o2[p]), true});
 
-    DevBuf<HbSweep> dsw;
-    DevBuf<HbSplit> dsp;
-    DevBuf<int32_t> drows, dmid, dscore;
+    // device buffers persist per host thread (hipMalloc/hipFree per call would serialise)
+    static thread_local DevBuf<HbSweep> dsw;
+    static thread_local DevBuf<HbSplit> dsp;
+    static thread_local DevBuf<int32_t> drows, dmid, dscore;
     std::vector<HbSweep> sw;
     std::vector<HbSplit> sp;
     std::vector<Sub> split, next;
     std::vector<int32_t> mid2, tops;
     while (!cur.empty()) {
         split.clear();
-        for (const Sub& s : cur) (s.m > kHbLeafRows && s.n >= 2 ? split : leaves).push_back(s);
+        for (const Sub& s : cur) (s.m > leaf_rows && s.n >= 2 ? split : leaves).push_back(s);
         if (split.empty()) break;
         sw.clear();
         sp.clear();
@@ -369,7 +449,7 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
         HB_HIP(dscore.alloc(sp.size()));
         HB_HIP(hipMemcpyAsync(dsw.p, sw.data(), sw.size() * sizeof(HbSweep), hipMemcpyHostToDevice, st));
         HB_HIP(hipMemcpyAsync(dsp.p, sp.data(), sp.size() * sizeof(HbSplit), hipMemcpyHostToDevice, st));
-        int R = 2;
+        int R = 1;
         while (R < 32 && 64 * R < maxa) R *= 2;
         HB_HIP(launch_sweeps(R, (uint32_t)sw.size(), d1, d2, dsw.p, drows.p, d_lutbits, sc, st));
         hipLaunchKernelGGL(hb_split_kernel, dim3((uint32_t)sp.size()), dim3(64), 0, st, dsp.p, drows.p, dmid.p,
@@ -389,6 +469,7 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
             next.push_back(Sub{s.pair, s.a0 + (uint64_t)mid, s.b0 + (uint64_t)j, s.m - mid, s.n - j, false});
         }
         cur.swap(next);
+        lap("level (sweeps + split)");
     }
 
     // leaves: one thread each
@@ -401,9 +482,9 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
         outpos += (uint64_t)s.m + (uint64_t)s.n;
     }
     if (!lv.empty()) {
-        DevBuf<HbLeaf> dlv;
-        DevBuf<int32_t> dscr, dnout, dlscore;
-        DevBuf<uint8_t> dout;
+        static thread_local DevBuf<HbLeaf> dlv;
+        static thread_local DevBuf<int32_t> dscr, dnout, dlscore;
+        static thread_local DevBuf<uint8_t> dout;
         HB_HIP(dlv.alloc(lv.size()));
         HB_HIP(dscr.alloc(scr));
         HB_HIP(dnout.alloc(lv.size()));
@@ -419,33 +500,44 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
         HB_HIP(hipMemcpyAsync(lscore.data(), dlscore.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
         if (outpos) HB_HIP(hipMemcpyAsync(lops.data(), dout.p, outpos, hipMemcpyDeviceToHost, st));
         HB_HIP(hipStreamSynchronize(st));
-        // assembly: a pair's leaves in Seq1 order, forward ops reversed into traceback order
-        std::vector<uint32_t> order(lv.size());
-        for (uint32_t k = 0; k < order.size(); ++k) order[k] = k;
-        std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
-            return leaves[x].pair != leaves[y].pair ? leaves[x].pair < leaves[y].pair : leaves[x].a0 < leaves[y].a0;
-        });
+        lap("leaves (kernel + D2H)");
+        // assembly: a pair's leaves in Seq1 order, forward ops reversed into traceback order.
+        // Leaves are bucketed by pair (counting sort), each pair assembled independently.
+        std::vector<uint32_t> start(npairs + 1, 0), order(lv.size());
+        for (const Sub& s : leaves) ++start[s.pair + 1];
+        for (uint32_t p = 0; p < npairs; ++p) start[p + 1] += start[p];
+        {
+            std::vector<uint32_t> pos(start.begin(), start.end() - 1);
+            for (uint32_t k = 0; k < lv.size(); ++k) order[pos[leaves[k].pair]++] = k;
+        }
         ops.assign(o1[npairs] + o2[npairs] + npairs, 0);
-        std::vector<uint32_t> fill(npairs, 0);
-        for (uint32_t p = 0; p < npairs; ++p) {
-            sa_result& r = res[p];
-            r.end_i = (int32_t)(o1[p + 1] - o1[p]);
-            r.end_j = (int32_t)(o2[p + 1] - o2[p]);
-        }
-        // count ops per pair, then write each leaf's ops reversed at the tail of its pair's stream
-        for (uint32_t k : order) fill[leaves[k].pair] += (uint32_t)nout[k];
-        std::vector<uint32_t> wpos(fill);   // forward position of the next leaf's first op (from the end)
-        for (uint32_t k : order) {
-            const Sub& s = leaves[k];
-            if (s.top) res[s.pair].score = lscore[k];
-            uint8_t* dst = ops.data() + o1[s.pair] + o2[s.pair] + s.pair;
-            // forward index f of this leaf's q-th op -> traceback index (total - 1 - f)
-            const uint32_t total = fill[s.pair];
-            const uint32_t f0 = total - wpos[s.pair];
-            for (int32_t q = 0; q < nout[k]; ++q) dst[total - 1 - (f0 + (uint32_t)q)] = lops[lv[k].out + (uint64_t)q];
-            wpos[s.pair] -= (uint32_t)nout[k];
-        }
-        for (uint32_t p = 0; p < npairs; ++p) res[p].nops = fill[p];
+        auto assemble = [&](uint32_t p0, uint32_t p1) {
+            for (uint32_t p = p0; p < p1; ++p) {
+                uint32_t* b0 = order.data() + start[p];
+                uint32_t* b1 = order.data() + start[p + 1];
+                std::sort(b0, b1, [&](uint32_t x, uint32_t y) { return leaves[x].a0 < leaves[y].a0; });
+                uint32_t total = 0;
+                for (uint32_t* q = b0; q < b1; ++q) total += (uint32_t)nout[*q];
+                sa_result& r = res[p];
+                r.end_i = (int32_t)(o1[p + 1] - o1[p]);
+                r.end_j = (int32_t)(o2[p + 1] - o2[p]);
+                r.nops = total;
+                // forward op f lands at traceback index total - 1 - f
+                uint8_t* dst = ops.data() + o1[p] + o2[p] + p + total;
+                for (uint32_t* q = b0; q < b1; ++q) {
+                    const uint32_t k = *q;
+                    if (leaves[k].top) r.score = lscore[k];
+                    const uint8_t* src = lops.data() + lv[k].out;
+                    for (int32_t c = 0; c < nout[k]; ++c) *--dst = src[c];
+                }
+            }
+        };
+        const uint32_t nth = std::max<uint32_t>(1, std::min<uint32_t>(16, npairs / 64));
+        std::vector<std::thread> pool;
+        for (uint32_t t = 0; t < nth; ++t)
+            pool.emplace_back(assemble, (uint32_t)((uint64_t)npairs * t / nth), (uint32_t)((uint64_t)npairs * (t + 1) / nth));
+        for (auto& th : pool) th.join();
+        lap("assembly (host)");
     } else {
         ops.assign(o1[npairs] + o2[npairs] + npairs, 0);
     }

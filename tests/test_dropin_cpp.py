@@ -41,7 +41,7 @@ def case_line(e):
 
 
 def test_driver_matches_reference_vectors(binaries, engine):
-    entries = [e for src in ("kat.jsonl", "random.jsonl") for e in load_golden(src)
+    entries = [e for src in ("kat.jsonl", "random.jsonl", "hirschberg.jsonl") for e in load_golden(src)
                if isinstance(e["s1"], str) and isinstance(e["s2"], str) and e["match"] in ("equal", "null", "purine")
                and "rows" in e]
     assert len(entries) > 2000
