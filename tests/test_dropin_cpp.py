@@ -7,6 +7,9 @@
   build container produced tests/golden/dropin_types.ref.txt; the drop-in build must print the
   identical text (std::vector<int> + predicate, ArrayView + StaticFuncs::useNW/bridgeNW, batch,
   SmithWaterman member persistence on empty input).
+* tests/cpp/dropin_bridge — anchor gaps of three sequence pairs bridged with NW: the reference
+  build calls StaticFuncs::bridgeNW per window (tests/golden/dropin_bridge.ref.txt); the
+  drop-in build sends every window through StaticFuncs::bridgeNWBatch in one GPU pass.
 """
 import os
 import subprocess
@@ -22,7 +25,8 @@ CPP = os.path.join(ROOT, "tests", "cpp")
 @pytest.fixture(scope="module")
 def binaries():
     subprocess.check_call(["make", "-s", "-C", CPP])
-    return os.path.join(CPP, "dropin_driver"), os.path.join(CPP, "dropin_types")
+    return (os.path.join(CPP, "dropin_driver"), os.path.join(CPP, "dropin_types"),
+            os.path.join(CPP, "dropin_bridge"))
 
 
 def case_line(e):
@@ -57,4 +61,10 @@ def test_driver_matches_reference_vectors(binaries, engine):
 def test_generic_types_match_reference_build(binaries, engine):
     ref = open(os.path.join(GOLDEN, "dropin_types.ref.txt")).read()
     out = subprocess.run([binaries[1]], capture_output=True, text=True, timeout=300, check=True).stdout
+    assert out == ref
+
+
+def test_batched_bridging_matches_reference_bridgeNW(binaries, engine):
+    ref = open(os.path.join(GOLDEN, "dropin_bridge.ref.txt")).read()
+    out = subprocess.run([binaries[2]], capture_output=True, text=True, timeout=300, check=True).stdout
     assert out == ref
