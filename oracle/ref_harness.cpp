@@ -46,6 +46,7 @@ using NW = NeedlemanWunschSA<std::string, char, '-'>;
 using LG = LocalGotohSA<std::string, char, '-'>;
 using GG = GlobalGotohSA<std::string, char, '-'>;
 using HB = HirschbergSA<std::string, char, '-'>;
+using MM = MyersMillerSA<std::string, char, '-'>;
 
 bool equal_char(char a, char b) { return a == b; }
 
@@ -145,6 +146,17 @@ int ref_align(int algo, int nargs, int a0, int a1, int a2, int a3, int allow, in
         AlignedSequence<char, '-'> hres = a.getAlignment(q, t);
         int len = 0;
         emit<int>(hres, row0, bars, row1, cap, &len);
+        out->len = len;
+        return len <= cap ? 0 : -1;
+    } else if (algo == 5) {
+        // MyersMillerSA::getAlignment (SAMyersMiller.h:412-420) exposes no score (none reported).
+        out->score = 0;
+        out->max_row = m;
+        out->max_col = n;
+        MM a(sc, fn);
+        AlignedSequence<char, '-'> mres = a.getAlignment(q, t);
+        int len = 0;
+        emit<int>(mres, row0, bars, row1, cap, &len);
         out->len = len;
         return len <= cap ? 0 : -1;
     } else {

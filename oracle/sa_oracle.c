@@ -382,6 +382,143 @@ static int align_hirschberg(const oracle_scoring* sc, const uint8_t* s1, int m, 
     return h.err;
 }
 
+/* ----------------------------------------------------- Myers–Miller (SAMyersMiller.h) */
+typedef struct {
+    const oracle_scoring* sc;
+    const uint8_t *s1, *s2, *lut;
+    int32_t *C, *D, *Cr, *Dr;   /* CC, DD (:167-168) and RR, SS (:242-243), n+1 each */
+    uint8_t* fwd;               /* forward-order op list of the whole alignment */
+    int nf;
+    int top_done;
+    int32_t score;              /* the top call's optimum (see align_myers_miller) */
+} mm_ctx;
+
+/* The forward sweep of buildResultRec (:172-238) over a[0..alen) x b[0..blen), each read
+ * forwards or (rev) backwards, with row-0 gap open t0 (tb).  Read backwards with t0 = te it is
+ * the reverse sweep (:247-313) in reversed coordinates: RR[j] = C[blen-j], SS[j] = D[blen-j]. */
+static void mm_sweep(mm_ctx* h, const uint8_t* a, int alen, int rev, const uint8_t* b, int blen,
+                     int32_t t0, int32_t* C, int32_t* D) {
+    const int32_t g = h->sc->gap_open, x = h->sc->gap_extend, MA = h->sc->match;
+    const int allow = h->sc->allow_mismatch;
+    const int32_t MI = allow ? h->sc->mismatch : INT_MIN;
+    int32_t t = g;
+    C[0] = 0;
+    for (int j = 1; j <= blen; ++j) { t += x; C[j] = t; D[j] = t + g; }   /* :183-188 */
+    t = t0;
+    for (int i = 1; i <= alen; ++i) {
+        const uint8_t ai = rev ? a[alen - i] : a[i - 1];
+        int32_t s = C[0];
+        t += x;
+        int32_t c = t;
+        C[0] = c;
+        int32_t e = t + g;
+        for (int j = 1; j <= blen; ++j) {
+            const uint8_t bj = rev ? b[blen - j] : b[j - 1];
+            e = (e > c + g ? e : c + g) + x;
+            D[j] = (D[j] > C[j] + g ? D[j] : C[j] + g) + x;
+            const int v = h->lut ? h->lut[ai * 256 + bj] != 0 : ai == bj;
+            const int32_t diag = (allow || v) ? s + (v ? MA : MI) : INT_MIN;   /* :218-232 */
+            c = max3(D[j], e, diag);
+            s = C[j];
+            C[j] = c;
+        }
+    }
+    D[0] = C[0];   /* :238 (and SS[N] = RR[N], :313) */
+}
+
+static void mm_put(mm_ctx* h, uint8_t op) { h->fwd[h->nf++] = op; }
+
+/* buildResultRec (:44-397) over s1[a0..a0+M) x s2[b0..b0+N) with boundary gap opens tb, te;
+ * appends forward-order ops. */
+static void mm_rec(mm_ctx* h, int a0, int M, int b0, int N, int32_t tb, int32_t te) {
+    const int32_t g = h->sc->gap_open, x = h->sc->gap_extend, MA = h->sc->match;
+    const int allow = h->sc->allow_mismatch;
+    const int32_t MI = allow ? h->sc->mismatch : INT_MIN;
+    const int top = !h->top_done;
+    h->top_done = 1;
+    if (N == 0) {                                                     /* :57-66 */
+        for (int k = 0; k < M; ++k) mm_put(h, 'U');
+        if (top) h->score = M > 0 ? tb + x * M : 0;
+    } else if (M == 0) {                                              /* :67-74 */
+        for (int k = 0; k < N; ++k) mm_put(h, 'L');
+        if (top) h->score = g + x * N;
+    } else if (M == 1) {                                              /* :75-160 */
+        const uint8_t a = h->s1[a0];
+        const int32_t base = (tb > te ? tb : te) + x + (g + x * N);
+        int32_t best = INT_MIN;
+        int index = 0;
+        for (int j = 1; j <= N; ++j) {
+            const uint8_t bj = h->s2[b0 + j - 1];
+            const int v = h->lut ? h->lut[a * 256 + bj] != 0 : a == bj;
+            int32_t t = base;
+            if (allow || v) {
+                const int32_t via = g + x * (j - 1) + (v ? MA : MI) + g + x * (N - j);
+                if (via > t) t = via;
+            }
+            if (t > best) { best = t; index = j; }
+        }
+        for (int j = 1; j <= N; ++j) {
+            if (j == index) {
+                const uint8_t bj = h->s2[b0 + j - 1];
+                const int v = h->lut ? h->lut[a * 256 + bj] != 0 : a == bj;
+                if (!allow && !v) {          /* :141-147: (a, Blank) then (Blank, b) */
+                    mm_put(h, 'U');
+                    mm_put(h, 'L');
+                } else {
+                    mm_put(h, v ? 'M' : 'S');  /* :148-152 */
+                }
+            } else {
+                mm_put(h, 'L');
+            }
+        }
+        if (top) h->score = best;
+    } else {
+        const int mid = M / 2;
+        mm_sweep(h, h->s1 + a0, mid, 0, h->s2 + b0, N, tb, h->C, h->D);
+        mm_sweep(h, h->s1 + a0 + mid, M - mid, 1, h->s2 + b0, N, te, h->Cr, h->Dr);
+        int index = 0, type2 = 0;
+        int32_t best = INT_MIN;
+        for (int j = 0; j <= N; ++j) {                                /* :320-340 */
+            const int32_t c1 = h->C[j] + h->Cr[N - j];
+            const int32_t c2 = h->D[j] + h->Dr[N - j] - g;
+            const int32_t t = c1 > c2 ? c1 : c2;
+            if (t > best) { best = t; index = j; type2 = !(c1 > c2); }
+        }
+        if (top) h->score = best;
+        if (!type2) {                                                 /* :358-374 */
+            mm_rec(h, a0, mid, b0, index, tb, g);
+            mm_rec(h, a0 + mid, M - mid, b0 + index, N - index, g, te);
+        } else {                                                      /* :375-395 */
+            mm_rec(h, a0, mid - 1, b0, index, tb, 0);
+            mm_put(h, 'U');
+            mm_put(h, 'U');
+            mm_rec(h, a0 + mid + 1, M - mid - 1, b0 + index, N - index, 0, te);
+        }
+    }
+}
+
+/* MyersMillerSA::getAlignment (:412-420): buildResultRec(.., M, N, GapOpen, GapOpen).  The
+ * reference exposes no score; res->score is the optimum the top call computes (its midpoint
+ * maximum :320-340, the M == 1 maximum :81-124, or the boundary value of an empty side). */
+static int align_myers_miller(const oracle_scoring* sc, const uint8_t* s1, int m, const uint8_t* s2,
+                              int n, const uint8_t* lut, oracle_result* res, opbuf* ob) {
+    mm_ctx h;
+    memset(&h, 0, sizeof(h));
+    h.sc = sc; h.s1 = s1; h.s2 = s2; h.lut = lut;
+    int32_t* base = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n + 1) * 4);
+    h.fwd = (uint8_t*)malloc((size_t)(m + n) + 1);
+    if (!base || !h.fwd) { free(base); free(h.fwd); return -2; }
+    h.C = base; h.D = base + (n + 1); h.Cr = base + 2 * (n + 1); h.Dr = base + 3 * (n + 1);
+    mm_rec(&h, 0, m, 0, n, sc->gap_open, sc->gap_open);
+    for (int k = h.nf - 1; k >= 0; --k) put(ob, h.fwd[k]);   /* back to traceback order */
+    res->score = h.score;
+    res->end_i = m; res->end_j = n;
+    res->start_i = 0; res->start_j = 0;
+    free(base);
+    free(h.fwd);
+    return 0;
+}
+
 /* SALocalGotoh.h:484-488: these three size pairs discard the Gotoh result and run
  * StaticFuncs::useNW (StaticFuncs.h:12-25) with the same (affine) ScoringSystem. */
 static int lg_size_hack(int m, int n) {
@@ -392,10 +529,11 @@ int oracle_align(int algo, const oracle_scoring* sc, const uint8_t* s1, int m, c
                  int n, const uint8_t* lut, oracle_result* res, uint8_t* ops, int ops_cap,
                  char* row0, char* bars, char* row1, int cap) {
     if (algo == OR_LOCAL_GOTOH && lg_size_hack(m, n)) algo = OR_NW;
-    if (algo == OR_HIRSCHBERG) {
+    if (algo == OR_HIRSCHBERG || algo == OR_MYERS_MILLER) {
         opbuf hb = {ops, ops_cap, 0, 0};
         memset(res, 0, sizeof(*res));
-        int rc = align_hirschberg(sc, s1, m, s2, n, lut, res, &hb);
+        int rc = algo == OR_HIRSCHBERG ? align_hirschberg(sc, s1, m, s2, n, lut, res, &hb)
+                                       : align_myers_miller(sc, s1, m, s2, n, lut, res, &hb);
         res->nops = hb.n;
         if (rc) return rc;
         if (hb.overflow) return -1;

@@ -6,7 +6,9 @@
  *   LocalGotohSA     (include/SALocalGotoh.h:36-526, incl. the size hack :484-488)
  *   GlobalGotohSA    (include/SAGlobalGotoh.h:33-459)
  * plus SequenceAligner::forceGlobal (include/SequenceAlignment.h:156-189)
- * and HirschbergSA (include/SAHirschberg.h:11-184; score = NW H[m][n], the reference reports none).
+ * and HirschbergSA (include/SAHirschberg.h:11-184; score = NW H[m][n], the reference reports none)
+ * and MyersMillerSA (include/SAMyersMiller.h:43-420; score = the top call's optimum, see
+ * align_myers_miller; the reference reports none).
  *
  * Parity is PINNED: tests/test_oracle_golden.py checks this restatement against golden vectors
  * produced by the unmodified reference (oracle/_ref, tests/golden/make_golden.py).
@@ -22,7 +24,7 @@
 extern "C" {
 #endif
 
-enum { OR_SW = 0, OR_NW = 1, OR_LOCAL_GOTOH = 2, OR_GLOBAL_GOTOH = 3, OR_HIRSCHBERG = 4 };
+enum { OR_SW = 0, OR_NW = 1, OR_LOCAL_GOTOH = 2, OR_GLOBAL_GOTOH = 3, OR_HIRSCHBERG = 4, OR_MYERS_MILLER = 5 };
 
 typedef struct {
     int32_t gap, match, mismatch, gap_open, gap_extend, allow_mismatch;

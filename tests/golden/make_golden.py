@@ -81,7 +81,7 @@ def ref_align(algo: int, args, match: str, s1: bytes, s2: bytes):
                                            r1.raw[:k].decode("latin-1"))
 
 
-ALGO = {"sw": 0, "nw": 1, "lg": 2, "gg": 3, "hb": 4}
+ALGO = {"sw": 0, "nw": 1, "lg": 2, "gg": 3, "hb": 4, "mm": 5}
 LINEAR = [(-1, 2), (-1, 1, -1), (-1, 2, -1), (-2, 1, -1, False), (-3, 2, -2), (-1, 1, -1, False)]
 AFFINE = [(-3, -1, 1, -1, False), (-3, -1, 1, -1, True), (-2, -1, 2, -1, True), (-5, -2, 3, -2, True),
           (0, -1, 1, -1, True), (-4, -1, 2, -3, False)]
@@ -141,6 +141,8 @@ def record(out, tag, algo, args, match, s1spec, s2spec):
     e = {"id": f"{tag}/{algo}/{'_'.join(str(int(x)) for x in args)}/{match}", "algo": algo, "scoring": list(args),
          "match": match, "s1": s1spec, "s2": s2spec, "m": len(s1), "n": len(s2), "score": score,
          "max_row": mr, "max_col": mc, "len": len(rows[0])}
+    if algo == "mm":
+        e["score"] = None   # MyersMillerSA exposes no score (SAMyersMiller.h:412-420)
     if not isinstance(s1spec, str):
         e["s1_sha"] = sha(s1)
     if not isinstance(s2spec, str):
@@ -182,11 +184,48 @@ def hirschberg_vectors():
     return hb
 
 
+def mm_vectors():
+    """MyersMillerSA (SAMyersMiller.h) vectors: KAT pairs x affine scorings x match fns, random
+    and mutated DNA up to 2k, empty and length-1 edges (the M == 1 / N == 0 / M == 0 cases
+    :57-160 and both midpoint types :358-395)."""
+    mm = []
+    for pi, (a, b) in enumerate(TEST_CPP_PAIRS):
+        for sc in AFFINE:
+            for mt in ("equal", "null", "purine"):
+                record(mm, f"testcpp{pi}", "mm", sc, mt, a, b)
+                if a != b:
+                    record(mm, f"testcpp{pi}r", "mm", sc, mt, b, a)
+    for a, b in (("", "ACGT"), ("ACGT", ""), ("", ""), ("A", "ACGTTGCA"), ("ACGTTGCA", "A"), ("A", "C"),
+                 ("C", "AGT"), ("AC", "CA"), ("AC", "GGGG"), ("ACGT" * 8, "TGCA" * 8), ("A" * 40, "A" * 3),
+                 ("A" * 3, "A" * 40), ("ACGTACGT" * 12, "T"), ("G", "ACGTACGT" * 12)):
+        for sc in ((-3, -1, 1, -1, False), (-3, -1, 1, -1, True), (-1, -2, 2, -1, True), (0, -1, 1, -1, True),
+                   (-4, -1, 2, -3, False)):
+            record(mm, "edge", "mm", sc, "equal", a, b)
+    for k, (m, n) in enumerate(((17, 23), (64, 64), (65, 63), (128, 97), (200, 3), (3, 200), (255, 300),
+                                (513, 511), (1000, 1024), (2048, 2048))):
+        s1 = {"kind": "dna", "seed": 3_200_000_001 + 2 * k, "len": m}
+        s2 = {"kind": "dna", "seed": 3_200_000_002 + 2 * k, "len": n}
+        for sc in ((-3, -1, 1, -1, True), (-2, -1, 2, -1, True), (-3, -1, 1, -1, False), (-5, -2, 3, -2, True)):
+            record(mm, f"rnd{m}x{n}", "mm", sc, "equal", s1, s2)
+        src = {"kind": "dna", "seed": 3_300_000_000 + k, "len": m}
+        record(mm, f"mut{m}", "mm", (-3, -1, 2, -1, True), "equal", src, {"kind": "mut", "src": src, "seed": 21 + k})
+        record(mm, f"mutP{m}", "mm", (-3, -1, 2, -1, True), "purine", src,
+               {"kind": "mut", "src": src, "seed": 21 + k})
+    return mm
+
+
 def main():
     global L
     if not os.path.exists(REF_SO):
         sys.exit("oracle/_ref/libsaref.so missing: run `make ref` (needs /root/reference)")
     L = ref_lib()
+    if "--only-mm" in sys.argv:
+        rows = mm_vectors()
+        with open(os.path.join(HERE, "myersmiller.jsonl"), "w") as f:
+            for e in rows:
+                f.write(json.dumps(e, separators=(",", ":")) + "\n")
+        print(f"myersmiller.jsonl: {len(rows)} vectors")
+        return
     if "--only-hirschberg" in sys.argv:
         rows = hirschberg_vectors()
         with open(os.path.join(HERE, "hirschberg.jsonl"), "w") as f:
@@ -272,7 +311,7 @@ def main():
     record(big, "mut4096", "lg", (-3, -1, 1, -1, True), "equal", src, {"kind": "mut", "src": src, "seed": 5})
 
     for name, rows in (("kat.jsonl", kat), ("random.jsonl", rnd), ("large.jsonl", big),
-                       ("hirschberg.jsonl", hirschberg_vectors())):
+                       ("hirschberg.jsonl", hirschberg_vectors()), ("myersmiller.jsonl", mm_vectors())):
         with open(os.path.join(HERE, name), "w") as f:
             for e in rows:
                 f.write(json.dumps(e, separators=(",", ":")) + "\n")

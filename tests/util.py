@@ -18,7 +18,7 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libsaref.so")
 
-ALGOS = {"sw": 0, "nw": 1, "lg": 2, "gg": 3, "hb": 4}
+ALGOS = {"sw": 0, "nw": 1, "lg": 2, "gg": 3, "hb": 4, "mm": 5}
 
 
 # ------------------------------------------------------------------ std::mt19937_64 (pure Python)
