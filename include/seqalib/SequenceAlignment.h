@@ -191,6 +191,7 @@ std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std
 #include "SANeedlemanWunsch.h"
 #include "StaticFuncs.h"
 #include "SAHirschberg.h"
+#include "SAMyersMiller.h"
 #include "SASmithWaterman.h"
 #include "SAGlobalGotoh.h"
 #include "SALocalGotoh.h"

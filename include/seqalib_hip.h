@@ -34,9 +34,13 @@ enum {
     SA_NW = 1,            /* NeedlemanWunschSA — linear gap, global (SANeedlemanWunsch.h) */
     SA_LOCAL_GOTOH = 2,   /* LocalGotohSA      — affine gap, local  (SALocalGotoh.h)      */
     SA_GLOBAL_GOTOH = 3,  /* GlobalGotohSA     — affine gap, global (SAGlobalGotoh.h)     */
-    SA_HIRSCHBERG = 4     /* HirschbergSA      — linear gap, global, linear space (SAHirschberg.h):
+    SA_HIRSCHBERG = 4,    /* HirschbergSA      — linear gap, global, linear space (SAHirschberg.h):
                              the reference's own split/tie rules, not just an optimal alignment;
                              score = NW H[m][n]; ops in traceback order like NW */
+    SA_MYERS_MILLER = 5   /* MyersMillerSA     — affine gap, global, linear space (SAMyersMiller.h):
+                             the reference's own midpoint/tie rules and base cases; reads
+                             gap_open/gap_extend/match/mismatch/allow_mismatch; score = the top
+                             call's optimum (the reference exposes none); ops like NW */
 };
 
 /* Status codes. */

@@ -28,14 +28,14 @@ import numpy as np
 __all__ = [
     "SA_SW", "SA_NW", "SA_LOCAL_GOTOH", "SA_GLOBAL_GOTOH", "ALGO_NAMES",
     "SeqalibError", "ScoringSystem", "Entry", "AlignedSequence", "PairResult", "Engine",
-    "SmithWatermanSA", "NeedlemanWunschSA", "LocalGotohSA", "GlobalGotohSA",
+    "SmithWatermanSA", "NeedlemanWunschSA", "LocalGotohSA", "GlobalGotohSA", "HirschbergSA", "MyersMillerSA",
     "load_library", "library_path", "expand_ops", "synth_dna", "synth_mutate", "synth_dna_batch",
     "SA_FLAG_DIVERGED", "SA_FLAG_BAD_SHAPE", "SA_FLAG_SIZE_HACK",
 ]
 
-SA_SW, SA_NW, SA_LOCAL_GOTOH, SA_GLOBAL_GOTOH, SA_HIRSCHBERG = 0, 1, 2, 3, 4
+SA_SW, SA_NW, SA_LOCAL_GOTOH, SA_GLOBAL_GOTOH, SA_HIRSCHBERG, SA_MYERS_MILLER = 0, 1, 2, 3, 4, 5
 ALGO_NAMES = {SA_SW: "sw", SA_NW: "nw", SA_LOCAL_GOTOH: "local_gotoh", SA_GLOBAL_GOTOH: "global_gotoh",
-              SA_HIRSCHBERG: "hirschberg"}
+              SA_HIRSCHBERG: "hirschberg", SA_MYERS_MILLER: "myers_miller"}
 SA_FLAG_DIVERGED, SA_FLAG_BAD_SHAPE, SA_FLAG_SIZE_HACK = 1, 2, 4
 SA_KERNEL_INT32, SA_KERNEL_T16, SA_KERNEL_T16_ENDCELL = 0, 1, 2
 INT32_MIN = -(2 ** 31)
@@ -262,7 +262,7 @@ def expand_ops(algo: int, s1: Sequence, s2: Sequence, r: PairResult, blank="-",
         else:
             raise SeqalibError(f"bad op {op!r}")
     local.reverse()   # push_front order -> forward order
-    if r.flags & SA_FLAG_SIZE_HACK or algo in (SA_NW, SA_GLOBAL_GOTOH, SA_HIRSCHBERG):
+    if r.flags & SA_FLAG_SIZE_HACK or algo in (SA_NW, SA_GLOBAL_GOTOH, SA_HIRSCHBERG, SA_MYERS_MILLER):
         return AlignedSequence(local, blank)
     idx1, idx2, end1, end2 = r.start_i, r.start_j, r.end_i, r.end_j
     front = [Entry(s1[k], blank, False) for k in range(idx1)] + [Entry(blank, s2[k], False) for k in range(idx2)]
@@ -512,3 +512,14 @@ class HirschbergSA(_Aligner):
 
 class GlobalGotohSA(_Aligner):
     ALGO = SA_GLOBAL_GOTOH
+
+
+class MyersMillerSA(_Aligner):
+    """MyersMillerSA (SAMyersMiller.h): linear-space affine global alignment with the reference's
+    own midpoint/tie rules and base cases.  Default scoring (-1, 2, -1) (:406) leaves the affine
+    terms unset in the reference; pass a 4/5-argument ScoringSystem."""
+    ALGO = SA_MYERS_MILLER
+
+    @staticmethod
+    def getDefaultScoring():
+        return ScoringSystem(-1, 2, -1)

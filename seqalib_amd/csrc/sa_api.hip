@@ -182,7 +182,7 @@ bool t16_ok(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
 
 int validate_scoring(sa_ctx* c, int algo, const sa_scoring* s) {
     if (!s) return fail(c, SA_ERR_ARG, "scoring is NULL");
-    if (algo < SA_SW || algo > SA_HIRSCHBERG) return fail(c, SA_ERR_ARG, "unknown algorithm");
+    if (algo < SA_SW || algo > SA_MYERS_MILLER) return fail(c, SA_ERR_ARG, "unknown algorithm");
     return SA_OK;
 }
 
@@ -378,13 +378,14 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         hipLaunchKernelGGL(lut_to_bits, dim3(8), dim3(256), 0, st, dlut, dbits);
         SA_HIP(c, hipGetLastError());
     }
-    if (npairs && algo == SA_HIRSCHBERG) {
+    if (npairs && (algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER)) {
         std::vector<sa_result> hres;
         std::vector<uint8_t> hops;
         std::string e;
         c->launches = 0;
-        if (hirschberg_run(sc, d1, do1, d2, do2, npairs, use_lut ? dbits : nullptr, st, hres, hops, &e))
-            return fail(c, SA_ERR_HIP, "hirschberg: " + e);
+        const auto run = algo == SA_HIRSCHBERG ? hirschberg_run : myersmiller_run;
+        if (run(sc, d1, do1, d2, do2, npairs, use_lut ? dbits : nullptr, st, hres, hops, &e))
+            return fail(c, SA_ERR_HIP, (algo == SA_HIRSCHBERG ? "hirschberg: " : "myers-miller: ") + e);
         memcpy(results, hres.data(), sizeof(sa_result) * npairs);
         memcpy(ops, hops.data(), std::min<uint64_t>(hops.size(), ops_cap));
         return SA_OK;
@@ -549,13 +550,14 @@ int sa_align_batch_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8
         hipLaunchKernelGGL(lut_to_bits, dim3(8), dim3(256), 0, st, d_lut, bits);
         SA_HIP(c, hipGetLastError());
     }
-    if (algo == SA_HIRSCHBERG) {
+    if (algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER) {
         std::vector<sa_result> hres;
         std::vector<uint8_t> hops;
         std::string e;
         c->launches = 0;
-        if (hirschberg_run(sc, d1, o1, d2, o2, npairs, bits, st, hres, hops, &e))
-            return fail(c, SA_ERR_HIP, "hirschberg: " + e);
+        const auto run = algo == SA_HIRSCHBERG ? hirschberg_run : myersmiller_run;
+        if (run(sc, d1, o1, d2, o2, npairs, bits, st, hres, hops, &e))
+            return fail(c, SA_ERR_HIP, (algo == SA_HIRSCHBERG ? "hirschberg: " : "myers-miller: ") + e);
         SA_HIP(c, hipMemcpyAsync(d_res, hres.data(), sizeof(sa_result) * npairs, hipMemcpyHostToDevice, st));
         if (!hops.empty()) SA_HIP(c, hipMemcpyAsync(d_ops, hops.data(), hops.size(), hipMemcpyHostToDevice, st));
         SA_HIP(c, hipStreamSynchronize(st));   // host vectors go out of scope

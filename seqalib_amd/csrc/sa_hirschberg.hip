@@ -30,6 +30,7 @@
 #include <thread>
 #include <vector>
 
+#include "sa_dc.h"
 #include "sa_internal.h"
 
 namespace sa {
@@ -60,10 +61,6 @@ struct HbLeaf {
 struct HbScore {
     int32_t gap, match, mismatch, allow;
 };
-
-__device__ __forceinline__ bool hb_match(const uint32_t* lut, uint32_t a, uint32_t b) {
-    return lut ? ((lut[(a << 3) | (b >> 5)] >> (b & 31)) & 1) : a == b;
-}
 
 // NW cell as NWScore computes it (:40-44 / :56-59).
 __device__ __forceinline__ int32_t hb_cell(int32_t hd, int32_t hu, int32_t hl, bool v, const HbScore& s) {
@@ -129,7 +126,7 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
                     int32_t hd = prev_up, hu = up_h;
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
-                        const int32_t h = hb_cell(hd, hu, Hp[r], hb_match(lut, a[r], sym), sc);
+                        const int32_t h = hb_cell(hd, hu, Hp[r], dc_match(lut, a[r], sym), sc);
                         hd = Hp[r];
                         Hp[r] = h;
                         hu = h;
@@ -180,29 +177,6 @@ __global__ __launch_bounds__(64) void hb_split_kernel(const HbSplit* splits, con
 }
 
 // ---------------------------------------------------------------------------- leaves
-// Row / symbol accessors for the leaf solver: global scratch, or LDS laid out item-major
-// (element k of thread t at k * 64 + t: conflict-free when the threads are in step).
-typedef int32_t __attribute__((address_space(3))) hb_lds_i32;
-typedef uint8_t __attribute__((address_space(3))) hb_lds_u8;
-struct GRow {
-    int32_t* p;
-    __device__ int32_t& operator[](int k) const { return p[k]; }
-};
-struct LRow {
-    hb_lds_i32* p;
-    __device__ hb_lds_i32& operator[](int k) const { return p[k * 64]; }
-};
-struct GSeq {
-    const uint8_t* p;
-    __device__ uint32_t operator[](int k) const { return p[k]; }
-    __device__ GSeq shifted(int k) const { return GSeq{p + k}; }
-};
-struct LSeq {
-    const hb_lds_u8* p;
-    __device__ uint32_t operator[](int k) const { return p[k * 64]; }
-    __device__ LSeq shifted(int k) const { return LSeq{p + k * 64}; }
-};
-
 template <typename Row, typename Seq>
 __device__ void hb_nwscore(Seq A, int alen, int arev, Seq B, int blen, int brev,
                            const uint32_t* lut, const HbScore& sc, Row& F, Row& X) {
@@ -215,7 +189,7 @@ __device__ void hb_nwscore(Seq A, int alen, int arev, Seq B, int blen, int brev,
         for (int j = 1; j <= blen; ++j) {
             const uint32_t bj = brev ? B[blen - j] : B[j - 1];
             const int32_t up = F[j];
-            left = hb_cell(diag, up, left, hb_match(lut, ai, bj), sc);
+            left = hb_cell(diag, up, left, dc_match(lut, ai, bj), sc);
             X[j] = left;
             diag = up;
         }
@@ -233,11 +207,11 @@ __device__ int hb_nw_small(const uint8_t* A, int m, const uint8_t* B, int n, con
     for (int i = 1; i <= m; ++i)
         for (int j = 1; j <= n; ++j)
             H[i * w + j] = hb_cell(H[(i - 1) * w + j - 1], H[(i - 1) * w + j], H[i * w + j - 1],
-                                   hb_match(lut, A[i - 1], B[j - 1]), sc);
+                                   dc_match(lut, A[i - 1], B[j - 1]), sc);
     int k = 0, i = m, j = n;
     while (i > 0 || j > 0) {
         if (i > 0 && j > 0) {
-            const bool v = hb_match(lut, A[i - 1], B[j - 1]);
+            const bool v = dc_match(lut, A[i - 1], B[j - 1]);
             const int32_t hd = H[(i - 1) * w + j - 1];
             const int32_t dt = sc.allow ? hd + (v ? sc.match : sc.mismatch) : (v ? hd + sc.match : INT_MIN);
             if (H[i * w + j] == dt) {
@@ -317,11 +291,11 @@ __global__ __launch_bounds__(64) void hb_leaf_kernel(const uint8_t* s1, const ui
     uint8_t* out = outops + L.out;
     int k;
     if (L.alen <= kHbLdsCols && L.blen <= kHbLdsCols) {
-        hb_lds_u8* q1 = (hb_lds_u8*)s_seq + t;
-        hb_lds_u8* q2 = q1 + kHbLdsCols * 64;
+        dc_lds_u8* q1 = (dc_lds_u8*)s_seq + t;
+        dc_lds_u8* q2 = q1 + kHbLdsCols * 64;
         for (int c = 0; c < L.alen; ++c) q1[c * 64] = g1[c];
         for (int c = 0; c < L.blen; ++c) q2[c * 64] = g2[c];
-        hb_lds_i32* r0 = (hb_lds_i32*)s_rows + t;
+        dc_lds_i32* r0 = (dc_lds_i32*)s_rows + t;
         const LRow F{r0}, X{r0 + (kHbLdsCols + 1) * 64}, Cc{r0 + 2 * (kHbLdsCols + 1) * 64};
         k = hb_leaf_solve(LSeq{q1}, LSeq{q2}, g1, g2, L.alen, L.blen, L.top != 0, F, X, Cc, Hs, out, score + id,
                           lut, sc);
@@ -342,28 +316,6 @@ struct Sub {
     int32_t m, n;
     bool top;
 };
-
-template <typename T>
-struct DevBuf {
-    T* p = nullptr;
-    size_t n = 0;
-    hipError_t alloc(size_t count) {
-        if (count <= n && p) return hipSuccess;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        n = 0;
-        hipError_t e = hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T));
-        if (e == hipSuccess) n = count;
-        return e;
-    }
-    ~DevBuf() { if (p) (void)hipFree(p); }
-};
-
-#define HB_HIP(call)                                                    \
-    do {                                                                \
-        hipError_t e_ = (call);                                         \
-        if (e_ != hipSuccess) { *err = std::string(#call) + ": " + hipGetErrorString(e_); return -1; } \
-    } while (0)
 
 hipError_t launch_sweeps(int R, uint32_t count, const uint8_t* d1, const uint8_t* d2, const HbSweep* sw,
                          int32_t* rows, const uint32_t* lut, const HbScore& sc, hipStream_t st) {
@@ -403,9 +355,9 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
     sc.allow = scoring->allow_mismatch != 0;
     sc.mismatch = sc.allow ? scoring->mismatch : INT_MIN;
     std::vector<uint64_t> o1(npairs + 1), o2(npairs + 1);
-    HB_HIP(hipMemcpyAsync(o1.data(), d_o1, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
-    HB_HIP(hipMemcpyAsync(o2.data(), d_o2, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
-    HB_HIP(hipStreamSynchronize(st));
+    SA_DC_HIP(hipMemcpyAsync(o1.data(), d_o1, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
+    SA_DC_HIP(hipMemcpyAsync(o2.data(), d_o2, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
+    SA_DC_HIP(hipStreamSynchronize(st));
     res.assign(npairs, sa_result{});
     std::vector<Sub> cur, leaves;
     cur.reserve(npairs);
@@ -442,24 +394,24 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
             sp.push_back(d);
             maxa = std::max(maxa, s.m - mid);
         }
-        HB_HIP(dsw.alloc(sw.size()));
-        HB_HIP(dsp.alloc(sp.size()));
-        HB_HIP(drows.alloc(rowpos));
-        HB_HIP(dmid.alloc(sp.size()));
-        HB_HIP(dscore.alloc(sp.size()));
-        HB_HIP(hipMemcpyAsync(dsw.p, sw.data(), sw.size() * sizeof(HbSweep), hipMemcpyHostToDevice, st));
-        HB_HIP(hipMemcpyAsync(dsp.p, sp.data(), sp.size() * sizeof(HbSplit), hipMemcpyHostToDevice, st));
+        SA_DC_HIP(dsw.alloc(sw.size()));
+        SA_DC_HIP(dsp.alloc(sp.size()));
+        SA_DC_HIP(drows.alloc(rowpos));
+        SA_DC_HIP(dmid.alloc(sp.size()));
+        SA_DC_HIP(dscore.alloc(sp.size()));
+        SA_DC_HIP(hipMemcpyAsync(dsw.p, sw.data(), sw.size() * sizeof(HbSweep), hipMemcpyHostToDevice, st));
+        SA_DC_HIP(hipMemcpyAsync(dsp.p, sp.data(), sp.size() * sizeof(HbSplit), hipMemcpyHostToDevice, st));
         int R = 1;
         while (R < 32 && 64 * R < maxa) R *= 2;
-        HB_HIP(launch_sweeps(R, (uint32_t)sw.size(), d1, d2, dsw.p, drows.p, d_lutbits, sc, st));
+        SA_DC_HIP(launch_sweeps(R, (uint32_t)sw.size(), d1, d2, dsw.p, drows.p, d_lutbits, sc, st));
         hipLaunchKernelGGL(hb_split_kernel, dim3((uint32_t)sp.size()), dim3(64), 0, st, dsp.p, drows.p, dmid.p,
                            dscore.p);
-        HB_HIP(hipGetLastError());
+        SA_DC_HIP(hipGetLastError());
         mid2.resize(sp.size());
         tops.resize(sp.size());
-        HB_HIP(hipMemcpyAsync(mid2.data(), dmid.p, sp.size() * 4, hipMemcpyDeviceToHost, st));
-        HB_HIP(hipMemcpyAsync(tops.data(), dscore.p, sp.size() * 4, hipMemcpyDeviceToHost, st));
-        HB_HIP(hipStreamSynchronize(st));
+        SA_DC_HIP(hipMemcpyAsync(mid2.data(), dmid.p, sp.size() * 4, hipMemcpyDeviceToHost, st));
+        SA_DC_HIP(hipMemcpyAsync(tops.data(), dscore.p, sp.size() * 4, hipMemcpyDeviceToHost, st));
+        SA_DC_HIP(hipStreamSynchronize(st));
         next.clear();
         for (size_t k = 0; k < split.size(); ++k) {
             const Sub& s = split[k];
@@ -485,58 +437,26 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
         static thread_local DevBuf<HbLeaf> dlv;
         static thread_local DevBuf<int32_t> dscr, dnout, dlscore;
         static thread_local DevBuf<uint8_t> dout;
-        HB_HIP(dlv.alloc(lv.size()));
-        HB_HIP(dscr.alloc(scr));
-        HB_HIP(dnout.alloc(lv.size()));
-        HB_HIP(dlscore.alloc(lv.size()));
-        HB_HIP(dout.alloc(outpos));
-        HB_HIP(hipMemcpyAsync(dlv.p, lv.data(), lv.size() * sizeof(HbLeaf), hipMemcpyHostToDevice, st));
+        SA_DC_HIP(dlv.alloc(lv.size()));
+        SA_DC_HIP(dscr.alloc(scr));
+        SA_DC_HIP(dnout.alloc(lv.size()));
+        SA_DC_HIP(dlscore.alloc(lv.size()));
+        SA_DC_HIP(dout.alloc(outpos));
+        SA_DC_HIP(hipMemcpyAsync(dlv.p, lv.data(), lv.size() * sizeof(HbLeaf), hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(hb_leaf_kernel, dim3((uint32_t)((lv.size() + 63) / 64)), dim3(64), 0, st, d1, d2, dlv.p,
                            (uint32_t)lv.size(), dscr.p, dout.p, dnout.p, dlscore.p, d_lutbits, sc);
-        HB_HIP(hipGetLastError());
+        SA_DC_HIP(hipGetLastError());
         std::vector<int32_t> nout(lv.size()), lscore(lv.size());
         std::vector<uint8_t> lops(outpos);
-        HB_HIP(hipMemcpyAsync(nout.data(), dnout.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
-        HB_HIP(hipMemcpyAsync(lscore.data(), dlscore.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
-        if (outpos) HB_HIP(hipMemcpyAsync(lops.data(), dout.p, outpos, hipMemcpyDeviceToHost, st));
-        HB_HIP(hipStreamSynchronize(st));
+        SA_DC_HIP(hipMemcpyAsync(nout.data(), dnout.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
+        SA_DC_HIP(hipMemcpyAsync(lscore.data(), dlscore.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
+        if (outpos) SA_DC_HIP(hipMemcpyAsync(lops.data(), dout.p, outpos, hipMemcpyDeviceToHost, st));
+        SA_DC_HIP(hipStreamSynchronize(st));
         lap("leaves (kernel + D2H)");
-        // assembly: a pair's leaves in Seq1 order, forward ops reversed into traceback order.
-        // Leaves are bucketed by pair (counting sort), each pair assembled independently.
-        std::vector<uint32_t> start(npairs + 1, 0), order(lv.size());
-        for (const Sub& s : leaves) ++start[s.pair + 1];
-        for (uint32_t p = 0; p < npairs; ++p) start[p + 1] += start[p];
-        {
-            std::vector<uint32_t> pos(start.begin(), start.end() - 1);
-            for (uint32_t k = 0; k < lv.size(); ++k) order[pos[leaves[k].pair]++] = k;
-        }
-        ops.assign(o1[npairs] + o2[npairs] + npairs, 0);
-        auto assemble = [&](uint32_t p0, uint32_t p1) {
-            for (uint32_t p = p0; p < p1; ++p) {
-                uint32_t* b0 = order.data() + start[p];
-                uint32_t* b1 = order.data() + start[p + 1];
-                std::sort(b0, b1, [&](uint32_t x, uint32_t y) { return leaves[x].a0 < leaves[y].a0; });
-                uint32_t total = 0;
-                for (uint32_t* q = b0; q < b1; ++q) total += (uint32_t)nout[*q];
-                sa_result& r = res[p];
-                r.end_i = (int32_t)(o1[p + 1] - o1[p]);
-                r.end_j = (int32_t)(o2[p + 1] - o2[p]);
-                r.nops = total;
-                // forward op f lands at traceback index total - 1 - f
-                uint8_t* dst = ops.data() + o1[p] + o2[p] + p + total;
-                for (uint32_t* q = b0; q < b1; ++q) {
-                    const uint32_t k = *q;
-                    if (leaves[k].top) r.score = lscore[k];
-                    const uint8_t* src = lops.data() + lv[k].out;
-                    for (int32_t c = 0; c < nout[k]; ++c) *--dst = src[c];
-                }
-            }
-        };
-        const uint32_t nth = std::max<uint32_t>(1, std::min<uint32_t>(16, npairs / 64));
-        std::vector<std::thread> pool;
-        for (uint32_t t = 0; t < nth; ++t)
-            pool.emplace_back(assemble, (uint32_t)((uint64_t)npairs * t / nth), (uint32_t)((uint64_t)npairs * (t + 1) / nth));
-        for (auto& th : pool) th.join();
+        std::vector<DcLeafRef> refs(lv.size());
+        for (size_t k = 0; k < lv.size(); ++k)
+            refs[k] = DcLeafRef{leaves[k].pair, leaves[k].a0, leaves[k].b0, lv[k].out, leaves[k].top};
+        dc_assemble(npairs, o1, o2, refs, nout, lscore, lops, res, ops);
         lap("assembly (host)");
     } else {
         ops.assign(o1[npairs] + o2[npairs] + npairs, 0);

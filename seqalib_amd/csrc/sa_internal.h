@@ -103,5 +103,9 @@ namespace sa {
 int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
                    const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
                    std::vector<sa_result>& res, std::vector<uint8_t>& ops, std::string* err);
+// MyersMillerSA (sa_myersmiller.hip): same contract as hirschberg_run.
+int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
+                    const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
+                    std::vector<sa_result>& res, std::vector<uint8_t>& ops, std::string* err);
 
 }  // namespace sa

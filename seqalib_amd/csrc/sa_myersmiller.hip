@@ -1,0 +1,522 @@
+// sa_myersmiller.hip — MyersMillerSA::getAlignment (SAMyersMiller.h:43-420) on the GPU, batched
+// over pairs: linear-space affine-gap global alignment whose result is exactly the reference's
+// (its midpoint tie rules, boundary gap opens tb/te and base cases), not merely an optimal one.
+//
+// Breadth-first over all pairs at once, like sa_hirschberg.hip:
+//   * device levels: every subproblem with more than kMmLeafRows rows of Seq1 and >= 1 column is
+//     split.  Its forward sweep (CC/DD over the top half, :172-238) and reverse sweep (RR/SS over
+//     the bottom half read backwards, :247-313) become two rows of one batched launch of
+//     mm_sweep_kernel (score-only affine DP, one wave per sweep, anti-diagonal wavefront; each
+//     sweep writes its last C and D rows); mm_split_kernel then takes, per subproblem, the FIRST
+//     j in [0, N] maximising max(CC[j] + RR[j], DD[j] + SS[j] - g) and the midpoint type
+//     (type 2 iff the gap term is not strictly smaller, :320-340); the host forms the children
+//     with their tb/te (:358-395).  A type-2 midpoint's two deletions (:390-392) become a leaf
+//     of 2 rows and 0 columns, which emits exactly those.
+//   * leaves: mm_leaf_kernel, one thread per subproblem, runs the same recursion iteratively
+//     (explicit stack, left child first) including the base cases N == 0, M == 0 and M == 1
+//     (:57-160, with its "failsafe" pair of gap entries).
+//   * assembly: dc_assemble (sa_dc.h).
+// Score reported (the reference exposes none): the top call's optimum — its midpoint maximum,
+// the M == 1 maximum, or the boundary value of an empty side (oracle: align_myers_miller).
+//
+// The reverse sweep is computed as a forward sweep over the reversed sequences with t0 = te, so
+// RR[j] = Crev[N - j] and SS[j] = Drev[N - j] (including SS[N] = RR[N], :313).
+#include <hip/hip_runtime.h>
+#include <limits.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "sa_dc.h"
+#include "sa_internal.h"
+
+namespace sa {
+
+constexpr int kMmLeafRows = 48;   // subproblems with <= this many Seq1 rows are leaves
+
+struct MmSweep {       // affine sweep over A (alen) x B (blen) -> C row at out, D row at out + blen + 1
+    uint64_t a, b;     // index of A[0] / B[0] in seq1 / seq2 (rev: of the LAST element, read first)
+    int32_t alen, blen;
+    int32_t rev;       // 1: A and B are both read backwards
+    int32_t t0;        // gap open charged on column 0 (tb forwards, te backwards)
+    uint64_t out;      // int32 index into the row buffer
+};
+
+struct MmSplit {
+    uint64_t fwd, rev; // row indices of the forward / reverse C rows (D follows at + n + 1)
+    int32_t n, pad;
+};
+
+struct MmLeaf {
+    uint64_t a0, b0;   // Seq1 / Seq2 start (indices into seq1 / seq2)
+    int32_t alen, blen;
+    int32_t tb, te;
+    uint64_t scratch;  // int32 index into the leaf scratch (4 * (blen + 1))
+    uint64_t out;      // byte index into the leaf op buffer (capacity alen + blen)
+    int32_t top, pad;
+};
+
+struct MmScore {
+    int32_t g, h, match, mismatch, allow;   // mismatch = INT_MIN when !allow (:15)
+};
+
+// diagonal candidate of c = max({DD, e, s + Similarity}) (:218-232); INT_MIN drops out of the max
+__device__ __forceinline__ int32_t mm_diag(int32_t s, bool v, const MmScore& sc) {
+    return (sc.allow || v) ? s + (v ? sc.match : sc.mismatch) : INT_MIN;
+}
+
+// ------------------------------------------------------------------ batched affine sweeps
+// Lane t owns R consecutive rows of a 64R-row band and computes column s - t at step s.  Per
+// row it keeps C and e (the horizontal-gap state) of the previous column; (C, D) of the row
+// above come from the lane above via DPP wave_shr:1 (lane 0: the previous band's last row,
+// written in place to the output rows, or the top boundary).
+template <int R>
+__global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const uint8_t* s2, const MmSweep* sweeps,
+                                                      int32_t* rows, const uint32_t* lutbits, MmScore sc) {
+    __shared__ uint32_t s_lut[2048];
+    const int lane = threadIdx.x;
+    const MmSweep d = sweeps[blockIdx.x];
+    if (lutbits) {
+        for (int k = lane; k < 2048; k += 64) s_lut[k] = lutbits[k];
+        __syncthreads();
+    }
+    const uint32_t* lut = lutbits ? s_lut : nullptr;
+    const int m = d.alen, n = d.blen, g = sc.g, h = sc.h;
+    int32_t* outC = rows + d.out;
+    int32_t* outD = outC + n + 1;
+    auto symA = [&](int k) -> uint32_t { return d.rev ? s1[d.a - k] : s1[d.a + k]; };
+    auto symB = [&](int k) -> uint32_t { return d.rev ? s2[d.b - k] : s2[d.b + k]; };
+    constexpr int BAND = 64 * R;
+    const int bands = (m + BAND - 1) / BAND;
+    const int lastb = bands - 1;
+    const int tl = ((m - 1) % BAND) / R, rl = (m - 1) % R;   // owner of row m-1 in the last band
+    int32_t cl = 0, dl = 0;                                   // this lane's last row: C, D
+    for (int band = 0; band < bands; ++band) {
+        const int row0 = band * BAND + lane * R;
+        uint32_t a[R];
+        int32_t Cp[R], Ep[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            a[r] = row0 + r < m ? symA(row0 + r) : 0u;
+            Cp[r] = d.t0 + h * (row0 + r + 1);               // C[i][0] = t0 + i h (:192-197)
+            Ep[r] = Cp[r] + g;                               // e = t + g (:198)
+        }
+        int32_t prev_up = row0 == 0 ? 0 : d.t0 + h * row0;   // C[row0][0]; C[0][0] = 0 (:172)
+        // Per 64-step chunk, lane k holds column c0+k's row-above (C, D) (for lane 0) and Seq2
+        // symbol, loaded one chunk ahead; they reach their lane by DPP like the fill kernel.
+        auto load_chunk = [&](int c0, int32_t& vc, int32_t& vd, uint32_t& vs) {
+            const int j = c0 + lane;
+            vc = 0;
+            vd = 0;
+            vs = 0;
+            if (j < n) {
+                if (band == 0) {
+                    vc = g + h * (j + 1);                    // CC[j] = g + j h, DD[j] = CC[j] + g (:183-188)
+                    vd = vc + g;
+                } else {
+                    vc = outC[j + 1];
+                    vd = outD[j + 1];
+                }
+                vs = symB(j);
+            }
+        };
+        int32_t vc, vd, nvc, nvd;
+        uint32_t vs, nvs, sym = 0;
+        load_chunk(0, vc, vd, vs);
+        for (int c0 = 0; c0 < n + 63; c0 += 64) {
+            load_chunk(c0 + 64, nvc, nvd, nvs);
+            const int steps = min(64, n + 63 - c0);
+            for (int q = 0; q < steps; ++q) {
+                const int s = c0 + q;
+                const int32_t up_c = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vc, q), cl, 0x138, 0xf, 0xf,
+                                                                 false);
+                const int32_t up_d = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vd, q), dl, 0x138, 0xf, 0xf,
+                                                                 false);
+                sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vs, q), sym, 0x138, 0xf, 0xf, false);
+                const int j0 = s - lane;
+                if (j0 >= 0 && j0 < n) {
+                    int32_t cd = prev_up, cu = up_c, du = up_d, dsel = 0;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int32_t e = max(Ep[r], Cp[r] + g) + h;   // :202
+                        const int32_t dd = max(du, cu + g) + h;        // :203
+                        const int32_t c = max(max(dd, e), mm_diag(cd, dc_match(lut, a[r], sym), sc));
+                        cd = Cp[r];
+                        Cp[r] = c;
+                        Ep[r] = e;
+                        cu = c;
+                        du = dd;
+                        if (r == rl) dsel = dd;
+                    }
+                    prev_up = up_c;
+                    cl = Cp[R - 1];
+                    dl = du;
+                    if (band < lastb) {
+                        if (lane == 63) {                     // this band's last row, in place
+                            outC[j0 + 1] = cl;
+                            outD[j0 + 1] = dl;
+                        }
+                    } else if (lane == tl) {
+                        outC[j0 + 1] = Cp[rl];                // row m of the sweep (uniform index)
+                        outD[j0 + 1] = dsel;
+                    }
+                }
+            }
+            vc = nvc;
+            vd = nvd;
+            vs = nvs;
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+    if (lane == 0) {
+        outC[0] = d.t0 + h * m;
+        outD[0] = outC[0];                                    // DD[0] = CC[0] (:238)
+    }
+}
+
+// ---------------------------------------------------------------------------- split
+// out3[3k] = index, out3[3k+1] = type (1: type 2), out3[3k+2] = the maximum (:320-340)
+__global__ __launch_bounds__(64) void mm_split_kernel(const MmSplit* splits, const int32_t* rows, int32_t* out3,
+                                                      int32_t g) {
+    const int lane = threadIdx.x;
+    const MmSplit d = splits[blockIdx.x];
+    const int n = d.n;
+    const int32_t* C = rows + d.fwd;
+    const int32_t* D = C + n + 1;
+    const int32_t* Cr = rows + d.rev;
+    const int32_t* Dr = Cr + n + 1;
+    int32_t best = INT_MIN;
+    int idx = 0, ty = 0;
+    for (int j = lane; j <= n; j += 64) {
+        const int32_t c1 = C[j] + Cr[n - j];
+        const int32_t c2 = D[j] + Dr[n - j] - g;
+        const int32_t t = max(c1, c2);
+        if (t > best) { best = t; idx = j; ty = c1 > c2 ? 0 : 1; }
+    }
+    // lexicographic (max, -j): the reference keeps the FIRST maximum (temp > max, :326)
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const int32_t ob = __shfl_xor(best, off);
+        const int oi = __shfl_xor(idx, off);
+        const int ot = __shfl_xor(ty, off);
+        if (ob > best || (ob == best && oi < idx)) { best = ob; idx = oi; ty = ot; }
+    }
+    if (lane == 0) {
+        out3[3 * blockIdx.x] = idx;
+        out3[3 * blockIdx.x + 1] = ty;
+        out3[3 * blockIdx.x + 2] = best;
+    }
+}
+
+// ---------------------------------------------------------------------------- leaves
+// One sweep of buildResultRec (forward :172-238, or reversed = :247-313) into C, D [0..blen].
+template <typename Row, typename Seq>
+__device__ void mm_sweep_thread(Seq A, int alen, int rev, Seq B, int blen, int32_t t0, const uint32_t* lut,
+                                const MmScore& sc, Row C, Row D) {
+    const int32_t g = sc.g, h = sc.h;
+    int32_t t = g;
+    C[0] = 0;
+    for (int j = 1; j <= blen; ++j) {
+        t += h;
+        C[j] = t;
+        D[j] = t + g;
+    }
+    t = t0;
+    for (int i = 1; i <= alen; ++i) {
+        const uint32_t ai = rev ? A[alen - i] : A[i - 1];
+        int32_t s = C[0];
+        t += h;
+        int32_t c = t;
+        C[0] = c;
+        int32_t e = t + g;
+        for (int j = 1; j <= blen; ++j) {
+            const uint32_t bj = rev ? B[blen - j] : B[j - 1];
+            e = max(e, c + g) + h;
+            const int32_t cj = C[j];
+            const int32_t dj = max(D[j], cj + g) + h;
+            D[j] = dj;
+            c = max(max(dj, e), mm_diag(s, dc_match(lut, ai, bj), sc));
+            s = cj;
+            C[j] = c;
+        }
+    }
+    D[0] = C[0];
+}
+
+template <typename Row, typename Seq>
+__device__ int mm_leaf_solve(Seq S1, Seq S2, int alen, int blen, int32_t tb0, int32_t te0, bool top, Row C, Row D,
+                             Row Cr, Row Dr, uint8_t* out, int32_t* score, const uint32_t* lut, const MmScore& sc) {
+    const int32_t g = sc.g, h = sc.h;
+    int k = 0;
+    int stk[48][6];   // pending subproblems (x0, xl, y0, yl, tb, te); <= 3 per level of a leaf
+    int sp = 0;
+    auto push = [&](int x0, int xl, int y0, int yl, int32_t tb, int32_t te) {
+        stk[sp][0] = x0; stk[sp][1] = xl; stk[sp][2] = y0; stk[sp][3] = yl; stk[sp][4] = tb; stk[sp][5] = te;
+        ++sp;
+    };
+    push(0, alen, 0, blen, tb0, te0);
+    bool first = top;
+    while (sp > 0) {
+        --sp;
+        const int x0 = stk[sp][0], M = stk[sp][1], y0 = stk[sp][2], N = stk[sp][3];
+        const int32_t tb = stk[sp][4], te = stk[sp][5];
+        int32_t sval = 0;
+        if (N == 0) {                                               // :57-66
+            for (int q = 0; q < M; ++q) out[k++] = 'U';
+            sval = M > 0 ? tb + h * M : 0;
+        } else if (M == 0) {                                        // :67-74
+            for (int q = 0; q < N; ++q) out[k++] = 'L';
+            sval = g + h * N;
+        } else if (M == 1) {                                        // :75-160
+            const uint32_t a = S1[x0];
+            const int32_t base = max(tb, te) + h + (g + h * N);
+            int32_t best = INT_MIN;
+            int index = 0;
+            for (int j = 1; j <= N; ++j) {
+                const bool v = dc_match(lut, a, S2[y0 + j - 1]);
+                int32_t t = base;
+                if (sc.allow || v) t = max(t, g + h * (j - 1) + (v ? sc.match : sc.mismatch) + g + h * (N - j));
+                if (t > best) { best = t; index = j; }
+            }
+            for (int j = 1; j <= N; ++j) {
+                if (j == index) {
+                    const bool v = dc_match(lut, a, S2[y0 + j - 1]);
+                    if (!sc.allow && !v) { out[k++] = 'U'; out[k++] = 'L'; }   // :141-147
+                    else out[k++] = v ? 'M' : 'S';
+                } else {
+                    out[k++] = 'L';
+                }
+            }
+            sval = best;
+        } else {
+            const int mid = M / 2;
+            mm_sweep_thread(S1.shifted(x0), mid, 0, S2.shifted(y0), N, tb, lut, sc, C, D);
+            mm_sweep_thread(S1.shifted(x0 + mid), M - mid, 1, S2.shifted(y0), N, te, lut, sc, Cr, Dr);
+            int index = 0, type2 = 0;
+            int32_t best = INT_MIN;
+            for (int j = 0; j <= N; ++j) {                          // :320-340
+                const int32_t c1 = C[j] + Cr[N - j];
+                const int32_t c2 = D[j] + Dr[N - j] - g;
+                const int32_t t = max(c1, c2);
+                if (t > best) { best = t; index = j; type2 = c1 > c2 ? 0 : 1; }
+            }
+            sval = best;
+            // children pushed right first: the left one is finished first (:371-372, :388-394)
+            if (!type2) {
+                push(x0 + mid, M - mid, y0 + index, N - index, g, te);
+                push(x0, mid, y0, index, tb, g);
+            } else {
+                push(x0 + mid + 1, M - mid - 1, y0 + index, N - index, 0, te);
+                push(x0 + mid - 1, 2, y0 + index, 0, 0, 0);         // the two deletions :390-392
+                push(x0, mid - 1, y0, index, tb, 0);
+            }
+        }
+        if (first) {
+            *score = sval;
+            first = false;
+        }
+    }
+    return k;
+}
+
+constexpr int kMmLdsCols = 64;   // leaves with |Seq1|, |Seq2| <= this run with LDS rows + symbols
+
+__global__ __launch_bounds__(64) void mm_leaf_kernel(const uint8_t* s1, const uint8_t* s2, const MmLeaf* leaves,
+                                                     uint32_t nleaves, int32_t* scratch, uint8_t* outops,
+                                                     int32_t* nout, int32_t* score, const uint32_t* lut,
+                                                     MmScore sc) {
+    __shared__ int32_t s_rows[4 * (kMmLdsCols + 1) * 64];
+    __shared__ uint8_t s_seq[2 * kMmLdsCols * 64];
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= nleaves) return;
+    const int t = threadIdx.x;
+    const MmLeaf L = leaves[id];
+    const uint8_t* g1 = s1 + L.a0;
+    const uint8_t* g2 = s2 + L.b0;
+    uint8_t* out = outops + L.out;
+    int k;
+    if (L.alen <= kMmLdsCols && L.blen <= kMmLdsCols) {
+        dc_lds_u8* q1 = (dc_lds_u8*)s_seq + t;
+        dc_lds_u8* q2 = q1 + kMmLdsCols * 64;
+        for (int c = 0; c < L.alen; ++c) q1[c * 64] = g1[c];
+        for (int c = 0; c < L.blen; ++c) q2[c * 64] = g2[c];
+        dc_lds_i32* r0 = (dc_lds_i32*)s_rows + t;
+        constexpr int W = (kMmLdsCols + 1) * 64;
+        k = mm_leaf_solve(LSeq{q1}, LSeq{q2}, L.alen, L.blen, L.tb, L.te, L.top != 0, LRow{r0}, LRow{r0 + W},
+                          LRow{r0 + 2 * W}, LRow{r0 + 3 * W}, out, score + id, lut, sc);
+    } else {
+        int32_t* F = scratch + L.scratch;
+        const int W = L.blen + 1;
+        k = mm_leaf_solve(GSeq{g1}, GSeq{g2}, L.alen, L.blen, L.tb, L.te, L.top != 0, GRow{F}, GRow{F + W},
+                          GRow{F + 2 * W}, GRow{F + 3 * W}, out, score + id, lut, sc);
+    }
+    nout[id] = k;
+}
+
+// ---------------------------------------------------------------------------- host driver
+namespace {
+
+struct Sub {
+    uint32_t pair;
+    uint64_t a0, b0;   // absolute indices into seq1 / seq2
+    int32_t m, n;
+    int32_t tb, te;
+    bool top;
+};
+
+hipError_t launch_mm_sweeps(int R, uint32_t count, const uint8_t* d1, const uint8_t* d2, const MmSweep* sw,
+                            int32_t* rows, const uint32_t* lut, const MmScore& sc, hipStream_t st) {
+    const dim3 grid(count), block(64);
+    switch (R) {
+        case 1: hipLaunchKernelGGL(mm_sweep_kernel<1>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 2: hipLaunchKernelGGL(mm_sweep_kernel<2>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 4: hipLaunchKernelGGL(mm_sweep_kernel<4>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 8: hipLaunchKernelGGL(mm_sweep_kernel<8>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        default: hipLaunchKernelGGL(mm_sweep_kernel<16>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// Host driver: inputs on the device (offsets too), results and the traceback-order op streams
+// returned in host memory (res[npairs], ops laid out at off1[p] + off2[p] + p).
+int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
+                    const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
+                    std::vector<sa_result>& res, std::vector<uint8_t>& ops, std::string* err) {
+    const bool timing = getenv("SEQALIB_MM_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto t_mark = now();
+    auto lap = [&](const char* what) {
+        if (!timing) return;
+        const auto t = now();
+        fprintf(stderr, "[mm] %-28s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_mark).count());
+        t_mark = t;
+    };
+    int leaf_rows = kMmLeafRows;   // tuning override: SEQALIB_MM_LEAF (the leaf stack bounds it)
+    if (const char* lr = getenv("SEQALIB_MM_LEAF")) leaf_rows = std::min(4096, std::max(2, atoi(lr)));
+    MmScore sc;
+    sc.g = scoring->gap_open;
+    sc.h = scoring->gap_extend;
+    sc.match = scoring->match;
+    sc.allow = scoring->allow_mismatch != 0;
+    sc.mismatch = sc.allow ? scoring->mismatch : INT_MIN;
+    std::vector<uint64_t> o1(npairs + 1), o2(npairs + 1);
+    SA_DC_HIP(hipMemcpyAsync(o1.data(), d_o1, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
+    SA_DC_HIP(hipMemcpyAsync(o2.data(), d_o2, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
+    SA_DC_HIP(hipStreamSynchronize(st));
+    res.assign(npairs, sa_result{});
+    std::vector<Sub> cur, leaves;
+    cur.reserve(npairs);
+    for (uint32_t p = 0; p < npairs; ++p)
+        cur.push_back(Sub{p, o1[p], o2[p], (int32_t)(o1[p + 1] - o1[p]), (int32_t)(o2[p + 1] - o2[p]), sc.g, sc.g,
+                          true});   // getAlignment: buildResultRec(.., GapOpen, GapOpen) (:417)
+
+    static thread_local DevBuf<MmSweep> dsw;
+    static thread_local DevBuf<MmSplit> dsp;
+    static thread_local DevBuf<int32_t> drows, dout3;
+    std::vector<MmSweep> sw;
+    std::vector<MmSplit> sp;
+    std::vector<Sub> split, next;
+    std::vector<int32_t> out3;
+    while (!cur.empty()) {
+        split.clear();
+        for (const Sub& s : cur) (s.m > leaf_rows && s.n >= 1 ? split : leaves).push_back(s);
+        if (split.empty()) break;
+        sw.clear();
+        sp.clear();
+        uint64_t rowpos = 0;
+        int maxa = 0;
+        for (const Sub& s : split) {
+            const int mid = s.m / 2;
+            MmSplit d;
+            d.n = s.n;
+            d.pad = 0;
+            d.fwd = rowpos;
+            sw.push_back(MmSweep{s.a0, s.b0, mid, s.n, 0, s.tb, rowpos});
+            rowpos += 2ull * ((uint64_t)s.n + 1);
+            d.rev = rowpos;
+            sw.push_back(MmSweep{s.a0 + (uint64_t)s.m - 1, s.b0 + (uint64_t)s.n - 1, s.m - mid, s.n, 1, s.te, rowpos});
+            rowpos += 2ull * ((uint64_t)s.n + 1);
+            sp.push_back(d);
+            maxa = std::max(maxa, s.m - mid);
+        }
+        SA_DC_HIP(dsw.alloc(sw.size()));
+        SA_DC_HIP(dsp.alloc(sp.size()));
+        SA_DC_HIP(drows.alloc(rowpos));
+        SA_DC_HIP(dout3.alloc(3 * sp.size()));
+        SA_DC_HIP(hipMemcpyAsync(dsw.p, sw.data(), sw.size() * sizeof(MmSweep), hipMemcpyHostToDevice, st));
+        SA_DC_HIP(hipMemcpyAsync(dsp.p, sp.data(), sp.size() * sizeof(MmSplit), hipMemcpyHostToDevice, st));
+        int R = 1;
+        while (R < 16 && 64 * R < maxa) R *= 2;
+        SA_DC_HIP(launch_mm_sweeps(R, (uint32_t)sw.size(), d1, d2, dsw.p, drows.p, d_lutbits, sc, st));
+        hipLaunchKernelGGL(mm_split_kernel, dim3((uint32_t)sp.size()), dim3(64), 0, st, dsp.p, drows.p, dout3.p, sc.g);
+        SA_DC_HIP(hipGetLastError());
+        out3.resize(3 * sp.size());
+        SA_DC_HIP(hipMemcpyAsync(out3.data(), dout3.p, out3.size() * 4, hipMemcpyDeviceToHost, st));
+        SA_DC_HIP(hipStreamSynchronize(st));
+        next.clear();
+        for (size_t k = 0; k < split.size(); ++k) {
+            const Sub& s = split[k];
+            if (s.top) res[s.pair].score = out3[3 * k + 2];
+            const int mid = s.m / 2, j = out3[3 * k];
+            if (!out3[3 * k + 1]) {   // type 1 (:358-374)
+                next.push_back(Sub{s.pair, s.a0, s.b0, mid, j, s.tb, sc.g, false});
+                next.push_back(Sub{s.pair, s.a0 + (uint64_t)mid, s.b0 + (uint64_t)j, s.m - mid, s.n - j, sc.g, s.te, false});
+            } else {                  // type 2 (:375-395)
+                next.push_back(Sub{s.pair, s.a0, s.b0, mid - 1, j, s.tb, 0, false});
+                next.push_back(Sub{s.pair, s.a0 + (uint64_t)mid - 1, s.b0 + (uint64_t)j, 2, 0, 0, 0, false});
+                next.push_back(Sub{s.pair, s.a0 + (uint64_t)mid + 1, s.b0 + (uint64_t)j, s.m - mid - 1, s.n - j, 0, s.te,
+                                   false});
+            }
+        }
+        cur.swap(next);
+        lap("level (sweeps + split)");
+    }
+
+    // leaves: one thread each
+    std::vector<MmLeaf> lv(leaves.size());
+    uint64_t scr = 0, outpos = 0;
+    for (size_t k = 0; k < leaves.size(); ++k) {
+        const Sub& s = leaves[k];
+        lv[k] = MmLeaf{s.a0, s.b0, s.m, s.n, s.tb, s.te, scr, outpos, s.top ? 1 : 0, 0};
+        if (s.m > kMmLdsCols || s.n > kMmLdsCols) scr += 4ull * ((uint64_t)s.n + 1);
+        outpos += (uint64_t)s.m + (uint64_t)s.n;
+    }
+    if (lv.empty()) {
+        ops.assign(o1[npairs] + o2[npairs] + npairs, 0);
+        return 0;
+    }
+    static thread_local DevBuf<MmLeaf> dlv;
+    static thread_local DevBuf<int32_t> dscr, dnout, dlscore;
+    static thread_local DevBuf<uint8_t> dout;
+    SA_DC_HIP(dlv.alloc(lv.size()));
+    SA_DC_HIP(dscr.alloc(scr));
+    SA_DC_HIP(dnout.alloc(lv.size()));
+    SA_DC_HIP(dlscore.alloc(lv.size()));
+    SA_DC_HIP(dout.alloc(outpos));
+    SA_DC_HIP(hipMemcpyAsync(dlv.p, lv.data(), lv.size() * sizeof(MmLeaf), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(mm_leaf_kernel, dim3((uint32_t)((lv.size() + 63) / 64)), dim3(64), 0, st, d1, d2, dlv.p,
+                       (uint32_t)lv.size(), dscr.p, dout.p, dnout.p, dlscore.p, d_lutbits, sc);
+    SA_DC_HIP(hipGetLastError());
+    std::vector<int32_t> nout(lv.size()), lscore(lv.size());
+    std::vector<uint8_t> lops(outpos);
+    SA_DC_HIP(hipMemcpyAsync(nout.data(), dnout.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
+    SA_DC_HIP(hipMemcpyAsync(lscore.data(), dlscore.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
+    if (outpos) SA_DC_HIP(hipMemcpyAsync(lops.data(), dout.p, outpos, hipMemcpyDeviceToHost, st));
+    SA_DC_HIP(hipStreamSynchronize(st));
+    lap("leaves (kernel + D2H)");
+    std::vector<DcLeafRef> refs(lv.size());
+    for (size_t k = 0; k < lv.size(); ++k)
+        refs[k] = DcLeafRef{leaves[k].pair, leaves[k].a0, leaves[k].b0, lv[k].out, leaves[k].top};
+    dc_assemble(npairs, o1, o2, refs, nout, lscore, lops, res, ops);
+    lap("assembly (host)");
+    return 0;
+}
+
+}  // namespace sa

@@ -48,6 +48,7 @@ int main() {
         else if (algo == "nw") { NeedlemanWunschSA<std::string, char, '-'> a(sc, fn); emit(a, s1, s2); }
         else if (algo == "lg") { LocalGotohSA<std::string, char, '-'> a(sc, fn); emit(a, s1, s2); }
         else if (algo == "hb") { HirschbergSA<std::string, char, '-'> a(sc, fn); emit(a, s1, s2); }
+        else if (algo == "mm") { MyersMillerSA<std::string, char, '-'> a(sc, fn); emit(a, s1, s2); }
         else { GlobalGotohSA<std::string, char, '-'> a(sc, fn); emit(a, s1, s2); }
     }
     return 0;
