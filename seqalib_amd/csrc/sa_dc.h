@@ -11,6 +11,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <string.h>
+
 #include <algorithm>
 #include <string>
 #include <thread>
@@ -36,6 +38,27 @@ struct DevBuf {
         return e;
     }
     ~DevBuf() { if (p) (void)hipFree(p); }
+};
+
+// Pinned host staging buffer that only grows (per host thread, like DevBuf): the drivers read
+// offsets, split results and leaf ops back every level, and pageable copies would stall.
+template <typename T>
+struct HostBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t alloc(size_t count) {
+        if (count <= n && p) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipHostMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) n = count;
+        return e;
+    }
+    T& operator[](size_t k) { return p[k]; }
+    const T& operator[](size_t k) const { return p[k]; }
+    T* data() { return p; }
+    ~HostBuf() { if (p) (void)hipHostFree(p); }
 };
 
 // ---- device helpers of the leaf solvers
@@ -67,6 +90,19 @@ struct LSeq {
     __device__ LSeq shifted(int k) const { return LSeq{p + k * 64}; }
 };
 
+// Wait for a stream by polling: the drivers synchronise once per level, and a blocking
+// hipStreamSynchronize here was observed to oversleep by ~20 ms per wait.
+inline hipError_t dc_sync(hipStream_t st) {
+    hipError_t e;
+    while ((e = hipStreamQuery(st)) == hipErrorNotReady) __builtin_ia32_pause();
+    return e;
+}
+
+// Upload pinned host bytes into device memory with a kernel that reads the host buffer directly
+// (hipHostMalloc memory is device-visible), instead of a copy-engine transfer.
+__global__ void dc_upload_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t bytes);
+hipError_t dc_upload(void* dst, const void* pinned_src, uint64_t bytes, hipStream_t st);
+
 #define SA_DC_HIP(call)                                                                              \
     do {                                                                                             \
         hipError_t e_ = (call);                                                                      \
@@ -81,11 +117,11 @@ struct DcLeafRef {
 };
 
 // Fill res[p] (end cell (m, n), nops, score of a top leaf) and ops for every pair.
-inline void dc_assemble(uint32_t npairs, const std::vector<uint64_t>& o1, const std::vector<uint64_t>& o2,
-                        const std::vector<DcLeafRef>& leaves, const std::vector<int32_t>& nout,
-                        const std::vector<int32_t>& lscore, const std::vector<uint8_t>& lops,
-                        std::vector<sa_result>& res, std::vector<uint8_t>& ops) {
-    ops.assign(o1[npairs] + o2[npairs] + npairs, 0);
+inline hipError_t dc_assemble(uint32_t npairs, const uint64_t* o1, const uint64_t* o2, const std::vector<DcLeafRef>& leaves,
+                        const int32_t* nout, const int32_t* lscore, const uint8_t* lops, std::vector<sa_result>& res,
+                        HostBuf<uint8_t>& ops) {
+    if (hipError_t e = ops.alloc(o1[npairs] + o2[npairs] + npairs)) return e;
+    memset(ops.data(), 0, o1[npairs] + o2[npairs] + npairs);
     // bucket leaves by pair (counting sort), then assemble pairs independently on host threads
     std::vector<uint32_t> start(npairs + 1, 0), order(leaves.size());
     for (const DcLeafRef& s : leaves) ++start[s.pair + 1];
@@ -112,7 +148,7 @@ inline void dc_assemble(uint32_t npairs, const std::vector<uint64_t>& o1, const 
             for (uint32_t* q = b0; q < b1; ++q) {
                 const uint32_t k = *q;
                 if (leaves[k].top) r.score = lscore[k];
-                const uint8_t* src = lops.data() + leaves[k].out;
+                const uint8_t* src = lops + leaves[k].out;
                 for (int32_t c = 0; c < nout[k]; ++c) *--dst = src[c];
             }
         }
@@ -122,6 +158,7 @@ inline void dc_assemble(uint32_t npairs, const std::vector<uint64_t>& o1, const 
     for (uint32_t t = 0; t < nth; ++t)
         pool.emplace_back(assemble, (uint32_t)((uint64_t)npairs * t / nth), (uint32_t)((uint64_t)npairs * (t + 1) / nth));
     for (auto& th : pool) th.join();
+    return hipSuccess;
 }
 
 }  // namespace sa

@@ -68,18 +68,31 @@ __device__ __forceinline__ int32_t hb_cell(int32_t hd, int32_t hu, int32_t hl, b
     return max(max(sub, hu + s.gap), hl + s.gap);
 }
 
+// The same cell with the match source (LUT) and AllowMismatch fixed at compile time: branch-free.
+template <bool LUT, bool ALLOW>
+__device__ __forceinline__ int32_t hb_cell_t(int32_t hd, int32_t hu, int32_t hl, uint32_t a, uint32_t b,
+                                             const uint32_t* lut, const HbScore& s) {
+    bool v;
+    if constexpr (LUT) v = (lut[(a << 3) | (b >> 5)] >> (b & 31)) & 1;
+    else v = a == b;
+    int32_t sub;
+    if constexpr (ALLOW) sub = hd + (v ? s.match : s.mismatch);
+    else sub = v ? hd + s.match : INT_MIN;
+    return max(max(sub, hu + s.gap), hl + s.gap);
+}
+
 // ------------------------------------------------------------------ batched NWScore sweeps
-template <int R>
+template <int R, bool LUT, bool ALLOW>
 __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const uint8_t* s2, const HbSweep* sweeps,
                                                       int32_t* rows, const uint32_t* lutbits, HbScore sc) {
-    __shared__ uint32_t s_lut[2048];
+    __shared__ uint32_t s_lut[LUT ? 2048 : 1];
     const int lane = threadIdx.x;
     const HbSweep d = sweeps[blockIdx.x];
-    if (lutbits) {
+    if constexpr (LUT) {
         for (int k = lane; k < 2048; k += 64) s_lut[k] = lutbits[k];
         __syncthreads();
     }
-    const uint32_t* lut = lutbits ? s_lut : nullptr;
+    const uint32_t* lut = s_lut;
     int32_t* out = rows + d.out;
     const int m = d.alen, n = d.blen, G = sc.gap;
     auto symA = [&](int k) -> uint32_t { return d.rev ? s1[d.a - k] : s1[d.a + k]; };
@@ -126,7 +139,7 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
                     int32_t hd = prev_up, hu = up_h;
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
-                        const int32_t h = hb_cell(hd, hu, Hp[r], dc_match(lut, a[r], sym), sc);
+                        const int32_t h = hb_cell_t<LUT, ALLOW>(hd, hu, Hp[r], a[r], sym, lut, sc);
                         hd = Hp[r];
                         Hp[r] = h;
                         hu = h;
@@ -317,16 +330,29 @@ struct Sub {
     bool top;
 };
 
+template <bool LUT, bool ALLOW>
+void launch_sweeps_t(int R, dim3 grid, const uint8_t* d1, const uint8_t* d2, const HbSweep* sw, int32_t* rows,
+                     const uint32_t* lut, const HbScore& sc, hipStream_t st) {
+    const dim3 block(64);
+    switch (R) {
+        case 1: hipLaunchKernelGGL((hb_sweep_kernel<1, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 2: hipLaunchKernelGGL((hb_sweep_kernel<2, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 4: hipLaunchKernelGGL((hb_sweep_kernel<4, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 8: hipLaunchKernelGGL((hb_sweep_kernel<8, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 16: hipLaunchKernelGGL((hb_sweep_kernel<16, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        default: hipLaunchKernelGGL((hb_sweep_kernel<32, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+    }
+}
+
 hipError_t launch_sweeps(int R, uint32_t count, const uint8_t* d1, const uint8_t* d2, const HbSweep* sw,
                          int32_t* rows, const uint32_t* lut, const HbScore& sc, hipStream_t st) {
-    const dim3 grid(count), block(64);
-    switch (R) {
-        case 1: hipLaunchKernelGGL(hb_sweep_kernel<1>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 2: hipLaunchKernelGGL(hb_sweep_kernel<2>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 4: hipLaunchKernelGGL(hb_sweep_kernel<4>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 8: hipLaunchKernelGGL(hb_sweep_kernel<8>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 16: hipLaunchKernelGGL(hb_sweep_kernel<16>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        default: hipLaunchKernelGGL(hb_sweep_kernel<32>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+    const dim3 grid(count);
+    if (lut) {
+        if (sc.allow) launch_sweeps_t<true, true>(R, grid, d1, d2, sw, rows, lut, sc, st);
+        else launch_sweeps_t<true, false>(R, grid, d1, d2, sw, rows, lut, sc, st);
+    } else {
+        if (sc.allow) launch_sweeps_t<false, true>(R, grid, d1, d2, sw, rows, lut, sc, st);
+        else launch_sweeps_t<false, false>(R, grid, d1, d2, sw, rows, lut, sc, st);
     }
     return hipGetLastError();
 }
@@ -337,7 +363,8 @@ hipError_t launch_sweeps(int R, uint32_t count, const uint8_t* d1, const uint8_t
 // returned in host memory (res[npairs], ops laid out at off1[p] + off2[p] + p).
 int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
                    const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
-                   std::vector<sa_result>& res, std::vector<uint8_t>& ops, std::string* err) {
+                   std::vector<sa_result>& res, const uint8_t** ops, uint64_t* ops_bytes,
+                   std::string* err) {
     const bool timing = getenv("SEQALIB_HB_TIMING") != nullptr;
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto t_start = now(), t_mark = t_start;
@@ -354,10 +381,14 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
     sc.match = scoring->match;
     sc.allow = scoring->allow_mismatch != 0;
     sc.mismatch = sc.allow ? scoring->mismatch : INT_MIN;
-    std::vector<uint64_t> o1(npairs + 1), o2(npairs + 1);
+    static thread_local HostBuf<uint64_t> o1, o2;
+    SA_DC_HIP(o1.alloc(npairs + 1));
+    SA_DC_HIP(o2.alloc(npairs + 1));
+    static thread_local HostBuf<uint8_t> hops;   // traceback-order op streams, returned in *ops
     SA_DC_HIP(hipMemcpyAsync(o1.data(), d_o1, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
     SA_DC_HIP(hipMemcpyAsync(o2.data(), d_o2, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
-    SA_DC_HIP(hipStreamSynchronize(st));
+    SA_DC_HIP(dc_sync(st));
+    lap("setup (offsets D2H)");
     res.assign(npairs, sa_result{});
     std::vector<Sub> cur, leaves;
     cur.reserve(npairs);
@@ -371,7 +402,7 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
     std::vector<HbSweep> sw;
     std::vector<HbSplit> sp;
     std::vector<Sub> split, next;
-    std::vector<int32_t> mid2, tops;
+    static thread_local HostBuf<int32_t> mid2, tops;
     while (!cur.empty()) {
         split.clear();
         for (const Sub& s : cur) (s.m > leaf_rows && s.n >= 2 ? split : leaves).push_back(s);
@@ -400,6 +431,7 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
         SA_DC_HIP(dmid.alloc(sp.size()));
         SA_DC_HIP(dscore.alloc(sp.size()));
         SA_DC_HIP(hipMemcpyAsync(dsw.p, sw.data(), sw.size() * sizeof(HbSweep), hipMemcpyHostToDevice, st));
+        lap("level: descriptors + H2D");
         SA_DC_HIP(hipMemcpyAsync(dsp.p, sp.data(), sp.size() * sizeof(HbSplit), hipMemcpyHostToDevice, st));
         int R = 1;
         while (R < 32 && 64 * R < maxa) R *= 2;
@@ -407,11 +439,11 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
         hipLaunchKernelGGL(hb_split_kernel, dim3((uint32_t)sp.size()), dim3(64), 0, st, dsp.p, drows.p, dmid.p,
                            dscore.p);
         SA_DC_HIP(hipGetLastError());
-        mid2.resize(sp.size());
-        tops.resize(sp.size());
+        SA_DC_HIP(mid2.alloc(sp.size()));
+        SA_DC_HIP(tops.alloc(sp.size()));
         SA_DC_HIP(hipMemcpyAsync(mid2.data(), dmid.p, sp.size() * 4, hipMemcpyDeviceToHost, st));
         SA_DC_HIP(hipMemcpyAsync(tops.data(), dscore.p, sp.size() * 4, hipMemcpyDeviceToHost, st));
-        SA_DC_HIP(hipStreamSynchronize(st));
+        SA_DC_HIP(dc_sync(st));
         next.clear();
         for (size_t k = 0; k < split.size(); ++k) {
             const Sub& s = split[k];
@@ -446,21 +478,27 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
         hipLaunchKernelGGL(hb_leaf_kernel, dim3((uint32_t)((lv.size() + 63) / 64)), dim3(64), 0, st, d1, d2, dlv.p,
                            (uint32_t)lv.size(), dscr.p, dout.p, dnout.p, dlscore.p, d_lutbits, sc);
         SA_DC_HIP(hipGetLastError());
-        std::vector<int32_t> nout(lv.size()), lscore(lv.size());
-        std::vector<uint8_t> lops(outpos);
+        static thread_local HostBuf<int32_t> nout, lscore;
+        static thread_local HostBuf<uint8_t> lops;
+        SA_DC_HIP(nout.alloc(lv.size()));
+        SA_DC_HIP(lscore.alloc(lv.size()));
+        SA_DC_HIP(lops.alloc(outpos));
         SA_DC_HIP(hipMemcpyAsync(nout.data(), dnout.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
         SA_DC_HIP(hipMemcpyAsync(lscore.data(), dlscore.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
         if (outpos) SA_DC_HIP(hipMemcpyAsync(lops.data(), dout.p, outpos, hipMemcpyDeviceToHost, st));
-        SA_DC_HIP(hipStreamSynchronize(st));
+        SA_DC_HIP(dc_sync(st));
         lap("leaves (kernel + D2H)");
         std::vector<DcLeafRef> refs(lv.size());
         for (size_t k = 0; k < lv.size(); ++k)
             refs[k] = DcLeafRef{leaves[k].pair, leaves[k].a0, leaves[k].b0, lv[k].out, leaves[k].top};
-        dc_assemble(npairs, o1, o2, refs, nout, lscore, lops, res, ops);
+        SA_DC_HIP(dc_assemble(npairs, o1.data(), o2.data(), refs, nout.data(), lscore.data(), lops.data(), res, hops));
         lap("assembly (host)");
     } else {
-        ops.assign(o1[npairs] + o2[npairs] + npairs, 0);
+        SA_DC_HIP(hops.alloc(o1[npairs] + o2[npairs] + npairs));
+        memset(hops.data(), 0, o1[npairs] + o2[npairs] + npairs);
     }
+    *ops = hops.data();
+    *ops_bytes = o1[npairs] + o2[npairs] + npairs;
     return 0;
 }
 

@@ -102,10 +102,14 @@ namespace sa {
 // off1[p] + off2[p] + p).  Returns 0 or -1 with *err set.
 int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
                    const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
-                   std::vector<sa_result>& res, std::vector<uint8_t>& ops, std::string* err);
-// MyersMillerSA (sa_myersmiller.hip): same contract as hirschberg_run.
+                   std::vector<sa_result>& res, const uint8_t** ops, uint64_t* ops_bytes,
+                   std::string* err);
+// MyersMillerSA (sa_myersmiller.hip): same contract as hirschberg_run.  *ops is set to a pinned
+// host buffer owned by the calling thread (valid until its next call) holding
+// off1[npairs] + off2[npairs] + npairs bytes.
 int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
                     const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
-                    std::vector<sa_result>& res, std::vector<uint8_t>& ops, std::string* err);
+                    std::vector<sa_result>& res, const uint8_t** ops, uint64_t* ops_bytes,
+                   std::string* err);
 
 }  // namespace sa

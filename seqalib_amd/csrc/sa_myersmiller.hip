@@ -73,108 +73,132 @@ __device__ __forceinline__ int32_t mm_diag(int32_t s, bool v, const MmScore& sc)
 // Lane t owns R consecutive rows of a 64R-row band and computes column s - t at step s.  Per
 // row it keeps C and e (the horizontal-gap state) of the previous column; (C, D) of the row
 // above come from the lane above via DPP wave_shr:1 (lane 0: the previous band's last row,
-// written in place to the output rows, or the top boundary).
-template <int R>
+// written in place to the output rows, or the top boundary).  LUT / ALLOW are compile-time so
+// the cell is branch-free; LAST (the band holding row m) also captures D of row m.
+template <bool LUT, bool ALLOW>
+__device__ __forceinline__ int32_t mm_diag_t(int32_t cd, uint32_t a, uint32_t b, const uint32_t* lut,
+                                             const MmScore& sc) {
+    bool v;
+    if constexpr (LUT) v = (lut[(a << 3) | (b >> 5)] >> (b & 31)) & 1;
+    else v = a == b;
+    if constexpr (ALLOW) return cd + (v ? sc.match : sc.mismatch);
+    else return v ? cd + sc.match : INT_MIN;
+}
+
+template <int R, bool LUT, bool ALLOW, bool LAST>
+__device__ __forceinline__ void mm_band(const MmSweep& d, const uint8_t* s1, const uint8_t* s2, const uint32_t* lut,
+                                        const MmScore& sc, int band, int32_t* outC, int32_t* outD, int tl, int rl,
+                                        int32_t& cl, int32_t& dl) {
+    const int lane = threadIdx.x;
+    const int m = d.alen, n = d.blen, g = sc.g, h = sc.h;
+    constexpr int BAND = 64 * R;
+    const int row0 = band * BAND + lane * R;
+    uint32_t a[R];
+    int32_t Cp[R], Ep[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        a[r] = row0 + r < m ? (d.rev ? s1[d.a - (row0 + r)] : s1[d.a + (row0 + r)]) : 0u;
+        Cp[r] = d.t0 + h * (row0 + r + 1);                   // C[i][0] = t0 + i h (:192-197)
+        Ep[r] = Cp[r] + g;                                   // e = t + g (:198)
+    }
+    int32_t prev_up = row0 == 0 ? 0 : d.t0 + h * row0;       // C[row0][0]; C[0][0] = 0 (:172)
+    // Per 64-step chunk, lane k holds column c0+k's row-above (C, D) (for lane 0) and Seq2
+    // symbol, loaded one chunk ahead; they reach their lane by DPP like the fill kernel.
+    auto load_chunk = [&](int c0, int32_t& vc, int32_t& vd, uint32_t& vs) {
+        const int j = c0 + lane;
+        vc = 0;
+        vd = 0;
+        vs = 0;
+        if (j < n) {
+            if (band == 0) {
+                vc = g + h * (j + 1);                        // CC[j] = g + j h, DD[j] = CC[j] + g (:183-188)
+                vd = vc + g;
+            } else {
+                vc = outC[j + 1];
+                vd = outD[j + 1];
+            }
+            vs = d.rev ? s2[d.b - j] : s2[d.b + j];
+        }
+    };
+    int32_t vc, vd, nvc, nvd;
+    uint32_t vs, nvs, sym = 0;
+    load_chunk(0, vc, vd, vs);
+    for (int c0 = 0; c0 < n + 63; c0 += 64) {
+        load_chunk(c0 + 64, nvc, nvd, nvs);
+        const int steps = min(64, n + 63 - c0);
+        for (int q = 0; q < steps; ++q) {
+            const int s = c0 + q;
+            const int32_t up_c = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vc, q), cl, 0x138, 0xf, 0xf, false);
+            const int32_t up_d = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vd, q), dl, 0x138, 0xf, 0xf, false);
+            sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vs, q), sym, 0x138, 0xf, 0xf, false);
+            const int j0 = s - lane;
+            if (j0 >= 0 && j0 < n) {
+                int32_t cd = prev_up, cu = up_c, du = up_d, dsel = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int32_t e = max(Ep[r], Cp[r] + g) + h;   // :202
+                    const int32_t dd = max(du, cu + g) + h;        // :203
+                    const int32_t c = max(max(dd, e), mm_diag_t<LUT, ALLOW>(cd, a[r], sym, lut, sc));
+                    cd = Cp[r];
+                    Cp[r] = c;
+                    Ep[r] = e;
+                    cu = c;
+                    du = dd;
+                    if constexpr (LAST) {
+                        if (r == rl) dsel = dd;
+                    }
+                }
+                prev_up = up_c;
+                cl = Cp[R - 1];
+                dl = du;
+                if constexpr (!LAST) {
+                    if (lane == 63) {                         // this band's last row, in place
+                        outC[j0 + 1] = cl;
+                        outD[j0 + 1] = dl;
+                    }
+                } else if (lane == tl) {
+                    int32_t csel = Cp[0];
+#pragma unroll
+                    for (int r = 1; r < R; ++r)
+                        if (r == rl) csel = Cp[r];
+                    outC[j0 + 1] = csel;                      // row m of the sweep
+                    outD[j0 + 1] = dsel;
+                }
+            }
+        }
+        vc = nvc;
+        vd = nvd;
+        vs = nvs;
+    }
+}
+
+template <int R, bool LUT, bool ALLOW>
 __global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const uint8_t* s2, const MmSweep* sweeps,
                                                       int32_t* rows, const uint32_t* lutbits, MmScore sc) {
-    __shared__ uint32_t s_lut[2048];
+    __shared__ uint32_t s_lut[LUT ? 2048 : 1];
     const int lane = threadIdx.x;
     const MmSweep d = sweeps[blockIdx.x];
-    if (lutbits) {
+    if constexpr (LUT) {
         for (int k = lane; k < 2048; k += 64) s_lut[k] = lutbits[k];
         __syncthreads();
     }
-    const uint32_t* lut = lutbits ? s_lut : nullptr;
-    const int m = d.alen, n = d.blen, g = sc.g, h = sc.h;
+    const int m = d.alen, n = d.blen;
     int32_t* outC = rows + d.out;
     int32_t* outD = outC + n + 1;
-    auto symA = [&](int k) -> uint32_t { return d.rev ? s1[d.a - k] : s1[d.a + k]; };
-    auto symB = [&](int k) -> uint32_t { return d.rev ? s2[d.b - k] : s2[d.b + k]; };
     constexpr int BAND = 64 * R;
     const int bands = (m + BAND - 1) / BAND;
-    const int lastb = bands - 1;
     const int tl = ((m - 1) % BAND) / R, rl = (m - 1) % R;   // owner of row m-1 in the last band
     int32_t cl = 0, dl = 0;                                   // this lane's last row: C, D
     for (int band = 0; band < bands; ++band) {
-        const int row0 = band * BAND + lane * R;
-        uint32_t a[R];
-        int32_t Cp[R], Ep[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            a[r] = row0 + r < m ? symA(row0 + r) : 0u;
-            Cp[r] = d.t0 + h * (row0 + r + 1);               // C[i][0] = t0 + i h (:192-197)
-            Ep[r] = Cp[r] + g;                               // e = t + g (:198)
-        }
-        int32_t prev_up = row0 == 0 ? 0 : d.t0 + h * row0;   // C[row0][0]; C[0][0] = 0 (:172)
-        // Per 64-step chunk, lane k holds column c0+k's row-above (C, D) (for lane 0) and Seq2
-        // symbol, loaded one chunk ahead; they reach their lane by DPP like the fill kernel.
-        auto load_chunk = [&](int c0, int32_t& vc, int32_t& vd, uint32_t& vs) {
-            const int j = c0 + lane;
-            vc = 0;
-            vd = 0;
-            vs = 0;
-            if (j < n) {
-                if (band == 0) {
-                    vc = g + h * (j + 1);                    // CC[j] = g + j h, DD[j] = CC[j] + g (:183-188)
-                    vd = vc + g;
-                } else {
-                    vc = outC[j + 1];
-                    vd = outD[j + 1];
-                }
-                vs = symB(j);
-            }
-        };
-        int32_t vc, vd, nvc, nvd;
-        uint32_t vs, nvs, sym = 0;
-        load_chunk(0, vc, vd, vs);
-        for (int c0 = 0; c0 < n + 63; c0 += 64) {
-            load_chunk(c0 + 64, nvc, nvd, nvs);
-            const int steps = min(64, n + 63 - c0);
-            for (int q = 0; q < steps; ++q) {
-                const int s = c0 + q;
-                const int32_t up_c = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vc, q), cl, 0x138, 0xf, 0xf,
-                                                                 false);
-                const int32_t up_d = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vd, q), dl, 0x138, 0xf, 0xf,
-                                                                 false);
-                sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vs, q), sym, 0x138, 0xf, 0xf, false);
-                const int j0 = s - lane;
-                if (j0 >= 0 && j0 < n) {
-                    int32_t cd = prev_up, cu = up_c, du = up_d, dsel = 0;
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        const int32_t e = max(Ep[r], Cp[r] + g) + h;   // :202
-                        const int32_t dd = max(du, cu + g) + h;        // :203
-                        const int32_t c = max(max(dd, e), mm_diag(cd, dc_match(lut, a[r], sym), sc));
-                        cd = Cp[r];
-                        Cp[r] = c;
-                        Ep[r] = e;
-                        cu = c;
-                        du = dd;
-                        if (r == rl) dsel = dd;
-                    }
-                    prev_up = up_c;
-                    cl = Cp[R - 1];
-                    dl = du;
-                    if (band < lastb) {
-                        if (lane == 63) {                     // this band's last row, in place
-                            outC[j0 + 1] = cl;
-                            outD[j0 + 1] = dl;
-                        }
-                    } else if (lane == tl) {
-                        outC[j0 + 1] = Cp[rl];                // row m of the sweep (uniform index)
-                        outD[j0 + 1] = dsel;
-                    }
-                }
-            }
-            vc = nvc;
-            vd = nvd;
-            vs = nvs;
-        }
+        if (band < bands - 1)
+            mm_band<R, LUT, ALLOW, false>(d, s1, s2, s_lut, sc, band, outC, outD, tl, rl, cl, dl);
+        else
+            mm_band<R, LUT, ALLOW, true>(d, s1, s2, s_lut, sc, band, outC, outD, tl, rl, cl, dl);
         __threadfence_block();
         __syncthreads();
     }
     if (lane == 0) {
-        outC[0] = d.t0 + h * m;
+        outC[0] = d.t0 + sc.h * m;
         outD[0] = outC[0];                                    // DD[0] = CC[0] (:238)
     }
 }
@@ -358,6 +382,24 @@ __global__ __launch_bounds__(64) void mm_leaf_kernel(const uint8_t* s1, const ui
     nout[id] = k;
 }
 
+// ---------------------------------------------------------------------------- upload (sa_dc.h)
+__global__ void dc_upload_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t bytes) {
+    const uint64_t n16 = bytes / 16;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n16; k += stride)
+        reinterpret_cast<uint4*>(dst)[k] = reinterpret_cast<const uint4*>(src)[k];
+    if (blockIdx.x == 0 && threadIdx.x < (bytes & 15)) dst[n16 * 16 + threadIdx.x] = src[n16 * 16 + threadIdx.x];
+}
+
+hipError_t dc_upload(void* dst, const void* pinned_src, uint64_t bytes, hipStream_t st) {
+    if (!bytes) return hipSuccess;
+    // both pointers must be 16-byte aligned for the vector path; fall back to bytes otherwise
+    if (((uintptr_t)dst | (uintptr_t)pinned_src) & 15) return hipMemcpyAsync(dst, pinned_src, bytes, hipMemcpyHostToDevice, st);
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(1024, (bytes / 16 + 255) / 256 + 1);
+    hipLaunchKernelGGL(dc_upload_kernel, dim3(blocks), dim3(256), 0, st, (const uint8_t*)pinned_src, (uint8_t*)dst, bytes);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------- host driver
 namespace {
 
@@ -369,15 +411,29 @@ struct Sub {
     bool top;
 };
 
+template <bool LUT, bool ALLOW>
+void launch_mm_sweeps_t(int R, dim3 grid, const uint8_t* d1, const uint8_t* d2, const MmSweep* sw, int32_t* rows,
+                        const uint32_t* lut, const MmScore& sc, hipStream_t st) {
+    const dim3 block(64);
+    switch (R) {
+        case 1: hipLaunchKernelGGL((mm_sweep_kernel<1, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 2: hipLaunchKernelGGL((mm_sweep_kernel<2, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 4: hipLaunchKernelGGL((mm_sweep_kernel<4, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 8: hipLaunchKernelGGL((mm_sweep_kernel<8, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 16: hipLaunchKernelGGL((mm_sweep_kernel<16, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        default: hipLaunchKernelGGL((mm_sweep_kernel<32, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+    }
+}
+
 hipError_t launch_mm_sweeps(int R, uint32_t count, const uint8_t* d1, const uint8_t* d2, const MmSweep* sw,
                             int32_t* rows, const uint32_t* lut, const MmScore& sc, hipStream_t st) {
-    const dim3 grid(count), block(64);
-    switch (R) {
-        case 1: hipLaunchKernelGGL(mm_sweep_kernel<1>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 2: hipLaunchKernelGGL(mm_sweep_kernel<2>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 4: hipLaunchKernelGGL(mm_sweep_kernel<4>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 8: hipLaunchKernelGGL(mm_sweep_kernel<8>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        default: hipLaunchKernelGGL(mm_sweep_kernel<16>, grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+    const dim3 grid(count);
+    if (lut) {
+        if (sc.allow) launch_mm_sweeps_t<true, true>(R, grid, d1, d2, sw, rows, lut, sc, st);
+        else launch_mm_sweeps_t<true, false>(R, grid, d1, d2, sw, rows, lut, sc, st);
+    } else {
+        if (sc.allow) launch_mm_sweeps_t<false, true>(R, grid, d1, d2, sw, rows, lut, sc, st);
+        else launch_mm_sweeps_t<false, false>(R, grid, d1, d2, sw, rows, lut, sc, st);
     }
     return hipGetLastError();
 }
@@ -388,7 +444,8 @@ hipError_t launch_mm_sweeps(int R, uint32_t count, const uint8_t* d1, const uint
 // returned in host memory (res[npairs], ops laid out at off1[p] + off2[p] + p).
 int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
                     const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
-                    std::vector<sa_result>& res, std::vector<uint8_t>& ops, std::string* err) {
+                    std::vector<sa_result>& res, const uint8_t** ops, uint64_t* ops_bytes,
+                   std::string* err) {
     const bool timing = getenv("SEQALIB_MM_TIMING") != nullptr;
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto t_mark = now();
@@ -398,6 +455,10 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
         fprintf(stderr, "[mm] %-28s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_mark).count());
         t_mark = t;
     };
+    if (timing) {
+        (void)hipDeviceSynchronize();
+        lap("entry: device idle");
+    }
     int leaf_rows = kMmLeafRows;   // tuning override: SEQALIB_MM_LEAF (the leaf stack bounds it)
     if (const char* lr = getenv("SEQALIB_MM_LEAF")) leaf_rows = std::min(4096, std::max(2, atoi(lr)));
     MmScore sc;
@@ -406,10 +467,14 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
     sc.match = scoring->match;
     sc.allow = scoring->allow_mismatch != 0;
     sc.mismatch = sc.allow ? scoring->mismatch : INT_MIN;
-    std::vector<uint64_t> o1(npairs + 1), o2(npairs + 1);
+    static thread_local HostBuf<uint64_t> o1, o2;
+    SA_DC_HIP(o1.alloc(npairs + 1));
+    SA_DC_HIP(o2.alloc(npairs + 1));
+    static thread_local HostBuf<uint8_t> hops;   // traceback-order op streams, returned in *ops
     SA_DC_HIP(hipMemcpyAsync(o1.data(), d_o1, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
     SA_DC_HIP(hipMemcpyAsync(o2.data(), d_o2, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
-    SA_DC_HIP(hipStreamSynchronize(st));
+    SA_DC_HIP(dc_sync(st));
+    lap("setup (offsets D2H)");
     res.assign(npairs, sa_result{});
     std::vector<Sub> cur, leaves;
     cur.reserve(npairs);
@@ -423,7 +488,7 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
     std::vector<MmSweep> sw;
     std::vector<MmSplit> sp;
     std::vector<Sub> split, next;
-    std::vector<int32_t> out3;
+    static thread_local HostBuf<int32_t> out3;
     while (!cur.empty()) {
         split.clear();
         for (const Sub& s : cur) (s.m > leaf_rows && s.n >= 1 ? split : leaves).push_back(s);
@@ -451,15 +516,16 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
         SA_DC_HIP(drows.alloc(rowpos));
         SA_DC_HIP(dout3.alloc(3 * sp.size()));
         SA_DC_HIP(hipMemcpyAsync(dsw.p, sw.data(), sw.size() * sizeof(MmSweep), hipMemcpyHostToDevice, st));
+        lap("level: descriptors + H2D");
         SA_DC_HIP(hipMemcpyAsync(dsp.p, sp.data(), sp.size() * sizeof(MmSplit), hipMemcpyHostToDevice, st));
         int R = 1;
-        while (R < 16 && 64 * R < maxa) R *= 2;
+        while (R < 32 && 64 * R < maxa) R *= 2;
         SA_DC_HIP(launch_mm_sweeps(R, (uint32_t)sw.size(), d1, d2, dsw.p, drows.p, d_lutbits, sc, st));
         hipLaunchKernelGGL(mm_split_kernel, dim3((uint32_t)sp.size()), dim3(64), 0, st, dsp.p, drows.p, dout3.p, sc.g);
         SA_DC_HIP(hipGetLastError());
-        out3.resize(3 * sp.size());
-        SA_DC_HIP(hipMemcpyAsync(out3.data(), dout3.p, out3.size() * 4, hipMemcpyDeviceToHost, st));
-        SA_DC_HIP(hipStreamSynchronize(st));
+        SA_DC_HIP(out3.alloc(3 * sp.size()));
+        SA_DC_HIP(hipMemcpyAsync(out3.data(), dout3.p, 3 * sp.size() * 4, hipMemcpyDeviceToHost, st));
+        SA_DC_HIP(dc_sync(st));
         next.clear();
         for (size_t k = 0; k < split.size(); ++k) {
             const Sub& s = split[k];
@@ -489,7 +555,10 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
         outpos += (uint64_t)s.m + (uint64_t)s.n;
     }
     if (lv.empty()) {
-        ops.assign(o1[npairs] + o2[npairs] + npairs, 0);
+        SA_DC_HIP(hops.alloc(o1[npairs] + o2[npairs] + npairs));
+        memset(hops.data(), 0, o1[npairs] + o2[npairs] + npairs);
+        *ops = hops.data();
+    *ops_bytes = o1[npairs] + o2[npairs] + npairs;
         return 0;
     }
     static thread_local DevBuf<MmLeaf> dlv;
@@ -504,18 +573,23 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
     hipLaunchKernelGGL(mm_leaf_kernel, dim3((uint32_t)((lv.size() + 63) / 64)), dim3(64), 0, st, d1, d2, dlv.p,
                        (uint32_t)lv.size(), dscr.p, dout.p, dnout.p, dlscore.p, d_lutbits, sc);
     SA_DC_HIP(hipGetLastError());
-    std::vector<int32_t> nout(lv.size()), lscore(lv.size());
-    std::vector<uint8_t> lops(outpos);
+    static thread_local HostBuf<int32_t> nout, lscore;
+    static thread_local HostBuf<uint8_t> lops;
+    SA_DC_HIP(nout.alloc(lv.size()));
+    SA_DC_HIP(lscore.alloc(lv.size()));
+    SA_DC_HIP(lops.alloc(outpos));
     SA_DC_HIP(hipMemcpyAsync(nout.data(), dnout.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
     SA_DC_HIP(hipMemcpyAsync(lscore.data(), dlscore.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
     if (outpos) SA_DC_HIP(hipMemcpyAsync(lops.data(), dout.p, outpos, hipMemcpyDeviceToHost, st));
-    SA_DC_HIP(hipStreamSynchronize(st));
+    SA_DC_HIP(dc_sync(st));
     lap("leaves (kernel + D2H)");
     std::vector<DcLeafRef> refs(lv.size());
     for (size_t k = 0; k < lv.size(); ++k)
         refs[k] = DcLeafRef{leaves[k].pair, leaves[k].a0, leaves[k].b0, lv[k].out, leaves[k].top};
-    dc_assemble(npairs, o1, o2, refs, nout, lscore, lops, res, ops);
+    SA_DC_HIP(dc_assemble(npairs, o1.data(), o2.data(), refs, nout.data(), lscore.data(), lops.data(), res, hops));
     lap("assembly (host)");
+    *ops = hops.data();
+    *ops_bytes = o1[npairs] + o2[npairs] + npairs;
     return 0;
 }
 

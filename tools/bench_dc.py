@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""HirschbergSA batch timing: P pairs of L x L synthetic DNA, inputs
-resident in HBM, sa_align_batch_device(SA_HIRSCHBERG).  Reports alignment-cell rate
-(m*n per pair / wall time; the linear-space method sweeps ~2*m*n cells) and, when
-oracle/_ref is present, the reference's own HirschbergSA on a CPU sample.
-    python3 tools/bench_hirschberg.py --pairs 1000 --len 4096
+"""Linear-space aligner batch timing: P pairs of L x L synthetic
+DNA, inputs resident in HBM, sa_align_batch_device(SA_HIRSCHBERG or SA_MYERS_MILLER).  Reports
+alignment-cell rate (m*n per pair / wall time; the linear-space methods sweep ~2*m*n cells) and,
+when oracle/_ref is present, the reference's own aligner on a CPU sample.
+    python3 tools/bench_dc.py --algo hb --pairs 1000 --len 4096
+    python3 tools/bench_dc.py --algo mm --pairs 1000 --len 4096
 """
 import argparse, json, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -17,6 +18,7 @@ def main():
     ap.add_argument("--len", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--cpu-pairs", type=int, default=4)
+    ap.add_argument("--algo", choices=("hb", "mm"), default="hb")
     a = ap.parse_args()
     import torch
     import seqalib_amd as sa
@@ -29,13 +31,18 @@ def main():
     res = torch.zeros(P * 32, dtype=torch.uint8, device=dev)
     ops = torch.zeros(len(s1) + len(s2) + P, dtype=torch.uint8, device=dev)
     eng = sa.Engine(0)
-    sc = sa.ScoringSystem(-1, 2, -1)
-    run = lambda: eng.align_device(sa.SA_HIRSCHBERG, sc, d1.data_ptr(), do1.data_ptr(), d2.data_ptr(), do2.data_ptr(),
+    algo = sa.SA_HIRSCHBERG if a.algo == "hb" else sa.SA_MYERS_MILLER
+    args = (-1, 2, -1) if a.algo == "hb" else (-3, -1, 1, -1, True)
+    sc = sa.ScoringSystem(*args)
+    run = lambda: eng.align_device(algo, sc, d1.data_ptr(), do1.data_ptr(), d2.data_ptr(), do2.data_ptr(),
                                    P, L, L, res.data_ptr(), ops.data_ptr(), 0)
     run(); torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
+        t1 = time.perf_counter()
         run()
+        if os.environ.get("SEQALIB_MM_TIMING") or os.environ.get("SEQALIB_HB_TIMING"):
+            print(f"[bench] call {1e3 * (time.perf_counter() - t1):.2f} ms", file=sys.stderr)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
     r = np.frombuffer(res.cpu().numpy().tobytes(), dtype=sa.RESULT_DTYPE)
@@ -43,10 +50,11 @@ def main():
     ok = 0
     for p in (0, P - 1):
         x, y = s1[o1[p]:o1[p + 1]].tobytes(), s2[o2[p]:o2[p + 1]].tobytes()
-        o = oracle_align(sa.SA_HIRSCHBERG, (-1, 2, -1), x, y)
+        o = oracle_align(algo, args, x, y)
         off = int(o1[p] + o2[p]) + p
         ok += int((int(r["score"][p]), hops[off:off + int(r["nops"][p])].tobytes()) == (o["score"], o["ops"]))
-    line = {"metric": "HirschbergSA alignment cells/s (m*n per pair)", "pairs": P, "len": L,
+    name = "HirschbergSA" if a.algo == "hb" else "MyersMillerSA"
+    line = {"metric": f"{name} alignment cells/s (m*n per pair)", "pairs": P, "len": L,
             "ms_per_batch": round(dt * 1e3, 2), "gcups": round(P * L * L / dt / 1e9, 1),
             "parity": f"{ok}/2 sampled pairs bit-exact vs oracle"}
     ref = os.path.join(ROOT, "oracle", "_ref", "libsaref.so")
@@ -61,10 +69,14 @@ def main():
         for p in range(a.cpu_pairs):
             x, y = s1[o1[p]:o1[p + 1]].tobytes(), s2[o2[p]:o2[p + 1]].tobytes()
             oo = RefOut()
-            Lr.ref_align(4, 3, -1, 2, -1, 0, 1, 0, None, x, len(x), y, len(y), C.byref(oo), *bufs, cap)
+            if a.algo == "hb":
+                Lr.ref_align(4, 3, -1, 2, -1, 0, 1, 0, None, x, len(x), y, len(y), C.byref(oo), *bufs, cap)
+            else:
+                Lr.ref_align(5, 5, -3, -1, 1, -1, 1, 0, None, x, len(x), y, len(y), C.byref(oo), *bufs, cap)
         cdt = time.perf_counter() - t0
         line["cpu_reference_gcups_1thread"] = round(a.cpu_pairs * L * L / cdt / 1e9, 4)
-        line["cpu_sample"] = f"{a.cpu_pairs} pairs, reference HirschbergSA (includes one NW score pass), 1 thread"
+        line["cpu_sample"] = (f"{a.cpu_pairs} pairs, reference {name}"
+                              + (" (includes one NW score pass)" if a.algo == "hb" else "") + ", 1 thread")
     print(json.dumps(line))
 
 
