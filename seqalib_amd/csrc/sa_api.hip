@@ -567,8 +567,8 @@ int sa_align_batch_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8
         static thread_local HostBuf<sa_result> pres;
         SA_HIP(c, pres.alloc(npairs));
         memcpy(pres.data(), hres.data(), sizeof(sa_result) * npairs);
-        SA_HIP(c, dc_upload(d_res, pres.data(), sizeof(sa_result) * npairs, st));
-        SA_HIP(c, dc_upload(d_ops, hops, hops_bytes, st));
+        SA_HIP(c, hipMemcpyAsync(d_res, pres.data(), sizeof(sa_result) * npairs, hipMemcpyHostToDevice, st));
+        if (hops_bytes) SA_HIP(c, hipMemcpyAsync(d_ops, hops, hops_bytes, hipMemcpyHostToDevice, st));
         SA_HIP(c, dc_sync(st));
         if (getenv("SEQALIB_MM_TIMING"))
             fprintf(stderr, "[api] after runner: %8.2f ms\n",

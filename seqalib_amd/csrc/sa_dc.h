@@ -11,6 +11,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -98,10 +99,15 @@ inline hipError_t dc_sync(hipStream_t st) {
     return e;
 }
 
-// Upload pinned host bytes into device memory with a kernel that reads the host buffer directly
-// (hipHostMalloc memory is device-visible), instead of a copy-engine transfer.
-__global__ void dc_upload_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t bytes);
-hipError_t dc_upload(void* dst, const void* pinned_src, uint64_t bytes, hipStream_t st);
+// Host vector -> device through a pinned staging buffer, so the copy is a plain async DMA.
+// The stage may be reused once the stream has passed the copy (the drivers wait every level).
+template <typename T>
+hipError_t dc_put(T* dst, const std::vector<T>& v, HostBuf<T>& stage, hipStream_t st) {
+    if (v.empty()) return hipSuccess;
+    if (hipError_t e = stage.alloc(v.size())) return e;
+    memcpy(stage.data(), v.data(), v.size() * sizeof(T));
+    return hipMemcpyAsync(dst, stage.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st);
+}
 
 #define SA_DC_HIP(call)                                                                              \
     do {                                                                                             \
@@ -153,7 +159,9 @@ inline hipError_t dc_assemble(uint32_t npairs, const uint64_t* o1, const uint64_
             }
         }
     };
-    const uint32_t nth = std::max<uint32_t>(1, std::min<uint32_t>(16, npairs / 64));
+    uint32_t cap = 16;   // host threads for assembly: SEQALIB_DC_THREADS overrides
+    if (const char* t = getenv("SEQALIB_DC_THREADS")) cap = std::max(1, atoi(t));
+    const uint32_t nth = std::max<uint32_t>(1, std::min<uint32_t>(cap, npairs / 64));
     std::vector<std::thread> pool;
     for (uint32_t t = 0; t < nth; ++t)
         pool.emplace_back(assemble, (uint32_t)((uint64_t)npairs * t / nth), (uint32_t)((uint64_t)npairs * (t + 1) / nth));

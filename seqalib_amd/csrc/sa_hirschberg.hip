@@ -430,9 +430,11 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
         SA_DC_HIP(drows.alloc(rowpos));
         SA_DC_HIP(dmid.alloc(sp.size()));
         SA_DC_HIP(dscore.alloc(sp.size()));
-        SA_DC_HIP(hipMemcpyAsync(dsw.p, sw.data(), sw.size() * sizeof(HbSweep), hipMemcpyHostToDevice, st));
+        static thread_local HostBuf<HbSweep> ssw;
+        static thread_local HostBuf<HbSplit> ssp;
+        SA_DC_HIP(dc_put(dsw.p, sw, ssw, st));
         lap("level: descriptors + H2D");
-        SA_DC_HIP(hipMemcpyAsync(dsp.p, sp.data(), sp.size() * sizeof(HbSplit), hipMemcpyHostToDevice, st));
+        SA_DC_HIP(dc_put(dsp.p, sp, ssp, st));
         int R = 1;
         while (R < 32 && 64 * R < maxa) R *= 2;
         SA_DC_HIP(launch_sweeps(R, (uint32_t)sw.size(), d1, d2, dsw.p, drows.p, d_lutbits, sc, st));
@@ -474,7 +476,8 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
         SA_DC_HIP(dnout.alloc(lv.size()));
         SA_DC_HIP(dlscore.alloc(lv.size()));
         SA_DC_HIP(dout.alloc(outpos));
-        SA_DC_HIP(hipMemcpyAsync(dlv.p, lv.data(), lv.size() * sizeof(HbLeaf), hipMemcpyHostToDevice, st));
+        static thread_local HostBuf<HbLeaf> slv;
+        SA_DC_HIP(dc_put(dlv.p, lv, slv, st));
         hipLaunchKernelGGL(hb_leaf_kernel, dim3((uint32_t)((lv.size() + 63) / 64)), dim3(64), 0, st, d1, d2, dlv.p,
                            (uint32_t)lv.size(), dscr.p, dout.p, dnout.p, dlscore.p, d_lutbits, sc);
         SA_DC_HIP(hipGetLastError());

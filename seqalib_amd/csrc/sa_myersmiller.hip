@@ -382,24 +382,6 @@ __global__ __launch_bounds__(64) void mm_leaf_kernel(const uint8_t* s1, const ui
     nout[id] = k;
 }
 
-// ---------------------------------------------------------------------------- upload (sa_dc.h)
-__global__ void dc_upload_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t bytes) {
-    const uint64_t n16 = bytes / 16;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n16; k += stride)
-        reinterpret_cast<uint4*>(dst)[k] = reinterpret_cast<const uint4*>(src)[k];
-    if (blockIdx.x == 0 && threadIdx.x < (bytes & 15)) dst[n16 * 16 + threadIdx.x] = src[n16 * 16 + threadIdx.x];
-}
-
-hipError_t dc_upload(void* dst, const void* pinned_src, uint64_t bytes, hipStream_t st) {
-    if (!bytes) return hipSuccess;
-    // both pointers must be 16-byte aligned for the vector path; fall back to bytes otherwise
-    if (((uintptr_t)dst | (uintptr_t)pinned_src) & 15) return hipMemcpyAsync(dst, pinned_src, bytes, hipMemcpyHostToDevice, st);
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>(1024, (bytes / 16 + 255) / 256 + 1);
-    hipLaunchKernelGGL(dc_upload_kernel, dim3(blocks), dim3(256), 0, st, (const uint8_t*)pinned_src, (uint8_t*)dst, bytes);
-    return hipGetLastError();
-}
-
 // ---------------------------------------------------------------------------- host driver
 namespace {
 
@@ -515,9 +497,11 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
         SA_DC_HIP(dsp.alloc(sp.size()));
         SA_DC_HIP(drows.alloc(rowpos));
         SA_DC_HIP(dout3.alloc(3 * sp.size()));
-        SA_DC_HIP(hipMemcpyAsync(dsw.p, sw.data(), sw.size() * sizeof(MmSweep), hipMemcpyHostToDevice, st));
+        static thread_local HostBuf<MmSweep> ssw;
+        static thread_local HostBuf<MmSplit> ssp;
+        SA_DC_HIP(dc_put(dsw.p, sw, ssw, st));
         lap("level: descriptors + H2D");
-        SA_DC_HIP(hipMemcpyAsync(dsp.p, sp.data(), sp.size() * sizeof(MmSplit), hipMemcpyHostToDevice, st));
+        SA_DC_HIP(dc_put(dsp.p, sp, ssp, st));
         int R = 1;
         while (R < 32 && 64 * R < maxa) R *= 2;
         SA_DC_HIP(launch_mm_sweeps(R, (uint32_t)sw.size(), d1, d2, dsw.p, drows.p, d_lutbits, sc, st));
@@ -569,7 +553,8 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
     SA_DC_HIP(dnout.alloc(lv.size()));
     SA_DC_HIP(dlscore.alloc(lv.size()));
     SA_DC_HIP(dout.alloc(outpos));
-    SA_DC_HIP(hipMemcpyAsync(dlv.p, lv.data(), lv.size() * sizeof(MmLeaf), hipMemcpyHostToDevice, st));
+    static thread_local HostBuf<MmLeaf> slv;
+    SA_DC_HIP(dc_put(dlv.p, lv, slv, st));
     hipLaunchKernelGGL(mm_leaf_kernel, dim3((uint32_t)((lv.size() + 63) / 64)), dim3(64), 0, st, d1, d2, dlv.p,
                        (uint32_t)lv.size(), dscr.p, dout.p, dnout.p, dlscore.p, d_lutbits, sc);
     SA_DC_HIP(hipGetLastError());
