@@ -371,16 +371,34 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     uint8_t* dlut = p; p += b_lut;
     uint32_t* dbits = reinterpret_cast<uint32_t*>(p);
     hipStream_t st = c->stream;
-    if (t1) SA_HIP(c, hipMemcpyAsync(d1, seq1, t1, hipMemcpyHostToDevice, st));
-    if (t2) SA_HIP(c, hipMemcpyAsync(d2, seq2, t2, hipMemcpyHostToDevice, st));
-    SA_HIP(c, hipMemcpyAsync(do1, off1, 8ull * (npairs + 1), hipMemcpyHostToDevice, st));
-    SA_HIP(c, hipMemcpyAsync(do2, off2, 8ull * (npairs + 1), hipMemcpyHostToDevice, st));
+    const bool dc = algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER;
+    if (dc) {
+        // the divide-and-conquer drivers wait on the stream every level: upload from pinned
+        // staging so no pageable copy is in flight (see sa_dc.h)
+        static thread_local HostBuf<uint8_t> stage;
+        const uint64_t bo = 8ull * (npairs + 1);
+        SA_HIP(c, stage.alloc(t1 + t2 + 2 * bo));
+        uint8_t* q = stage.data();
+        memcpy(q, seq1, t1);
+        memcpy(q + t1, seq2, t2);
+        memcpy(q + t1 + t2, off1, bo);
+        memcpy(q + t1 + t2 + bo, off2, bo);
+        if (t1) SA_HIP(c, hipMemcpyAsync(d1, q, t1, hipMemcpyHostToDevice, st));
+        if (t2) SA_HIP(c, hipMemcpyAsync(d2, q + t1, t2, hipMemcpyHostToDevice, st));
+        SA_HIP(c, hipMemcpyAsync(do1, q + t1 + t2, bo, hipMemcpyHostToDevice, st));
+        SA_HIP(c, hipMemcpyAsync(do2, q + t1 + t2 + bo, bo, hipMemcpyHostToDevice, st));
+    } else {
+        if (t1) SA_HIP(c, hipMemcpyAsync(d1, seq1, t1, hipMemcpyHostToDevice, st));
+        if (t2) SA_HIP(c, hipMemcpyAsync(d2, seq2, t2, hipMemcpyHostToDevice, st));
+        SA_HIP(c, hipMemcpyAsync(do1, off1, 8ull * (npairs + 1), hipMemcpyHostToDevice, st));
+        SA_HIP(c, hipMemcpyAsync(do2, off2, 8ull * (npairs + 1), hipMemcpyHostToDevice, st));
+    }
     if (use_lut) {
         SA_HIP(c, hipMemcpyAsync(dlut, lut, 65536, hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(lut_to_bits, dim3(8), dim3(256), 0, st, dlut, dbits);
         SA_HIP(c, hipGetLastError());
     }
-    if (npairs && (algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER)) {
+    if (npairs && dc) {
         std::vector<sa_result> hres;
         const uint8_t* hops = nullptr;
         uint64_t hops_bytes = 0;
