@@ -10,6 +10,11 @@ Multi-GPU: one process per GPU (torchrun); rank r aligns its own 10,000-pair sha
 batch (pair p uses seeds base+2p+1 / base+2p+2), with no data-path collective (pairs are
 independent); timing is barrier-bracketed and the max over ranks is reported.  scaling = weak.
 
+Steps are pipelined (sa_set_pipeline; --no-pipeline turns it off): step k's traceback runs on
+its own stream while step k+1's fill runs, with two workspace slots and two output buffer sets.
+Every step's fill and traceback still lies inside the timed region (it ends with sa_wait + a
+device synchronize); "serial_ms_per_step" reports the same step without overlap.
+
 Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
 """
 from __future__ import annotations
@@ -49,6 +54,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="run steps back to back without overlapping step k's traceback with step k+1's fill")
+    ap.add_argument("--serial-steps", type=int, default=3,
+                    help="after the timed run, also time this many non-pipelined steps (reported, not the value)")
     return ap.parse_args()
 
 
@@ -163,32 +172,46 @@ def main():
     s1, o1, s2, o2 = sa.synth_dna_batch(shard_seed_base(rank, world, P), P, Lq, Lq, threads=16)
     as_t = lambda x: torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)
     d1, do1, d2, do2 = as_t(s1), as_t(o1), as_t(s2), as_t(o2)
-    d_res = torch.zeros(P * 32, dtype=torch.uint8, device=dev)
-    d_ops = torch.zeros(len(s1) + len(s2) + P, dtype=torch.uint8, device=dev)
+    # two output sets: with the cross-call pipeline, step k's traceback still writes its results
+    # while step k+1 fills, so consecutive steps must not share result buffers
+    d_res = [torch.zeros(P * 32, dtype=torch.uint8, device=dev) for _ in range(2)]
+    d_ops = [torch.zeros(len(s1) + len(s2) + P, dtype=torch.uint8, device=dev) for _ in range(2)]
     eng = sa.Engine(local)
     scoring = sa.ScoringSystem(*SCORING)
     stream = torch.cuda.current_stream(dev)
+    pipelined = not args.no_pipeline
+    eng.set_pipeline(pipelined)
 
-    def step():
+    def step(k):
         eng.align_device(sa.SA_SW, scoring, d1.data_ptr(), do1.data_ptr(), d2.data_ptr(), do2.data_ptr(), P, Lq, Lq,
-                         d_res.data_ptr(), d_ops.data_ptr(), stream.cuda_stream)
+                         d_res[k % 2].data_ptr(), d_ops[k % 2].data_ptr(), stream.cuda_stream)
 
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        step(k)
+    eng.wait()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
+    for k in range(args.steps):
+        step(k)
+    eng.wait()                    # every step's fill AND traceback is inside the timed region
     torch.cuda.synchronize()
     barrier(world)
     t1 = time.perf_counter()
     elapsed = max_over_ranks(t1 - t0, world)
-    fill_ms, tb_ms, launches = eng.last_timings()   # HIP events of the last step, same stream
+    fill_ms, tb_ms, launches = eng.last_timings()   # HIP events of the last step (fill stream / traceback stream)
+    last = (args.steps - 1) % 2
+    serial_ms = None
+    if pipelined and args.serial_steps > 0:
+        # the same steps without overlap, for reference (outside the timed region above)
+        eng.set_pipeline(False)
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        for k in range(args.serial_steps):
+            step(last + 1 + 2 * k)   # the other output set: keeps the checked one intact
+        torch.cuda.synchronize()
+        serial_ms = max_over_ranks(time.perf_counter() - ts, world) / args.serial_steps * 1e3
     kernel, plan_R, plan_W = eng.last_plan()
     fill_ms = max_over_ranks(fill_ms, world)
 
@@ -198,8 +221,8 @@ def main():
 
     # parity spot check of this step's output (outside the timed region)
     from util import oracle_align
-    res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=sa.RESULT_DTYPE)
-    ops = d_ops.cpu().numpy()
+    res = np.frombuffer(d_res[last].cpu().numpy().tobytes(), dtype=sa.RESULT_DTYPE)
+    ops = d_ops[last].cpu().numpy()
     bad = int(np.count_nonzero(res["flags"]))
     checked = 0
     for p in (0, P - 1):
@@ -252,6 +275,7 @@ def main():
                    "scoring": list(SCORING), "match": "equal<char>", "parallelism": f"pair-shard x{world}"},
         "roofline": roof,
         "fill_ms": round(fill_ms, 2), "traceback_ms": round(tb_ms, 2),
+        "pipelined": pipelined, "serial_ms_per_step": round(serial_ms, 2) if serial_ms else None,
         "parity": f"{checked - bad}/{checked} sampled pairs bit-exact vs oracle, {int(np.count_nonzero(res['flags']))} flagged",
     }
     if world == 1 and not args.no_cpu:

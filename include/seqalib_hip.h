@@ -111,6 +111,16 @@ const char* sa_last_error(const sa_ctx* ctx);
 int sa_set_workspace_limit(sa_ctx* ctx, uint64_t bytes);   /* 0 = automatic (80% of free HBM) */
 int sa_trim(sa_ctx* ctx);                                   /* free the cached workspace */
 
+/* Cross-call pipeline of the device API (off by default).  When enabled, consecutive
+ * sa_align_batch_device calls overlap: call k's traceback runs on an internal stream while call
+ * k+1's fill runs on another, with two workspace slots (twice the HBM).  A call is ordered after
+ * work already enqueued on the caller's stream, but the caller's stream is NOT ordered after
+ * the call's results: wait with sa_wait(ctx) (or a device-wide synchronize) before reading
+ * d_results / d_ops, and give calls that may overlap distinct output buffers.  Disabling waits
+ * for pipelined work.  The host API (sa_align_batch) never pipelines. */
+int sa_set_pipeline(sa_ctx* ctx, int enable);
+int sa_wait(sa_ctx* ctx);
+
 /* Host-buffer batch API (used by the C++ drop-in headers).
  * seq1/seq2: concatenated symbol bytes; seq*_off: npairs+1 offsets (seq*_off[0] = 0).
  * match_lut: NULL for byte equality (the reference's `equal<char>` / nullptr match fn), or a

@@ -117,12 +117,14 @@ def load_library():
     L.sa_last_timings.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_float), i32p]
     L.sa_plan_query.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, i32p, i32p, u64p, u64p]
     L.sa_last_plan.argtypes = [vp, i32p, i32p, i32p]
+    L.sa_set_pipeline.argtypes = [vp, C.c_int]
+    L.sa_wait.argtypes = [vp]
     L.sa_synth_dna.argtypes = [C.c_uint64, C.c_uint32, vp]
     L.sa_synth_mutate.argtypes = [vp, C.c_uint32, C.c_uint64, vp, C.c_uint32, C.POINTER(C.c_uint32)]
     L.sa_synth_dna_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_int]
     for fn in ("sa_set_workspace_limit", "sa_trim", "sa_align_batch", "sa_align_batch_device",
                "sa_last_timings", "sa_last_plan", "sa_plan_query", "sa_synth_dna", "sa_synth_mutate", "sa_synth_dna_batch",
-               "sa_create", "sa_device_count"):
+               "sa_create", "sa_device_count", "sa_set_pipeline", "sa_wait"):
         getattr(L, fn).restype = C.c_int
     if L.sa_version() != 1:
         raise SeqalibError("libseqalib_hip ABI version mismatch")
@@ -376,6 +378,14 @@ class Engine:
         rc = self.L.sa_align_batch_device(self.h, algo, C.byref(sc), d_s1, d_off1, d_s2, d_off2, npairs, max_m,
                                           max_n, d_lut or None, d_res, d_ops, stream or None)
         self._check(rc, "sa_align_batch_device")
+
+    def set_pipeline(self, enable: bool):
+        """Overlap consecutive align_device calls (sa_set_pipeline); results need wait()."""
+        self._check(self.L.sa_set_pipeline(self.h, 1 if enable else 0), "sa_set_pipeline")
+
+    def wait(self):
+        """Wait for all pipelined align_device work (sa_wait)."""
+        self._check(self.L.sa_wait(self.h), "sa_wait")
 
     def last_timings(self) -> Tuple[float, float, int]:
         f, t, n = C.c_float(), C.c_float(), C.c_int()

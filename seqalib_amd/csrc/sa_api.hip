@@ -31,9 +31,15 @@ struct sa_ctx {
     std::vector<hipEvent_t> events;  // 3 per fill launch: start, fill end, traceback end
     int launches = 0;
     hipStream_t timed_stream = nullptr;
-    // alphabet bitmap (8 words) + T16 profile (4 words)
+    // alphabet bitmap (8 words) + T16 profile (4 words), one 64-word slot per pipeline slot
     uint32_t* aux = nullptr;
     int last_kernel = SA_KERNEL_INT32, last_R = 0, last_W = 0;
+    // cross-call pipeline of the device API (sa_set_pipeline): fills on s_fill, tracebacks on
+    // s_tb, two workspace slots; ev_slot[k] = traceback of the last call that used slot k done
+    int pipeline = 0;
+    hipStream_t s_fill = nullptr, s_tb = nullptr;
+    hipEvent_t ev_in = nullptr, ev_slot[2] = {nullptr, nullptr};
+    uint64_t pipe_k = 0;
 };
 
 namespace {
@@ -117,6 +123,8 @@ int ensure_ws(sa_ctx* c, uint64_t need) {
     if (c->ws_bytes >= need) return SA_OK;
     if (c->ws) {
         SA_HIP(c, hipStreamSynchronize(c->stream));
+        if (c->s_fill) SA_HIP(c, hipStreamSynchronize(c->s_fill));
+        if (c->s_tb) SA_HIP(c, hipStreamSynchronize(c->s_tb));
         (void)hipFree(c->ws);
         c->ws = nullptr;
         c->ws_bytes = 0;
@@ -189,10 +197,13 @@ int validate_scoring(sa_ctx* c, int algo, const sa_scoring* s) {
 }
 
 // Enqueue fill + traceback for pairs [0, npairs) whose inputs are on the device.
+// pipe: (device API with sa_set_pipeline) fills go to c->s_fill and tracebacks to c->s_tb after
+// the caller's stream reaches this call; workspace and aux use slot pipe_k % 2, and the call
+// returns without ordering `stream` after the results (sa_wait).
 int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, const uint64_t* o1,
                const uint8_t* d2, const uint64_t* o2, uint32_t npairs, uint32_t max_m,
                uint32_t max_n, const uint32_t* d_lutbits, sa_result* d_res, uint8_t* d_ops,
-               hipStream_t stream) {
+               hipStream_t stream, bool pipe = false) {
     if (max_m >= (1u << 24) || max_n >= (1u << 24))
         return fail(c, SA_ERR_UNSUPPORTED, "sequence lengths must be < 2^24");
     const bool keyed = keyed_ok(algo, sc, max_m, max_n);
@@ -202,11 +213,18 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     bool t16 = t16_ok(algo, sc, max_m, max_n) && (algo == SA_NW || keyed);
     if (const char* e16 = getenv("SEQALIB_T16")) if (e16[0] == '0') t16 = false;
     uint32_t sym_pack = 0;
-    if (!c->aux) SA_HIP(c, hipMalloc(&c->aux, 256));
+    if (!c->aux) SA_HIP(c, hipMalloc(&c->aux, 512));
+    if (!pipe && c->s_fill) {   // a non-pipelined call reuses slot 0: drain pipelined work first
+        SA_HIP(c, hipStreamSynchronize(c->s_fill));
+        SA_HIP(c, hipStreamSynchronize(c->s_tb));
+    }
+    const int slot = pipe ? (int)(c->pipe_k & 1) : 0;
+    uint32_t* aux = c->aux + 64 * slot;
+    if (pipe && c->ev_slot[slot]) SA_HIP(c, hipStreamWaitEvent(stream, c->ev_slot[slot], 0));   // slot free
     if (t16) {
-        SA_HIP(c, launch_alphabet_scan(d1, o1, d2, o2, npairs, c->aux, stream));
+        SA_HIP(c, launch_alphabet_scan(d1, o1, d2, o2, npairs, aux, stream));
         uint32_t bm[8];
-        SA_HIP(c, hipMemcpyAsync(bm, c->aux, 32, hipMemcpyDeviceToHost, stream));
+        SA_HIP(c, hipMemcpyAsync(bm, aux, 32, hipMemcpyDeviceToHost, stream));
         SA_HIP(c, hipStreamSynchronize(stream));
         int nsym = 0;
         uint8_t syms[4];
@@ -225,7 +243,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 if (!used) syms[nsym++] = (uint8_t)b;
             }
             sym_pack = syms[0] | (uint32_t)syms[1] << 8 | (uint32_t)syms[2] << 16 | (uint32_t)syms[3] << 24;
-            SA_HIP(c, launch_build_profile(d_lutbits, sym_pack, sc->match, sc->mismatch, c->aux + 8, stream));
+            SA_HIP(c, launch_build_profile(d_lutbits, sym_pack, sc->match, sc->mismatch, aux + 8, stream));
         }
     }
     Plan pl = make_plan(algo, max_m, max_n, npairs, t16);
@@ -244,17 +262,19 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     c->last_R = pl.R;
     c->last_W = pl.W;
     const uint64_t slot_bytes = pl.g.dir_slot + pl.rowbuf_elems * 4 + (snap_h_slot + snap_p_slot) * 4;
-    const uint64_t budget = ws_budget(c);
+    const uint64_t budget = pipe ? ws_budget(c) / 2 : ws_budget(c);
     uint64_t per_launch = slot_bytes ? std::max<uint64_t>(1, budget / std::max<uint64_t>(slot_bytes, 1)) : npairs;
     per_launch = std::min<uint64_t>(per_launch, npairs ? npairs : 1);
     per_launch = std::min<uint64_t>(per_launch, 1u << 30);
-    const uint64_t need = per_launch * slot_bytes + 4096;
+    const uint64_t need = (per_launch * slot_bytes + 4096 + 255) & ~(uint64_t)255;
     if (need > budget && per_launch == 1 && c->ws_limit)
         return fail(c, SA_ERR_NOMEM, "one pair needs " + std::to_string(slot_bytes) +
                                          " bytes of workspace, above the limit");
-    int rc = ensure_ws(c, std::max<uint64_t>(need, 4096));
+    int rc = ensure_ws(c, std::max<uint64_t>(pipe ? 2 * need : need, 4096));
     if (rc) return rc;
-    uint8_t* dirs = c->ws;
+    // pipeline slots are fixed halves of the workspace, so a later call with a smaller need
+    // cannot overlap the slot a running traceback still reads
+    uint8_t* dirs = c->ws + (pipe ? slot * ((c->ws_bytes / 2) & ~(uint64_t)255) : 0);
     int32_t* rowbuf = reinterpret_cast<int32_t*>(c->ws + per_launch * pl.g.dir_slot);
     uint32_t* snap_h = reinterpret_cast<uint32_t*>(rowbuf + per_launch * pl.rowbuf_elems);
     int32_t* snap_p = reinterpret_cast<int32_t*>(snap_h + per_launch * snap_h_slot);
@@ -262,6 +282,13 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     // reset timing
     c->launches = 0;
     c->timed_stream = stream;
+    hipStream_t sf = stream, stb = stream;
+    if (pipe) {
+        sf = c->s_fill;
+        stb = c->s_tb;
+        SA_HIP(c, hipEventRecord(c->ev_in, stream));
+        SA_HIP(c, hipStreamWaitEvent(sf, c->ev_in, 0));
+    }
 
     for (uint64_t base = 0; base < npairs; base += per_launch) {
         const uint32_t cnt = (uint32_t)std::min<uint64_t>(per_launch, npairs - base);
@@ -277,7 +304,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         fp.gap_open = sc->gap_open; fp.gap_extend = sc->gap_extend;
         fp.waves = pl.W;
         fp.stage_seq2 = max_n <= kMaxStagedSeq2 ? 1 : 0;
-        fp.prof = c->aux + 8;
+        fp.prof = aux + 8;
         fp.sym_pack = sym_pack;
         fp.snap_h = snap_h; fp.snap_p = snap_p;
         fp.snap_h_slot = snap_h_slot; fp.snap_p_slot = snap_p_slot; fp.snap_nch = snap_nch;
@@ -300,9 +327,9 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             c->events.push_back(ev);
         }
         hipEvent_t* ev = &c->events[3 * c->launches];
-        SA_HIP(c, hipEventRecord(ev[0], stream));
+        SA_HIP(c, hipEventRecord(ev[0], sf));
         const FillVariant fv = {pl.R, lut, allow, keyed, t16, cmax};
-        hipError_t e = launch_fill(algo, fv, fp, cnt, stream);
+        hipError_t e = launch_fill(algo, fv, fp, cnt, sf);
         if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
         if (cmax) {
             EndcellParams ep;
@@ -313,14 +340,20 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             ep.rowbuf = rowbuf; ep.rowbuf_slot = pl.rowbuf_elems; ep.max_n = max_n;
             ep.res = d_res; ep.pair_base = (uint32_t)base; ep.count = cnt;
             ep.gap = sc->gap;
-            e = launch_endcell(pl.R, ep, stream);
+            e = launch_endcell(pl.R, ep, sf);
             if (e != hipSuccess) return hip_fail(c, e, "end-cell kernel launch");
         }
-        SA_HIP(c, hipEventRecord(ev[1], stream));
-        e = launch_traceback(algo, pl.R, lut, tp, stream);
+        SA_HIP(c, hipEventRecord(ev[1], sf));
+        if (pipe) SA_HIP(c, hipStreamWaitEvent(stb, ev[1], 0));
+        e = launch_traceback(algo, pl.R, lut, tp, stb);
         if (e != hipSuccess) return hip_fail(c, e, "traceback kernel launch");
-        SA_HIP(c, hipEventRecord(ev[2], stream));
+        SA_HIP(c, hipEventRecord(ev[2], stb));
         c->launches++;
+    }
+    if (pipe) {
+        if (!c->ev_slot[slot]) SA_HIP(c, hipEventCreateWithFlags(&c->ev_slot[slot], hipEventDisableTiming));
+        SA_HIP(c, hipEventRecord(c->ev_slot[slot], stb));
+        c->pipe_k++;
     }
     return SA_OK;
 }
@@ -471,7 +504,13 @@ void sa_destroy(sa_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->s_fill) (void)hipStreamSynchronize(c->s_fill);
+    if (c->s_tb) (void)hipStreamSynchronize(c->s_tb);
     for (auto ev : c->events) (void)hipEventDestroy(ev);
+    for (auto ev : {c->ev_in, c->ev_slot[0], c->ev_slot[1]})
+        if (ev) (void)hipEventDestroy(ev);
+    if (c->s_fill) (void)hipStreamDestroy(c->s_fill);
+    if (c->s_tb) (void)hipStreamDestroy(c->s_tb);
     if (c->ws) (void)hipFree(c->ws);
     if (c->io) (void)hipFree(c->io);
     if (c->aux) (void)hipFree(c->aux);
@@ -491,6 +530,8 @@ int sa_trim(sa_ctx* c) {
     if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->s_fill) (void)hipStreamSynchronize(c->s_fill);
+    if (c->s_tb) (void)hipStreamSynchronize(c->s_tb);
     if (c->ws) (void)hipFree(c->ws);
     if (c->io) (void)hipFree(c->io);
     c->ws = nullptr; c->ws_bytes = 0;
@@ -593,7 +634,32 @@ int sa_align_batch_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_run).count());
         return SA_OK;
     }
-    return run_device(c, algo, sc, d1, o1, d2, o2, npairs, max_m, max_n, bits, d_res, d_ops, st);
+    return run_device(c, algo, sc, d1, o1, d2, o2, npairs, max_m, max_n, bits, d_res, d_ops, st, c->pipeline != 0);
+}
+
+int sa_set_pipeline(sa_ctx* c, int enable) {
+    if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
+    SA_HIP(c, hipSetDevice(c->device));
+    if (enable && !c->s_fill) {
+        SA_HIP(c, hipStreamCreateWithFlags(&c->s_fill, hipStreamNonBlocking));
+        SA_HIP(c, hipStreamCreateWithFlags(&c->s_tb, hipStreamNonBlocking));
+        SA_HIP(c, hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
+    }
+    if (!enable && c->pipeline) {
+        int rc = sa_wait(c);
+        if (rc) return rc;
+    }
+    c->pipeline = enable ? 1 : 0;
+    return SA_OK;
+}
+
+int sa_wait(sa_ctx* c) {
+    if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
+    SA_HIP(c, hipSetDevice(c->device));
+    if (c->s_fill) SA_HIP(c, hipStreamSynchronize(c->s_fill));
+    if (c->s_tb) SA_HIP(c, hipStreamSynchronize(c->s_tb));
+    SA_HIP(c, hipStreamSynchronize(c->stream));
+    return SA_OK;
 }
 
 int sa_last_timings(sa_ctx* c, float* fill_ms, float* tb_ms, int* launches) {

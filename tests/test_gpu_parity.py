@@ -359,6 +359,47 @@ def test_device_api_and_timings(engine):
     assert n >= 1 and fill_ms > 0
 
 
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+def test_pipelined_device_api_matches_serial(engine, algo):
+    """sa_set_pipeline: consecutive device calls overlap (traceback of call k with the fill of
+    call k+1, two workspace slots); every call's results equal the host API's once sa_wait
+    returns.  Different batches per call, so a slot mix-up cannot go unnoticed."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    t = lambda x: torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)
+    args = SCORINGS[algo][0]
+    sc = sc_obj(args)
+    stream = torch.cuda.current_stream().cuda_stream
+    calls = []
+    for k in range(5):
+        L = (256, 700, 300, 1024, 128)[k]
+        s1, o1, s2, o2 = sa.synth_dna_batch(900 + 17 * k, 48 + 16 * k, L, L - 5 * k)
+        d = [t(x) for x in (s1, o1, s2, o2)]
+        n = len(o1) - 1
+        res = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
+        ops = torch.zeros(len(s1) + len(s2) + n, dtype=torch.uint8, device=dev)
+        calls.append(((s1, o1, s2, o2), d, n, L, res, ops))
+    engine.set_pipeline(True)
+    try:
+        for (h, d, n, L, res, ops) in calls:
+            engine.align_device(algo, sc, d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), n, L, L,
+                                res.data_ptr(), ops.data_ptr(), stream)
+        engine.wait()
+    finally:
+        engine.set_pipeline(False)
+    torch.cuda.synchronize()
+    for (h, d, n, L, res, ops) in calls:
+        s1, o1, s2, o2 = h
+        got = np.frombuffer(res.cpu().numpy().tobytes(), dtype=sa.RESULT_DTYPE)
+        ref, ref_ops = engine.align_packed(algo, sc, s1, o1, s2, o2)
+        for f in ("score", "end_i", "end_j", "start_i", "start_j", "nops", "flags"):
+            assert (got[f] == ref[f]).all(), (algo, f)
+        g_ops = ops.cpu().numpy()
+        for p in range(n):
+            off = int(o1[p] + o2[p]) + p
+            assert g_ops[off:off + int(ref["nops"][p])].tobytes() == ref_ops[off:off + int(ref["nops"][p])].tobytes()
+
+
 def test_multi_gpu_threads_match_single(engine):
     """align_multi_gpu (one host thread + context per device; here two contexts on GPU 0) returns
     exactly what one sa_align_batch returns."""
