@@ -40,6 +40,7 @@ public:
         std::vector<AlignedSequence<Ty, Blank>> done;
         if (!work.empty()) done = seqalib::detail::run<SA_SW, SmithWatermanSA, ContainerType, Ty, Blank>(*this, work, res);
         std::vector<AlignedSequence<Ty, Blank>> out;
+        out.reserve(pairs.size());
         size_t k = 0;
         for (auto& p : pairs) {
             if (p.first->size() && p.second->size()) {

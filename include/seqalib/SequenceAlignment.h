@@ -8,16 +8,19 @@
 // getAlignment() runs the DP fill and traceback on an MI355X through libseqalib_hip.so
 // (include/seqalib_hip.h); the AlignedSequence list and forceGlobal are assembled here, on the
 // host, exactly as the reference's buildResult does.  Link with -lseqalib_hip.
-// Not provided (outside the tier's hot path): Hirschberg, Myers-Miller, FOGSAA,
-// BLAT, MUMmer, SuffixTree and SequenceAligner::longestIncreasingSubsequence.
+// Also provided: HirschbergSA and MyersMillerSA (linear-space, on the GPU).
+// Not provided (outside the tier's hot path): FOGSAA, BLAT, MUMmer, SuffixTree and
+// SequenceAligner::longestIncreasingSubsequence.
 #pragma once
 
 #include <algorithm>
 #include <cassert>
 #include <climits>
+#include <exception>
 #include <functional>
 #include <limits>
 #include <list>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -55,7 +58,7 @@ public:
 
     AlignedSequence() {}
     AlignedSequence(const AlignedSequence& Other) : Data(Other.Data) {}
-    AlignedSequence(AlignedSequence&& Other) : Data(std::move(Other.Data)) {}
+    AlignedSequence(AlignedSequence&& Other) noexcept : Data(std::move(Other.Data)) {}
     AlignedSequence& operator=(const AlignedSequence& Other) {
         Data = Other.Data;
         return *this;
@@ -174,13 +177,42 @@ std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std
     std::vector<uint64_t> off;
     align<Ty>(ALGO, sc, fn, has_fn, pairs, res, ops, off);
     std::vector<AlignedSequence<Ty, Blank>> out(pairs.size());
-    for (size_t p = 0; p < pairs.size(); ++p) {
-        build_from_ops<Ty, Blank>(*pairs[p].first, *pairs[p].second, res[p], ops.data() + off[p], out[p]);
-        const bool local = (ALGO == SA_SW || ALGO == SA_LOCAL_GOTOH) && !(res[p].flags & SA_FLAG_SIZE_HACK);
-        if (local)
-            self.forceGlobal(*pairs[p].first, *pairs[p].second, out[p], res[p].start_i, res[p].start_j,
-                             res[p].end_i, res[p].end_j);
+    // Building the std::list of every pair dominates a large batch end to end (one allocation per
+    // Entry), and pairs are independent: split them over host threads.
+    auto build = [&](size_t p0, size_t p1) {
+        for (size_t p = p0; p < p1; ++p) {
+            build_from_ops<Ty, Blank>(*pairs[p].first, *pairs[p].second, res[p], ops.data() + off[p], out[p]);
+            const bool local = (ALGO == SA_SW || ALGO == SA_LOCAL_GOTOH) && !(res[p].flags & SA_FLAG_SIZE_HACK);
+            if (local)
+                self.forceGlobal(*pairs[p].first, *pairs[p].second, out[p], res[p].start_i, res[p].start_j,
+                                 res[p].end_i, res[p].end_j);
+        }
+    };
+    const size_t P = pairs.size();
+    PhaseTimer tm;
+    struct Lap {
+        PhaseTimer& t;
+        ~Lap() { t.lap("AlignedSequence lists"); }
+    } lap{tm};
+    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t nth = std::min<size_t>(std::min<size_t>(hw, 16), P / 32);
+    if (nth <= 1) {
+        build(0, P);
+        return out;
     }
+    std::vector<std::exception_ptr> errs(nth);
+    std::vector<std::thread> pool;
+    for (size_t t = 0; t < nth; ++t)
+        pool.emplace_back([&, t] {
+            try {
+                build(P * t / nth, P * (t + 1) / nth);
+            } catch (...) {
+                errs[t] = std::current_exception();
+            }
+        });
+    for (auto& th : pool) th.join();
+    for (auto& e : errs)
+        if (e) std::rethrow_exception(e);
     return out;
 }
 

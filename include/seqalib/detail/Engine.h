@@ -3,8 +3,10 @@
 // table built from the user's MatchFnTy, and op-stream -> AlignedSequence assembly.
 #pragma once
 
+#include <chrono>
 #include <climits>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -40,6 +42,19 @@ inline sa_ctx* context() {
     }
     return c.h;
 }
+
+// $SEQALIB_HOST_TIMING: print the host-side phases of each batch to stderr.
+struct PhaseTimer {
+    bool on = std::getenv("SEQALIB_HOST_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(const char* what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[seqalib host] %-22s %8.2f ms\n", what,
+                     std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
 
 inline void check(int rc, const char* what) {
     if (rc != SA_OK)
@@ -102,30 +117,38 @@ template <typename Ty, typename ContainerType, typename MatchFnTy>
 void align(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
            const std::vector<std::pair<ContainerType*, ContainerType*>>& pairs,
            std::vector<sa_result>& res, std::vector<uint8_t>& ops, std::vector<uint64_t>& ops_off) {
+    PhaseTimer tm;
     SymbolCoder<Ty> coder;
-    std::vector<uint8_t> s1, s2;
     std::vector<uint64_t> o1(1, 0), o2(1, 0);
+    o1.reserve(pairs.size() + 1);
+    o2.reserve(pairs.size() + 1);
     for (auto& p : pairs) {
-        ContainerType& a = *p.first;
-        ContainerType& b = *p.second;
-        for (size_t k = 0; k < (size_t)a.size(); ++k) s1.push_back(coder.code(a[k]));
-        for (size_t k = 0; k < (size_t)b.size(); ++k) s2.push_back(coder.code(b[k]));
-        o1.push_back(s1.size());
-        o2.push_back(s2.size());
+        o1.push_back(o1.back() + (uint64_t)p.first->size());
+        o2.push_back(o2.back() + (uint64_t)p.second->size());
     }
+    std::vector<uint8_t> s1(o1.back() + 1), s2(o2.back() + 1);   // +1: never a NULL pointer
+    for (size_t q = 0; q < pairs.size(); ++q) {
+        ContainerType& a = *pairs[q].first;
+        ContainerType& b = *pairs[q].second;
+        uint8_t* d1 = s1.data() + o1[q];
+        uint8_t* d2 = s2.data() + o2[q];
+        for (size_t k = 0; k < (size_t)a.size(); ++k) d1[k] = coder.code(a[k]);
+        for (size_t k = 0; k < (size_t)b.size(); ++k) d2[k] = coder.code(b[k]);
+    }
+    tm.lap("symbol coding");
     std::vector<uint8_t> lut;
     if (has_fn) lut = build_lut(coder, fn);
     const uint32_t n = (uint32_t)pairs.size();
     res.assign(n, sa_result{});
     const uint64_t cap = s1.size() + s2.size() + n + 1;
-    ops.assign(cap, 0);
+    ops.resize(cap);
     ops_off.resize(n);
     for (uint32_t p = 0; p < n; ++p) ops_off[p] = o1[p] + o2[p] + p;
-    s1.push_back(0);   // never hand a NULL pointer for an empty batch
-    s2.push_back(0);
+    tm.lap("match table + buffers");
     check(sa_align_batch(context(), algo, &sc, s1.data(), o1.data(), s2.data(), o2.data(), n,
                          has_fn ? lut.data() : nullptr, res.data(), ops.data(), cap),
           "sa_align_batch");
+    tm.lap("sa_align_batch (GPU)");
     for (auto& r : res)
         if (r.flags & SA_FLAG_DIVERGED)
             throw std::runtime_error("seqalib: the reference traceback does not terminate for this scoring");
