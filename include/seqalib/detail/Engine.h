@@ -149,9 +149,12 @@ void align(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
                          has_fn ? lut.data() : nullptr, res.data(), ops.data(), cap),
           "sa_align_batch");
     tm.lap("sa_align_batch (GPU)");
-    for (auto& r : res)
+    for (auto& r : res) {
         if (r.flags & SA_FLAG_DIVERGED)
             throw std::runtime_error("seqalib: the reference traceback does not terminate for this scoring");
+        if (r.flags & SA_FLAG_TIMEOUT)
+            throw std::runtime_error("seqalib: device band hand-off timed out; result invalid");
+    }
 }
 
 }  // namespace detail

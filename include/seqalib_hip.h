@@ -58,7 +58,9 @@ enum {
     SA_FLAG_DIVERGED = 1,     /* the reference's traceback would never terminate here
                                  (only reachable with scorings whose gap terms are >= 0) */
     SA_FLAG_BAD_SHAPE = 2,    /* device API: pair longer than the max_m/max_n it was given */
-    SA_FLAG_SIZE_HACK = 4     /* LocalGotoh pair replaced by NW (SALocalGotoh.h:484-488)   */
+    SA_FLAG_SIZE_HACK = 4,    /* LocalGotoh pair replaced by NW (SALocalGotoh.h:484-488)   */
+    SA_FLAG_TIMEOUT = 8       /* multi-workgroup plan: a band's bounded wait for the band
+                                 above it expired; the pair's result is invalid           */
 };
 
 /* ScoringSystem (include/SequenceAlignment.h:82-131).  Which fields are meaningful depends on

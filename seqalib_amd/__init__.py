@@ -30,13 +30,13 @@ __all__ = [
     "SeqalibError", "ScoringSystem", "Entry", "AlignedSequence", "PairResult", "Engine",
     "SmithWatermanSA", "NeedlemanWunschSA", "LocalGotohSA", "GlobalGotohSA", "HirschbergSA", "MyersMillerSA",
     "load_library", "library_path", "expand_ops", "synth_dna", "synth_mutate", "synth_dna_batch",
-    "SA_FLAG_DIVERGED", "SA_FLAG_BAD_SHAPE", "SA_FLAG_SIZE_HACK",
+    "SA_FLAG_DIVERGED", "SA_FLAG_BAD_SHAPE", "SA_FLAG_SIZE_HACK", "SA_FLAG_TIMEOUT",
 ]
 
 SA_SW, SA_NW, SA_LOCAL_GOTOH, SA_GLOBAL_GOTOH, SA_HIRSCHBERG, SA_MYERS_MILLER = 0, 1, 2, 3, 4, 5
 ALGO_NAMES = {SA_SW: "sw", SA_NW: "nw", SA_LOCAL_GOTOH: "local_gotoh", SA_GLOBAL_GOTOH: "global_gotoh",
               SA_HIRSCHBERG: "hirschberg", SA_MYERS_MILLER: "myers_miller"}
-SA_FLAG_DIVERGED, SA_FLAG_BAD_SHAPE, SA_FLAG_SIZE_HACK = 1, 2, 4
+SA_FLAG_DIVERGED, SA_FLAG_BAD_SHAPE, SA_FLAG_SIZE_HACK, SA_FLAG_TIMEOUT = 1, 2, 4, 8
 SA_KERNEL_INT32, SA_KERNEL_T16, SA_KERNEL_T16_ENDCELL = 0, 1, 2
 INT32_MIN = -(2 ** 31)
 
@@ -394,7 +394,9 @@ class Engine:
 
 
     def last_plan(self) -> Tuple[int, int, int]:
-        """(kernel, R, W) of the last call: kernel is SA_KERNEL_INT32 or SA_KERNEL_T16."""
+        """(kernel, R, W) of the last call: kernel is SA_KERNEL_INT32, SA_KERNEL_T16 or
+        SA_KERNEL_T16_ENDCELL; W = 0 for the multi-workgroup plan (one single-wave workgroup per
+        band of 64*R rows)."""
         k, R, W = C.c_int(), C.c_int(), C.c_int()
         self._check(self.L.sa_last_plan(self.h, C.byref(k), C.byref(R), C.byref(W)), "sa_last_plan")
         return k.value, R.value, W.value
@@ -486,6 +488,8 @@ class _Aligner:
         for (a, b), r in zip(pairs, res):
             if r.flags & SA_FLAG_DIVERGED:
                 raise SeqalibError("the reference traceback does not terminate for this scoring")
+            if r.flags & SA_FLAG_TIMEOUT:
+                raise SeqalibError("device hand-off timed out; result invalid")
             out.append(expand_ops(self.ALGO if not (r.flags & SA_FLAG_SIZE_HACK) else SA_NW,
                                   a, b, r, self.blank))
         self.last = res[-1] if res else None

@@ -40,6 +40,9 @@ struct sa_ctx {
     hipStream_t s_fill = nullptr, s_tb = nullptr;
     hipEvent_t ev_in = nullptr, ev_slot[2] = {nullptr, nullptr};
     uint64_t pipe_k = 0;
+    // SPLIT plans (few pairs, one workgroup per band): [ticket, pad to 256 B][granules][partials]
+    uint8_t* split = nullptr;
+    uint64_t split_bytes = 0;
 };
 
 namespace {
@@ -67,7 +70,15 @@ struct Plan {
     int R, W;
     Geom g;
     uint64_t rowbuf_elems;  // int32 per slot
+    bool split = false;     // one single-wave workgroup per (pair, band), cross-workgroup hand-off
 };
+
+// SPLIT plan when a batch is too small to fill the chip one workgroup per pair and its pairs
+// have at least two bands of 256 rows.  SEQALIB_SPLIT=0 disables it.
+bool split_ok(uint32_t max_m, uint32_t max_n, uint32_t npairs) {
+    if (const char* e = getenv("SEQALIB_SPLIT")) if (e[0] == '0') return false;
+    return npairs < 1024 && max_m > 4u * kWave && max_n > 0;
+}
 
 Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t16 = false) {
     Plan p;
@@ -84,6 +95,13 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t
         p.W = 4;
         p.R = 4;
         while (p.R < rmax && (uint64_t)kWave * p.R * p.W < max_m) p.R *= 2;
+    } else if (split_ok(max_m, max_n, npairs)) {
+        // Few pairs, several bands each: every band its own single-wave workgroup (on its own
+        // SIMD, anywhere on the chip), bands of a pair chained through HBM/L2 hand-offs.  Short
+        // bands (R = 4) give the most concurrent bands; R = 8 once there are plenty.
+        p.W = 1;
+        p.R = (uint64_t)npairs * ((max_m + 8 * kWave - 1) / (8 * kWave)) >= 2048 ? 8 : 4;
+        p.split = true;
     } else {
         // Few pairs: widen the workgroup instead (up to 16 waves) to use one CU fully.
         p.R = rmax;
@@ -92,13 +110,18 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t
         p.W = (int)std::max<uint64_t>(1, std::min<uint64_t>(16, w));
         while (p.R > 4 && (uint64_t)kWave * (p.R / 2) * p.W >= max_m) p.R /= 2;
     }
-    // tuning override: SEQALIB_PLAN="R,W"
+    // tuning override: SEQALIB_PLAN="R,W" (W = 0: SPLIT plan with R in {4, 8})
     if (const char* ov = getenv("SEQALIB_PLAN")) {
         int r = 0, w = 0;
-        if (sscanf(ov, "%d,%d", &r, &w) == 2 && (r == 4 || r == 8 || r == 16 || ((r == 32 || r == 64) && t16)) &&
+        if (sscanf(ov, "%d,%d", &r, &w) == 2 && w == 0 && (r == 4 || r == 8)) {
+            p.R = r;
+            p.W = 1;
+            p.split = true;
+        } else if (sscanf(ov, "%d,%d", &r, &w) == 2 && (r == 4 || r == 8 || r == 16 || ((r == 32 || r == 64) && t16)) &&
             w >= 1 && w <= 16) {
             p.R = r;
             p.W = w;
+            p.split = false;
         }
     }
     if (p.R >= 32 && p.W > 4) p.W = 4;   // fill_max_threads<32>
@@ -258,9 +281,10 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         snap_h_slot = snap_p_slot * (pl.R / 2);
         pl.rowbuf_elems = (uint64_t)pl.g.bands * std::max<uint32_t>(max_n, 1);
     }
+    if (pl.split) pl.rowbuf_elems = 0;   // hand-off granules live in c->split
     c->last_kernel = cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
     c->last_R = pl.R;
-    c->last_W = pl.W;
+    c->last_W = pl.split ? 0 : pl.W;   // 0: SPLIT plan (one single-wave workgroup per band)
     const uint64_t slot_bytes = pl.g.dir_slot + pl.rowbuf_elems * 4 + (snap_h_slot + snap_p_slot) * 4;
     const uint64_t budget = pipe ? ws_budget(c) / 2 : ws_budget(c);
     uint64_t per_launch = slot_bytes ? std::max<uint64_t>(1, budget / std::max<uint64_t>(slot_bytes, 1)) : npairs;
@@ -272,6 +296,25 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                                          " bytes of workspace, above the limit");
     int rc = ensure_ws(c, std::max<uint64_t>(pipe ? 2 * need : need, 4096));
     if (rc) return rc;
+    // SPLIT scratch (the fills of all calls run on one stream, so one copy serves the pipeline)
+    const uint64_t sp_bands = pl.g.bands;
+    const uint64_t sp_gran = pl.split ? per_launch * sp_bands * std::max<uint32_t>(max_n, 1) * (is_affine(algo) ? 2 : 1) : 0;
+    const uint64_t sp_zero = 256 + sp_gran * 8;   // ticket + granules: zeroed before every launch
+    const uint64_t sp_need = pl.split ? sp_zero + per_launch * sp_bands * 16 : 0;
+    if (pl.split && c->split_bytes < sp_need) {
+        if (c->split) {
+            SA_HIP(c, hipStreamSynchronize(c->stream));
+            if (c->s_fill) SA_HIP(c, hipStreamSynchronize(c->s_fill));
+            (void)hipFree(c->split);
+            c->split = nullptr;
+            c->split_bytes = 0;
+        }
+        if (hipMalloc(&c->split, sp_need) != hipSuccess) {
+            c->split = nullptr;
+            return fail(c, SA_ERR_NOMEM, "hipMalloc of the split-plan scratch failed");
+        }
+        c->split_bytes = sp_need;
+    }
     // pipeline slots are fixed halves of the workspace, so a later call with a smaller need
     // cannot overlap the slot a running traceback still reads
     uint8_t* dirs = c->ws + (pipe ? slot * ((c->ws_bytes / 2) & ~(uint64_t)255) : 0);
@@ -308,6 +351,11 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         fp.sym_pack = sym_pack;
         fp.snap_h = snap_h; fp.snap_p = snap_p;
         fp.snap_h_slot = snap_h_slot; fp.snap_p_slot = snap_p_slot; fp.snap_nch = snap_nch;
+        fp.split_bands = (uint32_t)sp_bands;
+        fp.ticket = pl.split ? reinterpret_cast<uint32_t*>(c->split) : nullptr;
+        fp.hand = pl.split ? reinterpret_cast<unsigned long long*>(c->split + 256) : nullptr;
+        fp.hand_x_off = pl.split ? (uint64_t)cnt * sp_bands * std::max<uint32_t>(max_n, 1) : 0;
+        fp.part = pl.split ? reinterpret_cast<int32_t*>(c->split + sp_zero) : nullptr;
 
         TbParams tp;
         tp.seq1 = d1; tp.off1 = o1; tp.seq2 = d2; tp.off2 = o2;
@@ -328,16 +376,34 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         }
         hipEvent_t* ev = &c->events[3 * c->launches];
         SA_HIP(c, hipEventRecord(ev[0], sf));
-        const FillVariant fv = {pl.R, lut, allow, keyed, t16, cmax};
-        hipError_t e = launch_fill(algo, fv, fp, cnt, sf);
+        const FillVariant fv = {pl.R, lut, allow, keyed, t16, cmax, pl.split};
+        if (pl.split) SA_HIP(c, hipMemsetAsync(c->split, 0, 256 + fp.hand_x_off * 8 * (is_affine(algo) ? 2 : 1), sf));
+        hipError_t e = launch_fill(algo, fv, fp, pl.split ? (uint32_t)(cnt * sp_bands) : cnt, sf);
         if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
+        if (pl.split) {
+            SplitReduceParams rp;
+            rp.off1 = o1; rp.off2 = o2; rp.part = fp.part; rp.res = d_res;
+            rp.pair_base = (uint32_t)base; rp.count = cnt; rp.split_bands = (uint32_t)sp_bands;
+            rp.band_rows = (uint32_t)kWave * pl.R; rp.max_m = max_m; rp.max_n = max_n;
+            rp.gap = sc->gap; rp.gap_open = sc->gap_open; rp.gap_extend = sc->gap_extend;
+            rp.cmax = cmax ? 1 : 0;
+            e = launch_split_reduce(algo, rp, sf);
+            if (e != hipSuccess) return hip_fail(c, e, "split reduce kernel launch");
+        }
         if (cmax) {
             EndcellParams ep;
             ep.seq1 = d1; ep.off1 = o1; ep.seq2 = d2; ep.off2 = o2;
             ep.prof = fp.prof; ep.sym_pack = sym_pack;
             ep.snap_h = snap_h; ep.snap_p = snap_p;
             ep.snap_h_slot = snap_h_slot; ep.snap_p_slot = snap_p_slot; ep.snap_nch = snap_nch;
-            ep.rowbuf = rowbuf; ep.rowbuf_slot = pl.rowbuf_elems; ep.max_n = max_n;
+            if (pl.split) {
+                ep.rowbuf = reinterpret_cast<const int32_t*>(fp.hand);
+                ep.rowbuf_slot = 2 * sp_bands * std::max<uint32_t>(max_n, 1);
+                ep.rowbuf_stride = 2;
+            } else {
+                ep.rowbuf = rowbuf; ep.rowbuf_slot = pl.rowbuf_elems; ep.rowbuf_stride = 1;
+            }
+            ep.max_n = max_n;
             ep.res = d_res; ep.pair_base = (uint32_t)base; ep.count = cnt;
             ep.gap = sc->gap;
             e = launch_endcell(pl.R, ep, sf);
@@ -514,6 +580,7 @@ void sa_destroy(sa_ctx* c) {
     if (c->ws) (void)hipFree(c->ws);
     if (c->io) (void)hipFree(c->io);
     if (c->aux) (void)hipFree(c->aux);
+    if (c->split) (void)hipFree(c->split);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

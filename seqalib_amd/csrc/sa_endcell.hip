@@ -11,6 +11,8 @@
 // unscaled scores, so it yields the same cell values the fill produced.
 //
 // One wave per pair; 32 steps x R rows per lane: ~0.05% of the fill's work at 4096 x 4096.
+#include <limits.h>
+
 #include "sa_internal.h"
 
 namespace sa {
@@ -64,13 +66,14 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
         prev_up = P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] >> 2;
     }
     int hl = Hp[R - 1];
-    const int32_t* top = b > 0 ? P.rowbuf + (uint64_t)slot * P.rowbuf_slot + (uint64_t)(b - 1) * P.max_n : nullptr;
+    const uint32_t rs = P.rowbuf_stride;
+    const int32_t* top = b > 0 ? P.rowbuf + (uint64_t)slot * P.rowbuf_slot + (uint64_t)(b - 1) * P.max_n * rs : nullptr;
     int jbest = -1;
     for (int q = 0; q < kChunk; ++q) {
         const int s = c * kChunk + q;
         const int j0 = s - lane;
         int up_h = __shfl_up(hl, 1);
-        if (lane == 0) up_h = (top && s < n) ? (top[s] >> 2) : 0;
+        if (lane == 0) up_h = (top && s < n) ? (top[(uint64_t)s * rs] >> 2) : 0;
         if (j0 >= 0 && j0 < n) {
             const uint32_t sym = ec_code8(P.sym_pack, s2[j0]);
             int hd = prev_up, hu = up_h;
@@ -96,6 +99,69 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
         res.reserved = 0;
         P.res[pidx] = res;
     }
+}
+
+// SPLIT fills (sa_fill_impl.h): fold each pair's per-band partials {score, i, j, timeout} into
+// its result — local modes: the lexicographic max over (score, i, j), i.e. the reference's last
+// row-major maximum; global modes: H[m][n] from the band holding row m.  One thread per pair.
+template <int ALG>
+__global__ void split_reduce_kernel(SplitReduceParams P) {
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= P.count) return;
+    const uint32_t pidx = P.pair_base + slot;
+    const int m = (int)(P.off1[pidx + 1] - P.off1[pidx]);
+    const int n = (int)(P.off2[pidx + 1] - P.off2[pidx]);
+    sa_result r = {};
+    if ((uint32_t)m > P.max_m || (uint32_t)n > P.max_n) {
+        r.flags = SA_FLAG_BAD_SHAPE;
+        P.res[pidx] = r;
+        return;
+    }
+    const int BR = (int)P.band_rows;
+    const int B = (m > 0 && n > 0) ? (m + BR - 1) / BR : 0;
+    const int32_t* q = P.part + (uint64_t)slot * P.split_bands * 4;
+    uint32_t tmo = 0;
+    for (int b = 0; b < B; ++b) tmo |= (uint32_t)q[4 * b + 3];
+    if (tmo) r.flags |= SA_FLAG_TIMEOUT;
+    constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
+    if constexpr (LOCAL) {
+        int h = INT_MIN, bi = 0, bj = 0;
+        for (int b = 0; b < B; ++b) {
+            const int oh = q[4 * b], oi = q[4 * b + 1], oj = q[4 * b + 2];
+            if (oh > h || (oh == h && (oi > bi || (oi == bi && oj > bj)))) { h = oh; bi = oi; bj = oj; }
+        }
+        if (B == 0) {
+            r.score = (ALG == SA_SW) ? INT_MIN : 0;   // as the single-workgroup fill reports it
+        } else if (P.cmax) {
+            r.score = h; r.end_i = bi; r.end_j = 0;
+            r.reserved = (uint32_t)bj;   // chunk + 1: endcell_kernel resolves the column
+        } else {
+            r.score = h; r.end_i = bi; r.end_j = bj;
+        }
+    } else {
+        r.end_i = m;
+        r.end_j = n;
+        if (B == 0) {
+            const int k = m > n ? m : n;
+            if constexpr (ALG == SA_NW) r.score = k * P.gap;
+            else r.score = k == 0 ? 0 : P.gap_open + k * P.gap_extend;
+        } else {
+            r.score = q[4 * (B - 1)];
+        }
+    }
+    P.res[pidx] = r;
+}
+
+hipError_t launch_split_reduce(int algo, const SplitReduceParams& p, hipStream_t stream) {
+    const dim3 grid((p.count + 255) / 256), block(256);
+    switch (algo) {
+        case SA_SW: hipLaunchKernelGGL(split_reduce_kernel<SA_SW>, grid, block, 0, stream, p); break;
+        case SA_NW: hipLaunchKernelGGL(split_reduce_kernel<SA_NW>, grid, block, 0, stream, p); break;
+        case SA_LOCAL_GOTOH: hipLaunchKernelGGL(split_reduce_kernel<SA_LOCAL_GOTOH>, grid, block, 0, stream, p); break;
+        case SA_GLOBAL_GOTOH: hipLaunchKernelGGL(split_reduce_kernel<SA_GLOBAL_GOTOH>, grid, block, 0, stream, p); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_endcell(int R, const EndcellParams& p, hipStream_t stream) {

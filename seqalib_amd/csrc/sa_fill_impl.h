@@ -90,7 +90,11 @@ __device__ __forceinline__ bool match_bit(const uint32_t* s_lut, int a, int b) {
 template <int R>
 constexpr int fill_max_threads() { return R >= 32 ? 256 : 1024; }
 
-template <int ALG, int R, bool LUT, bool ALLOW, bool KEYED, bool T16, bool CMAX>
+// Bounded wait of a SPLIT band for its producer, in s_memrealtime ticks (100 MHz): 0.2 s.  After
+// one expiry the workgroup stops waiting altogether (the pair is flagged SA_FLAG_TIMEOUT).
+constexpr uint64_t kSplitWaitTicks = 20000000ull;
+
+template <int ALG, int R, bool LUT, bool ALLOW, bool KEYED, bool T16, bool CMAX, bool SPLIT>
 __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams P) {
     constexpr bool AFF = ALG >= SA_LOCAL_GOTOH;
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
@@ -119,7 +123,19 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
     const int W = P.waves;
-    const uint32_t slot = blockIdx.x;
+    // SPLIT (few pairs): one single-wave workgroup per (pair, band).  Bands are handed out by a
+    // ticket counter in the order workgroups actually start, so band b's producer (ticket - 1)
+    // is always already running or done: no wait can deadlock whatever the residency.
+    uint32_t slot, band0 = 0;
+    if constexpr (SPLIT) {
+        uint32_t t = 0;
+        if (threadIdx.x == 0) t = atomicAdd(P.ticket, 1u);
+        t = __builtin_amdgcn_readfirstlane(t);
+        slot = t / P.split_bands;
+        band0 = t - slot * P.split_bands;
+    } else {
+        slot = blockIdx.x;
+    }
     const uint32_t pidx = P.pair_base + slot;
     const uint64_t o1 = P.off1[pidx];
     const uint64_t o2 = P.off2[pidx];
@@ -127,7 +143,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     const int n = (int)(P.off2[pidx + 1] - o2);
 
     if ((uint32_t)m > P.max_m || (uint32_t)n > P.max_n) {  // whole block leaves together
-        if (threadIdx.x == 0) {
+        if (!SPLIT && threadIdx.x == 0) {   // SPLIT: split_reduce_kernel reports it
             sa_result r = {};
             r.flags = SA_FLAG_BAD_SHAPE;
             P.res[pidx] = r;
@@ -154,9 +170,16 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     const uint32_t CU = (uint32_t)(4 * G + 2), CL = (uint32_t)(4 * G + 1);   // T16 tagged gaps
 
     const int B = (m > 0 && n > 0) ? (m + BAND - 1) / BAND : 0;
+    if (SPLIT && (int)band0 >= B) return;   // uniform: this pair has fewer bands
     const uint32_t nch = chunks_per_band((uint32_t)n);
     const uint32_t period = sched_period(nch, W);
-    const uint32_t total = total_phases((uint32_t)B, (uint32_t)n, W);
+    const uint32_t total = SPLIT ? nch : total_phases((uint32_t)B, (uint32_t)n, W);
+    // SPLIT hand-off: band b's last row as 8-byte {tag = 1, value} granules written
+    // write-through (sc1) per column, polled by band b+1 with sc1 loads; the data is its own flag
+    // (cdna_hip_programming.md Guideline 16, R2).  The host zeroes them before every launch.
+    typedef unsigned long long __attribute__((address_space(1))) gu64;
+    gu64* const hand_pair = SPLIT ? (gu64*)(P.hand + (uint64_t)slot * P.split_bands * P.max_n) : nullptr;
+    uint32_t tmo = 0;   // SPLIT: a bounded wait expired
 
     uint8_t* const dslot = P.dirs + (uint64_t)slot * P.dir_slot;
     int32_t* const rb_h = P.rowbuf + (uint64_t)slot * P.rowbuf_slot;
@@ -380,6 +403,18 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     auto ring = [&](int wave, int comp) -> int32_t* {
         return s_ring + (wave * (AFF ? 2 : 1) + comp) * kRing;
     };
+    // SPLIT: granules of the producer band for the chunk at column c0 (lane q: column c0 + q,
+    // clamped to the row, so every lane loads and no value is conditionally defined -- that keeps
+    // the prefetched registers in place instead of a copy that would wait for the load).
+    unsigned long long pre_h = 0, pre_x = 0;
+    auto split_load = [&](int band, int c0, unsigned long long& x, unsigned long long& y) {
+        if constexpr (SPLIT) {
+            const int cl = min(c0 + lane, n - 1);
+            gu64* const gh = hand_pair + (uint64_t)(band > 0 ? band - 1 : 0) * P.max_n + cl;
+            x = __hip_atomic_load(gh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if constexpr (AFF) y = __hip_atomic_load(gh + P.hand_x_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
     // Lane q < kChunk of the returned registers holds column c0 + q: the row-above value for
     // lane 0 (top border, or the previous band's last row) and Seq2[c].
     auto load_chunk = [&](int band, int c0, int& vh, int& vx, int& vs) {
@@ -392,6 +427,8 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 const int J = c + 1;
                 if constexpr (ALG == SA_NW) vh = SC * J * G;
                 else if constexpr (ALG == SA_GLOBAL_GOTOH) vh = GO + J * GE;
+            } else if constexpr (SPLIT) {
+                // polled below, after the branch (the wave must poll together)
             } else if (band % W != 0) {
                 vh = ring(band % W, 0)[c % kRing];
                 if constexpr (AFF) vx = ring(band % W, 1)[c % kRing];
@@ -400,14 +437,36 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 if constexpr (AFF) vx = rb_x[c];
             }
         }
+        if constexpr (SPLIT) {
+            if (band > 0) {
+                // The granules of this chunk were loaded one chunk ahead, so the memory latency
+                // overlaps the previous chunk; while any lane's tag is still 0 the wave re-polls.
+                const bool need = lane < kChunk && c < n;
+                uint64_t t0 = 0;
+                for (;;) {
+                    const bool pend = need && ((pre_h >> 32) == 0 || (AFF && (pre_x >> 32) == 0));
+                    if (__builtin_amdgcn_ballot_w64(pend) == 0 || tmo) break;
+                    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                    if (t0 == 0) t0 = now;
+                    else if (now - t0 > kSplitWaitTicks) { tmo = 1; break; }
+                    __builtin_amdgcn_s_sleep(2);
+                    split_load(band, c0, pre_h, pre_x);
+                }
+                if (need) {
+                    vh = (int)(uint32_t)pre_h;
+                    if constexpr (AFF) vx = (int)(uint32_t)pre_x;
+                }
+                split_load(band, c0 + kChunk, pre_h, pre_x);   // next chunk's, in flight meanwhile
+            }
+        }
     };
 
     for (uint32_t ph = 0; ph < total; ++ph) {
         const int rel = (int)ph - w * kLagPhases;
-        if (rel >= 0) {
-            const uint32_t k = (uint32_t)rel / period;
-            const uint32_t chunk = (uint32_t)rel - k * period;
-            const int band = w + (int)k * W;
+        if (SPLIT || rel >= 0) {
+            const uint32_t k = SPLIT ? 0u : (uint32_t)rel / period;
+            const uint32_t chunk = SPLIT ? ph : (uint32_t)rel - k * period;
+            const int band = SPLIT ? (int)band0 : w + (int)k * W;
             if (chunk < nch && band < B) {
                 // ---------------------------------------------------------------- band start
                 if (chunk == 0) {
@@ -426,6 +485,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                         cm[r] = 0x8000u;
                         bj[r] = 0;
                     }
+                    split_load(band, 0, pre_h, pre_x);
                     if constexpr (ALG == SA_NW) prev_up = SC * row0 * G;
                     else if constexpr (ALG == SA_GLOBAL_GOTOH) prev_up = row0 == 0 ? 0 : GO + row0 * GE;
                     else prev_up = 0;
@@ -443,7 +503,14 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                     const int cc = kC + lane - (kWave - 1);
                     if (lane < kChunk && cc >= 0 && cc < n) {
                         const int nw = (band + 1) % W;
-                        if (nw != 0) {
+                        if constexpr (SPLIT) {
+                            gu64* const gh = hand_pair + (uint64_t)band * P.max_n;
+                            __hip_atomic_store(gh + cc, (1ull << 32) | (uint32_t)acc_h, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                            if constexpr (AFF)
+                                __hip_atomic_store(gh + P.hand_x_off + cc, (1ull << 32) | (uint32_t)acc_x,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        } else if (nw != 0) {
                             ring(nw, 0)[cc % kRing] = acc_h;
                             if constexpr (AFF) ring(nw, 1)[cc % kRing] = acc_x;
                         } else {
@@ -501,7 +568,25 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     }
 
     // ------------------------------------------------------------------------ results
-    if constexpr (LOCAL) {
+    if constexpr (SPLIT) {
+        // per-band partial {score, i, j, timeout}; split_reduce_kernel folds them per pair
+        if constexpr (LOCAL) {
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                const int oh = __shfl_xor(best_h, off);
+                const int oi = __shfl_xor(best_i, off);
+                const int oj = __shfl_xor(best_j, off);
+                const bool take = oh > best_h || (oh == best_h && (oi > best_i || (oi == best_i && oj > best_j)));
+                if (take) { best_h = oh; best_i = oi; best_j = oj; }
+            }
+        } else {
+            best_h = ((m - 1) / BAND == (int)band0) ? s_score : 0;   // ordered by the loop's barrier
+        }
+        if (threadIdx.x == 0) {
+            int32_t* q = P.part + ((uint64_t)slot * P.split_bands + band0) * 4;
+            q[0] = best_h; q[1] = best_i; q[2] = best_j; q[3] = (int32_t)tmo;
+        }
+    } else if constexpr (LOCAL) {
         // lexicographic max over (score, i, j): the reference's last row-major maximum
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
@@ -557,37 +642,49 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
     const bool keyed = LOCAL && v.keyed;
     const dim3 block(kWave * p.waves);
     const size_t lds = lds_layout(lut, is_affine(ALG), p.waves, p.stage_seq2 ? p.max_n : 0).total;
+    const bool split = v.split;
+    if (split && (p.waves != 1 || (R != 4 && R != 8))) return hipErrorInvalidConfiguration;
     if constexpr (ALG == SA_SW || ALG == SA_NW) {
         if (v.t16) {
             if (!allow || (LOCAL && !keyed)) return hipErrorInvalidValue;
             if ((int)block.x > (R >= 32 ? fill_max_threads<32>() : fill_max_threads<16>()))
                 return hipErrorInvalidConfiguration;
-#define SA_LAUNCH16(RR)                                                                              \
-    if (R == RR) {                                                                                   \
+#define SA_LAUNCH16S(RR, SP)                                                                         \
+    if (R == RR && split == SP) {                                                                    \
         if constexpr (ALG == SA_SW) {                                                                \
             if (v.cmax) {                                                                            \
-                hipLaunchKernelGGL((fill_kernel<ALG, RR, false, true, LOCAL, true, true>), dim3(grid), \
+                hipLaunchKernelGGL((fill_kernel<ALG, RR, false, true, LOCAL, true, true, SP>), dim3(grid), \
                                    block, lds, stream, p);                                           \
                 return hipGetLastError();                                                            \
             }                                                                                        \
         }                                                                                            \
-        hipLaunchKernelGGL((fill_kernel<ALG, RR, false, true, LOCAL, true, false>), dim3(grid), block, \
+        hipLaunchKernelGGL((fill_kernel<ALG, RR, false, true, LOCAL, true, false, SP>), dim3(grid), block, \
                            lds, stream, p);                                                          \
         return hipGetLastError();                                                                    \
     }
-            SA_LAUNCH16(4)
-            SA_LAUNCH16(8)
-            SA_LAUNCH16(16)
-            SA_LAUNCH16(32)
-            SA_LAUNCH16(64)
-#undef SA_LAUNCH16
+            SA_LAUNCH16S(4, false)
+            SA_LAUNCH16S(8, false)
+            SA_LAUNCH16S(16, false)
+            SA_LAUNCH16S(32, false)
+            SA_LAUNCH16S(64, false)
+            SA_LAUNCH16S(4, true)
+            SA_LAUNCH16S(8, true)
+#undef SA_LAUNCH16S
             return hipErrorInvalidValue;
         }
     }
     if (v.t16 || v.cmax) return hipErrorInvalidValue;
 #define SA_LAUNCH(RR, LL, AA, KK)                                                              \
     if (R == RR && lut == LL && allow == AA && keyed == KK) {                                  \
-        hipLaunchKernelGGL((fill_kernel<ALG, RR, LL, AA, KK, false, false>), dim3(grid), block, lds, stream, p); \
+        if (split) {                                                                           \
+            if constexpr (RR <= 8) {                                                           \
+                hipLaunchKernelGGL((fill_kernel<ALG, RR, LL, AA, KK, false, false, true>), dim3(grid), block, lds, \
+                                   stream, p);                                                 \
+                return hipGetLastError();                                                      \
+            }                                                                                  \
+            return hipErrorInvalidConfiguration;                                               \
+        }                                                                                      \
+        hipLaunchKernelGGL((fill_kernel<ALG, RR, LL, AA, KK, false, false, false>), dim3(grid), block, lds, stream, p); \
         return hipGetLastError();                                                              \
     }
 #define SA_LAUNCH_K(RR, LL, AA) \

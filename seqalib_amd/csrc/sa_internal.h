@@ -35,7 +35,28 @@ struct FillParams {
     int32_t* snap_p;
     uint64_t snap_h_slot, snap_p_slot;
     uint32_t snap_nch;
+    // SPLIT only: one single-wave workgroup per (pair slot, band), split_bands bands per slot,
+    // bands handed out by *ticket.  hand: per slot and band, max_n 8-byte {tag, H} granules of
+    // the band's last row (Ix: at + hand_x_off); part: per slot and band {score, i, j, timeout}.
+    unsigned long long* hand;
+    uint64_t hand_x_off;
+    uint32_t* ticket;
+    int32_t* part;
+    uint32_t split_bands;
 };
+
+// SPLIT fills: per-pair fold of the per-band partials into sa_result (split_reduce_kernel).
+struct SplitReduceParams {
+    const uint64_t* off1;
+    const uint64_t* off2;
+    const int32_t* part;
+    sa_result* res;
+    uint32_t pair_base, count, split_bands, band_rows;
+    uint32_t max_m, max_n;
+    int32_t gap, gap_open, gap_extend;
+    int cmax;
+};
+hipError_t launch_split_reduce(int algo, const SplitReduceParams& p, hipStream_t stream);
 
 // End-cell replay (sa_endcell.hip) after a CMAX fill: res.reserved = chunk + 1 of the maximum.
 struct EndcellParams {
@@ -51,6 +72,7 @@ struct EndcellParams {
     uint32_t snap_nch;
     const int32_t* rowbuf;
     uint64_t rowbuf_slot;
+    uint32_t rowbuf_stride;    // int32 per column: 1 (row buffer) or 2 (SPLIT {value, tag} granules)
     uint32_t max_n;
     sa_result* res;
     uint32_t pair_base, count;
@@ -73,13 +95,14 @@ struct TbParams {
     int allow;
     int tagged;                // records hold T16 max tags (sa_layout.h)
 };
+// SA_FLAG_TIMEOUT: a SPLIT band's bounded wait for its producer expired (results invalid)
 
 // R in {4, 8, 16}; keyed: 16-bit (score, column) max keys (local modes only); t16: the tagged
 // 16-bit profile kernel (SW/NW with allow-mismatch, see sa_fill_impl.h).
 // Returns hipSuccess or the launch error.
 struct FillVariant {
     int R;
-    bool lut, allow, keyed, t16, cmax;
+    bool lut, allow, keyed, t16, cmax, split;
 };
 hipError_t launch_fill(int algo, const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream);
 hipError_t launch_fill_sw(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);

@@ -171,11 +171,52 @@ def test_many_pairs_plan_vs_oracle(engine, algo):
 
 
 @pytest.mark.parametrize("algo", [0, 1, 2, 3])
-def test_multiband_wrap_vs_oracle(engine, algo):
-    """More bands than waves (m > 64*R*W): bands wrap round-robin over the waves."""
+def test_multiband_wrap_vs_oracle(engine, algo, monkeypatch):
+    """More bands than waves (m > 64*R*W): bands wrap round-robin over the waves of one
+    workgroup (the single-workgroup few-pairs plan; SEQALIB_SPLIT=0 keeps it selected)."""
+    monkeypatch.setenv("SEQALIB_SPLIT", "0")
     pairs = [(sa.synth_dna(31, 21000), sa.synth_dna(32, 97)), (sa.synth_dna(33, 9000), sa.synth_dna(34, 300)),
              (sa.synth_dna(35, 130), sa.synth_dna(36, 9000))]
     compare_with_oracle(engine, algo, SCORINGS[algo][1 % len(SCORINGS[algo])], pairs)
+    assert engine.last_plan()[2] > 0
+
+
+def split_pairs(seed):
+    """Few pairs with 1..40 bands of 256 rows: ragged band counts inside one launch, thin and wide
+    shapes, related pairs (long local paths crossing many bands), and empty sides."""
+    rng = np.random.default_rng(seed)
+    pairs = [(sa.synth_dna(seed, 10000), sa.synth_mutate(sa.synth_dna(seed, 10000), seed)[:9000]),
+             (sa.synth_dna(seed + 1, 4096), sa.synth_dna(seed + 2, 4096)),
+             (sa.synth_dna(seed + 3, 3000), sa.synth_dna(seed + 4, 70)),
+             (sa.synth_dna(seed + 5, 300), sa.synth_dna(seed + 6, 5000)),
+             (sa.synth_dna(seed + 7, 257), sa.synth_dna(seed + 8, 1)),
+             (b"", sa.synth_dna(seed + 9, 40)), (sa.synth_dna(seed + 10, 600), b"")]
+    for k in range(12):
+        m, n = int(rng.integers(1, 2600)), int(rng.integers(1, 2600))
+        a = sa.synth_dna(seed * 100 + 2 * k, m)
+        b = sa.synth_mutate(a, k)[:n] if k % 2 else sa.synth_dna(seed * 100 + 2 * k + 1, n)
+        pairs.append((a, b))
+    return pairs
+
+
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+def test_split_plan_vs_oracle(engine, algo, monkeypatch):
+    """Few pairs take the multi-workgroup plan: one single-wave workgroup per (pair, band), band
+    b+1 polling band b's last row through write-through {tag, value} granules (sa_fill_impl.h,
+    SPLIT).  Every scoring of the algorithm (T16 + end-cell replay for DNA SW/NW with
+    allow-mismatch, int32 otherwise), R = 4 and R = 8, and a custom match table, against the
+    oracle; the result must not depend on the plan."""
+    pairs = split_pairs(40 + algo)
+    for args in SCORINGS[algo]:
+        compare_with_oracle(engine, algo, args, pairs)
+        assert engine.last_plan()[1:] == (4, 0), args
+        assert all(r.flags & sa.SA_FLAG_TIMEOUT == 0 for r in engine.align(algo, sc_obj(args), pairs[:2]))
+    monkeypatch.setenv("SEQALIB_PLAN", "8,0")
+    compare_with_oracle(engine, algo, SCORINGS[algo][0], pairs)
+    assert engine.last_plan()[1:] == (8, 0)
+    monkeypatch.delenv("SEQALIB_PLAN")
+    compare_with_oracle(engine, algo, SCORINGS[algo][0], pairs, "purine")
+    assert engine.last_plan()[1:] == (4, 0)
 
 
 T16_KERNELS = (sa.SA_KERNEL_T16, sa.SA_KERNEL_T16_ENDCELL)
