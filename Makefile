@@ -13,7 +13,7 @@ OBJDIR    = build/obj
 LIB       = seqalib_amd/lib/libseqalib_hip.so
 
 HIP_SRCS  = $(CSRC)/sa_fill_sw.hip $(CSRC)/sa_fill_nw.hip $(CSRC)/sa_fill_lg.hip $(CSRC)/sa_fill_gg.hip \
-            $(CSRC)/sa_traceback.hip $(CSRC)/sa_alphabet.hip $(CSRC)/sa_endcell.hip $(CSRC)/sa_hirschberg.hip \
+            $(CSRC)/sa_traceback.hip $(CSRC)/sa_traceback_wave.hip $(CSRC)/sa_alphabet.hip $(CSRC)/sa_endcell.hip $(CSRC)/sa_hirschberg.hip \
             $(CSRC)/sa_myersmiller.hip $(CSRC)/sa_api.hip
 CPP_SRCS  = $(CSRC)/sa_synth.cpp
 HDRS      = $(CSRC)/sa_internal.h $(CSRC)/sa_layout.h $(CSRC)/sa_fill_impl.h $(CSRC)/sa_dc.h include/seqalib_hip.h
@@ -33,6 +33,14 @@ $(LIB): $(OBJS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -lpthread
 
+# debug build with traceback counters (tools/tb_stats.py): build/libstats.so
+STATS_LIB = build/libstats.so
+stats: $(STATS_LIB)
+$(STATS_LIB): $(HIP_SRCS) $(CPP_SRCS) $(HDRS)
+	@mkdir -p build/stats
+	for f in $(HIP_SRCS) $(CPP_SRCS); do $(HIPCC) $(HIPFLAGS) -DSA_TB_STATS -c $$f -o build/stats/$$(basename $$f).o || exit 1; done
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ build/stats/*.o -lpthread
+
 oracle:
 	$(MAKE) -C oracle
 
@@ -45,4 +53,4 @@ clean:
 	rm -rf build $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: lib oracle ref all-checkers clean
+.PHONY: lib stats oracle ref all-checkers clean

@@ -142,6 +142,16 @@ __global__ void lut_to_bits(const uint8_t* lut, uint32_t* bits) {
     bits[w] = v;
 }
 
+// Traceback flavour per launch: one wave per pair (sa_traceback_wave.hip) for few pairs, one lane
+// per pair (sa_traceback.hip) for batches.  SEQALIB_TB=wave|lane overrides.
+bool tb_wave(uint32_t count) {
+    if (const char* e = getenv("SEQALIB_TB")) {
+        if (!strcmp(e, "wave")) return true;
+        if (!strcmp(e, "lane")) return false;
+    }
+    return count < 1024;
+}
+
 int ensure_ws(sa_ctx* c, uint64_t need) {
     if (c->ws_bytes >= need) return SA_OK;
     if (c->ws) {
@@ -411,7 +421,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         }
         SA_HIP(c, hipEventRecord(ev[1], sf));
         if (pipe) SA_HIP(c, hipStreamWaitEvent(stb, ev[1], 0));
-        e = launch_traceback(algo, pl.R, lut, tp, stb);
+        e = tb_wave(cnt) ? launch_traceback_wave(algo, pl.R, lut, tp, stb) : launch_traceback(algo, pl.R, lut, tp, stb);
         if (e != hipSuccess) return hip_fail(c, e, "traceback kernel launch");
         SA_HIP(c, hipEventRecord(ev[2], stb));
         c->launches++;

@@ -116,6 +116,8 @@ hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uin
 hipError_t launch_build_profile(const uint32_t* lutbits, uint32_t sym_pack, int match, int mismatch,
                                 uint32_t* prof, hipStream_t s);
 hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
+// One wave per pair (sa_traceback_wave.hip): the few-pairs traceback.
+hipError_t launch_traceback_wave(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
 hipError_t launch_endcell(int R, const EndcellParams& p, hipStream_t stream);
 }  // namespace sa
 #include <string>

@@ -454,3 +454,22 @@ def test_multi_gpu_threads_match_single(engine):
         off = int(o1[p] + o2[p]) + p
         n = int(ref["nops"][p])
         assert ops[off:off + n].tobytes() == ref_ops[off:off + n].tobytes()
+
+
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+@pytest.mark.parametrize("tb", ["wave", "lane"])
+def test_traceback_flavours_vs_oracle(engine, algo, tb, monkeypatch):
+    """Both traceback kernels on both plans: one wave per pair (sa_traceback_wave.hip, default
+    below 1024 pairs) and one lane per pair (sa_traceback.hip, default for batches), forced with
+    SEQALIB_TB.  Long related pairs cross many decode windows (128 rows x 16 diagonals) and drift
+    across diagonals through gaps; the many-pairs batch takes the one-wave-per-pair fill."""
+    monkeypatch.setenv("SEQALIB_TB", tb)
+    pairs = split_pairs(60 + algo)
+    for args in SCORINGS[algo][:2]:
+        compare_with_oracle(engine, algo, args, pairs)
+    many = []
+    for k in range(1030):
+        a = sa.synth_dna(90_000 + 2 * k, 100 + k % 300)
+        b = sa.synth_mutate(a, k)[: 90 + k % 250] if k % 2 else sa.synth_dna(90_001 + 2 * k, 80 + k % 200)
+        many.append((a, b))
+    compare_with_oracle(engine, algo, SCORINGS[algo][0], many, "purine" if algo == 3 else None)
