@@ -38,7 +38,7 @@ SCORING = (-1, 1, -1)         # SmithWatermanSA::getDefaultScoring (SASmithWater
 # The fill kernel is VALU-issue bound.  Its roofline peak is the issue ceiling of the steady
 # loop's own instruction mix, every opcode priced at its measured gfx950 issue rate
 # (tools/issue_model.py -> ISSUE_MODEL, rates from profiles/microbench_valu_issue_r01.txt).
-ISSUE_MODEL = os.path.join(ROOT, "profiles", "issue_model_r02.json")
+ISSUE_MODEL = os.path.join(ROOT, "profiles", "issue_model_r03.json")
 HBM_PEAK_GBPS = 8000.0
 SW_FLAG_BYTES_PER_CELL = 0.25  # 2 traceback bits per cell written to HBM
 
@@ -263,7 +263,7 @@ def main():
                  "fill_gcups": round(fill_gcups, 1),
                  "issue_ceiling_gcups": model["peak_gcups"] if model else None, "valu_per_cell": vpc,
                  "peak_basis": "steady-loop VALU mix x measured per-opcode issue rates (tools/issue_model.py, "
-                               "profiles/issue_model_r02.json)",
+                               "profiles/issue_model_r03.json)",
                  "bytes_per_cell": round(bytes_per_cell, 4), "hbm_achieved_GBps": round(hbm_gbps, 1),
                  "hbm_peak_GBps": HBM_PEAK_GBPS, "hbm_frac": round(hbm_gbps / HBM_PEAK_GBPS, 4)})
     line = {

@@ -212,6 +212,7 @@ bool t16_ok(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
     const int64_t MA = sc->match, MI = sc->mismatch, G = sc->gap;
     if (MA < -32 || MA > 31 || MI < -32 || MI > 31) return false;
     if (G > 0 || MI > MA || G < -4096) return false;
+    if (algo == SA_SW && G == 0) return false;   // the clamped up term needs gap < 0 (sa_fill_impl.h)
     const int64_t m = max_m, n = max_n, k = std::min(m, n);
     const int64_t hi = std::max<int64_t>(MA, 0) * k;
     int64_t lo = 0;
@@ -356,7 +357,9 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         fp.gap = sc->gap; fp.match = sc->match; fp.mismatch = allow ? sc->mismatch : INT_MIN;
         fp.gap_open = sc->gap_open; fp.gap_extend = sc->gap_extend;
         fp.waves = pl.W;
-        fp.stage_seq2 = max_n <= kMaxStagedSeq2 ? 1 : 0;
+        fp.stage_seq2 = (max_n <= kMaxStagedSeq2 &&
+                         lds_layout(t16 ? false : lut, is_affine(algo), pl.W, max_n, t16 ? pl.R : 0).total <= kMaxLds)
+                            ? 1 : 0;
         fp.prof = aux + 8;
         fp.sym_pack = sym_pack;
         fp.snap_h = snap_h; fp.snap_p = snap_p;

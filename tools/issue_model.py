@@ -12,38 +12,42 @@ instruction at its measured issue rate and reports
     cycles_per_lane_cell = sum(count / rate) / cells_per_lane_in_block   [SIMD cycles / 64 cells]
     peak_gcups = SIMDs * clock * 64 / cycles_per_lane_cell / 1e9
 Scalar and memory instructions issue on other units and are not charged.
-    python3 tools/issue_model.py [--out profiles/issue_model_r02.json]
+    python3 tools/issue_model.py [--out profiles/issue_model_r03.json]
 """
 import argparse, collections, json, os, re, subprocess, sys, tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-RATES_FILE = os.path.join(ROOT, "profiles", "microbench_valu_issue_r01.txt")
+RATES_FILES = [os.path.join(ROOT, "profiles", f) for f in ("microbench_valu_issue_r01.txt", "microbench_sdwa_r01.txt")]
 SIMDS, CLOCK = 256 * 4, 2.4e9
 
 ALIAS = {"v_mov_b32_dpp": "v_mov_b32_dpp_shr", "v_readlane_b32": "readlane", "v_writelane_b32": "readlane",
          "v_mov_b32": "mov_b32", "v_max_i16": "max_i16", "v_add_u16": "add_u16", "v_alignbit_b32": "alignbit_b32",
          "v_bfe_i32": "v_bfe_u32", "v_addc_co_u32": "addc_only", "v_cndmask_b32": "cndmask_e64_sgpr",
+         "v_add_u16_sdwa": "add_u16_sdwa_byte1_sext", "v_sub_u16": "sub_u16_e64_clamp",
          "v_cmp_eq_u32": "cmp_only", "v_cmp_gt_u32": "cmp_only", "v_cmp_le_u32": "cmp_only",
          "v_lshl_add_u64": "v_lshl_add_u32", "v_max3_i32": "v_max3_i32", "v_add_co_u32": "add_co_e64"}
 
 KERNELS = {  # label -> (TU, mangled name, cells per lane in one steady block = SPP * R)
-    "sw_t16_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELb0ELb1ELb1ELb1ELb0EEEvNS_10FillParamsE", 64),
-    "sw_t16c_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELb0ELb1ELb1ELb1ELb1EEEvNS_10FillParamsE", 64),
-    "sw_t16c_r32": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi32ELb0ELb1ELb1ELb1ELb1EEEvNS_10FillParamsE", 64),
-    "sw_t16_r32": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi32ELb0ELb1ELb1ELb1ELb0EEEvNS_10FillParamsE", 64),
-    "nw_t16_r32": ("sa_fill_nw.hip", "_ZN2sa11fill_kernelILi1ELi32ELb0ELb1ELb0ELb1ELb0EEEvNS_10FillParamsE", 64),
-    "sw_int32_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELb0ELb1ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
-    "nw_t16_r16": ("sa_fill_nw.hip", "_ZN2sa11fill_kernelILi1ELi16ELb0ELb1ELb0ELb1ELb0EEEvNS_10FillParamsE", 64),
-    "lg_int32_r16": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi16ELb0ELb1ELb1ELb0ELb0EEEvNS_10FillParamsE", 32),
+    "sw_t16_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELb0ELb1ELb1ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
+    "sw_t16c_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELb0ELb1ELb1ELb1ELb1ELb0EEEvNS_10FillParamsE", 64),
+    "sw_t16c_r32": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi32ELb0ELb1ELb1ELb1ELb1ELb0EEEvNS_10FillParamsE", 64),
+    "sw_t16_r32": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi32ELb0ELb1ELb1ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
+    "nw_t16_r32": ("sa_fill_nw.hip", "_ZN2sa11fill_kernelILi1ELi32ELb0ELb1ELb0ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
+    "sw_int32_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELb0ELb1ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 64),
+    "nw_t16_r16": ("sa_fill_nw.hip", "_ZN2sa11fill_kernelILi1ELi16ELb0ELb1ELb0ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
+    "lg_int32_r16": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi16ELb0ELb1ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 32),
 }
 
 
 def rates():
     r = {}
-    for line in open(RATES_FILE):
-        m = re.match(r"^(\S+)\s+[\d.]+ ms\s+([\d.]+) wave-instr", line)
-        if m:
-            r[m.group(1)] = float(m.group(2))
+    for f in RATES_FILES:
+        if not os.path.exists(f):
+            continue
+        for line in open(f):
+            m = re.match(r"^(\S+)\s+[\d.]+ ms\s+([\d.]+) wave-instr", line)
+            if m:
+                r.setdefault(m.group(1), float(m.group(2)))
     return r
 
 
@@ -77,7 +81,7 @@ def main():
     ap.add_argument("--kernels", default=",".join(KERNELS))
     a = ap.parse_args()
     R = rates()
-    out = {"rates_file": os.path.relpath(RATES_FILE, ROOT), "simds": SIMDS, "clock_hz": CLOCK, "kernels": {}}
+    out = {"rates_files": [os.path.relpath(f, ROOT) for f in RATES_FILES], "simds": SIMDS, "clock_hz": CLOCK, "kernels": {}}
     cache = {}
     with tempfile.TemporaryDirectory() as td:
         for label in a.kernels.split(","):
