@@ -357,9 +357,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         fp.gap = sc->gap; fp.match = sc->match; fp.mismatch = allow ? sc->mismatch : INT_MIN;
         fp.gap_open = sc->gap_open; fp.gap_extend = sc->gap_extend;
         fp.waves = pl.W;
-        fp.stage_seq2 = (max_n <= kMaxStagedSeq2 &&
-                         lds_layout(t16 ? false : lut, is_affine(algo), pl.W, max_n, t16 ? pl.R : 0).total <= kMaxLds)
-                            ? 1 : 0;
+        fp.stage_seq2 = max_n <= kMaxStagedSeq2 ? 1 : 0;
         fp.prof = aux + 8;
         fp.sym_pack = sym_pack;
         fp.snap_h = snap_h; fp.snap_p = snap_p;

@@ -53,7 +53,6 @@
 namespace sa {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 constexpr int kDppWaveShr1 = 0x138;  // DPP wave_shr:1 (GFX9-family wave-wide shift)
 
 __device__ __forceinline__ int shr1(int old, int src) {
@@ -151,13 +150,10 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
         }
         return;
     }
-    const LdsLayout lay = lds_layout(LUT, AFF, W, P.stage_seq2 ? P.max_n : 0, T16 ? R : 0);
+    const LdsLayout lay = lds_layout(LUT, AFF, W, P.stage_seq2 ? P.max_n : 0);
     uint32_t* const s_lut = smem;
     int32_t* const s_ring = reinterpret_cast<int32_t*>(smem + lay.ring_off / 4);
     uint8_t* const s_seq2 = reinterpret_cast<uint8_t*>(smem) + lay.seq_off;
-    // T16: this lane's column profiles, [code c][row r] = tagged s(Seq1[row r], symbol c)
-    uint8_t* const s_tab = reinterpret_cast<uint8_t*>(smem) + lay.tab_off +
-                           (uint32_t)(w * kWave + lane) * t16_tab_stride(R);
     const uint8_t* s1 = P.seq1 + o1;
     const uint8_t* s2 = P.seq2 + o2;
     if constexpr (LUT) {
@@ -207,28 +203,6 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     // score, then last row, then last chunk -- the row-major order the end cell needs
     uint32_t lkey = 0;
     int hl = 0, xl = 0, sym = 0, prev_up = 0;
-    // T16: the profile bytes of my R rows against the current step's column symbol (4 rows per
-    // word, row r = byte r % 4 of word r / 4, consumed by SDWA byte selects), read from the LDS
-    // table one step ahead of their use.
-    constexpr int TW = T16 ? R / 4 : 1;
-    uint32_t cp[TW];
-#pragma unroll
-    for (int k = 0; k < TW; ++k) cp[k] = 0;
-    auto load_cp = [&](int code8, uint32_t (&d)[TW]) {
-        const uint8_t* p = s_tab + (uint32_t)(code8 >> 3) * R;
-        if constexpr (TW % 4 == 0) {
-#pragma unroll
-            for (int k = 0; k < TW / 4; ++k) {
-                const u32x4 v = *reinterpret_cast<const u32x4*>(p + 16 * k);
-                d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
-            }
-        } else if constexpr (TW == 2) {
-            const u32x2 v = *reinterpret_cast<const u32x2*>(p);
-            d[0] = v.x; d[1] = v.y;
-        } else {
-            d[0] = *reinterpret_cast<const uint32_t*>(p);
-        }
-    };
     int row0 = 0;
     // Running best of this lane over its bands: (score, i, j), 1-based cell.
     int best_h = INT_MIN, best_i = 0, best_j = 0;
@@ -245,16 +219,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
         const int up_h = shr1(__builtin_amdgcn_readlane(bch, q), hl);
         int up_x = 0;
         if constexpr (AFF) up_x = shr1(__builtin_amdgcn_readlane(bcx, q), xl);
-        int symn = 0;
-        uint32_t cpn[TW];
-        if constexpr (T16) {
-            // this step's symbol and profile were fetched by the previous step; fetch the next
-            // (lane 0's from lane q + 1 <= kChunk of the chunk's symbols)
-            symn = shr1(__builtin_amdgcn_readlane(symc, q + 1), sym);
-            load_cp(symn, cpn);
-        } else {
-            sym = shr1(__builtin_amdgcn_readlane(symc, q), sym);
-        }
+        sym = shr1(__builtin_amdgcn_readlane(symc, q), sym);
         const int j = s - lane;
 #pragma unroll
         for (int e = 0; e < RW; ++e) rec[e] = 0;
@@ -265,9 +230,8 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
             int xu = up_x;               // Ix[i-1][j]
             uint32_t dcur = 0;           // T16: tagged diagonal candidate of the current row
             if constexpr (T16) {
-                asm("v_add_u16_sdwa %0, %1, sext(%2) dst_sel:WORD_0 dst_unused:UNUSED_PAD "
-                    "src0_sel:WORD_0 src1_sel:BYTE_0"
-                    : "=v"(dcur) : "v"(hd), "v"(cp[0]));
+                asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0"
+                    : "=&v"(dcur) : "v"(a[0]), "v"(sym), "v"(hd));
             }
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -277,9 +241,10 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                     // One asm block per cell (plain VALU->VALU dependences need no wait
                     // states; the compiler pads s_nop between separate asm statements).  The
                     // block also forms the NEXT row's diagonal candidate from Hp[r] before
-                    // updating Hp[r] in place, so no register copies are needed; its
-                    // substitution byte comes straight out of the profile word by an SDWA
-                    // byte select (BYTE_k, k = (r + 1) % 4, sign-extended).
+                    // updating Hp[r] in place, so no register copies are needed.  Its
+                    // substitution term is v_bfe_i32 of the row's 4-byte profile at 8 x the
+                    // column's symbol code (an SDWA byte select from a per-step LDS column profile
+                    // is one instruction fewer but measured slower: tools/microbench_cellmix.hip).
                     uint32_t t0, t1;
                     // R >= 32: the row-max key update (lshl_or + max_u32, in place) joins the
                     // block -- separate statements would cost s_nops and register renaming.
@@ -292,8 +257,8 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     "v_max_i16 %[t0], %[dr], %[t0]\n\t"                                                      \
     "v_max_i16 %[t0], %[t1], %[t0]\n\t"
 #define SA_T16_NEXT                                                                          \
-    "v_add_u16_sdwa %[dn], %[hp], sext(%[pw]) dst_sel:WORD_0 dst_unused:UNUSED_PAD "         \
-    "src0_sel:WORD_0 src1_sel:BYTE_%c[kb]\n\t"
+    "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\t"                                                \
+    "v_add_u16 %[dn], %[hp], %[dn]\n\t"
 #define SA_T16_TAIL                                                                          \
     "v_and_b32 %[hp], -4, %[t0]\n\t"                                                         \
     "v_alignbit_b32 %[rec], %[t0], %[rec], 2\n\t"
@@ -302,11 +267,11 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     "v_max_u32 %[bh], %[bh], %[t1]\n\t"
 #define SA_T16_OUT [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r]), [rec] "+v"(rw)
 #define SA_T16_IN [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL)
-#define SA_T16_PW [pw] "v"(pw), [kb] "i"((r + 1) & 3)
+#define SA_T16_PW [tabn] "v"(tabn), [sym] "v"(sym)
 #define SA_T16_CM "v_max_i16 %[cm], %[cm], %[hp]\n\t"
                     if (r + 1 < R) {
                         uint32_t dn;
-                        const uint32_t pw = cp[(r + 1 < R ? r + 1 : r) / 4];
+                        const uint32_t tabn = (uint32_t)a[r + 1 < R ? r + 1 : r];
                         if constexpr (CMAX)
                             asm(SA_T16_LEFT SA_T16_NEXT SA_T16_UPC SA_T16_MAX SA_T16_TAIL SA_T16_CM
                                 : SA_T16_OUT, [dn] "=&v"(dn), [cm] "+v"(cm[r])
@@ -403,11 +368,6 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
             if constexpr (AFF) xl = xu;
             if constexpr (T16 && RB < 32) rec[0] >>= (32 - RB);   // alignbit filled from the top
         }
-        if constexpr (T16) {
-            sym = symn;
-#pragma unroll
-            for (int k = 0; k < TW; ++k) cp[k] = cpn[k];
-        }
     };
 
     // One chunk of kChunk steps of one band.
@@ -475,12 +435,9 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     auto load_chunk = [&](int band, int c0, int& vh, int& vx, int& vs) {
         const int c = c0 + lane;
         vh = 0; vx = -10000; vs = 0;
-        // T16 also loads lane kChunk: a chunk's last step prefetches the next chunk's first symbol
-        if ((lane < kChunk || (T16 && lane == kChunk)) && c < n) {
+        if (lane < kChunk && c < n) {
             if (P.stage_seq2) vs = (int)s_seq2[c];
             else vs = T16 ? (int)t16_code8(P.sym_pack, s2[c]) : (int)s2[c];
-        }
-        if (lane < kChunk && c < n) {
             if (band == 0) {
                 const int J = c + 1;
                 if constexpr (ALG == SA_NW) vh = SC * J * G;
@@ -532,14 +489,8 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
                         const int row = row0 + r;
-                        if constexpr (T16) {
-                            // column profiles: [code c] byte r = tagged s(Seq1[row], symbol c)
-                            const uint32_t pw = row < m ? P.prof[t16_code8(P.sym_pack, s1[row]) >> 3] : 0u;
-#pragma unroll
-                            for (int cc = 0; cc < 4; ++cc) s_tab[cc * R + r] = (uint8_t)(pw >> (8 * cc));
-                        } else {
-                            a[r] = row < m ? (int)s1[row] : 0;
-                        }
+                        if constexpr (T16) a[r] = row < m ? (int)P.prof[t16_code8(P.sym_pack, s1[row]) >> 3] : 0;
+                        else a[r] = row < m ? (int)s1[row] : 0;
                         const int i = row + 1;
                         if constexpr (ALG == SA_NW) Hp[r] = SC * i * G;
                         else if constexpr (ALG == SA_GLOBAL_GOTOH) Hp[r] = GO + i * GE;
@@ -559,12 +510,6 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 const int kC = (int)chunk * kChunk;
                 int bch, bcx, symc;
                 load_chunk(band, kC, bch, bcx, symc);
-                if constexpr (T16) {
-                    if (chunk == 0) {   // the band's first step: its symbol and column profile
-                        sym = shr1(__builtin_amdgcn_readlane(symc, 0), sym);
-                        load_cp(sym, cp);
-                    }
-                }
                 int acc_h = 0, acc_x = 0;
                 const bool steady = kC >= kWave - 1 && kC + kChunk <= n;
                 if (steady) run_chunk(std::true_type{}, band, kC, bch, bcx, symc, acc_h, acc_x);
@@ -720,7 +665,7 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
     const bool lut = v.t16 ? false : v.lut, allow = v.allow;
     const bool keyed = LOCAL && v.keyed;
     const dim3 block(kWave * p.waves);
-    const size_t lds = lds_layout(lut, is_affine(ALG), p.waves, p.stage_seq2 ? p.max_n : 0, v.t16 ? R : 0).total;
+    const size_t lds = lds_layout(lut, is_affine(ALG), p.waves, p.stage_seq2 ? p.max_n : 0).total;
     if (lds > kMaxLds) return hipErrorInvalidConfiguration;
     const bool split = v.split;
     if (split && (p.waves != 1 || (R != 4 && R != 8))) return hipErrorInvalidConfiguration;

@@ -47,20 +47,15 @@ constexpr int kLagPhases = (kChunk + 62) / kChunk + 1;
 constexpr int kRing = 128;
 static_assert(kLagPhases == 3 && kRing >= 4 * kChunk, "re-derive the ring bound");
 
-// T16 column-profile table (sa_fill_impl.h): per wave, per lane, 4 symbol codes x R bytes, padded
-// by 16 bytes per lane so the lanes' 16-byte reads spread over the banks.
-SA_HD uint32_t t16_tab_stride(int R) { return 4u * (uint32_t)R + 16u; }
-
-// Dynamic LDS of the fill kernel: [match bits (LUT)][hand-off rings][staged Seq2][T16 table].
+// Dynamic LDS of the fill kernel: [match bits (LUT)][hand-off rings][staged Seq2].
 struct LdsLayout {
-    uint32_t ring_off, seq_off, tab_off, total;
+    uint32_t ring_off, seq_off, total;
 };
-SA_HD LdsLayout lds_layout(bool lut, bool affine, int W, uint32_t staged_n, int t16_R = 0) {
+SA_HD LdsLayout lds_layout(bool lut, bool affine, int W, uint32_t staged_n) {
     LdsLayout L;
     L.ring_off = lut ? 2048 * 4 : 0;
     L.seq_off = L.ring_off + (uint32_t)W * (affine ? 2 : 1) * kRing * 4;
-    L.tab_off = L.seq_off + ((staged_n + 15) / 16) * 16;
-    L.total = L.tab_off + (t16_R ? (uint32_t)W * 64u * t16_tab_stride(t16_R) : 0u);
+    L.total = L.seq_off + ((staged_n + 15) / 16) * 16;
     return L;
 }
 // LDS a workgroup may allocate on gfx950 (MI355X_MICROARCH.md: 160 KiB per CU, all of it to one
