@@ -39,6 +39,9 @@ SCORING = (-1, 1, -1)         # SmithWatermanSA::getDefaultScoring (SASmithWater
 # loop's own instruction mix, every opcode priced at its measured gfx950 issue rate
 # (tools/issue_model.py -> ISSUE_MODEL, rates from profiles/microbench_valu_issue_r01.txt).
 ISSUE_MODEL = os.path.join(ROOT, "profiles", "issue_model_r03.json")
+# Register-only cell-level measurement of the same instruction mix (tools/microbench_cellmix.hip,
+# variant V2 = the shipped T16 end-cell cell): what the mix really issues at, no memory traffic.
+CELL_MIX_CEILING = {"sw_t16c_r32": (5291.4, "profiles/microbench_cellmix_r01.txt (V2)")}
 HBM_PEAK_GBPS = 8000.0
 SW_FLAG_BYTES_PER_CELL = 0.25  # 2 traceback bits per cell written to HBM
 
@@ -264,6 +267,9 @@ def main():
                  "issue_ceiling_gcups": model["peak_gcups"] if model else None, "valu_per_cell": vpc,
                  "peak_basis": "steady-loop VALU mix x measured per-opcode issue rates (tools/issue_model.py, "
                                "profiles/issue_model_r03.json)",
+                 "cell_mix_ceiling_gcups": CELL_MIX_CEILING.get(label, (None,))[0],
+                 "cell_mix_frac": (round(fill_gcups / CELL_MIX_CEILING[label][0], 4) if label in CELL_MIX_CEILING else None),
+                 "cell_mix_source": CELL_MIX_CEILING.get(label, (None, None))[1],
                  "bytes_per_cell": round(bytes_per_cell, 4), "hbm_achieved_GBps": round(hbm_gbps, 1),
                  "hbm_peak_GBps": HBM_PEAK_GBPS, "hbm_frac": round(hbm_gbps / HBM_PEAK_GBPS, 4)})
     line = {
