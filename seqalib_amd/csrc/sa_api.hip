@@ -296,7 +296,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     c->last_kernel = cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
     c->last_R = pl.R;
     c->last_W = pl.split ? 0 : pl.W;   // 0: SPLIT plan (one single-wave workgroup per band)
-    const uint64_t slot_bytes = pl.g.dir_slot + pl.rowbuf_elems * 4 + (snap_h_slot + snap_p_slot) * 4;
+    const uint64_t slot_bytes = pl.g.dir_slot + pl.rowbuf_elems * 4 + (snap_h_slot + 2 * snap_p_slot) * 4;
     const uint64_t budget = pipe ? ws_budget(c) / 2 : ws_budget(c);
     uint64_t per_launch = slot_bytes ? std::max<uint64_t>(1, budget / std::max<uint64_t>(slot_bytes, 1)) : npairs;
     per_launch = std::min<uint64_t>(per_launch, npairs ? npairs : 1);
@@ -332,6 +332,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     int32_t* rowbuf = reinterpret_cast<int32_t*>(c->ws + per_launch * pl.g.dir_slot);
     uint32_t* snap_h = reinterpret_cast<uint32_t*>(rowbuf + per_launch * pl.rowbuf_elems);
     int32_t* snap_p = reinterpret_cast<int32_t*>(snap_h + per_launch * snap_h_slot);
+    int32_t* snap_m = snap_p + per_launch * snap_p_slot;
 
     // reset timing
     c->launches = 0;
@@ -360,7 +361,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         fp.stage_seq2 = max_n <= kMaxStagedSeq2 ? 1 : 0;
         fp.prof = aux + 8;
         fp.sym_pack = sym_pack;
-        fp.snap_h = snap_h; fp.snap_p = snap_p;
+        fp.snap_h = snap_h; fp.snap_p = snap_p; fp.snap_m = snap_m;
         fp.snap_h_slot = snap_h_slot; fp.snap_p_slot = snap_p_slot; fp.snap_nch = snap_nch;
         fp.split_bands = (uint32_t)sp_bands;
         fp.ticket = pl.split ? reinterpret_cast<uint32_t*>(c->split) : nullptr;
@@ -405,7 +406,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             EndcellParams ep;
             ep.seq1 = d1; ep.off1 = o1; ep.seq2 = d2; ep.off2 = o2;
             ep.prof = fp.prof; ep.sym_pack = sym_pack;
-            ep.snap_h = snap_h; ep.snap_p = snap_p;
+            ep.snap_h = snap_h; ep.snap_p = snap_p; ep.snap_m = snap_m;
             ep.snap_h_slot = snap_h_slot; ep.snap_p_slot = snap_p_slot; ep.snap_nch = snap_nch;
             if (pl.split) {
                 ep.rowbuf = reinterpret_cast<const int32_t*>(fp.hand);

@@ -2,15 +2,18 @@
 //
 // The reference keeps the LAST row-major maximum of the score matrix (SASmithWaterman.h:110:
 // Score >= MaxScore inside the i-then-j loops).  A CMAX fill reports, per pair, the maximum
-// score S, the largest row i holding it, and the last 32-step chunk c of i's band in which row i
-// reached S.  This kernel replays that one chunk of that band from the snapshot the fill stored
-// at the end of chunk c-1 (every lane's R row values and its diagonal input; the band's top row
-// comes from the per-band row buffer) and keeps the last column of row i whose value equals S.
+// score S, the last lane (band b, lane t) holding it and the last 32-step chunk c in which lane t
+// reached S; it also stores every lane's maximum of every chunk.  This kernel replays, in order,
+// each chunk c' <= c of band b in which lane t's maximum equals S, from the snapshot the fill
+// stored at the end of chunk c'-1 (every lane's R row values and its diagonal input; the band's
+// top row comes from the per-band row buffer), and keeps the last row of lane t holding S and
+// that row's last column.  An all-zero matrix (S = 0) ends at (m, n) without a replay.
 // The replay repeats the fill's recurrence and its wavefront order exactly (lane t computes
 // column s - t at step s; the row above comes from lane t-1's previous step), in int32 on the
 // unscaled scores, so it yields the same cell values the fill produced.
 //
-// One wave per pair; 32 steps x R rows per lane: ~0.05% of the fill's work at 4096 x 4096.
+// One wave per pair; 32 steps x R rows per lane per replayed chunk (usually one): ~0.05% of the
+// fill's work at 4096 x 4096.
 #include <limits.h>
 
 #include "sa_internal.h"
@@ -41,61 +44,79 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
     constexpr int BAND = kWave * R;
     const int b = (iend - 1) / BAND;
     const int tstar = ((iend - 1) % BAND) / R;
-    const int rstar = (iend - 1) % R;
     const int row0 = b * BAND + lane * R;
     const int G = P.gap;
 
+    if (S == 0) {   // every cell is 0: the last cell is the reference's maximum (MaxScore from INT_MIN)
+        if (lane == 0) {
+            res.end_i = m;
+            res.end_j = n;
+            res.reserved = 0;
+            P.res[pidx] = res;
+        }
+        return;
+    }
     uint32_t tab[R];
-    int Hp[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int row = row0 + r;
         tab[r] = row < m ? P.prof[ec_code8(P.sym_pack, s1[row]) >> 3] : 0u;
-        Hp[r] = 0;
     }
-    int prev_up = 0;
-    if (c > 0) {
-        const uint64_t e = (uint64_t)b * P.snap_nch + (c - 1);
-        const uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + (e * kWave + lane) * (R / 2);
-#pragma unroll
-        for (int q = 0; q < R / 2; ++q) {
-            const uint32_t w = sh[q];
-            Hp[2 * q] = (int)(w & 0xffffu) >> 2;        // stored as 4H (non-negative)
-            Hp[2 * q + 1] = (int)(w >> 16) >> 2;
-        }
-        prev_up = P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] >> 2;
-    }
-    int hl = Hp[R - 1];
     const uint32_t rs = P.rowbuf_stride;
     const int32_t* top = b > 0 ? P.rowbuf + (uint64_t)slot * P.rowbuf_slot + (uint64_t)(b - 1) * P.max_n * rs : nullptr;
-    int jbest = -1;
-    for (int q = 0; q < kChunk; ++q) {
-        const int s = c * kChunk + q;
-        const int j0 = s - lane;
-        int up_h = __shfl_up(hl, 1);
-        if (lane == 0) up_h = (top && s < n) ? (top[(uint64_t)s * rs] >> 2) : 0;
-        if (j0 >= 0 && j0 < n) {
-            const uint32_t sym = ec_code8(P.sym_pack, s2[j0]);
-            int hd = prev_up, hu = up_h;
+    const int32_t* lmax = P.snap_m + (uint64_t)slot * P.snap_p_slot + (uint64_t)b * P.snap_nch * kWave + tstar;
+    int rbest = -1, jbest = -1;
+    for (int cc = 0; cc <= c; ++cc) {
+        if (lmax[(uint64_t)cc * kWave] != 4 * S) continue;   // uniform: lane tstar never reached S here
+        int Hp[R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                // profile byte = 4s+3 (signed); the builtin returns unsigned: shift as int
-                const int sub = ((int)__builtin_amdgcn_sbfe(tab[r], sym, 8) - 3) >> 2;
-                int H = hd + sub;
-                H = max(H, hu + G);
-                H = max(H, Hp[r] + G);
-                H = max(H, 0);
-                hd = Hp[r];
-                Hp[r] = H;
-                hu = H;
-                if (lane == tstar && r == rstar && H == S) jbest = j0;
+        for (int r = 0; r < R; ++r) Hp[r] = 0;
+        int prev_up = 0;
+        if (cc > 0) {
+            const uint64_t e = (uint64_t)b * P.snap_nch + (cc - 1);
+            const uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + (e * kWave + lane) * (R / 2);
+#pragma unroll
+            for (int q = 0; q < R / 2; ++q) {
+                const uint32_t w = sh[q];
+                Hp[2 * q] = (int)(w & 0xffffu) >> 2;        // stored as 4H (non-negative)
+                Hp[2 * q + 1] = (int)(w >> 16) >> 2;
             }
-            prev_up = up_h;
-            hl = Hp[R - 1];
+            prev_up = P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] >> 2;
+        }
+        int hl = Hp[R - 1];
+        for (int q = 0; q < kChunk; ++q) {
+            const int s = cc * kChunk + q;
+            const int j0 = s - lane;
+            int up_h = __shfl_up(hl, 1);
+            if (lane == 0) up_h = (top && s < n) ? (top[(uint64_t)s * rs] >> 2) : 0;
+            if (j0 >= 0 && j0 < n) {
+                const uint32_t sym = ec_code8(P.sym_pack, s2[j0]);
+                int hd = prev_up, hu = up_h;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    // profile byte = 4s+3 (signed); the builtin returns unsigned: shift as int
+                    const int sub = ((int)__builtin_amdgcn_sbfe(tab[r], sym, 8) - 3) >> 2;
+                    int H = hd + sub;
+                    H = max(H, hu + G);
+                    H = max(H, Hp[r] + G);
+                    H = max(H, 0);
+                    hd = Hp[r];
+                    Hp[r] = H;
+                    hu = H;
+                    // last row of the lane holding S, then its last column (chunks ascend)
+                    if (lane == tstar && row0 + r < m && H == S && (r > rbest || (r == rbest && j0 > jbest))) {
+                        rbest = r;
+                        jbest = j0;
+                    }
+                }
+                prev_up = up_h;
+                hl = Hp[R - 1];
+            }
         }
     }
     if (lane == tstar) {
-        res.end_j = jbest + 1;   // 1-based; jbest >= 0 whenever the fill's report is consistent
+        res.end_i = row0 + rbest + 1;   // 1-based; rbest >= 0 whenever the fill's report is consistent
+        res.end_j = jbest + 1;
         res.reserved = 0;
         P.res[pidx] = res;
     }

@@ -197,17 +197,16 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     int Yp[R];     // Iy of my rows at the previous column (affine)
     int bh[R];     // best per row: key (KEYED) or score
     int bj[R];     // its column (0-based), !KEYED
-    uint32_t cm[R];  // CMAX: per-row max over the current chunk (int16, 0x8000 = none)
-    // CMAX: the lane's best cell of the band so far as one key H << 18 | r << 12 | chunk + 1
-    // (H < 2^13 by t16_ok, r < 64, chunks < 4096 since n < 65535): lexicographic max = highest
-    // score, then last row, then last chunk -- the row-major order the end cell needs
+    uint32_t cml = 0;  // CMAX: the lane's maximum over the current chunk (4H >= 0)
+    // CMAX: the lane's best chunk of the band so far as one key H << 12 | chunk + 1 (H < 2^13 by
+    // t16_ok, chunks < 4096 since n < 65535): highest score, then last chunk
     uint32_t lkey = 0;
     int hl = 0, xl = 0, sym = 0, prev_up = 0;
     int row0 = 0;
     // Running best of this lane over its bands: (score, i, j), 1-based cell.
     int best_h = INT_MIN, best_i = 0, best_j = 0;
 #pragma unroll
-    for (int r = 0; r < R; ++r) { a[r] = 0; Hp[r] = 0; Yp[r] = 0; bh[r] = 0; bj[r] = 0; cm[r] = 0x8000u; }
+    for (int r = 0; r < R; ++r) { a[r] = 0; Hp[r] = 0; Yp[r] = 0; bh[r] = 0; bj[r] = 0; }
 
     // One step: lane computes column j = s - lane for its R rows.  STEADY: every lane is in
     // range, no exec-mask branch.  Returns the packed record words in rec.
@@ -268,15 +267,10 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
 #define SA_T16_OUT [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r]), [rec] "+v"(rw)
 #define SA_T16_IN [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL)
 #define SA_T16_PW [tabn] "v"(tabn), [sym] "v"(sym)
-#define SA_T16_CM "v_max_i16 %[cm], %[cm], %[hp]\n\t"
                     if (r + 1 < R) {
                         uint32_t dn;
                         const uint32_t tabn = (uint32_t)a[r + 1 < R ? r + 1 : r];
-                        if constexpr (CMAX)
-                            asm(SA_T16_LEFT SA_T16_NEXT SA_T16_UPC SA_T16_MAX SA_T16_TAIL SA_T16_CM
-                                : SA_T16_OUT, [dn] "=&v"(dn), [cm] "+v"(cm[r])
-                                : SA_T16_IN, SA_T16_PW);
-                        else if constexpr (KIN)
+                        if constexpr (KIN)
                             asm(SA_T16_LEFT SA_T16_NEXT SA_T16_UPC SA_T16_MAX SA_T16_TAIL SA_T16_KEY
                                 : SA_T16_OUT, [dn] "=&v"(dn), [bh] "+v"(bh[r])
                                 : SA_T16_IN, SA_T16_PW, [jk] "v"(jk));
@@ -290,10 +284,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                                 : SA_T16_IN, SA_T16_PW);
                         dcur = dn;
                     } else {
-                        if constexpr (CMAX)
-                            asm(SA_T16_LEFT SA_T16_UPC SA_T16_MAX SA_T16_TAIL SA_T16_CM
-                                : SA_T16_OUT, [cm] "+v"(cm[r]) : SA_T16_IN);
-                        else if constexpr (KIN)
+                        if constexpr (KIN)
                             asm(SA_T16_LEFT SA_T16_UPC SA_T16_MAX SA_T16_TAIL SA_T16_KEY
                                 : SA_T16_OUT, [bh] "+v"(bh[r]) : SA_T16_IN, [jk] "v"(jk));
                         else if constexpr (LOCAL)
@@ -301,7 +292,12 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                         else
                             asm(SA_T16_LEFT SA_T16_UP SA_T16_MAX SA_T16_TAIL : SA_T16_OUT : SA_T16_IN);
                     }
-#undef SA_T16_CM
+                    if constexpr (CMAX) {
+                        // the lane's chunk maximum: one v_max3_u32 per two rows instead of a
+                        // v_max_i16 per cell (tools/microbench_cellmix.hip V8 vs V2)
+                        if (r & 1)
+                            asm("v_max3_u32 %0, %0, %1, %2" : "+v"(cml) : "v"(Hp[r >= 1 ? r - 1 : 0]), "v"(Hp[r]));
+                    }
 #undef SA_T16_UPC
 #undef SA_T16_LEFT
 #undef SA_T16_UP
@@ -489,7 +485,9 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
                         const int row = row0 + r;
-                        if constexpr (T16) a[r] = row < m ? (int)P.prof[t16_code8(P.sym_pack, s1[row]) >> 3] : 0;
+                        // CMAX: rows past m get substitution -128 (with gap < 0 their values stay
+                        // below the matrix maximum, so they never win the lane's chunk maximum)
+                        if constexpr (T16) a[r] = row < m ? (int)P.prof[t16_code8(P.sym_pack, s1[row]) >> 3] : (CMAX ? (int)0x80808080u : 0);
                         else a[r] = row < m ? (int)s1[row] : 0;
                         const int i = row + 1;
                         if constexpr (ALG == SA_NW) Hp[r] = SC * i * G;
@@ -497,10 +495,10 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                         else Hp[r] = 0;
                         Yp[r] = -10000;
                         bh[r] = KEYED ? 0 : INT_MIN;
-                        cm[r] = 0x8000u;
                         bj[r] = 0;
                     }
                     lkey = 0;
+                    cml = 0;
                     split_load(band, 0, pre_h, pre_x);
                     if constexpr (ALG == SA_NW) prev_up = SC * row0 * G;
                     else if constexpr (ALG == SA_GLOBAL_GOTOH) prev_up = row0 == 0 ? 0 : GO + row0 * GE;
@@ -538,15 +536,11 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 // ------------------------------------------------ CMAX: chunk maxima, snapshot
                 if constexpr (CMAX) {
                     const uint32_t ck = chunk + 1;
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        const int v = (int)(int16_t)(cm[r] & 0xffffu);   // 4H, or -32768 = none
-                        if (v >= 0 && row0 + r < m)
-                            lkey = max(lkey, ((uint32_t)v >> 2) << 18 | (uint32_t)r << 12 | ck);
-                        cm[r] = 0x8000u;
-                    }
+                    const uint64_t e = (uint64_t)band * P.snap_nch + chunk;
+                    P.snap_m[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = (int32_t)cml;
+                    lkey = max(lkey, (cml >> 2) << 12 | ck);
+                    cml = 0;
                     if (chunk + 1 < nch) {   // state entering chunk + 1, for the end-cell replay
-                        const uint64_t e = (uint64_t)band * P.snap_nch + chunk;
                         uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + (e * kWave + lane) * (R / 2);
 #pragma unroll
                         for (int q = 0; q < R / 2; ++q)
@@ -557,10 +551,12 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 // ---------------------------------------------------------------- band end
                 if (chunk == nch - 1) {
                     if constexpr (CMAX) {
-                        const int h = (int)(lkey >> 18);
+                        // (score, lane, chunk): best_i names the lane by its last row; the end-cell
+                        // replay (sa_endcell.hip) finds the row and the column
+                        const int h = (int)(lkey >> 12);
                         if (lkey != 0 && h >= best_h) {
                             best_h = h;
-                            best_i = row0 + (int)((lkey >> 12) & 63u) + 1;
+                            best_i = row0 + R;
                             best_j = (int)(lkey & 4095u);
                         }
                     } else if constexpr (LOCAL) {

@@ -33,7 +33,8 @@ struct FillParams {
     // values (R/2 words) and of the diagonal input (1 word); snap_nch = chunks per band.
     uint32_t* snap_h;
     int32_t* snap_p;
-    uint64_t snap_h_slot, snap_p_slot;
+    int32_t* snap_m;   // per [band][chunk][lane]: the lane's maximum over the chunk (4H)
+    uint64_t snap_h_slot, snap_p_slot;   // snap_m slots are snap_p_slot words too
     uint32_t snap_nch;
     // SPLIT only: one single-wave workgroup per (pair slot, band), split_bands bands per slot,
     // bands handed out by *ticket.  hand: per slot and band, max_n 8-byte {tag, H} granules of
@@ -68,6 +69,7 @@ struct EndcellParams {
     uint32_t sym_pack;
     const uint32_t* snap_h;
     const int32_t* snap_p;
+    const int32_t* snap_m;
     uint64_t snap_h_slot, snap_p_slot;
     uint32_t snap_nch;
     const int32_t* rowbuf;

@@ -12,6 +12,7 @@
 //   V5  V1 without the and (scores keep their tags: timing only)                               (7)
 //   V6  V2 with one v_max3_i16 for the two maxes                                               (8)
 //   V7  V6 without the chunk max (the NW / keyless form)                                       (7)
+//   V8  V2 with the per-row chunk max replaced by one lane max: v_max3_u32 per two rows      (8.5)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -64,6 +65,16 @@ __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, i
                 else if constexpr (V == 3) asm volatile(MB_HEAD MB_AND MB_ALIGN MB_OPS);
                 else if constexpr (V == 4) asm volatile(MB_HEAD MB_AND MB_CM MB_OPS);
                 else asm volatile(MB_HEAD MB_ALIGN MB_CM MB_OPS);
+            } else if constexpr (V == 8) {
+                asm volatile("v_add_u16 %[t0], %[cl], %[hp]\n\t"
+                             "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\tv_add_u16 %[dn], %[hp], %[dn]\n\t"
+                             "v_sub_u16_e64 %[t1], %[hu], %[cu] clamp\n\t"
+                             "v_max_i16 %[t0], %[dr], %[t0]\n\tv_max_i16 %[t0], %[t1], %[t0]\n\t"
+                             "v_and_b32 %[hp], -4, %[t0]\n\t"
+                             "v_alignbit_b32 %[rec], %[t0], %[rec], 2"
+                             : [t0] "=&v"(t0), [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r]), [rec] "+v"(rec)
+                             : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL), [tabn] "v"(tabn), [sym] "v"(sym));
+                if (r & 1) asm volatile("v_max3_u32 %0, %0, %1, %2" : "+v"(cm[0]) : "v"(Hp[r - 1 >= 0 ? r - 1 : 0]), "v"(Hp[r]));
             } else if constexpr (V == 6 || V == 7) {
 #define MB6 "v_add_u16 %[t0], %[cl], %[hp]\n\t" \
     "v_sub_u16_e64 %[t1], %[hu], %[cu] clamp\n\t" \
@@ -108,7 +119,8 @@ int main() {
         {"V0 previous cell (10 ops)", cells<0>, 10}, {"V1 current cell (8 ops)", cells<1>, 8},
         {"V2 current, bfe+add (9 ops)", cells<2>, 9}, {"V3 V1 - chunk max (7)", cells<3>, 7},
         {"V4 V1 - alignbit (7)", cells<4>, 7}, {"V5 V1 - and (7)", cells<5>, 7},
-        {"V6 V2 with max3 (8)", cells<6>, 8}, {"V7 V6 - chunk max (7)", cells<7>, 7}};
+        {"V6 V2 with max3 (8)", cells<6>, 8}, {"V7 V6 - chunk max (7)", cells<7>, 7},
+        {"V8 V2, lane max3 (8.5)", cells<8>, 8}};
     const int steps = 4000;
     for (auto& k : ks) {
         float best = 1e9f;
