@@ -1,12 +1,12 @@
 // Cell-level issue microbenchmark for the T16 fill (not part of the product): R = 32 rows per lane
 // in registers, one DPP row-above shift per step, the exact inline-asm cell of each variant, no
-// memory traffic in the loop.  2048 single-wave workgroups = 2 waves per SIMD, as the fill runs.
+// memory traffic in the loop.  argv[1] = waves per SIMD (default 2; 1024 single-wave workgroups each).
 // Answers what the per-opcode additive model (tools/issue_model.py) cannot: the real issue rate
 // of a MIX of fast (VOP2 16-bit) and slow (VOP3 / SDWA / 32-bit) instructions.
 //   V0  previous cell: add, max, add, max, max(clamp), bfe, add, and, alignbit, max(chunk)   (10)
-//   V1  current cell:  add(L), sdwa add(next diag), sub_u16 clamp(U), max, max, and, alignbit,
+//   V1  SDWA cell:     add(L), sdwa add(next diag), sub_u16 clamp(U), max, max, and, alignbit,
 //                      max(chunk)                                                              (8)
-//   V2  current cell with bfe + add instead of the SDWA add                                    (9)
+//   V2  V1 with bfe + add instead of the SDWA add                                    (9)
 //   V3  V1 without the chunk max                                                               (7)
 //   V4  V1 without the alignbit                                                                (7)
 //   V5  V1 without the and (scores keep their tags: timing only)                               (7)
@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 constexpr int R = 32;
 
@@ -110,17 +111,19 @@ __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, i
     out[blockIdx.x * 64 + lane] = x;
 }
 
-int main() {
+int main(int argc, char** argv) {
+    const int wps = argc > 1 ? atoi(argv[1]) : 2;
+    const int nblk = 1024 * wps;
     uint32_t *din, *dout;
-    if (hipMalloc(&din, 4096 * 4) != hipSuccess || hipMalloc(&dout, 2048 * 64 * 4) != hipSuccess) return 1;
+    if (hipMalloc(&din, 4096 * 4) != hipSuccess || hipMalloc(&dout, (size_t)nblk * 64 * 4) != hipSuccess) return 1;
     if (hipMemset(din, 1, 4096 * 4) != hipSuccess) return 1;
     typedef void (*kfn)(const uint32_t*, uint32_t*, int);
     struct K { const char* name; kfn f; int ops; } ks[] = {
-        {"V0 previous cell (10 ops)", cells<0>, 10}, {"V1 current cell (8 ops)", cells<1>, 8},
-        {"V2 current, bfe+add (9 ops)", cells<2>, 9}, {"V3 V1 - chunk max (7)", cells<3>, 7},
+        {"V0 previous cell (10 ops)", cells<0>, 10}, {"V1 SDWA cell (8 ops)", cells<1>, 8},
+        {"V2 bfe+add cell (9 ops)", cells<2>, 9}, {"V3 V1 - chunk max (7)", cells<3>, 7},
         {"V4 V1 - alignbit (7)", cells<4>, 7}, {"V5 V1 - and (7)", cells<5>, 7},
         {"V6 V2 with max3 (8)", cells<6>, 8}, {"V7 V6 - chunk max (7)", cells<7>, 7},
-        {"V8 V2, lane max3 (8.5)", cells<8>, 8}};
+        {"V8 shipped: V2 + lane max3 (8.5)", cells<8>, 8}};
     const int steps = 4000;
     for (auto& k : ks) {
         float best = 1e9f;
@@ -128,16 +131,16 @@ int main() {
             hipEvent_t e0, e1;
             (void)hipEventCreate(&e0);
             (void)hipEventCreate(&e1);
-            hipLaunchKernelGGL(k.f, dim3(2048), dim3(64), 0, 0, din, dout, 100);
+            hipLaunchKernelGGL(k.f, dim3(nblk), dim3(64), 0, 0, din, dout, 100);
             (void)hipEventRecord(e0);
-            hipLaunchKernelGGL(k.f, dim3(2048), dim3(64), 0, 0, din, dout, steps);
+            hipLaunchKernelGGL(k.f, dim3(nblk), dim3(64), 0, 0, din, dout, steps);
             (void)hipEventRecord(e1);
             (void)hipEventSynchronize(e1);
             float ms;
             (void)hipEventElapsedTime(&ms, e0, e1);
             if (ms < best) best = ms;
         }
-        const double cells = 2048.0 * 64 * R * steps;
+        const double cells = (double)nblk * 64 * R * steps;
         printf("%-30s %8.3f ms  %8.1f GCUPS-equivalent  %.2f cycles/lane-cell@2.4GHz\n", k.name, best,
                cells / best / 1e6, 1024 * 2.4e9 * best * 1e-3 / (cells / 64));
     }
