@@ -269,6 +269,11 @@ def test_t16_eligibility(engine, algo):
     # !allowMismatch -> int32 kernel
     compare_with_oracle(engine, algo, (-2, 1, -1, False), dna)
     assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
+    if algo == 0:
+        # SW with gap 0: the T16 cell folds the zero clamp into a saturating up term, which needs
+        # gap < 0 (sa_fill_impl.h), so the int32 kernel takes it
+        compare_with_oracle(engine, algo, (0, 1, -1), dna)
+        assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
 
 
 def test_endcell_replay_vs_oracle(engine):
