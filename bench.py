@@ -8,7 +8,8 @@ equal<char> — the same pairs the reference's SmithWatermanSA would see.
 
 Multi-GPU: one process per GPU (torchrun); rank r aligns its own 10,000-pair shard of a global
 batch (pair p uses seeds base+2p+1 / base+2p+2), with no data-path collective (pairs are
-independent); timing is barrier-bracketed and the max over ranks is reported.  scaling = weak.
+independent); timing is barrier-bracketed (gloo, host memory: no RCCL anywhere) and the max over
+ranks is reported.  scaling = weak.
 
 Steps are pipelined (sa_set_pipeline; --no-pipeline turns it off): step k's traceback runs on
 its own stream while step k+1's fill runs, with two workspace slots and two output buffer sets.
@@ -43,6 +44,9 @@ ISSUE_MODEL = os.path.join(ROOT, "profiles", "issue_model_r03.json")
 # variant V8 = the shipped T16 end-cell cell): what the mix really issues at, no memory traffic.
 CELL_MIX_CEILING = {"sw_t16c_r32": (5677.8, "profiles/microbench_cellmix_r01.txt (V8, 3 waves/SIMD as the fill runs)")}
 HBM_PEAK_GBPS = 8000.0
+# VALU peak of the guide (/opt/skills/guides/MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 VALU
+# instruction issues over 2 cycles, 2400 MHz max clock): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz.
+VALU_PEAK_TLANE = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.64 T lane-instructions/s
 SW_FLAG_BYTES_PER_CELL = 0.25  # 2 traceback bits per cell written to HBM
 
 
@@ -53,8 +57,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pairs", type=int, default=10000, help="pairs per GPU")
     ap.add_argument("--len", type=int, default=4096, help="length of both sequences")
-    ap.add_argument("--cpu-pairs", type=int, default=128, help="CPU baseline sample (pairs)")
+    ap.add_argument("--cpu-pairs", type=int, default=256, help="CPU baseline sample, all-core leg (pairs)")
+    ap.add_argument("--cpu-pairs-1t", type=int, default=12, help="CPU baseline sample, 1-thread leg (pairs)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--e2e-steps", type=int, default=2,
+                    help="host-API steps (H2D + fill + traceback + D2H of results and ops) timed after the run")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -71,12 +78,13 @@ def dist_setup(args):
     import torch
 
     if world > 1:
+        # pairs are independent: the data path has no collective at all; the timing barrier and
+        # the max-over-ranks reduction go through gloo on host memory (no RCCL)
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
+        if torch.cuda.is_available():
             torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend)
+        dist.init_process_group(backend="gloo")
     return world, rank, local
 
 
@@ -91,8 +99,7 @@ def max_over_ranks(x: float, world: int) -> float:
         return x
     import torch
     import torch.distributed as dist
-    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -105,11 +112,11 @@ def shard_seed_base(rank: int, world: int, pairs_per_gpu: int) -> int:
     return SEED_BASE + 2 * start
 
 
-def cpu_baseline(args, s1, o1, s2, o2):
+def cpu_baseline(args, s1, o1, s2, o2, threads=None, pairs=None):
     """The reference (oracle/_ref, compiled from /root/reference) — or the oracle port if that is
     not built — on a bounded sample of the same pairs, on the host cores."""
-    k = min(args.cpu_pairs, len(o1) - 1)
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    k = min(pairs or args.cpu_pairs, len(o1) - 1)
+    threads = max(1, min(threads or args.cpu_threads, os.cpu_count() or 1))
     sub1, sub2 = s1[: int(o1[k])].copy(), s2[: int(o2[k])].copy()
     so1, so2 = o1[: k + 1].copy(), o2[: k + 1].copy()
     cells = float(np.sum((so1[1:] - so1[:-1]).astype(np.float64) * (so2[1:] - so2[:-1])))
@@ -217,6 +224,17 @@ def main():
         serial_ms = max_over_ranks(time.perf_counter() - ts, world) / args.serial_steps * 1e3
     kernel, plan_R, plan_W = eng.last_plan()
     fill_ms = max_over_ranks(fill_ms, world)
+    # end to end through the host API (what the C++ drop-in does): sequences H2D, fill, end cell,
+    # traceback, results + op streams D2H; outside the timed region
+    e2e_ms = None
+    if args.e2e_steps > 0:
+        eng.set_pipeline(False)
+        sc_ = sa.ScoringSystem(*SCORING)
+        eng.align_packed(sa.SA_SW, sc_, s1, o1, s2, o2)   # warm the host-API buffers
+        te = time.perf_counter()
+        for _ in range(args.e2e_steps):
+            eng.align_packed(sa.SA_SW, sc_, s1, o1, s2, o2)
+        e2e_ms = max_over_ranks(time.perf_counter() - te, world) / args.e2e_steps * 1e3
 
     cells_rank = float(P) * Lq * Lq
     value = world * cells_rank * args.steps / elapsed / 1e9
@@ -254,19 +272,19 @@ def main():
     traffic = load_pmc_traffic(workload)
     kname = (f"fill_kernel<SW,R={plan_R},W={plan_W}," + ("T16 tagged int16 profile" if t16 else "int32 flags")
              + (",chunk-max end cell>" if endcell else ",KEYED>"))
-    if model:
-        vpc = model["valu_per_cell"]
-        roof = {"bound": "valu", "achieved": round(fill_gcups * vpc / 1e3, 2),
-                "peak": round(model["peak_gcups"] * vpc / 1e3, 2), "unit": "Tops/s",
-                "frac": round(fill_gcups / model["peak_gcups"], 4)}
-    else:
-        vpc = None
-        roof = {"bound": "valu", "achieved": None, "peak": None, "unit": "Tops/s", "frac": None}
+    # achieved = fill cells/s x ISA-counted VALU instructions per cell (each lane computes its own
+    # cells, so lane-instructions); peak = the guide's VALU issue peak (VALU_PEAK_TLANE)
+    vpc = model["valu_per_cell"] if model else None
+    achieved = fill_gcups * vpc / 1e3 if vpc else None
+    roof = {"bound": "valu", "achieved": round(achieved, 2) if achieved else None, "peak": round(VALU_PEAK_TLANE, 2),
+            "unit": "T lane-instr/s", "frac": round(achieved / VALU_PEAK_TLANE, 4) if achieved else None}
     roof.update({"traffic": traffic, "kernel": kname, "avg_launch_ms": round(fill_ms / max(launches, 1), 3),
-                 "fill_gcups": round(fill_gcups, 1),
-                 "issue_ceiling_gcups": model["peak_gcups"] if model else None, "valu_per_cell": vpc,
-                 "peak_basis": "steady-loop VALU mix x measured per-opcode issue rates (tools/issue_model.py, "
-                               "profiles/issue_model_r03.json)",
+                 "fill_gcups": round(fill_gcups, 1), "valu_per_cell": vpc,
+                 "peak_basis": "MI355X_MICROARCH.md: 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz (wave64 VALU op = 2 cycles)",
+                 "issue_ceiling_gcups": model["peak_gcups"] if model else None,
+                 "issue_ceiling_frac": round(fill_gcups / model["peak_gcups"], 4) if model else None,
+                 "issue_ceiling_basis": "steady-loop VALU mix x measured per-opcode issue rates (tools/issue_model.py, "
+                                        "profiles/issue_model_r03.json)",
                  "cell_mix_ceiling_gcups": CELL_MIX_CEILING.get(label, (None,))[0],
                  "cell_mix_frac": (round(fill_gcups / CELL_MIX_CEILING[label][0], 4) if label in CELL_MIX_CEILING else None),
                  "cell_mix_source": CELL_MIX_CEILING.get(label, (None, None))[1],
@@ -280,12 +298,17 @@ def main():
         "config": {"workload": workload, "pairs_per_gpu": P, "m": Lq, "n": Lq, "algo": "SmithWatermanSA",
                    "scoring": list(SCORING), "match": "equal<char>", "parallelism": f"pair-shard x{world}"},
         "roofline": roof,
-        "fill_ms": round(fill_ms, 2), "traceback_ms": round(tb_ms, 2),
+        "fill_ms": round(fill_ms, 2), "endcell_traceback_ms": round(tb_ms, 2),
+        "e2e_ms_per_step": round(e2e_ms, 2) if e2e_ms else None,
+        "e2e_gcups": round(world * cells_rank / (e2e_ms / 1e3) / 1e9, 1) if e2e_ms else None,
+        "e2e_basis": "host API sa_align_batch: pageable H2D of sequences + offsets, fill, end cell, traceback, "
+                     "D2H of results and op streams, one call at a time",
         "pipelined": pipelined, "serial_ms_per_step": round(serial_ms, 2) if serial_ms else None,
         "parity": f"{checked - bad}/{checked} sampled pairs bit-exact vs oracle, {int(np.count_nonzero(res['flags']))} flagged",
     }
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args, s1, o1, s2, o2)
+        line["cpu_baseline_1thread"] = cpu_baseline(args, s1, o1, s2, o2, threads=1, pairs=args.cpu_pairs_1t)
     else:
         line["cpu_baseline"] = None
     txt = json.dumps(line)

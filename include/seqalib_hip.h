@@ -162,11 +162,23 @@ int sa_last_timings(sa_ctx* ctx, float* fill_ms, float* traceback_ms, int* fill_
 #define SA_KERNEL_T16_ENDCELL 2   /* T16 SW with per-chunk maxima + end-cell replay */
 int sa_last_plan(sa_ctx* ctx, int* kernel, int* rows_per_lane, int* waves);
 
-/* Kernel plan the engine would use for a batch (host-only query, no device needed):
- * rows per lane R, waves per workgroup W, direction bytes per pair, row-buffer bytes per pair. */
+/* Plan of the int32 kernel for a batch (host-only query, no device needed): rows per lane R,
+ * waves per workgroup W, direction bytes per pair, row-buffer bytes per pair.  The plan the
+ * engine actually selects (T16 for DNA) is sa_plan_query_ex's. */
 int sa_plan_query(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs,
                   int* rows_per_lane, int* waves, uint64_t* dir_bytes_per_pair,
                   uint64_t* rowbuf_bytes_per_pair);
+
+/* Plan of a batch for a given scoring (host-only query, no device needed): the kernel the
+ * engine selects when the batch holds `nsym` distinct symbols (SA_KERNEL_*; T16 needs nsym <= 4
+ * and a scoring whose scores provably fit 16 bits), its R and W (W = 0: the multi-workgroup
+ * plan), and the device workspace one pair occupies (direction records + row buffers + end-cell
+ * snapshots; the larger of the T16 and int32 variants when the scoring admits T16, since the
+ * variant is chosen on the device and both are provisioned).  A pipelined context
+ * (sa_set_pipeline) holds two such slots per pair of a launch. */
+int sa_plan_query_ex(int algo, const sa_scoring* scoring, uint32_t max_m, uint32_t max_n,
+                     uint32_t npairs, int nsym, int* kernel, int* rows_per_lane, int* waves,
+                     uint64_t* workspace_bytes_per_pair);
 
 /* Synthetic DNA: std::mt19937_64(seed), symbol = "ACGT"[g() & 3]. */
 int sa_synth_dna(uint64_t seed, uint32_t len, uint8_t* out);

@@ -575,6 +575,9 @@ typedef struct {
     volatile int next;
     pthread_mutex_t mu;
     int err;
+    int algo;                 /* oracle_batch: algorithm, full results and op streams */
+    oracle_result* res;
+    uint8_t* ops;             /* pair p's ops at o1[p] + o2[p] + p */
 } batch_job;
 
 static void* batch_worker(void* arg) {
@@ -591,10 +594,14 @@ static void* batch_worker(void* arg) {
         uint8_t* ops = (uint8_t*)malloc((size_t)cap);
         char* r = (char*)malloc((size_t)cap * 3);
         oracle_result res;
-        int rc = (ops && r) ? oracle_align(OR_SW, J->sc, a, m, b, n, NULL, &res, ops, cap, r, r + cap,
+        int rc = (ops && r) ? oracle_align(J->algo, J->sc, a, m, b, n, NULL, &res, ops, cap, r, r + cap,
                                            r + 2 * cap, cap)
                             : -2;
-        J->out[p] = rc ? INT_MIN : res.score;
+        if (J->out) J->out[p] = rc ? INT_MIN : res.score;
+        if (J->res) {
+            J->res[p] = res;
+            memcpy(J->ops + J->o1[p] + J->o2[p] + p, ops, (size_t)res.nops);
+        }
         if (rc) J->err = rc;
         free(ops); free(r);
     }
@@ -608,6 +615,7 @@ int oracle_sw_batch(const oracle_scoring* sc, const uint8_t* s1cat, const uint64
     batch_job J;
     J.sc = sc; J.s1 = s1cat; J.s2 = s2cat; J.o1 = off1; J.o2 = off2;
     J.npairs = npairs; J.out = out_score; J.next = 0; J.err = 0;
+    J.algo = OR_SW; J.res = NULL; J.ops = NULL;
     pthread_mutex_init(&J.mu, NULL);
     pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
     if (!th) return -2;
@@ -616,4 +624,104 @@ int oracle_sw_batch(const oracle_scoring* sc, const uint8_t* s1cat, const uint64
     free(th);
     pthread_mutex_destroy(&J.mu);
     return J.err;
+}
+
+/* Full results and op streams of a batch (test infrastructure: the GPU parity tests' checker at
+ * large sizes), `threads` host threads, pair p's ops at off1[p] + off2[p] + p. */
+int oracle_batch(int algo, const oracle_scoring* sc, const uint8_t* s1cat, const uint64_t* off1,
+                 const uint8_t* s2cat, const uint64_t* off2, int npairs, int threads,
+                 oracle_result* res, uint8_t* ops) {
+    if (threads < 1) threads = 1;
+    batch_job J;
+    J.sc = sc; J.s1 = s1cat; J.s2 = s2cat; J.o1 = off1; J.o2 = off2;
+    J.npairs = npairs; J.out = NULL; J.next = 0; J.err = 0;
+    J.algo = algo; J.res = res; J.ops = ops;
+    pthread_mutex_init(&J.mu, NULL);
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
+    if (!th) return -2;
+    for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, batch_worker, &J);
+    for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+    free(th);
+    pthread_mutex_destroy(&J.mu);
+    return J.err;
+}
+
+/* Score and end cell only, linear space: SW (SASmithWaterman.h:89-117) with byte equality as
+ * the match fn -- the same recurrence, border and last row-major maximum as align_sw above, two
+ * rows instead of the full matrix, so whole north-star batches can be checked on the host.
+ * out[3p..3p+2] = (MaxScore, MaxRow, MaxCol); an empty side gives (INT_MIN, 0, 0). */
+typedef struct {
+    const oracle_scoring* sc;
+    const uint8_t *s1, *s2;
+    const uint64_t *o1, *o2;
+    int npairs;
+    int32_t* out;
+    volatile int next;
+    pthread_mutex_t mu;
+} score_job;
+
+static void sw_score_one(const oracle_scoring* sc, const uint8_t* a, int m, const uint8_t* b, int n,
+                         int32_t* row, int32_t* out) {
+    const int32_t G = sc->gap, MA = sc->match, MI = sc->mismatch;
+    const int allow = sc->allow_mismatch;
+    int32_t best = INT_MIN;
+    int bi = 0, bj = 0;
+    for (int j = 0; j <= n; ++j) row[j] = 0;
+    for (int i = 1; i <= m; ++i) {
+        int32_t diag = 0, left = 0;            /* H[i-1][0] and H[i][0] */
+        const uint8_t ai = a[i - 1];
+        for (int j = 1; j <= n; ++j) {
+            const int32_t up = row[j];
+            const int v = ai == b[j - 1];
+            int32_t d = v ? diag + MA : (allow ? diag + MI : INT_MIN);
+            int32_t h = d;
+            if (up + G > h) h = up + G;
+            if (left + G > h) h = left + G;
+            if (h < 0) h = 0;
+            diag = up;
+            row[j] = h;
+            left = h;
+            if (h >= best) { best = h; bi = i; bj = j; }
+        }
+    }
+    if (m == 0 || n == 0) { best = INT_MIN; bi = 0; bj = 0; }
+    out[0] = best; out[1] = bi; out[2] = bj;
+}
+
+static void* score_worker(void* arg) {
+    score_job* J = (score_job*)arg;
+    int32_t* row = NULL;
+    int cap = -1;
+    for (;;) {
+        pthread_mutex_lock(&J->mu);
+        int p = J->next++;
+        pthread_mutex_unlock(&J->mu);
+        if (p >= J->npairs) break;
+        int m = (int)(J->o1[p + 1] - J->o1[p]), n = (int)(J->o2[p + 1] - J->o2[p]);
+        if (n > cap) {
+            free(row);
+            row = (int32_t*)malloc(sizeof(int32_t) * ((size_t)n + 1));
+            cap = n;
+        }
+        sw_score_one(J->sc, J->s1 + J->o1[p], m, J->s2 + J->o2[p], n, row, J->out + 3 * (size_t)p);
+    }
+    free(row);
+    return NULL;
+}
+
+int oracle_sw_score_batch(const oracle_scoring* sc, const uint8_t* s1cat, const uint64_t* off1,
+                          const uint8_t* s2cat, const uint64_t* off2, int npairs, int threads,
+                          int32_t* out) {
+    if (threads < 1) threads = 1;
+    score_job J;
+    J.sc = sc; J.s1 = s1cat; J.s2 = s2cat; J.o1 = off1; J.o2 = off2;
+    J.npairs = npairs; J.out = out; J.next = 0;
+    pthread_mutex_init(&J.mu, NULL);
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
+    if (!th) return -2;
+    for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, score_worker, &J);
+    for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+    free(th);
+    pthread_mutex_destroy(&J.mu);
+    return 0;
 }

@@ -57,6 +57,12 @@ int oracle_align(int algo, const oracle_scoring* sc, const uint8_t* s1, int m, c
 /* CPU baseline ("port"): SW over a batch of pairs on `threads` threads, full reference-shaped
  * computation (bool match cache, int32 row-major matrix, traceback, forceGlobal).
  * Writes each pair's max score into out_score.  Returns 0 or -2. */
+int oracle_batch(int algo, const oracle_scoring* sc, const uint8_t* s1cat, const uint64_t* off1,
+                 const uint8_t* s2cat, const uint64_t* off2, int npairs, int threads,
+                 oracle_result* res, uint8_t* ops);
+int oracle_sw_score_batch(const oracle_scoring* sc, const uint8_t* s1cat, const uint64_t* off1,
+                          const uint8_t* s2cat, const uint64_t* off2, int npairs, int threads,
+                          int32_t* out);
 int oracle_sw_batch(const oracle_scoring* sc, const uint8_t* s1cat, const uint64_t* off1,
                     const uint8_t* s2cat, const uint64_t* off2, int npairs, int threads,
                     int32_t* out_score);

@@ -116,6 +116,8 @@ def load_library():
                                         C.c_uint32, C.c_uint32, vp, vp, vp, vp]
     L.sa_last_timings.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_float), i32p]
     L.sa_plan_query.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, i32p, i32p, u64p, u64p]
+    L.sa_plan_query_ex.argtypes = [C.c_int, C.POINTER(_Scoring), C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
+                                   i32p, i32p, i32p, u64p]
     L.sa_last_plan.argtypes = [vp, i32p, i32p, i32p]
     L.sa_set_pipeline.argtypes = [vp, C.c_int]
     L.sa_wait.argtypes = [vp]
@@ -123,7 +125,7 @@ def load_library():
     L.sa_synth_mutate.argtypes = [vp, C.c_uint32, C.c_uint64, vp, C.c_uint32, C.POINTER(C.c_uint32)]
     L.sa_synth_dna_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_int]
     for fn in ("sa_set_workspace_limit", "sa_trim", "sa_align_batch", "sa_align_batch_device",
-               "sa_last_timings", "sa_last_plan", "sa_plan_query", "sa_synth_dna", "sa_synth_mutate", "sa_synth_dna_batch",
+               "sa_last_timings", "sa_last_plan", "sa_plan_query", "sa_plan_query_ex", "sa_synth_dna", "sa_synth_mutate", "sa_synth_dna_batch",
                "sa_create", "sa_device_count", "sa_set_pipeline", "sa_wait"):
         getattr(L, fn).restype = C.c_int
     if L.sa_version() != 1:
@@ -410,6 +412,19 @@ def plan_query(algo: int, max_m: int, max_n: int, npairs: int):
     if rc:
         raise SeqalibError("sa_plan_query failed")
     return R.value, W.value, db.value, rb.value
+
+
+def plan_query_ex(algo: int, scoring: "ScoringSystem", max_m: int, max_n: int, npairs: int, nsym: int = 4):
+    """(kernel, R, W, workspace bytes per pair) the engine selects for a batch with `nsym`
+    distinct symbols under `scoring` (sa_plan_query_ex)."""
+    L = load_library()
+    k, R, W, ws = C.c_int(), C.c_int(), C.c_int(), C.c_uint64()
+    sc = scoring._c()
+    rc = L.sa_plan_query_ex(algo, C.byref(sc), max_m, max_n, npairs, nsym, C.byref(k), C.byref(R), C.byref(W),
+                            C.byref(ws))
+    if rc:
+        raise SeqalibError("sa_plan_query_ex failed")
+    return k.value, R.value, W.value, ws.value
 
 
 # ------------------------------------------------------------------- synthetic inputs (host)

@@ -56,20 +56,40 @@ __global__ __launch_bounds__(256) void alphabet_scan(const uint8_t* d1, const ui
     if (threadIdx.x < 8 && sb[threadIdx.x]) atomicOr(&bitmap[threadIdx.x], sb[threadIdx.x]);
 }
 
-// prof[c] byte c' = (int8)(4 * s(sym c, sym c') + 3), s = match ? match : mismatch.
-__global__ void build_profile(const uint32_t* lutbits, uint32_t sym_pack, int match, int mismatch,
-                              uint32_t* prof) {
-    const int c = threadIdx.x;
-    if (c >= 4) return;
-    const uint32_t a = (sym_pack >> (8 * c)) & 255u;
-    uint32_t w = 0;
-    for (int c2 = 0; c2 < 4; ++c2) {
-        const uint32_t b = (sym_pack >> (8 * c2)) & 255u;
-        const bool v = lutbits ? ((lutbits[(a << 3) | (b >> 5)] >> (b & 31u)) & 1u) : (a == b);
-        const int t = 4 * (v ? match : mismatch) + 3;
-        w |= ((uint32_t)t & 255u) << (8 * c2);
+// The T16 decision, on the device (so the host never waits for the scan): with <= 4 distinct
+// symbols, sym_pack = the symbols padded with absent byte values (codes stay distinct),
+// prof[c] byte c' = (int8)(4 * s(sym c, sym c') + 3), s = match ? match : mismatch; sel = 1.
+// More symbols: sel = 0 (the int32 kernel's launches run, the T16 ones return at once).
+__global__ void decide_t16(const uint32_t* lutbits, int match, int mismatch, uint32_t* aux) {
+    if (threadIdx.x != 0) return;
+    uint32_t syms[4] = {0, 0, 0, 0};
+    int nsym = 0;
+    for (int b = 0; b < 256; ++b)
+        if ((aux[b >> 5] >> (b & 31)) & 1u) {
+            if (nsym < 4) syms[nsym] = (uint32_t)b;
+            ++nsym;
+        }
+    if (nsym > 4) {
+        aux[kAuxSel] = 0;
+        return;
     }
-    prof[c] = w;
+    for (int b = 0; nsym < 4 && b < 256; ++b) {
+        bool used = false;
+        for (int q = 0; q < nsym; ++q) used |= syms[q] == (uint32_t)b;
+        if (!used) syms[nsym++] = (uint32_t)b;
+    }
+    for (int c = 0; c < 4; ++c) {
+        uint32_t w = 0;
+        for (int c2 = 0; c2 < 4; ++c2) {
+            const uint32_t a = syms[c], b = syms[c2];
+            const bool v = lutbits ? ((lutbits[(a << 3) | (b >> 5)] >> (b & 31u)) & 1u) : (a == b);
+            const int t = 4 * (v ? match : mismatch) + 3;
+            w |= ((uint32_t)t & 255u) << (8 * c2);
+        }
+        aux[kAuxProf + c] = w;
+    }
+    aux[kAuxProf + 4] = syms[0] | syms[1] << 8 | syms[2] << 16 | syms[3] << 24;
+    aux[kAuxSel] = 1;
 }
 
 hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uint8_t* d2,
@@ -80,9 +100,8 @@ hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uin
     return hipGetLastError();
 }
 
-hipError_t launch_build_profile(const uint32_t* lutbits, uint32_t sym_pack, int match, int mismatch,
-                                uint32_t* prof, hipStream_t s) {
-    hipLaunchKernelGGL(build_profile, dim3(1), dim3(64), 0, s, lutbits, sym_pack, match, mismatch, prof);
+hipError_t launch_decide_t16(const uint32_t* lutbits, int match, int mismatch, uint32_t* aux, hipStream_t s) {
+    hipLaunchKernelGGL(decide_t16, dim3(1), dim3(64), 0, s, lutbits, match, mismatch, aux);
     return hipGetLastError();
 }
 

@@ -31,9 +31,15 @@ struct sa_ctx {
     std::vector<hipEvent_t> events;  // 3 per fill launch: start, fill end, traceback end
     int launches = 0;
     hipStream_t timed_stream = nullptr;
-    // alphabet bitmap (8 words) + T16 profile (4 words), one 64-word slot per pipeline slot
+    // aux words of the T16 decision (sa_internal.h kAux*), one kAuxWords slot per pipeline slot
     uint32_t* aux = nullptr;
-    int last_kernel = SA_KERNEL_INT32, last_R = 0, last_W = 0;
+    // plan of the last call: one entry per kernel variant it enqueued (T16 first when the batch
+    // was T16-eligible by scoring and shape; the device picked one by the batch alphabet, and
+    // h_sel receives that choice asynchronously, ev_sel marks its arrival)
+    int nvar = 0, var_kernel[2] = {0, 0}, var_R[2] = {0, 0}, var_W[2] = {0, 0};
+    uint32_t* h_sel = nullptr;
+    hipEvent_t ev_sel = nullptr;
+    bool no_split = false;   // host API re-run after a SPLIT wait expired
     // cross-call pipeline of the device API (sa_set_pipeline): fills on s_fill, tracebacks on
     // s_tb, two workspace slots; ev_slot[k] = traceback of the last call that used slot k done
     int pipeline = 0;
@@ -75,12 +81,13 @@ struct Plan {
 
 // SPLIT plan when a batch is too small to fill the chip one workgroup per pair and its pairs
 // have at least two bands of 256 rows.  SEQALIB_SPLIT=0 disables it.
-bool split_ok(uint32_t max_m, uint32_t max_n, uint32_t npairs) {
+bool split_ok(uint32_t max_m, uint32_t max_n, uint32_t npairs, bool allow_split) {
+    if (!allow_split) return false;
     if (const char* e = getenv("SEQALIB_SPLIT")) if (e[0] == '0') return false;
     return npairs < 1024 && max_m > 4u * kWave && max_n > 0;
 }
 
-Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t16 = false) {
+Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t16, bool allow_split = true) {
     Plan p;
     const bool aff = is_affine(algo);
     const int rmax = aff ? 16 : 16;
@@ -95,7 +102,7 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t
         p.W = 4;
         p.R = 4;
         while (p.R < rmax && (uint64_t)kWave * p.R * p.W < max_m) p.R *= 2;
-    } else if (split_ok(max_m, max_n, npairs)) {
+    } else if (split_ok(max_m, max_n, npairs, allow_split)) {
         // Few pairs, several bands each: every band its own single-wave workgroup (on its own
         // SIMD, anywhere on the chip), bands of a pair chained through HBM/L2 hand-offs.  Short
         // bands (R = 4) give the most concurrent bands; R = 8 once there are plenty.
@@ -131,6 +138,37 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t
     p.g = make_geom(algo, p.R, max_m, max_n, t16);
     p.rowbuf_elems = (uint64_t)(aff ? 2 : 1) * std::max<uint32_t>(max_n, 1);
     return p;
+}
+
+// One kernel variant of a batch: its plan, end-cell tracking and per-pair workspace
+// ([dirs][row buffer][end-cell snapshots h][p][m], in that order inside a launch's block).
+struct Variant {
+    Plan pl;
+    bool t16 = false, cmax = false;
+    uint32_t snap_nch = 0;
+    uint64_t snap_h_slot = 0, snap_p_slot = 0;   // 32-bit words per pair
+    uint64_t slot_bytes = 0;
+    int kernel = SA_KERNEL_INT32;
+};
+
+Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t16, bool allow_split) {
+    Variant v;
+    v.t16 = t16;
+    v.pl = make_plan(algo, max_m, max_n, npairs, t16, allow_split);
+    // CMAX end-cell tracking (sa_fill_impl.h / sa_endcell.hip): T16 SW on one-wave plans with an
+    // end-cell replay instantiation (R <= 32)
+    v.cmax = t16 && algo == SA_SW && v.pl.W == 1 && v.pl.R >= 4 && v.pl.R <= 32;
+    if (const char* ec = getenv("SEQALIB_CMAX")) if (ec[0] == '0') v.cmax = false;
+    if (v.cmax) {
+        v.snap_nch = chunks_per_band(max_n);
+        v.snap_p_slot = (uint64_t)v.pl.g.bands * v.snap_nch * kWave;
+        v.snap_h_slot = v.snap_p_slot * (v.pl.R / 2);
+        v.pl.rowbuf_elems = (uint64_t)v.pl.g.bands * std::max<uint32_t>(max_n, 1);
+    }
+    if (v.pl.split) v.pl.rowbuf_elems = 0;   // hand-off granules live in c->split
+    v.kernel = v.cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
+    v.slot_bytes = v.pl.g.dir_slot + v.pl.rowbuf_elems * 4 + (v.snap_h_slot + 2 * v.snap_p_slot) * 4;
+    return v;
 }
 
 __global__ void lut_to_bits(const uint8_t* lut, uint32_t* bits) {
@@ -230,10 +268,20 @@ int validate_scoring(sa_ctx* c, int algo, const sa_scoring* s) {
     return SA_OK;
 }
 
-// Enqueue fill + traceback for pairs [0, npairs) whose inputs are on the device.
-// pipe: (device API with sa_set_pipeline) fills go to c->s_fill and tracebacks to c->s_tb after
-// the caller's stream reaches this call; workspace and aux use slot pipe_k % 2, and the call
-// returns without ordering `stream` after the results (sa_wait).
+// T16 by scoring and shape (the batch alphabet is checked on the device, decide_t16).
+bool t16_candidate(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
+    bool t16 = t16_ok(algo, sc, max_m, max_n) && (algo == SA_NW || keyed_ok(algo, sc, max_m, max_n));
+    if (const char* e16 = getenv("SEQALIB_T16")) if (e16[0] == '0') t16 = false;
+    return t16;
+}
+
+// Enqueue fill + traceback for pairs [0, npairs) whose inputs are on the device.  Nothing here
+// waits on the host: when the scoring and shapes admit the T16 kernel, the batch alphabet is
+// scanned on the device and BOTH variants (T16 and int32) are enqueued, each launch guarded by
+// the device's decision (sa_skip), so the launches of the variant not taken return at once.
+// pipe: (device API with sa_set_pipeline) fills and end-cell replays go to c->s_fill and
+// tracebacks to c->s_tb after the caller's stream reaches this call; workspace and aux use slot
+// pipe_k % 2, and the call returns without ordering `stream` after the results (sa_wait).
 int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, const uint64_t* o1,
                const uint8_t* d2, const uint64_t* o2, uint32_t npairs, uint32_t max_m,
                uint32_t max_n, const uint32_t* d_lutbits, sa_result* d_res, uint8_t* d_ops,
@@ -243,60 +291,44 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     const bool keyed = keyed_ok(algo, sc, max_m, max_n);
     const bool allow = sc->allow_mismatch != 0;
     const bool lut = d_lutbits != nullptr;
-    // T16 eligibility: scoring/shape bounds on the host, then the batch alphabet from the device
-    bool t16 = t16_ok(algo, sc, max_m, max_n) && (algo == SA_NW || keyed);
-    if (const char* e16 = getenv("SEQALIB_T16")) if (e16[0] == '0') t16 = false;
-    uint32_t sym_pack = 0;
-    if (!c->aux) SA_HIP(c, hipMalloc(&c->aux, 512));
+    const bool t16 = t16_candidate(algo, sc, max_m, max_n);
+    if (!c->aux) SA_HIP(c, hipMalloc(&c->aux, 2 * kAuxWords * 4));
+    if (!c->h_sel) {
+        SA_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_sel), 64, hipHostMallocDefault));
+        SA_HIP(c, hipEventCreateWithFlags(&c->ev_sel, hipEventDisableTiming));
+    }
     if (!pipe && c->s_fill) {   // a non-pipelined call reuses slot 0: drain pipelined work first
         SA_HIP(c, hipStreamSynchronize(c->s_fill));
         SA_HIP(c, hipStreamSynchronize(c->s_tb));
     }
     const int slot = pipe ? (int)(c->pipe_k & 1) : 0;
-    uint32_t* aux = c->aux + 64 * slot;
+    uint32_t* aux = c->aux + kAuxWords * slot;
     if (pipe && c->ev_slot[slot]) SA_HIP(c, hipStreamWaitEvent(stream, c->ev_slot[slot], 0));   // slot free
+    Variant vars[2];
+    int nv = 0;
+    const uint32_t* sel = nullptr;
     if (t16) {
         SA_HIP(c, launch_alphabet_scan(d1, o1, d2, o2, npairs, aux, stream));
-        uint32_t bm[8];
-        SA_HIP(c, hipMemcpyAsync(bm, aux, 32, hipMemcpyDeviceToHost, stream));
-        SA_HIP(c, hipStreamSynchronize(stream));
-        int nsym = 0;
-        uint8_t syms[4];
-        for (int b = 0; b < 256; ++b)
-            if ((bm[b >> 5] >> (b & 31)) & 1u) {
-                if (nsym < 4) syms[nsym] = (uint8_t)b;
-                ++nsym;
-            }
-        if (nsym > 4) {
-            t16 = false;
-        } else {
-            // pad with byte values absent from the batch so codes stay distinct
-            for (int b = 0; nsym < 4 && b < 256; ++b) {
-                bool used = false;
-                for (int q = 0; q < nsym; ++q) used |= syms[q] == b;
-                if (!used) syms[nsym++] = (uint8_t)b;
-            }
-            sym_pack = syms[0] | (uint32_t)syms[1] << 8 | (uint32_t)syms[2] << 16 | (uint32_t)syms[3] << 24;
-            SA_HIP(c, launch_build_profile(d_lutbits, sym_pack, sc->match, sc->mismatch, aux + 8, stream));
+        SA_HIP(c, launch_decide_t16(d_lutbits, sc->match, sc->mismatch, aux, stream));
+        SA_HIP(c, hipMemcpyAsync(c->h_sel, aux + kAuxSel, 4, hipMemcpyDeviceToHost, stream));
+        SA_HIP(c, hipEventRecord(c->ev_sel, stream));
+        sel = aux + kAuxSel;
+        vars[nv++] = make_variant(algo, max_m, max_n, npairs, true, !c->no_split);
+    }
+    vars[nv++] = make_variant(algo, max_m, max_n, npairs, false, !c->no_split);
+    c->nvar = nv;
+    uint64_t slot_bytes = 0, sp_bands = 0;
+    bool any_split = false;
+    for (int k = 0; k < nv; ++k) {
+        c->var_kernel[k] = vars[k].kernel;
+        c->var_R[k] = vars[k].pl.R;
+        c->var_W[k] = vars[k].pl.split ? 0 : vars[k].pl.W;   // 0: SPLIT plan (one single-wave workgroup per band)
+        slot_bytes = std::max(slot_bytes, vars[k].slot_bytes);
+        if (vars[k].pl.split) {
+            any_split = true;
+            sp_bands = std::max<uint64_t>(sp_bands, vars[k].pl.g.bands);
         }
     }
-    Plan pl = make_plan(algo, max_m, max_n, npairs, t16);
-    // CMAX end-cell tracking (sa_fill_impl.h / sa_endcell.hip): T16 SW on one-wave plans
-    bool cmax = t16 && algo == SA_SW && pl.W == 1 && pl.R >= 4;
-    if (const char* ec = getenv("SEQALIB_CMAX")) if (ec[0] == '0') cmax = false;
-    uint32_t snap_nch = 0;
-    uint64_t snap_h_slot = 0, snap_p_slot = 0;
-    if (cmax) {
-        snap_nch = chunks_per_band(max_n);
-        snap_p_slot = (uint64_t)pl.g.bands * snap_nch * kWave;
-        snap_h_slot = snap_p_slot * (pl.R / 2);
-        pl.rowbuf_elems = (uint64_t)pl.g.bands * std::max<uint32_t>(max_n, 1);
-    }
-    if (pl.split) pl.rowbuf_elems = 0;   // hand-off granules live in c->split
-    c->last_kernel = cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
-    c->last_R = pl.R;
-    c->last_W = pl.split ? 0 : pl.W;   // 0: SPLIT plan (one single-wave workgroup per band)
-    const uint64_t slot_bytes = pl.g.dir_slot + pl.rowbuf_elems * 4 + (snap_h_slot + 2 * snap_p_slot) * 4;
     const uint64_t budget = pipe ? ws_budget(c) / 2 : ws_budget(c);
     uint64_t per_launch = slot_bytes ? std::max<uint64_t>(1, budget / std::max<uint64_t>(slot_bytes, 1)) : npairs;
     per_launch = std::min<uint64_t>(per_launch, npairs ? npairs : 1);
@@ -308,11 +340,11 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     int rc = ensure_ws(c, std::max<uint64_t>(pipe ? 2 * need : need, 4096));
     if (rc) return rc;
     // SPLIT scratch (the fills of all calls run on one stream, so one copy serves the pipeline)
-    const uint64_t sp_bands = pl.g.bands;
-    const uint64_t sp_gran = pl.split ? per_launch * sp_bands * std::max<uint32_t>(max_n, 1) * (is_affine(algo) ? 2 : 1) : 0;
+    const uint64_t aff2 = is_affine(algo) ? 2 : 1;
+    const uint64_t sp_gran = any_split ? per_launch * sp_bands * std::max<uint32_t>(max_n, 1) * aff2 : 0;
     const uint64_t sp_zero = 256 + sp_gran * 8;   // ticket + granules: zeroed before every launch
-    const uint64_t sp_need = pl.split ? sp_zero + per_launch * sp_bands * 16 : 0;
-    if (pl.split && c->split_bytes < sp_need) {
+    const uint64_t sp_need = any_split ? sp_zero + per_launch * sp_bands * 16 : 0;
+    if (any_split && c->split_bytes < sp_need) {
         if (c->split) {
             SA_HIP(c, hipStreamSynchronize(c->stream));
             if (c->s_fill) SA_HIP(c, hipStreamSynchronize(c->s_fill));
@@ -326,13 +358,9 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         }
         c->split_bytes = sp_need;
     }
-    // pipeline slots are fixed halves of the workspace, so a later call with a smaller need
-    // cannot overlap the slot a running traceback still reads
-    uint8_t* dirs = c->ws + (pipe ? slot * ((c->ws_bytes / 2) & ~(uint64_t)255) : 0);
-    int32_t* rowbuf = reinterpret_cast<int32_t*>(c->ws + per_launch * pl.g.dir_slot);
-    uint32_t* snap_h = reinterpret_cast<uint32_t*>(rowbuf + per_launch * pl.rowbuf_elems);
-    int32_t* snap_p = reinterpret_cast<int32_t*>(snap_h + per_launch * snap_h_slot);
-    int32_t* snap_m = snap_p + per_launch * snap_p_slot;
+    // A pipeline slot is one contiguous half of the workspace holding everything its calls
+    // write (dirs, row buffers, snapshots), so calls on the other slot never touch it.
+    uint8_t* const wbase = c->ws + (pipe ? slot * ((c->ws_bytes / 2) & ~(uint64_t)255) : 0);
 
     // reset timing
     c->launches = 0;
@@ -347,84 +375,105 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
 
     for (uint64_t base = 0; base < npairs; base += per_launch) {
         const uint32_t cnt = (uint32_t)std::min<uint64_t>(per_launch, npairs - base);
-        FillParams fp;
-        fp.seq1 = d1; fp.off1 = o1; fp.seq2 = d2; fp.off2 = o2;
-        fp.lutbits = d_lutbits;
-        fp.dirs = dirs; fp.dir_slot = pl.g.dir_slot; fp.band_stride = pl.g.band_stride;
-        fp.rowbuf = rowbuf; fp.rowbuf_slot = pl.rowbuf_elems;
-        fp.res = d_res;
-        fp.pair_base = (uint32_t)base;
-        fp.max_m = max_m; fp.max_n = max_n;
-        fp.gap = sc->gap; fp.match = sc->match; fp.mismatch = allow ? sc->mismatch : INT_MIN;
-        fp.gap_open = sc->gap_open; fp.gap_extend = sc->gap_extend;
-        fp.waves = pl.W;
-        fp.stage_seq2 = max_n <= kMaxStagedSeq2 ? 1 : 0;
-        fp.prof = aux + 8;
-        fp.sym_pack = sym_pack;
-        fp.snap_h = snap_h; fp.snap_p = snap_p; fp.snap_m = snap_m;
-        fp.snap_h_slot = snap_h_slot; fp.snap_p_slot = snap_p_slot; fp.snap_nch = snap_nch;
-        fp.split_bands = (uint32_t)sp_bands;
-        fp.ticket = pl.split ? reinterpret_cast<uint32_t*>(c->split) : nullptr;
-        fp.hand = pl.split ? reinterpret_cast<unsigned long long*>(c->split + 256) : nullptr;
-        fp.hand_x_off = pl.split ? (uint64_t)cnt * sp_bands * std::max<uint32_t>(max_n, 1) : 0;
-        fp.part = pl.split ? reinterpret_cast<int32_t*>(c->split + sp_zero) : nullptr;
-
-        TbParams tp;
-        tp.seq1 = d1; tp.off1 = o1; tp.seq2 = d2; tp.off2 = o2;
-        tp.lutbits = d_lutbits;
-        tp.dirs = dirs; tp.dir_slot = pl.g.dir_slot;
-        tp.ops = d_ops; tp.res = d_res;
-        tp.pair_base = (uint32_t)base; tp.count = cnt;
-        tp.max_m = max_m; tp.max_n = max_n;
-        tp.gap = fp.gap; tp.match = fp.match; tp.mismatch = fp.mismatch;
-        tp.gap_open = fp.gap_open; tp.gap_extend = fp.gap_extend;
-        tp.allow = allow ? 1 : 0;
-        tp.tagged = t16 ? 1 : 0;
-
         while ((int)c->events.size() < 3 * (c->launches + 1)) {
             hipEvent_t ev;
             SA_HIP(c, hipEventCreate(&ev));
             c->events.push_back(ev);
         }
         hipEvent_t* ev = &c->events[3 * c->launches];
+        // the launches of one call share the slot: launch k+1's fill overwrites the records
+        // launch k's traceback reads (on the other stream when pipelined)
+        if (pipe && c->launches > 0) SA_HIP(c, hipStreamWaitEvent(sf, c->events[3 * c->launches - 1], 0));
         SA_HIP(c, hipEventRecord(ev[0], sf));
-        const FillVariant fv = {pl.R, lut, allow, keyed, t16, cmax, pl.split};
-        if (pl.split) SA_HIP(c, hipMemsetAsync(c->split, 0, 256 + fp.hand_x_off * 8 * (is_affine(algo) ? 2 : 1), sf));
-        hipError_t e = launch_fill(algo, fv, fp, pl.split ? (uint32_t)(cnt * sp_bands) : cnt, sf);
-        if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
-        if (pl.split) {
-            SplitReduceParams rp;
-            rp.off1 = o1; rp.off2 = o2; rp.part = fp.part; rp.res = d_res;
-            rp.pair_base = (uint32_t)base; rp.count = cnt; rp.split_bands = (uint32_t)sp_bands;
-            rp.band_rows = (uint32_t)kWave * pl.R; rp.max_m = max_m; rp.max_n = max_n;
-            rp.gap = sc->gap; rp.gap_open = sc->gap_open; rp.gap_extend = sc->gap_extend;
-            rp.cmax = cmax ? 1 : 0;
-            e = launch_split_reduce(algo, rp, sf);
-            if (e != hipSuccess) return hip_fail(c, e, "split reduce kernel launch");
-        }
-        if (cmax) {
-            EndcellParams ep;
-            ep.seq1 = d1; ep.off1 = o1; ep.seq2 = d2; ep.off2 = o2;
-            ep.prof = fp.prof; ep.sym_pack = sym_pack;
-            ep.snap_h = snap_h; ep.snap_p = snap_p; ep.snap_m = snap_m;
-            ep.snap_h_slot = snap_h_slot; ep.snap_p_slot = snap_p_slot; ep.snap_nch = snap_nch;
+        const uint64_t hand_x_off = any_split ? (uint64_t)cnt * sp_bands * std::max<uint32_t>(max_n, 1) : 0;
+        if (any_split) SA_HIP(c, hipMemsetAsync(c->split, 0, 256 + hand_x_off * 8 * aff2, sf));
+        FillParams fps[2];
+        for (int k = 0; k < nv; ++k) {
+            const Variant& v = vars[k];
+            const Plan& pl = v.pl;
+            uint8_t* dirs = wbase;
+            int32_t* rowbuf = reinterpret_cast<int32_t*>(wbase + per_launch * pl.g.dir_slot);
+            uint32_t* snap_h = reinterpret_cast<uint32_t*>(rowbuf + per_launch * pl.rowbuf_elems);
+            int32_t* snap_p = reinterpret_cast<int32_t*>(snap_h + per_launch * v.snap_h_slot);
+            int32_t* snap_m = snap_p + per_launch * v.snap_p_slot;
+            FillParams& fp = fps[k];
+            fp = FillParams{};
+            fp.seq1 = d1; fp.off1 = o1; fp.seq2 = d2; fp.off2 = o2;
+            fp.lutbits = d_lutbits;
+            fp.dirs = dirs; fp.dir_slot = pl.g.dir_slot; fp.band_stride = pl.g.band_stride;
+            fp.rowbuf = rowbuf; fp.rowbuf_slot = pl.rowbuf_elems;
+            fp.res = d_res;
+            fp.pair_base = (uint32_t)base;
+            fp.max_m = max_m; fp.max_n = max_n;
+            fp.gap = sc->gap; fp.match = sc->match; fp.mismatch = allow ? sc->mismatch : INT_MIN;
+            fp.gap_open = sc->gap_open; fp.gap_extend = sc->gap_extend;
+            fp.waves = pl.W;
+            fp.stage_seq2 = max_n <= kMaxStagedSeq2 ? 1 : 0;
+            fp.prof = aux + kAuxProf;
+            fp.sel = sel; fp.sel_want = v.t16 ? 1u : 0u;
+            fp.snap_h = snap_h; fp.snap_p = snap_p; fp.snap_m = snap_m;
+            fp.snap_h_slot = v.snap_h_slot; fp.snap_p_slot = v.snap_p_slot; fp.snap_nch = v.snap_nch;
+            fp.split_bands = (uint32_t)sp_bands;
+            fp.ticket = pl.split ? reinterpret_cast<uint32_t*>(c->split) : nullptr;
+            fp.hand = pl.split ? reinterpret_cast<unsigned long long*>(c->split + 256) : nullptr;
+            fp.hand_x_off = pl.split ? hand_x_off : 0;
+            fp.part = pl.split ? reinterpret_cast<int32_t*>(c->split + sp_zero) : nullptr;
+            const FillVariant fv = {pl.R, lut, allow, keyed, v.t16, v.cmax, pl.split};
+            hipError_t e = launch_fill(algo, fv, fp, pl.split ? (uint32_t)(cnt * sp_bands) : cnt, sf);
+            if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
             if (pl.split) {
-                ep.rowbuf = reinterpret_cast<const int32_t*>(fp.hand);
-                ep.rowbuf_slot = 2 * sp_bands * std::max<uint32_t>(max_n, 1);
-                ep.rowbuf_stride = 2;
-            } else {
-                ep.rowbuf = rowbuf; ep.rowbuf_slot = pl.rowbuf_elems; ep.rowbuf_stride = 1;
+                SplitReduceParams rp;
+                rp.off1 = o1; rp.off2 = o2; rp.part = fp.part; rp.res = d_res;
+                rp.pair_base = (uint32_t)base; rp.count = cnt; rp.split_bands = (uint32_t)sp_bands;
+                rp.band_rows = (uint32_t)kWave * pl.R; rp.max_m = max_m; rp.max_n = max_n;
+                rp.gap = sc->gap; rp.gap_open = sc->gap_open; rp.gap_extend = sc->gap_extend;
+                rp.cmax = v.cmax ? 1 : 0;
+                rp.sel = sel; rp.sel_want = fp.sel_want;
+                e = launch_split_reduce(algo, rp, sf);
+                if (e != hipSuccess) return hip_fail(c, e, "split reduce kernel launch");
             }
-            ep.max_n = max_n;
-            ep.res = d_res; ep.pair_base = (uint32_t)base; ep.count = cnt;
-            ep.gap = sc->gap;
-            e = launch_endcell(pl.R, ep, sf);
-            if (e != hipSuccess) return hip_fail(c, e, "end-cell kernel launch");
+            if (v.cmax) {
+                EndcellParams ep{};
+                ep.seq1 = d1; ep.off1 = o1; ep.seq2 = d2; ep.off2 = o2;
+                ep.prof = fp.prof; ep.sel = sel; ep.sel_want = fp.sel_want;
+                ep.snap_h = snap_h; ep.snap_p = snap_p; ep.snap_m = snap_m;
+                ep.snap_h_slot = v.snap_h_slot; ep.snap_p_slot = v.snap_p_slot; ep.snap_nch = v.snap_nch;
+                if (pl.split) {
+                    ep.rowbuf = reinterpret_cast<const int32_t*>(fp.hand);
+                    ep.rowbuf_slot = 2 * sp_bands * std::max<uint32_t>(max_n, 1);
+                    ep.rowbuf_stride = 2;
+                } else {
+                    ep.rowbuf = rowbuf; ep.rowbuf_slot = pl.rowbuf_elems; ep.rowbuf_stride = 1;
+                }
+                ep.max_n = max_n;
+                ep.res = d_res; ep.pair_base = (uint32_t)base; ep.count = cnt;
+                ep.gap = sc->gap;
+                // on the fill stream, right after the fill: run beside the next call's fill (on the
+                // traceback stream) its 10,000 short waves slowed that fill by 4 % (measured)
+                e = launch_endcell(pl.R, ep, sf);
+                if (e != hipSuccess) return hip_fail(c, e, "end-cell kernel launch");
+            }
         }
         SA_HIP(c, hipEventRecord(ev[1], sf));
         if (pipe) SA_HIP(c, hipStreamWaitEvent(stb, ev[1], 0));
-        e = tb_wave(cnt) ? launch_traceback_wave(algo, pl.R, lut, tp, stb) : launch_traceback(algo, pl.R, lut, tp, stb);
-        if (e != hipSuccess) return hip_fail(c, e, "traceback kernel launch");
+        for (int k = 0; k < nv; ++k) {
+            const Variant& v = vars[k];
+            TbParams tp;
+            tp.seq1 = d1; tp.off1 = o1; tp.seq2 = d2; tp.off2 = o2;
+            tp.lutbits = d_lutbits;
+            tp.dirs = fps[k].dirs; tp.dir_slot = v.pl.g.dir_slot;
+            tp.ops = d_ops; tp.res = d_res;
+            tp.pair_base = (uint32_t)base; tp.count = cnt;
+            tp.max_m = max_m; tp.max_n = max_n;
+            tp.gap = fps[k].gap; tp.match = fps[k].match; tp.mismatch = fps[k].mismatch;
+            tp.gap_open = fps[k].gap_open; tp.gap_extend = fps[k].gap_extend;
+            tp.allow = allow ? 1 : 0;
+            tp.tagged = v.t16 ? 1 : 0;
+            tp.sel = sel; tp.sel_want = fps[k].sel_want;
+            hipError_t e = tb_wave(cnt) ? launch_traceback_wave(algo, v.pl.R, lut, tp, stb)
+                                        : launch_traceback(algo, v.pl.R, lut, tp, stb);
+            if (e != hipSuccess) return hip_fail(c, e, "traceback kernel launch");
+        }
         SA_HIP(c, hipEventRecord(ev[2], stb));
         c->launches++;
     }
@@ -530,6 +579,21 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         SA_HIP(c, hipMemcpyAsync(ops, dops, ops_total, hipMemcpyDeviceToHost, st));
     }
     SA_HIP(c, hipStreamSynchronize(st));
+    // A SPLIT band whose bounded wait for its producer expired (SA_FLAG_TIMEOUT, e.g. the GPU
+    // was time-sliced with another process) leaves an invalid pair: the host API never returns
+    // one -- it re-runs the batch on the single-workgroup plans.
+    bool tmo = false;
+    for (uint32_t p = 0; p < npairs && !tmo; ++p) tmo = (results[p].flags & SA_FLAG_TIMEOUT) != 0;
+    if (tmo && !c->no_split) {
+        c->no_split = true;
+        int rc = run_device(c, algo, sc, d1, do1, d2, do2, npairs, max_m, max_n,
+                            use_lut ? dbits : nullptr, dres, dops, st);
+        c->no_split = false;
+        if (rc) return rc;
+        SA_HIP(c, hipMemcpyAsync(results, dres, sizeof(sa_result) * npairs, hipMemcpyDeviceToHost, st));
+        SA_HIP(c, hipMemcpyAsync(ops, dops, ops_total, hipMemcpyDeviceToHost, st));
+        SA_HIP(c, hipStreamSynchronize(st));
+    }
     return SA_OK;
 }
 
@@ -585,13 +649,14 @@ void sa_destroy(sa_ctx* c) {
     if (c->s_fill) (void)hipStreamSynchronize(c->s_fill);
     if (c->s_tb) (void)hipStreamSynchronize(c->s_tb);
     for (auto ev : c->events) (void)hipEventDestroy(ev);
-    for (auto ev : {c->ev_in, c->ev_slot[0], c->ev_slot[1]})
+    for (auto ev : {c->ev_in, c->ev_slot[0], c->ev_slot[1], c->ev_sel})
         if (ev) (void)hipEventDestroy(ev);
     if (c->s_fill) (void)hipStreamDestroy(c->s_fill);
     if (c->s_tb) (void)hipStreamDestroy(c->s_tb);
     if (c->ws) (void)hipFree(c->ws);
     if (c->io) (void)hipFree(c->io);
     if (c->aux) (void)hipFree(c->aux);
+    if (c->h_sel) (void)hipHostFree(c->h_sel);
     if (c->split) (void)hipFree(c->split);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -761,20 +826,41 @@ int sa_last_timings(sa_ctx* c, float* fill_ms, float* tb_ms, int* launches) {
 
 int sa_last_plan(sa_ctx* c, int* kernel, int* R, int* W) {
     if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
-    if (kernel) *kernel = c->last_kernel;
-    if (R) *R = c->last_R;
-    if (W) *W = c->last_W;
+    int k = 0;
+    if (c->nvar == 2) {   // T16 and int32 were both enqueued: the device's choice decides
+        SA_HIP(c, hipEventSynchronize(c->ev_sel));
+        k = *c->h_sel == 1 ? 0 : 1;
+    }
+    if (kernel) *kernel = c->var_kernel[k];
+    if (R) *R = c->var_R[k];
+    if (W) *W = c->var_W[k];
     return SA_OK;
 }
 
 int sa_plan_query(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, int* R, int* W,
                   uint64_t* dir_bytes, uint64_t* rowbuf_bytes) {
     if (algo < SA_SW || algo > SA_GLOBAL_GOTOH) return fail(nullptr, SA_ERR_ARG, "unknown algorithm");
-    const Plan p = make_plan(algo, max_m, max_n, npairs);
+    const Plan p = make_plan(algo, max_m, max_n, npairs, false);
     if (R) *R = p.R;
     if (W) *W = p.W;
     if (dir_bytes) *dir_bytes = p.g.dir_slot;
     if (rowbuf_bytes) *rowbuf_bytes = p.rowbuf_elems * 4;
+    return SA_OK;
+}
+
+int sa_plan_query_ex(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n, uint32_t npairs,
+                     int nsym, int* kernel, int* R, int* W, uint64_t* ws_bytes_per_pair) {
+    if (algo < SA_SW || algo > SA_GLOBAL_GOTOH) return fail(nullptr, SA_ERR_ARG, "unknown algorithm");
+    if (!sc) return fail(nullptr, SA_ERR_ARG, "scoring is NULL");
+    const bool cand = t16_candidate(algo, sc, max_m, max_n);
+    const Variant v16 = make_variant(algo, max_m, max_n, npairs, true, true);
+    const Variant v32 = make_variant(algo, max_m, max_n, npairs, false, true);
+    const Variant& v = (cand && nsym <= 4) ? v16 : v32;
+    if (kernel) *kernel = v.kernel;
+    if (R) *R = v.pl.R;
+    if (W) *W = v.pl.split ? 0 : v.pl.W;
+    // what a call allocates: both variants are enqueued when the scoring admits T16
+    if (ws_bytes_per_pair) *ws_bytes_per_pair = cand ? std::max(v16.slot_bytes, v32.slot_bytes) : v32.slot_bytes;
     return SA_OK;
 }
 

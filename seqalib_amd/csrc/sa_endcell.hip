@@ -27,9 +27,11 @@ __device__ __forceinline__ uint32_t ec_code8(uint32_t sp, uint32_t b) {
 
 template <int R>
 __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
+    if (sa_skip(P.sel, P.sel_want)) return;
     const int lane = threadIdx.x;
     const uint32_t slot = blockIdx.x;
     if (slot >= P.count) return;
+    const uint32_t symp = P.prof[4];
     const uint32_t pidx = P.pair_base + slot;
     sa_result res = P.res[pidx];
     if (res.reserved == 0 || (res.flags & SA_FLAG_BAD_SHAPE)) return;   // uniform over the wave
@@ -60,7 +62,7 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int row = row0 + r;
-        tab[r] = row < m ? P.prof[ec_code8(P.sym_pack, s1[row]) >> 3] : 0u;
+        tab[r] = row < m ? P.prof[ec_code8(symp, s1[row]) >> 3] : 0u;
     }
     const uint32_t rs = P.rowbuf_stride;
     const int32_t* top = b > 0 ? P.rowbuf + (uint64_t)slot * P.rowbuf_slot + (uint64_t)(b - 1) * P.max_n * rs : nullptr;
@@ -90,7 +92,7 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
             int up_h = __shfl_up(hl, 1);
             if (lane == 0) up_h = (top && s < n) ? (top[(uint64_t)s * rs] >> 2) : 0;
             if (j0 >= 0 && j0 < n) {
-                const uint32_t sym = ec_code8(P.sym_pack, s2[j0]);
+                const uint32_t sym = ec_code8(symp, s2[j0]);
                 int hd = prev_up, hu = up_h;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
@@ -127,6 +129,7 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
 // row-major maximum; global modes: H[m][n] from the band holding row m.  One thread per pair.
 template <int ALG>
 __global__ void split_reduce_kernel(SplitReduceParams P) {
+    if (sa_skip(P.sel, P.sel_want)) return;
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     if (slot >= P.count) return;
     const uint32_t pidx = P.pair_base + slot;

@@ -120,9 +120,11 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     __shared__ int s_red[16 * 3];
     __shared__ int s_score;   // H[m][n] for the global modes, stored by the owning lane
 
+    if (sa_skip(P.sel, P.sel_want)) return;   // the batch selected the other kernel variant
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
     const int W = P.waves;
+    const uint32_t symp = T16 ? P.prof[4] : 0u;   // T16: the symbols of codes 0..3
     // SPLIT (few pairs): one single-wave workgroup per (pair, band).  Bands are handed out by a
     // ticket counter in the order workgroups actually start, so band b's producer (ticket - 1)
     // is always already running or done: no wait can deadlock whatever the residency.
@@ -161,7 +163,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     }
     if (P.stage_seq2) {
         for (int k = threadIdx.x; k < n; k += blockDim.x)
-            s_seq2[k] = T16 ? (uint8_t)t16_code8(P.sym_pack, s2[k]) : s2[k];
+            s_seq2[k] = T16 ? (uint8_t)t16_code8(symp, s2[k]) : s2[k];
     }
     __syncthreads();
     const int G = P.gap, MA = P.match, MI = P.mismatch;
@@ -433,7 +435,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
         vh = 0; vx = -10000; vs = 0;
         if (lane < kChunk && c < n) {
             if (P.stage_seq2) vs = (int)s_seq2[c];
-            else vs = T16 ? (int)t16_code8(P.sym_pack, s2[c]) : (int)s2[c];
+            else vs = T16 ? (int)t16_code8(symp, s2[c]) : (int)s2[c];
             if (band == 0) {
                 const int J = c + 1;
                 if constexpr (ALG == SA_NW) vh = SC * J * G;
@@ -487,7 +489,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                         const int row = row0 + r;
                         // CMAX: rows past m get substitution -128 (with gap < 0 their values stay
                         // below the matrix maximum, so they never win the lane's chunk maximum)
-                        if constexpr (T16) a[r] = row < m ? (int)P.prof[t16_code8(P.sym_pack, s1[row]) >> 3] : (CMAX ? (int)0x80808080u : 0);
+                        if constexpr (T16) a[r] = row < m ? (int)P.prof[t16_code8(symp, s1[row]) >> 3] : (CMAX ? (int)0x80808080u : 0);
                         else a[r] = row < m ? (int)s1[row] : 0;
                         const int i = row + 1;
                         if constexpr (ALG == SA_NW) Hp[r] = SC * i * G;

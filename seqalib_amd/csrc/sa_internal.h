@@ -25,10 +25,13 @@ struct FillParams {
     int32_t gap, match, mismatch, gap_open, gap_extend;
     int waves;                 // waves per workgroup (blockDim.x / 64)
     int stage_seq2;            // 1: Seq2 of the pair is copied to LDS (max_n <= kMaxStagedSeq2)
-    // T16 kernel only: the batch alphabet is <= 4 symbols (bytes of sym_pack = code 0..3) and
-    // prof[c] holds, in byte c', the tagged substitution term 4*s(sym c, sym c') + 3 as int8.
+    // T16 kernel only: the batch alphabet is <= 4 symbols, prof[4] = sym_pack (byte c = the
+    // symbol of code c) and prof[c] holds, in byte c', the tagged substitution term
+    // 4*s(sym c, sym c') + 3 as int8 (written on the device by decide_t16, sa_alphabet.hip).
     const uint32_t* prof;
-    uint32_t sym_pack;
+    // device-side kernel selection: the launch runs only if *sel == sel_want (sel NULL: always)
+    const uint32_t* sel;
+    uint32_t sel_want;
     // CMAX only (see sa_fill_impl.h): per-slot snapshots [band][chunk][lane] of the R 16-bit row
     // values (R/2 words) and of the diagonal input (1 word); snap_nch = chunks per band.
     uint32_t* snap_h;
@@ -56,6 +59,8 @@ struct SplitReduceParams {
     uint32_t max_m, max_n;
     int32_t gap, gap_open, gap_extend;
     int cmax;
+    const uint32_t* sel;
+    uint32_t sel_want;
 };
 hipError_t launch_split_reduce(int algo, const SplitReduceParams& p, hipStream_t stream);
 
@@ -65,8 +70,9 @@ struct EndcellParams {
     const uint64_t* off1;
     const uint8_t* seq2;
     const uint64_t* off2;
-    const uint32_t* prof;
-    uint32_t sym_pack;
+    const uint32_t* prof;      // as FillParams::prof (prof[4] = sym_pack)
+    const uint32_t* sel;
+    uint32_t sel_want;
     const uint32_t* snap_h;
     const int32_t* snap_p;
     const int32_t* snap_m;
@@ -96,6 +102,8 @@ struct TbParams {
     int32_t gap, match, mismatch, gap_open, gap_extend;
     int allow;
     int tagged;                // records hold T16 max tags (sa_layout.h)
+    const uint32_t* sel;
+    uint32_t sel_want;
 };
 // SA_FLAG_TIMEOUT: a SPLIT band's bounded wait for its producer expired (results invalid)
 
@@ -112,11 +120,19 @@ hipError_t launch_fill_nw(const FillVariant& v, const FillParams& p, uint32_t gr
 hipError_t launch_fill_lg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_fill_gg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
 // Batch alphabet scan (presence bitmap of every byte of both sequence sets, 8 words) and the
-// T16 substitution profile.
+// device-side T16 decision.  aux layout (kAux* below): [bitmap 8][profile 4][sym_pack][sel].
+constexpr int kAuxProf = 8, kAuxSel = 13, kAuxWords = 64;
 hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uint8_t* d2,
-                                const uint64_t* o2, uint32_t npairs, uint32_t* bitmap, hipStream_t s);
-hipError_t launch_build_profile(const uint32_t* lutbits, uint32_t sym_pack, int match, int mismatch,
-                                uint32_t* prof, hipStream_t s);
+                                const uint64_t* o2, uint32_t npairs, uint32_t* aux, hipStream_t s);
+// decide_t16: from the bitmap, aux[kAuxSel] = 1 if the batch has <= 4 distinct symbols (then the
+// profile and sym_pack are written), else 0.
+hipError_t launch_decide_t16(const uint32_t* lutbits, int match, int mismatch, uint32_t* aux, hipStream_t s);
+
+// Device-side kernel selection: a launch whose variant the batch did not select returns at once
+// (uniform over the grid; sel NULL = unconditional).
+__device__ __forceinline__ bool sa_skip(const uint32_t* sel, uint32_t want) {
+    return sel != nullptr && *sel != want;
+}
 hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
 // One wave per pair (sa_traceback_wave.hip): the few-pairs traceback.
 hipError_t launch_traceback_wave(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);

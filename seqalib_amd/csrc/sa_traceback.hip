@@ -72,6 +72,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
     constexpr int kTbGroups = 32 / SPP;
     static_assert(kTbLanes * kTbGroups <= kTbChunks, "flag window <= 32 packets");
     __shared__ __attribute__((aligned(16))) uint8_t s_tb[kTbLdsBytes];
+    if (sa_skip(P.sel, P.sel_want)) return;   // the batch selected the other kernel variant
     const int lane = threadIdx.x;
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     if (slot >= P.count) return;

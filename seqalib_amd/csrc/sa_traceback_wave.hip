@@ -118,6 +118,7 @@ __global__ __launch_bounds__(64) void traceback_wave_kernel(TbParams P) {
     constexpr bool AFF = is_affine(ALG);
     constexpr uint32_t FD = AFF ? 8u : 2u;                               // fD bit of a cell byte
     __shared__ __attribute__((aligned(16))) uint8_t s_win[kTwD * kTwP];
+    if (sa_skip(P.sel, P.sel_want)) return;   // the batch selected the other kernel variant
     __shared__ __attribute__((aligned(16))) uint8_t s_seq1[kTwS1];
     __shared__ __attribute__((aligned(16))) uint8_t s_seq2[kTwS2];
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];

@@ -74,10 +74,45 @@ def test_plan_and_layout(algo, shape):
 
 
 def test_headline_plan_fits_hbm():
-    # north-star batch: 10,000 pairs of 4096 x 4096 SW in one launch on a 288 GB MI355X
-    R, W, dir_bytes, row_bytes = sa.plan_query(0, 4096, 4096, 10000)
-    assert (R, W) == (16, 4)
+    # north-star batch: 10,000 pairs of 4096 x 4096 SW (DNA, default scoring).  The shipped plan is
+    # the T16 end-cell kernel, one wave per pair, R = 32; the int32 plan is the fallback.
+    sw = sa.ScoringSystem(-1, 1, -1)
+    kernel, R, W, ws = sa.plan_query_ex(0, sw, 4096, 4096, 10000, nsym=4)
+    assert (kernel, R, W) == (sa.SA_KERNEL_T16_ENDCELL, 32, 1)
+    # both variants are provisioned (the choice is made on the device): dirs + row buffers +
+    # snapshots of the larger one; the pipelined context keeps two slots per pair of a launch
+    steps_pad = -(-(4096 + 63) // 32) * 32
+    t16_dirs = 2 * steps_pad * 64 * 8
+    assert ws >= t16_dirs
+    assert 2 * 10000 * ws + 2 * 4096 < 0.5 * 288e9, ws   # one launch, both slots, well inside HBM
+    R32, W32, dir_bytes, row_bytes = sa.plan_query(0, 4096, 4096, 10000)
+    assert (R32, W32) == (16, 4)
     assert 10000 * (dir_bytes + row_bytes) < 64e9
+    # more than four symbols: the int32 kernel
+    assert sa.plan_query_ex(0, sw, 4096, 4096, 10000, nsym=5)[:3] == (sa.SA_KERNEL_INT32, 16, 4)
+
+
+@pytest.mark.parametrize("m,n,npairs,plan", [
+    (1024, 1024, 10000, (sa.SA_KERNEL_T16_ENDCELL, 16, 1)),    # config 3
+    (2048, 2048, 12500, (sa.SA_KERNEL_T16_ENDCELL, 32, 1)),    # config 5 shard (1 of 8 GPUs)
+    (4096, 4096, 1, None),                                      # config 2: few pairs
+])
+def test_config_plans(m, n, npairs, plan):
+    sw = sa.ScoringSystem(-1, 1, -1)
+    got = sa.plan_query_ex(0, sw, m, n, npairs, nsym=4)
+    if plan is not None:
+        assert got[:3] == plan
+    assert got[3] * npairs * 2 < 0.5 * 288e9
+
+
+def test_plan_t16_eligibility_by_scoring():
+    # NW at its default scoring (-1, 2, -1) on 4096^2: 4 * 2 * 4096 + 3 > 32767 -> int32
+    assert sa.plan_query_ex(1, sa.ScoringSystem(-1, 2, -1), 4096, 4096, 10000)[0] == sa.SA_KERNEL_INT32
+    assert sa.plan_query_ex(1, sa.ScoringSystem(-1, 1, -1), 4096, 4096, 10000)[0] == sa.SA_KERNEL_T16
+    # gap 0: the clamped up term needs gap < 0
+    assert sa.plan_query_ex(0, sa.ScoringSystem(0, 1, -1), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32
+    # affine: int32 flags
+    assert sa.plan_query_ex(2, sa.ScoringSystem(-3, -1, 1, -1), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32
 
 
 def cell_byte(R, bpc, max_n, i, j, tagged=False):

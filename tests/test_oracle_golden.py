@@ -67,3 +67,45 @@ def test_oracle_random():
 @pytest.mark.parametrize("e", BIG, ids=[e["id"] for e in BIG])
 def test_oracle_large(e):
     check(e)
+
+
+def _sw_equal_entries():
+    return [e for e in KAT + RND + BIG if e["algo"] == "sw" and e["match"] in ("equal", None)]
+
+
+def test_oracle_sw_score_batch_vs_golden():
+    """The linear-space SW score/end-cell oracle (used to check whole north-star batches) against
+    every SW golden vector with byte equality, batched as the GPU tests batch it."""
+    import numpy as np
+    from util import oracle_sw_scores, pack_bytes
+    groups = {}
+    for e in _sw_equal_entries():
+        groups.setdefault(tuple(e["scoring"]), []).append(e)
+    n = 0
+    for args, es in groups.items():
+        pairs = [golden_sequences(e) for e in es]
+        s1, o1, s2, o2 = pack_bytes(pairs)
+        out = oracle_sw_scores(args, s1, o1, s2, o2, threads=4)
+        for e, row in zip(es, out):
+            exp_score = e["score"] if e["m"] and e["n"] else -(2 ** 31)
+            assert (int(row[0]), int(row[1]), int(row[2])) == (exp_score, e["max_row"], e["max_col"]), e["id"]
+            n += 1
+    assert n > 200
+
+
+def test_oracle_batch_matches_single():
+    """oracle_batch (threaded, packed) returns exactly what oracle_align returns per pair."""
+    import numpy as np
+    from util import oracle_batch, pack_bytes
+    import seqalib_amd as sa
+    pairs = [(sa.synth_dna(40 + k, 50 + 13 * k), sa.synth_mutate(sa.synth_dna(40 + k, 50 + 13 * k), k))
+             for k in range(24)] + [(b"", b"ACGT"), (b"A", b"")]
+    for algo, args in ((0, (-1, 1, -1)), (1, (-1, 2, -1)), (2, (-3, -1, 1, -1)), (3, (-3, -1, 1, -1))):
+        s1, o1, s2, o2 = pack_bytes(pairs)
+        res, ops = oracle_batch(algo, args, s1, o1, s2, o2, threads=3)
+        for p, (a, b) in enumerate(pairs):
+            o = oracle_align(algo, args, a, b)
+            off = int(o1[p] + o2[p]) + p
+            got = (int(res["score"][p]), int(res["end_i"][p]), int(res["end_j"][p]), int(res["start_i"][p]),
+                   int(res["start_j"][p]), ops[off:off + int(res["nops"][p])].tobytes())
+            assert got == (o["score"], o["end_i"], o["end_j"], o["start_i"], o["start_j"], o["ops"]), (algo, p)

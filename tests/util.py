@@ -131,6 +131,10 @@ def oracle_lib():
         L.oracle_align.restype = C.c_int
         L.oracle_sw_batch.argtypes = [C.POINTER(OracleScoring), vp, vp, vp, vp, C.c_int, C.c_int, vp]
         L.oracle_sw_batch.restype = C.c_int
+        L.oracle_batch.argtypes = [C.c_int, C.POINTER(OracleScoring), vp, vp, vp, vp, C.c_int, C.c_int, vp, vp]
+        L.oracle_batch.restype = C.c_int
+        L.oracle_sw_score_batch.argtypes = [C.POINTER(OracleScoring), vp, vp, vp, vp, C.c_int, C.c_int, vp]
+        L.oracle_sw_score_batch.restype = C.c_int
         _oracle = L
     return _oracle
 
@@ -169,6 +173,88 @@ def oracle_align(algo: int, args, s1: bytes, s2: bytes, lut: Optional[np.ndarray
     return dict(rc=rc, score=res.score, end_i=res.end_i, end_j=res.end_j, start_i=res.start_i,
                 start_j=res.start_j, ops=ops.raw[: res.nops],
                 rows=(r0.raw[:k].decode("latin-1"), bars.raw[:k].decode("latin-1"), r1.raw[:k].decode("latin-1")))
+
+
+ORACLE_RESULT_DTYPE = np.dtype([("score", "<i4"), ("end_i", "<i4"), ("end_j", "<i4"), ("start_i", "<i4"),
+                                 ("start_j", "<i4"), ("nops", "<i4"), ("len", "<i4")])
+
+
+def _oracle_sc(args):
+    g, ma, mi, go, ge, al = scoring_fields(args)
+    if not al:
+        mi = -(2 ** 31)
+    return OracleScoring(g, ma, mi, go, ge, al)
+
+
+def oracle_batch(algo: int, args, s1, o1, s2, o2, threads: int = 16):
+    """Full oracle results (ORACLE_RESULT_DTYPE) and op streams (pair p at o1[p]+o2[p]+p) of a
+    packed batch, byte-equality match fn, on `threads` host threads."""
+    L = oracle_lib()
+    n = len(o1) - 1
+    s1 = np.ascontiguousarray(s1, dtype=np.uint8)
+    s2 = np.ascontiguousarray(s2, dtype=np.uint8)
+    o1 = np.ascontiguousarray(o1, dtype=np.uint64)
+    o2 = np.ascontiguousarray(o2, dtype=np.uint64)
+    res = np.zeros(n, dtype=ORACLE_RESULT_DTYPE)
+    ops = np.zeros(int(o1[-1] + o2[-1]) + n + 1, dtype=np.uint8)
+    sc = _oracle_sc(args)
+    rc = L.oracle_batch(algo, C.byref(sc), s1.ctypes.data, o1.ctypes.data, s2.ctypes.data, o2.ctypes.data, n,
+                        threads, res.ctypes.data, ops.ctypes.data)
+    assert rc == 0, rc
+    return res, ops
+
+
+def oracle_sw_scores(args, s1, o1, s2, o2, threads: int = 16):
+    """(MaxScore, MaxRow, MaxCol) per pair of a packed SW batch, linear-space oracle: (n, 3) int32."""
+    L = oracle_lib()
+    n = len(o1) - 1
+    s1 = np.ascontiguousarray(s1, dtype=np.uint8)
+    s2 = np.ascontiguousarray(s2, dtype=np.uint8)
+    o1 = np.ascontiguousarray(o1, dtype=np.uint64)
+    o2 = np.ascontiguousarray(o2, dtype=np.uint64)
+    out = np.zeros((n, 3), dtype=np.int32)
+    sc = _oracle_sc(args)
+    rc = L.oracle_sw_score_batch(C.byref(sc), s1.ctypes.data, o1.ctypes.data, s2.ctypes.data, o2.ctypes.data,
+                                 n, threads, out.ctypes.data)
+    assert rc == 0, rc
+    return out
+
+
+def pack_bytes(pairs):
+    """Packed batch (s1, o1, s2, o2) of (bytes, bytes) pairs, no library needed."""
+    o1 = np.zeros(len(pairs) + 1, dtype=np.uint64)
+    o2 = np.zeros(len(pairs) + 1, dtype=np.uint64)
+    o1[1:] = np.cumsum([len(a) for a, _ in pairs])
+    o2[1:] = np.cumsum([len(b) for _, b in pairs])
+    s1 = np.frombuffer(b"".join(a for a, _ in pairs) + b"\0", dtype=np.uint8)[:-1].copy()
+    s2 = np.frombuffer(b"".join(b for _, b in pairs) + b"\0", dtype=np.uint8)[:-1].copy()
+    return s1, o1, s2, o2
+
+
+def subset(s1, o1, s2, o2, idx):
+    """Pack pairs idx of a packed batch into a new packed batch."""
+    a = [s1[int(o1[p]):int(o1[p + 1])] for p in idx]
+    b = [s2[int(o2[p]):int(o2[p + 1])] for p in idx]
+    ro1 = np.zeros(len(idx) + 1, dtype=np.uint64)
+    ro2 = np.zeros(len(idx) + 1, dtype=np.uint64)
+    ro1[1:] = np.cumsum([len(x) for x in a])
+    ro2[1:] = np.cumsum([len(x) for x in b])
+    cat = lambda xs: np.concatenate(xs).astype(np.uint8) if xs else np.zeros(0, np.uint8)
+    return cat(a), ro1, cat(b), ro2
+
+
+def linear_rescore(args, res, ops, o1, o2):
+    """Vectorised re-score of every emitted linear-gap alignment: #M*match + #S*mismatch +
+    (#U + #L)*gap per pair (ops of pair p at o1[p]+o2[p]+p, res['nops'][p] of them)."""
+    g, ma, mi, _, _, _ = scoring_fields(args)
+    val = np.zeros(256, dtype=np.int64)
+    val[ord("M")], val[ord("S")], val[ord("U")], val[ord("L")] = ma, mi, g, g
+    n = len(res)
+    starts = (o1[:n].astype(np.int64) + o2[:n].astype(np.int64) + np.arange(n))
+    nops = res["nops"].astype(np.int64)
+    contrib = val[ops.astype(np.int64)]
+    csum = np.concatenate([[0], np.cumsum(contrib)])
+    return csum[starts + nops] - csum[starts]
 
 
 # ------------------------------------------------------------------------------ fixtures
