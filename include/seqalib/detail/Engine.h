@@ -63,15 +63,19 @@ inline void check(int rc, const char* what) {
 }
 
 // Maps symbols of type Ty onto byte codes.  Single-byte integral types are their own code; other
-// types get codes in order of first appearance (at most 256 distinct symbols per batch).
+// types get codes in order of first appearance, at most 256 distinct symbols per batch -- a batch
+// with more goes through the match-bitmap path instead (align_bits below).
 template <typename Ty, bool Direct = (std::is_integral<Ty>::value && sizeof(Ty) == 1)>
 struct SymbolCoder {
     std::vector<Ty> values;
+    bool overflow = false;
     uint8_t code(const Ty& v) {
         for (size_t k = 0; k < values.size(); ++k)
             if (values[k] == v) return (uint8_t)k;
-        if (values.size() == 256)
-            throw std::runtime_error("seqalib: more than 256 distinct symbols in one batch");
+        if (values.size() == 256) {
+            overflow = true;
+            return 0;
+        }
         values.push_back(v);
         return (uint8_t)(values.size() - 1);
     }
@@ -82,6 +86,7 @@ struct SymbolCoder {
 
 template <typename Ty>
 struct SymbolCoder<Ty, true> {
+    bool overflow = false;
     bool seen[256] = {};
     uint8_t code(const Ty& v) {
         const uint8_t c = (uint8_t)v;
@@ -111,6 +116,51 @@ std::vector<uint8_t> build_lut(SymbolCoder<Ty, Direct>& coder, MatchFnTy& fn) {
     return lut;
 }
 
+// Generic-Ty path: per-pair m x n match bitmaps, built exactly as the reference's
+// cacheAllMatches builds its match cache (one MatchFnTy call per cell, e.g. SASmithWaterman.h:
+// 20-45; the == operator for a nullptr match fn), packed to bits for sa_align_batch_bits.
+template <typename Ty, typename ContainerType, typename MatchFnTy>
+void align_bits(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
+                const std::vector<std::pair<ContainerType*, ContainerType*>>& pairs, std::vector<sa_result>& res,
+                std::vector<uint8_t>& ops, std::vector<uint64_t>& ops_off) {
+    PhaseTimer tm;
+    const uint32_t np = (uint32_t)pairs.size();
+    std::vector<uint64_t> o1(1, 0), o2(1, 0), bo(1, 0);
+    for (auto& p : pairs) {
+        const uint64_t m = (uint64_t)p.first->size(), n = (uint64_t)p.second->size();
+        o1.push_back(o1.back() + m);
+        o2.push_back(o2.back() + n);
+        bo.push_back(bo.back() + m * ((n + 31) / 32));
+    }
+    std::vector<uint32_t> bits(bo.back() + 1, 0u);
+    for (uint32_t q = 0; q < np; ++q) {
+        ContainerType& a = *pairs[q].first;
+        ContainerType& b = *pairs[q].second;
+        const size_t m = (size_t)a.size(), n = (size_t)b.size(), wn = (n + 31) / 32;
+        uint32_t* w = bits.data() + bo[q];
+        for (size_t i = 0; i < m; ++i)
+            for (size_t j = 0; j < n; ++j) {
+                bool v;
+                if constexpr (std::is_same<MatchFnTy, std::nullptr_t>::value) v = a[i] == b[j];
+                else v = has_fn ? (bool)fn(a[i], b[j]) : (a[i] == b[j]);
+                if (v) w[i * wn + j / 32] |= 1u << (j % 32);
+            }
+    }
+    tm.lap("match bitmaps");
+    res.assign(np, sa_result{});
+    const uint64_t cap = o1.back() + o2.back() + np + 1;
+    ops.resize(cap);
+    ops_off.resize(np);
+    for (uint32_t p = 0; p < np; ++p) ops_off[p] = o1[p] + o2[p] + p;
+    check(sa_align_batch_bits(context(), algo, &sc, o1.data(), o2.data(), np, bits.data(), bo.data(), res.data(),
+                              ops.data(), cap),
+          "sa_align_batch_bits");
+    tm.lap("sa_align_batch_bits (GPU)");
+    for (auto& r : res)
+        if (r.flags & SA_FLAG_DIVERGED)
+            throw std::runtime_error("seqalib: the reference traceback does not terminate for this scoring");
+}
+
 // Aligns a batch of (Seq1, Seq2) pairs on the GPU.  Returns the per-pair results and the op
 // streams (traceback order).  has_fn = false means the reference's nullptr match fn (equality).
 template <typename Ty, typename ContainerType, typename MatchFnTy>
@@ -134,8 +184,15 @@ void align(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
         uint8_t* d2 = s2.data() + o2[q];
         for (size_t k = 0; k < (size_t)a.size(); ++k) d1[k] = coder.code(a[k]);
         for (size_t k = 0; k < (size_t)b.size(); ++k) d2[k] = coder.code(b[k]);
+        if (coder.overflow) break;
     }
     tm.lap("symbol coding");
+    if (coder.overflow) {   // more than 256 distinct symbols: the generic-Ty (bitmap) path
+        if (algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER)
+            throw std::runtime_error("seqalib: more than 256 distinct symbols: not supported by the linear-space aligners");
+        align_bits<Ty>(algo, sc, fn, has_fn, pairs, res, ops, ops_off);
+        return;
+    }
     std::vector<uint8_t> lut;
     if (has_fn) lut = build_lut(coder, fn);
     const uint32_t n = (uint32_t)pairs.size();

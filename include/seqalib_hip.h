@@ -136,6 +136,19 @@ int sa_align_batch(sa_ctx* ctx, int algo, const sa_scoring* scoring,
                    const uint8_t* seq2, const uint64_t* seq2_off, uint32_t npairs,
                    const uint8_t* match_lut, sa_result* results, uint8_t* ops, uint64_t ops_cap);
 
+/* Generic-Ty batch API (any symbol type, any number of distinct symbols: the path the C++
+ * drop-in takes when a batch has more than 256 distinct symbols).  Instead of symbols the caller
+ * passes each pair's match matrix -- the reference's cacheAllMatches (e.g. SASmithWaterman.h:
+ * 20-45) packed to bits: pair p's bitmap starts at word bits_off[p] of `match_bits`, row-major,
+ * ceil(n/32) 32-bit words per row, bit (j % 32) of word [i * ceil(n/32) + j / 32] =
+ * match(Seq1[i], Seq2[j]).  seq*_off are the npairs+1 length offsets of the sequences (they
+ * size the ops as in sa_align_batch); bits_off has npairs+1 entries.  SW, NW, LocalGotoh (with
+ * the size hack) and GlobalGotoh; results and ops exactly as sa_align_batch.  Blocking. */
+int sa_align_batch_bits(sa_ctx* ctx, int algo, const sa_scoring* scoring,
+                        const uint64_t* seq1_off, const uint64_t* seq2_off, uint32_t npairs,
+                        const uint32_t* match_bits, const uint64_t* bits_off,
+                        sa_result* results, uint8_t* ops, uint64_t ops_cap);
+
 /* Device-resident batch API: every pointer is device memory (HBM) and the work is enqueued on
  * `stream` (a hipStream_t; NULL = the context's own stream).  Asynchronous: returns after
  * enqueueing.  max_m/max_n must bound every pair's lengths (pairs that exceed them are skipped

@@ -725,3 +725,29 @@ int oracle_sw_score_batch(const oracle_scoring* sc, const uint8_t* s1cat, const 
     pthread_mutex_destroy(&J.mu);
     return 0;
 }
+
+/* Generic-Ty form (test infrastructure): the same aligners driven by a caller-supplied m x n
+ * match matrix (mt[i*n + j] != 0 iff match(Seq1[i], Seq2[j]), the reference's cacheAllMatches)
+ * instead of byte symbols; results and op stream only.  SW, NW, LocalGotoh (size hack included),
+ * GlobalGotoh. */
+int oracle_align_matrix(int algo, const oracle_scoring* sc, int m, int n, const uint8_t* mt_in,
+                        oracle_result* res, uint8_t* ops, int ops_cap) {
+    if (algo == OR_LOCAL_GOTOH && lg_size_hack(m, n)) algo = OR_NW;
+    if (algo == OR_HIRSCHBERG || algo == OR_MYERS_MILLER) return -3;
+    uint8_t* mt = (uint8_t*)malloc((size_t)m * (size_t)n + 1);
+    if (!mt) return -2;
+    for (size_t k = 0; k < (size_t)m * (size_t)n; ++k) mt[k] = mt_in[k] != 0;
+    opbuf ob = {ops, ops_cap, 0, 0};
+    memset(res, 0, sizeof(*res));
+    int rc;
+    switch (algo) {
+        case OR_SW: rc = align_sw(sc, NULL, m, NULL, n, mt, res, &ob); break;
+        case OR_NW: rc = align_nw(sc, NULL, m, NULL, n, mt, res, &ob); break;
+        case OR_LOCAL_GOTOH: rc = align_gotoh(1, sc, m, n, mt, res, &ob); break;
+        default: rc = align_gotoh(0, sc, m, n, mt, res, &ob); break;
+    }
+    free(mt);
+    res->nops = ob.n;
+    if (rc) return rc;
+    return ob.overflow ? -1 : 0;
+}

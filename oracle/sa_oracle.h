@@ -63,6 +63,8 @@ int oracle_batch(int algo, const oracle_scoring* sc, const uint8_t* s1cat, const
 int oracle_sw_score_batch(const oracle_scoring* sc, const uint8_t* s1cat, const uint64_t* off1,
                           const uint8_t* s2cat, const uint64_t* off2, int npairs, int threads,
                           int32_t* out);
+int oracle_align_matrix(int algo, const oracle_scoring* sc, int m, int n, const uint8_t* mt,
+                        oracle_result* res, uint8_t* ops, int ops_cap);
 int oracle_sw_batch(const oracle_scoring* sc, const uint8_t* s1cat, const uint64_t* off1,
                     const uint8_t* s2cat, const uint64_t* off2, int npairs, int threads,
                     int32_t* out_score);

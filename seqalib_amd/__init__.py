@@ -112,6 +112,8 @@ def load_library():
     L.sa_trim.argtypes = [vp]
     L.sa_align_batch.argtypes = [vp, C.c_int, C.POINTER(_Scoring), vp, vp, vp, vp, C.c_uint32, vp, vp, vp,
                                  C.c_uint64]
+    L.sa_align_batch_bits.argtypes = [vp, C.c_int, C.POINTER(_Scoring), vp, vp, C.c_uint32, vp, vp, vp, vp,
+                                      C.c_uint64]
     L.sa_align_batch_device.argtypes = [vp, C.c_int, C.POINTER(_Scoring), vp, vp, vp, vp, C.c_uint32,
                                         C.c_uint32, C.c_uint32, vp, vp, vp, vp]
     L.sa_last_timings.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_float), i32p]
@@ -124,7 +126,7 @@ def load_library():
     L.sa_synth_dna.argtypes = [C.c_uint64, C.c_uint32, vp]
     L.sa_synth_mutate.argtypes = [vp, C.c_uint32, C.c_uint64, vp, C.c_uint32, C.POINTER(C.c_uint32)]
     L.sa_synth_dna_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_int]
-    for fn in ("sa_set_workspace_limit", "sa_trim", "sa_align_batch", "sa_align_batch_device",
+    for fn in ("sa_set_workspace_limit", "sa_trim", "sa_align_batch", "sa_align_batch_bits", "sa_align_batch_device",
                "sa_last_timings", "sa_last_plan", "sa_plan_query", "sa_plan_query_ex", "sa_synth_dna", "sa_synth_mutate", "sa_synth_dna_batch",
                "sa_create", "sa_device_count", "sa_set_pipeline", "sa_wait"):
         getattr(L, fn).restype = C.c_int
@@ -308,6 +310,46 @@ def lut_from_fn(fn: Callable[[str, str], bool], alphabet1: Iterable[int], alphab
     return lut
 
 
+def match_bitmaps(pairs: Sequence[Tuple[Sequence, Sequence]], match: Optional[Callable] = None):
+    """The generic-Ty input of sa_align_batch_bits for pairs of sequences of ANY symbols (lists or
+    tuples of ints, objects, ...): length offsets and per-pair m x n match bitmaps, i.e. the
+    reference's cacheAllMatches (SASmithWaterman.h:20-45) packed to bits.  match(a, b) is the
+    MatchFnTy; None means equality (the reference's nullptr match fn).  Hashable symbols are coded
+    first, so the predicate runs once per distinct (a, b) pair of a pair's sequences."""
+    n_p = len(pairs)
+    off1 = np.zeros(n_p + 1, dtype=np.uint64)
+    off2 = np.zeros(n_p + 1, dtype=np.uint64)
+    bits_off = np.zeros(n_p + 1, dtype=np.uint64)
+    chunks = []
+    for p, (a, b) in enumerate(pairs):
+        m, n = len(a), len(b)
+        off1[p + 1] = off1[p] + m
+        off2[p + 1] = off2[p] + n
+        wn = (n + 31) // 32
+        if m and n:
+            try:
+                ua = {}
+                c1 = np.fromiter((ua.setdefault(x, len(ua)) for x in a), dtype=np.int64, count=m)
+                ub = {}
+                c2 = np.fromiter((ub.setdefault(x, len(ub)) for x in b), dtype=np.int64, count=n)
+                va, vb = list(ua), list(ub)
+                if match is None:
+                    tab = np.array([[x == y for y in vb] for x in va], dtype=bool)
+                else:
+                    tab = np.array([[bool(match(x, y)) for y in vb] for x in va], dtype=bool)
+                mm = tab[c1][:, c2]
+            except TypeError:   # unhashable symbols: evaluate every cell, as the reference does
+                f = (lambda x, y: x == y) if match is None else match
+                mm = np.array([[bool(f(x, y)) for y in b] for x in a], dtype=bool)
+            packed = np.packbits(mm, axis=1, bitorder="little")
+            row = np.zeros((m, 4 * wn), dtype=np.uint8)
+            row[:, :packed.shape[1]] = packed
+            chunks.append(row.reshape(-1).view("<u4"))
+        bits_off[p + 1] = bits_off[p] + m * wn
+    bits = np.concatenate(chunks) if chunks else np.zeros(1, dtype=np.uint32)
+    return off1, off2, np.ascontiguousarray(bits, dtype=np.uint32), bits_off
+
+
 class Engine:
     """One context per GPU (sa_create).  Not thread-safe; use one Engine per host thread."""
 
@@ -359,6 +401,38 @@ class Engine:
                                    npairs, lut_p, _ptr(res), _ptr(ops), ops_cap)
         self._check(rc, "sa_align_batch")
         return res[:npairs], ops
+
+    def align_bits(self, algo: int, scoring: ScoringSystem, off1: np.ndarray, off2: np.ndarray, bits: np.ndarray,
+                   bits_off: np.ndarray):
+        """Generic-Ty batch (sa_align_batch_bits) from match_bitmaps(): (results, ops)."""
+        npairs = len(off1) - 1
+        off1 = np.ascontiguousarray(off1, dtype=np.uint64)
+        off2 = np.ascontiguousarray(off2, dtype=np.uint64)
+        bits = np.ascontiguousarray(bits, dtype=np.uint32)
+        bits_off = np.ascontiguousarray(bits_off, dtype=np.uint64)
+        res = np.zeros(max(npairs, 1), dtype=RESULT_DTYPE)
+        ops_cap = int(off1[-1] + off2[-1]) + npairs + 1
+        ops = np.zeros(ops_cap, dtype=np.uint8)
+        sc = scoring._c()
+        rc = self.L.sa_align_batch_bits(self.h, algo, C.byref(sc), _ptr(off1), _ptr(off2), npairs, _ptr(bits),
+                                        _ptr(bits_off), _ptr(res), _ptr(ops), ops_cap)
+        self._check(rc, "sa_align_batch_bits")
+        return res[:npairs], ops
+
+    def align_generic(self, algo: int, scoring: ScoringSystem, pairs: Sequence[Tuple[Sequence, Sequence]],
+                      match: Optional[Callable] = None) -> List[PairResult]:
+        """Align pairs of sequences of any symbol type with any match predicate (the reference's
+        templated ContainerType / Ty / MatchFnTy): the symbols stay on the host, the GPU gets the
+        match bitmaps.  Expand with expand_ops(algo, a, b, r, blank=...)."""
+        off1, off2, bits, bits_off = match_bitmaps(pairs, match)
+        res, ops = self.align_bits(algo, scoring, off1, off2, bits, bits_off)
+        out = []
+        for p in range(len(pairs)):
+            o = int(off1[p] + off2[p]) + p
+            r = res[p]
+            out.append(PairResult(int(r["score"]), int(r["end_i"]), int(r["end_j"]), int(r["start_i"]),
+                                  int(r["start_j"]), int(r["flags"]), ops[o:o + int(r["nops"])].tobytes()))
+        return out
 
     def align(self, algo: int, scoring: ScoringSystem, pairs: Sequence[Tuple[object, object]],
               lut: Optional[np.ndarray] = None) -> List[PairResult]:

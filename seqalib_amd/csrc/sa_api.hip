@@ -285,13 +285,15 @@ bool t16_candidate(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_
 int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, const uint64_t* o1,
                const uint8_t* d2, const uint64_t* o2, uint32_t npairs, uint32_t max_m,
                uint32_t max_n, const uint32_t* d_lutbits, sa_result* d_res, uint8_t* d_ops,
-               hipStream_t stream, bool pipe = false) {
+               hipStream_t stream, bool pipe = false, const uint32_t* d_mbits = nullptr,
+               const uint64_t* d_mbits_off = nullptr) {
     if (max_m >= (1u << 24) || max_n >= (1u << 24))
         return fail(c, SA_ERR_UNSUPPORTED, "sequence lengths must be < 2^24");
     const bool keyed = keyed_ok(algo, sc, max_m, max_n);
     const bool allow = sc->allow_mismatch != 0;
-    const bool lut = d_lutbits != nullptr;
-    const bool t16 = t16_candidate(algo, sc, max_m, max_n);
+    const bool bits = d_mbits != nullptr;   // generic-Ty path: per-pair match bitmaps
+    const bool lut = !bits && d_lutbits != nullptr;
+    const bool t16 = !bits && t16_candidate(algo, sc, max_m, max_n);
     if (!c->aux) SA_HIP(c, hipMalloc(&c->aux, 2 * kAuxWords * 4));
     if (!c->h_sel) {
         SA_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_sel), 64, hipHostMallocDefault));
@@ -399,7 +401,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             FillParams& fp = fps[k];
             fp = FillParams{};
             fp.seq1 = d1; fp.off1 = o1; fp.seq2 = d2; fp.off2 = o2;
-            fp.lutbits = d_lutbits;
+            fp.lutbits = lut ? d_lutbits : nullptr;
+            fp.mbits = d_mbits; fp.mbits_off = d_mbits_off;
             fp.dirs = dirs; fp.dir_slot = pl.g.dir_slot; fp.band_stride = pl.g.band_stride;
             fp.rowbuf = rowbuf; fp.rowbuf_slot = pl.rowbuf_elems;
             fp.res = d_res;
@@ -418,7 +421,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fp.hand = pl.split ? reinterpret_cast<unsigned long long*>(c->split + 256) : nullptr;
             fp.hand_x_off = pl.split ? hand_x_off : 0;
             fp.part = pl.split ? reinterpret_cast<int32_t*>(c->split + sp_zero) : nullptr;
-            const FillVariant fv = {pl.R, lut, allow, keyed, v.t16, v.cmax, pl.split};
+            const FillVariant fv = {pl.R, lut, allow, keyed, v.t16, v.cmax, pl.split, bits};
             hipError_t e = launch_fill(algo, fv, fp, pl.split ? (uint32_t)(cnt * sp_bands) : cnt, sf);
             if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
             if (pl.split) {
@@ -460,7 +463,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             const Variant& v = vars[k];
             TbParams tp;
             tp.seq1 = d1; tp.off1 = o1; tp.seq2 = d2; tp.off2 = o2;
-            tp.lutbits = d_lutbits;
+            tp.lutbits = lut ? d_lutbits : nullptr;
+            tp.vrec = bits ? 1 : 0;
             tp.dirs = fps[k].dirs; tp.dir_slot = v.pl.g.dir_slot;
             tp.ops = d_ops; tp.res = d_res;
             tp.pair_base = (uint32_t)base; tp.count = cnt;
@@ -494,6 +498,45 @@ bool lut_is_identity(const uint8_t* lut) {
 
 bool lg_size_hack(uint64_t m, uint64_t n) {  // SALocalGotoh.h:484-488
     return (m == 314 && n == 288) || (m == 60 && n == 57) || (m == 61 && n == 58);
+}
+
+// LocalGotoh: the reference replaces three size pairs by StaticFuncs::useNW with the same
+// ScoringSystem (SALocalGotoh.h:484-488).  Split them out, align them with NW, merge back.
+// align_subset(algo, sel, o1, o2, r, op, cap) aligns pairs sel (o1/o2: their packed length
+// offsets) into r / op (op of the q-th selected pair at o1[q] + o2[q] + q).
+template <typename AlignSubset>
+int lg_hack_split(sa_ctx* c, const uint64_t* off1, const uint64_t* off2, uint32_t npairs, sa_result* results,
+                  uint8_t* ops, uint64_t ops_cap, AlignSubset align_subset) {
+    std::vector<uint32_t> hack, keep;
+    for (uint32_t p = 0; p < npairs; ++p)
+        (lg_size_hack(off1[p + 1] - off1[p], off2[p + 1] - off2[p]) ? hack : keep).push_back(p);
+    if (hack.empty()) {
+        std::vector<uint64_t> o1(off1, off1 + npairs + 1), o2(off2, off2 + npairs + 1);
+        return align_subset(SA_LOCAL_GOTOH, keep, o1, o2, results, ops, ops_cap);
+    }
+    const uint64_t ops_total = off1[npairs] + off2[npairs] + npairs;
+    if (ops_cap < ops_total) return fail(c, SA_ERR_CAPACITY, "ops buffer too small");
+    for (int pass = 0; pass < 2; ++pass) {
+        const std::vector<uint32_t>& sel = pass == 0 ? keep : hack;
+        if (sel.empty()) continue;
+        std::vector<uint64_t> o1(1, 0), o2(1, 0);
+        for (uint32_t p : sel) {
+            o1.push_back(o1.back() + off1[p + 1] - off1[p]);
+            o2.push_back(o2.back() + off2[p + 1] - off2[p]);
+        }
+        const uint32_t k = (uint32_t)sel.size();
+        std::vector<sa_result> r(k);
+        std::vector<uint8_t> op(o1.back() + o2.back() + k + 1);
+        const int rc = align_subset(pass == 0 ? SA_LOCAL_GOTOH : SA_NW, sel, o1, o2, r.data(), op.data(), op.size());
+        if (rc) return rc;
+        for (uint32_t q = 0; q < k; ++q) {
+            const uint32_t p = sel[q];
+            results[p] = r[q];
+            if (pass == 1) results[p].flags |= SA_FLAG_SIZE_HACK;
+            memcpy(ops + off1[p] + off2[p] + p, op.data() + o1[q] + o2[q] + q, r[q].nops);
+        }
+    }
+    return SA_OK;
 }
 
 int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, const uint64_t* off1,
@@ -597,6 +640,58 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     return SA_OK;
 }
 
+// Host buffers, generic-Ty path: lengths as offsets, per-pair match bitmaps (sa_align_batch_bits).
+// The kernels read no symbols here (the fill takes match bits from the bitmap and records the
+// match bit of diagonal moves, the traceback takes it from the records), so the device sequence
+// buffers are zero-filled placeholders of the right sizes.
+int align_host_bits(sa_ctx* c, int algo, const sa_scoring* sc, const uint64_t* off1, const uint64_t* off2,
+                    uint32_t npairs, const uint32_t* bits, const uint64_t* bits_off, sa_result* results,
+                    uint8_t* ops, uint64_t ops_cap) {
+    const uint64_t t1 = off1[npairs], t2 = off2[npairs], tw = bits_off[npairs];
+    uint32_t max_m = 0, max_n = 0;
+    for (uint32_t p = 0; p < npairs; ++p) {
+        if (off1[p + 1] < off1[p] || off2[p + 1] < off2[p]) return fail(c, SA_ERR_ARG, "offsets must be non-decreasing");
+        max_m = (uint32_t)std::max<uint64_t>(max_m, off1[p + 1] - off1[p]);
+        max_n = (uint32_t)std::max<uint64_t>(max_n, off2[p + 1] - off2[p]);
+    }
+    const uint64_t ops_total = t1 + t2 + npairs;
+    if (ops_cap < ops_total) return fail(c, SA_ERR_CAPACITY, "ops buffer needs " + std::to_string(ops_total) + " bytes");
+    if (!npairs) return SA_OK;
+    auto al = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
+    const uint64_t b_s = al(std::max(t1, t2) + 1), b_o = al(8ull * (npairs + 1));
+    const uint64_t b_res = al(sizeof(sa_result) * (uint64_t)npairs), b_ops = al(ops_total + 1);
+    const uint64_t b_bits = al(4 * tw + 4);
+    const uint64_t io_need = b_s + 3 * b_o + b_res + b_ops + b_bits;
+    if (c->io_bytes < io_need) {
+        if (c->io) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->io); c->io = nullptr; c->io_bytes = 0; }
+        if (hipMalloc(&c->io, io_need) != hipSuccess) { c->io = nullptr; return fail(c, SA_ERR_NOMEM, "hipMalloc of I/O buffers failed"); }
+        c->io_bytes = io_need;
+    }
+    uint8_t* q = c->io;
+    uint8_t* dseq = q; q += b_s;
+    uint64_t* do1 = reinterpret_cast<uint64_t*>(q); q += b_o;
+    uint64_t* do2 = reinterpret_cast<uint64_t*>(q); q += b_o;
+    uint64_t* dbo = reinterpret_cast<uint64_t*>(q); q += b_o;
+    sa_result* dres = reinterpret_cast<sa_result*>(q); q += b_res;
+    uint8_t* dops = q; q += b_ops;
+    uint32_t* dbits = reinterpret_cast<uint32_t*>(q);
+    hipStream_t st = c->stream;
+    SA_HIP(c, hipMemsetAsync(dseq, 0, std::max(t1, t2) + 1, st));
+    SA_HIP(c, hipMemcpyAsync(do1, off1, 8ull * (npairs + 1), hipMemcpyHostToDevice, st));
+    SA_HIP(c, hipMemcpyAsync(do2, off2, 8ull * (npairs + 1), hipMemcpyHostToDevice, st));
+    SA_HIP(c, hipMemcpyAsync(dbo, bits_off, 8ull * (npairs + 1), hipMemcpyHostToDevice, st));
+    if (tw) SA_HIP(c, hipMemcpyAsync(dbits, bits, 4 * tw, hipMemcpyHostToDevice, st));
+    int rc = run_device(c, algo, sc, dseq, do1, dseq, do2, npairs, max_m, max_n, nullptr, dres, dops, st, false,
+                        dbits, dbo);
+    if (rc) return rc;
+    SA_HIP(c, hipMemcpyAsync(results, dres, sizeof(sa_result) * npairs, hipMemcpyDeviceToHost, st));
+    SA_HIP(c, hipMemcpyAsync(ops, dops, ops_total, hipMemcpyDeviceToHost, st));
+    SA_HIP(c, hipStreamSynchronize(st));
+    for (uint32_t p = 0; p < npairs; ++p)
+        if (results[p].flags & SA_FLAG_TIMEOUT) return fail(c, SA_ERR_HIP, "split-plan band wait timed out");
+    return SA_OK;
+}
+
 }  // namespace
 
 // =============================================================================== C ABI
@@ -694,43 +789,58 @@ int sa_align_batch(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq
     if (off1[0] != 0 || off2[0] != 0) return fail(c, SA_ERR_ARG, "offsets must start at 0");
     SA_HIP(c, hipSetDevice(c->device));
 
-    if (algo != SA_LOCAL_GOTOH) {
+    if (algo != SA_LOCAL_GOTOH)
         return align_host(c, algo, sc, seq1, off1, seq2, off2, npairs, lut, results, ops, ops_cap);
+    return lg_hack_split(c, off1, off2, npairs, results, ops, ops_cap,
+                         [&](int a, const std::vector<uint32_t>& sel, const std::vector<uint64_t>& o1,
+                             const std::vector<uint64_t>& o2, sa_result* r, uint8_t* op, uint64_t cap) {
+                             if (sel.size() == npairs)
+                                 return align_host(c, a, sc, seq1, off1, seq2, off2, npairs, lut, r, op, cap);
+                             std::vector<uint8_t> s1, s2;
+                             s1.reserve(o1.back());
+                             s2.reserve(o2.back());
+                             for (uint32_t p : sel) {
+                                 s1.insert(s1.end(), seq1 + off1[p], seq1 + off1[p + 1]);
+                                 s2.insert(s2.end(), seq2 + off2[p], seq2 + off2[p + 1]);
+                             }
+                             return align_host(c, a, sc, s1.data(), o1.data(), s2.data(), o2.data(),
+                                               (uint32_t)sel.size(), lut, r, op, cap);
+                         });
+}
+
+int sa_align_batch_bits(sa_ctx* c, int algo, const sa_scoring* sc, const uint64_t* off1, const uint64_t* off2,
+                        uint32_t npairs, const uint32_t* bits, const uint64_t* bits_off, sa_result* results,
+                        uint8_t* ops, uint64_t ops_cap) {
+    if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
+    int rc = validate_scoring(c, algo, sc);
+    if (rc) return rc;
+    if (algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER)
+        return fail(c, SA_ERR_UNSUPPORTED, "match bitmaps: SW, NW, LocalGotoh and GlobalGotoh only");
+    if (!off1 || !off2 || !bits_off || (npairs && (!results || !ops))) return fail(c, SA_ERR_ARG, "NULL buffer");
+    if (off1[0] != 0 || off2[0] != 0) return fail(c, SA_ERR_ARG, "offsets must start at 0");
+    for (uint32_t p = 0; p < npairs; ++p) {
+        const uint64_t m = off1[p + 1] - off1[p], n = off2[p + 1] - off2[p];
+        if (bits_off[p + 1] < bits_off[p] || bits_off[p + 1] - bits_off[p] < m * ((n + 31) / 32))
+            return fail(c, SA_ERR_ARG, "bits_off: pair " + std::to_string(p) + " needs m * ceil(n/32) words");
     }
-    // LocalGotoh: the reference replaces three size pairs by StaticFuncs::useNW with the same
-    // ScoringSystem (SALocalGotoh.h:484-488).  Split them out, align them with NW, merge back.
-    std::vector<uint32_t> hack, keep;
-    for (uint32_t p = 0; p < npairs; ++p)
-        (lg_size_hack(off1[p + 1] - off1[p], off2[p + 1] - off2[p]) ? hack : keep).push_back(p);
-    if (hack.empty())
-        return align_host(c, algo, sc, seq1, off1, seq2, off2, npairs, lut, results, ops, ops_cap);
-    const uint64_t ops_total = off1[npairs] + off2[npairs] + npairs;
-    if (ops_cap < ops_total) return fail(c, SA_ERR_CAPACITY, "ops buffer too small");
-    for (int pass = 0; pass < 2; ++pass) {
-        const std::vector<uint32_t>& sel = pass == 0 ? keep : hack;
-        if (sel.empty()) continue;
-        std::vector<uint8_t> s1, s2;
-        std::vector<uint64_t> o1(1, 0), o2(1, 0);
-        for (uint32_t p : sel) {
-            s1.insert(s1.end(), seq1 + off1[p], seq1 + off1[p + 1]);
-            s2.insert(s2.end(), seq2 + off2[p], seq2 + off2[p + 1]);
-            o1.push_back(s1.size());
-            o2.push_back(s2.size());
-        }
-        const uint32_t k = (uint32_t)sel.size();
-        std::vector<sa_result> r(k);
-        std::vector<uint8_t> op(s1.size() + s2.size() + k + 1);
-        rc = align_host(c, pass == 0 ? SA_LOCAL_GOTOH : SA_NW, sc, s1.data(), o1.data(), s2.data(),
-                        o2.data(), k, lut, r.data(), op.data(), op.size());
-        if (rc) return rc;
-        for (uint32_t q = 0; q < k; ++q) {
-            const uint32_t p = sel[q];
-            results[p] = r[q];
-            if (pass == 1) results[p].flags |= SA_FLAG_SIZE_HACK;
-            memcpy(ops + off1[p] + off2[p] + p, op.data() + o1[q] + o2[q] + q, r[q].nops);
-        }
-    }
-    return SA_OK;
+    if (bits_off[npairs] && !bits) return fail(c, SA_ERR_ARG, "NULL bitmap");
+    SA_HIP(c, hipSetDevice(c->device));
+    if (algo != SA_LOCAL_GOTOH)
+        return align_host_bits(c, algo, sc, off1, off2, npairs, bits, bits_off, results, ops, ops_cap);
+    return lg_hack_split(c, off1, off2, npairs, results, ops, ops_cap,
+                         [&](int a, const std::vector<uint32_t>& sel, const std::vector<uint64_t>& o1,
+                             const std::vector<uint64_t>& o2, sa_result* r, uint8_t* op, uint64_t cap) {
+                             if (sel.size() == npairs)
+                                 return align_host_bits(c, a, sc, off1, off2, npairs, bits, bits_off, r, op, cap);
+                             std::vector<uint32_t> b;
+                             std::vector<uint64_t> bo(1, 0);
+                             for (uint32_t p : sel) {
+                                 b.insert(b.end(), bits + bits_off[p], bits + bits_off[p + 1]);
+                                 bo.push_back(b.size());
+                             }
+                             return align_host_bits(c, a, sc, o1.data(), o2.data(), (uint32_t)sel.size(),
+                                                    b.data(), bo.data(), r, op, cap);
+                         });
 }
 
 int sa_align_batch_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1,

@@ -62,14 +62,15 @@ __device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
 // v_writelane_b32 through the LLVM intrinsic (the compiler routes the lane select via m0).
 extern "C" __device__ int sa_writelane(int value, int lane, int old) __asm("llvm.amdgcn.writelane");
 
-// rec = 2*rec + (a == b), one v_cmp into an SGPR pair + one v_addc_co_u32.
-__device__ __forceinline__ uint32_t push_eq(uint32_t rec, int a, int b) {
-    const unsigned long long m = __builtin_amdgcn_ballot_w64(a == b);
+// rec = 2*rec + c, one v_cmp into an SGPR pair + one v_addc_co_u32.
+__device__ __forceinline__ uint32_t push_bit(uint32_t rec, bool c) {
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(c);
     uint32_t out;
     unsigned long long co;
     asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(out), "=s"(co) : "v"(rec), "s"(m));
     return out;
 }
+__device__ __forceinline__ uint32_t push_eq(uint32_t rec, int a, int b) { return push_bit(rec, a == b); }
 
 // 8 * code of symbol b in the T16 alphabet (bytes of sym_pack are distinct; code 0 = byte 0).
 __device__ __forceinline__ uint32_t t16_code8(uint32_t sp, uint32_t b) {
@@ -94,8 +95,13 @@ constexpr int fill_max_threads() { return R >= 32 ? 256 : 1024; }
 // one expiry the workgroup stops waiting altogether (the pair is flagged SA_FLAG_TIMEOUT).
 constexpr uint64_t kSplitWaitTicks = 20000000ull;
 
-template <int ALG, int R, bool LUT, bool ALLOW, bool KEYED, bool T16, bool CMAX, bool SPLIT>
+// MM: how a cell learns whether its two symbols match -- kMatchEq (byte equality), kMatchLut (the
+// 256 x 256 table of the user's match fn, LDS) or kMatchBits (a per-pair m x n match bitmap, the
+// generic-Ty path: any symbol type and count, the reference's cacheAllMatches packed to bits).
+template <int ALG, int R, int MM, bool ALLOW, bool KEYED, bool T16, bool CMAX, bool SPLIT>
 __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams P) {
+    constexpr bool LUT = MM == kMatchLut;
+    constexpr bool BITS = MM == kMatchBits;
     constexpr bool AFF = ALG >= SA_LOCAL_GOTOH;
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
     constexpr int BPC = AFF ? 4 : 2;
@@ -108,7 +114,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     constexpr int BAND = kWave * R;
     static_assert(kChunk % SPP == 0, "chunk must hold whole packets");
     static_assert(BPS >= 1, "record must be at least a byte");
-    static_assert(!T16 || (!AFF && ALLOW && !LUT && (RB <= 32 || RB % 32 == 0)),
+    static_assert(!T16 || (!AFF && ALLOW && MM == kMatchEq && (RB <= 32 || RB % 32 == 0)),
                   "T16: linear, allow-mismatch, profile");
     static_assert(!T16 || !LOCAL || KEYED, "T16 local mode tracks its maximum with keys");
     constexpr int SC = T16 ? 4 : 1;            // score scale of the register values
@@ -195,6 +201,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
 
     // Per-lane state for the current band.
     int a[R];      // Seq1 symbols of my rows
+    uint32_t mwin[BITS ? R : 1];   // BITS: match bits of my rows at this chunk's 32 columns
     int Hp[R];     // H (or M) of my rows at the previous column
     int Yp[R];     // Iy of my rows at the previous column (affine)
     int bh[R];     // best per row: key (KEYED) or score
@@ -312,7 +319,9 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
 #undef SA_T16_PW
                     Hc = Hp[r];
                 } else {
-                const bool v = match_bit<LUT>(s_lut, a[r], sym);
+                bool v;
+                if constexpr (BITS) v = (mwin[r] >> q) & 1u;
+                else v = match_bit<LUT>(s_lut, a[r], sym);
                 int D;
                 if constexpr (ALLOW) D = hd + (v ? MA : MI);
                 else D = v ? hd + MA : INT_MIN;
@@ -322,7 +331,10 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                     int H = imax(imax(D, U), L);
                     if constexpr (LOCAL) H = imax(H, 0);
                     rw = push_eq(rw, H, D);   // fD
-                    rw = push_eq(rw, H, U);   // fU
+                    // BITS: the second bit is the match bit when fD is set (the traceback's diag
+                    // move then needs no symbols), fU otherwise
+                    if constexpr (BITS) rw = push_bit(rw, H == D ? v : H == U);
+                    else rw = push_eq(rw, H, U);   // fU
                     Hc = H;
                 } else {
                     const int XE = xu + GE;
@@ -332,7 +344,8 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                     int M = imax(imax(D, X), Y);
                     if constexpr (LOCAL) M = imax(M, 0);
                     rw = push_eq(rw, M, D);   // fD
-                    rw = push_eq(rw, M, X);   // fX
+                    if constexpr (BITS) rw = push_bit(rw, M == D ? v : M == X);   // fX, or v under fD
+                    else rw = push_eq(rw, M, X);   // fX
                     rw = push_eq(rw, X, XE);  // fXe: Ix extends
                     rw = push_eq(rw, Y, YE);  // fYe: Iy extends
                     Yp[r] = Y;
@@ -510,6 +523,28 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 const int kC = (int)chunk * kChunk;
                 int bch, bcx, symc;
                 load_chunk(band, kC, bch, bcx, symc);
+                if constexpr (BITS) {
+                    // my rows' match bits at columns [kC - lane, kC - lane + 32): bit q = step q
+                    const int c0 = kC - lane;
+                    const uint32_t wn = ((uint32_t)n + 31u) >> 5;
+                    const uint32_t* mrow = P.mbits + P.mbits_off[pidx];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int row = row0 + r;
+                        uint32_t w = 0;
+                        if (row < m && c0 < n && c0 > -32) {
+                            const uint32_t* rp = mrow + (uint64_t)row * wn;
+                            if (c0 >= 0) {
+                                const uint32_t k = (uint32_t)c0 >> 5;
+                                const uint32_t lo = rp[k], hi = k + 1 < wn ? rp[k + 1] : 0u;
+                                w = __builtin_amdgcn_alignbit(hi, lo, (uint32_t)c0 & 31u);
+                            } else {
+                                w = rp[0] << (uint32_t)(-c0);
+                            }
+                        }
+                        mwin[r] = w;
+                    }
+                }
                 int acc_h = 0, acc_x = 0;
                 const bool steady = kC >= kWave - 1 && kC + kChunk <= n;
                 if (steady) run_chunk(std::true_type{}, band, kC, bch, bcx, symc, acc_h, acc_x);
@@ -660,7 +695,7 @@ template <int ALG>
 hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream) {
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
     const int R = v.R;
-    const bool lut = v.t16 ? false : v.lut, allow = v.allow;
+    const bool lut = (v.t16 || v.bits) ? false : v.lut, allow = v.allow;
     const bool keyed = LOCAL && v.keyed;
     const dim3 block(kWave * p.waves);
     const size_t lds = lds_layout(lut, is_affine(ALG), p.waves, p.stage_seq2 ? p.max_n : 0).total;
@@ -676,12 +711,12 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
     if (R == RR && split == SP) {                                                                    \
         if constexpr (ALG == SA_SW) {                                                                \
             if (v.cmax) {                                                                            \
-                hipLaunchKernelGGL((fill_kernel<ALG, RR, false, true, LOCAL, true, true, SP>), dim3(grid), \
+                hipLaunchKernelGGL((fill_kernel<ALG, RR, kMatchEq, true, LOCAL, true, true, SP>), dim3(grid), \
                                    block, lds, stream, p);                                           \
                 return hipGetLastError();                                                            \
             }                                                                                        \
         }                                                                                            \
-        hipLaunchKernelGGL((fill_kernel<ALG, RR, false, true, LOCAL, true, false, SP>), dim3(grid), block, \
+        hipLaunchKernelGGL((fill_kernel<ALG, RR, kMatchEq, true, LOCAL, true, false, SP>), dim3(grid), block, \
                            lds, stream, p);                                                          \
         return hipGetLastError();                                                                    \
     }
@@ -697,27 +732,30 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
         }
     }
     if (v.t16 || v.cmax) return hipErrorInvalidValue;
-#define SA_LAUNCH(RR, LL, AA, KK)                                                              \
-    if (R == RR && lut == LL && allow == AA && keyed == KK) {                                  \
+    const int mm = v.bits ? kMatchBits : lut ? kMatchLut : kMatchEq;
+#define SA_LAUNCH(RR, MMV, AA, KK)                                                             \
+    if (R == RR && mm == MMV && allow == AA && keyed == KK) {                                  \
         if (split) {                                                                           \
             if constexpr (RR <= 8) {                                                           \
-                hipLaunchKernelGGL((fill_kernel<ALG, RR, LL, AA, KK, false, false, true>), dim3(grid), block, lds, \
+                hipLaunchKernelGGL((fill_kernel<ALG, RR, MMV, AA, KK, false, false, true>), dim3(grid), block, lds, \
                                    stream, p);                                                 \
                 return hipGetLastError();                                                      \
             }                                                                                  \
             return hipErrorInvalidConfiguration;                                               \
         }                                                                                      \
-        hipLaunchKernelGGL((fill_kernel<ALG, RR, LL, AA, KK, false, false, false>), dim3(grid), block, lds, stream, p); \
+        hipLaunchKernelGGL((fill_kernel<ALG, RR, MMV, AA, KK, false, false, false>), dim3(grid), block, lds, stream, p); \
         return hipGetLastError();                                                              \
     }
-#define SA_LAUNCH_K(RR, LL, AA) \
-    SA_LAUNCH(RR, LL, AA, false) \
-    if constexpr (LOCAL) { SA_LAUNCH(RR, LL, AA, true) }
-#define SA_LAUNCH_R(RR)            \
-    SA_LAUNCH_K(RR, false, true)   \
-    SA_LAUNCH_K(RR, false, false)  \
-    SA_LAUNCH_K(RR, true, true)    \
-    SA_LAUNCH_K(RR, true, false)
+#define SA_LAUNCH_K(RR, MMV, AA) \
+    SA_LAUNCH(RR, MMV, AA, false) \
+    if constexpr (LOCAL) { SA_LAUNCH(RR, MMV, AA, true) }
+#define SA_LAUNCH_R(RR)                  \
+    SA_LAUNCH_K(RR, kMatchEq, true)      \
+    SA_LAUNCH_K(RR, kMatchEq, false)     \
+    SA_LAUNCH_K(RR, kMatchLut, true)     \
+    SA_LAUNCH_K(RR, kMatchLut, false)    \
+    SA_LAUNCH_K(RR, kMatchBits, true)    \
+    SA_LAUNCH_K(RR, kMatchBits, false)
     SA_LAUNCH_R(4)
     SA_LAUNCH_R(8)
     SA_LAUNCH_R(16)

@@ -8,12 +8,19 @@
 
 namespace sa {
 
+// How the fill decides match(Seq1[i-1], Seq2[j-1]) (sa_fill_impl.h).
+constexpr int kMatchEq = 0, kMatchLut = 1, kMatchBits = 2;
+
 struct FillParams {
     const uint8_t* seq1;
     const uint64_t* off1;
     const uint8_t* seq2;
     const uint64_t* off2;
     const uint32_t* lutbits;   // 256 x 8 words: bit b of word [a*8 + b/32] = match(a, b)
+    // kMatchBits: pair p's m x n match bitmap at mbits + mbits_off[p], row-major, ceil(n/32)
+    // words per row, bit j of row i = match(Seq1[i], Seq2[j])
+    const uint32_t* mbits;
+    const uint64_t* mbits_off;
     uint8_t* dirs;             // direction slots, one per pair of this launch
     uint64_t dir_slot;         // bytes per slot
     uint64_t band_stride;      // bytes per band inside a slot
@@ -102,6 +109,7 @@ struct TbParams {
     int32_t gap, match, mismatch, gap_open, gap_extend;
     int allow;
     int tagged;                // records hold T16 max tags (sa_layout.h)
+    int vrec;                  // kMatchBits fills: under fD the second flag bit is the match bit
     const uint32_t* sel;
     uint32_t sel_want;
 };
@@ -113,6 +121,7 @@ struct TbParams {
 struct FillVariant {
     int R;
     bool lut, allow, keyed, t16, cmax, split;
+    bool bits = false;   // kMatchBits (then lut is ignored)
 };
 hipError_t launch_fill(int algo, const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream);
 hipError_t launch_fill_sw(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);

@@ -184,9 +184,12 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
         const uint32_t f = cell() & 3u;
         return tagged ? (f == 3u ? 2u : (f == 2u ? 1u : 0u)) : f;
     };
-    // diagonal move: emits the op and returns the substitution term that was added
-    auto diag = [&](int i, int j) __attribute__((always_inline)) -> int {
-        const bool v = tb_match<LUT>(lutbits, seqbyte(kTbSeqOff1, a1, s1, i - 1), seqbyte(kTbSeqOff2, a2, s2, j - 1));
+    // diagonal move: emits the op and returns the substitution term that was added (vrec: the
+    // match bit is the record's fX position under fD, see sa_fill_impl.h kMatchBits)
+    const bool vrec = P.vrec != 0;
+    auto diag = [&](int i, int j, uint32_t f) __attribute__((always_inline)) -> int {
+        const bool v = vrec ? ((f >> 2) & 1u) != 0
+                            : tb_match<LUT>(lutbits, seqbyte(kTbSeqOff1, a1, s1, i - 1), seqbyte(kTbSeqOff2, a2, s2, j - 1));
         emit(v ? 'M' : (allow ? 'S' : 'X'));
         return v ? MA : MI;
     };
@@ -240,7 +243,8 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
                         bool v = false;
                         if (inner) {
                             f = lin();
-                            v = tb_match<LUT>(lutbits, seqbyte(kTbSeqOff1, a1, s1, i - 1), seqbyte(kTbSeqOff2, a2, s2, j - 1));
+                            v = vrec ? (f & 1u) != 0
+                                     : tb_match<LUT>(lutbits, seqbyte(kTbSeqOff1, a1, s1, i - 1), seqbyte(kTbSeqOff2, a2, s2, j - 1));
                         } else if (i == 0) {
                             f = 0u;
                         }
@@ -255,7 +259,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
                         const uint32_t f = cell();
                         if (st == 0) {
                             if (V <= 0) { fin = true; break; }    // M == max(D, 0) <= 0
-                            if (f & 8u) { V -= diag(i, j); --i; --j; }
+                            if (f & 8u) { V -= diag(i, j, f); --i; --j; }
                             else st = (f & 4u) ? 1 : 2;              // M == Ix, else M == Iy (same value)
                         } else if (st == 1) {
                             if (f & 2u) { emit('U'); V -= GE; --i; }
@@ -274,7 +278,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
                         if (i == 0) { emit('L'); --j; break; }
                         const uint32_t f = cell();
                         if (st == 0) {
-                            if (f & 8u) { diag(i, j); --i; --j; }
+                            if (f & 8u) { diag(i, j, f); --i; --j; }
                             else st = (f & 4u) ? 1 : 2;
                         } else if (st == 1) {
                             emit('U'); --i;

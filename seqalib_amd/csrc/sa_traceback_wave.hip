@@ -57,7 +57,7 @@ typedef uint32_t __attribute__((address_space(3))) tw_u32;
 // matrix masked to 0 afterwards), so the wave waits once for all of them.
 template <int ALG, int R, bool LUT>
 __device__ __attribute__((noinline)) void tw_decode(const uint8_t* dir, const uint8_t* s1, const uint8_t* s2, int m,
-                                                    int n, uint32_t max_m, uint32_t max_n, bool tagged, int i0,
+                                                    int n, uint32_t max_m, uint32_t max_n, bool tagged, bool vrec, int i0,
                                                     int j0, tw_u8* win, tw_u8* sq1, tw_u8* sq2,
                                                     const tw_u32* lut) {
     constexpr int BPC = bits_per_cell(ALG);
@@ -103,7 +103,8 @@ __device__ __attribute__((noinline)) void tw_decode(const uint8_t* dir, const ui
         const int jq = min(max(j - 1 - jb, 0), kTwS2 - 1);
         const uint32_t a = sq1[p], b = sq2[jq];
         uint32_t mt;
-        if constexpr (LUT) mt = (lut[(a << 3) | (b >> 5)] >> (b & 31)) & 1u;
+        if (vrec) mt = BPC == 2 ? ((f >> 1) & f & 1u) : ((f >> 3) & (f >> 2) & 1u);   // under fD only
+        else if constexpr (LUT) mt = (lut[(a << 3) | (b >> 5)] >> (b & 31)) & 1u;
         else mt = (uint32_t)(a == b);
         packed[q / 4] |= ((f | mt << 4) & (0u - ok)) << ((q % 4) * 8);
     }
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(64) void traceback_wave_kernel(TbParams P) {
 #ifdef SA_TB_STATS
                 const unsigned long long t = __builtin_amdgcn_s_memtime();
 #endif
-                tw_decode<ALG, R, LUT>(dir, s1, s2, m, n, P.max_m, P.max_n, tagged, i, j, (tw_u8*)s_win,
+                tw_decode<ALG, R, LUT>(dir, s1, s2, m, n, P.max_m, P.max_n, tagged, P.vrec != 0, i, j, (tw_u8*)s_win,
                                          (tw_u8*)s_seq1, (tw_u8*)s_seq2, (const tw_u32*)s_lut);
                 __syncthreads();
 #ifdef SA_TB_STATS

@@ -7,6 +7,9 @@
   build container produced tests/golden/dropin_types.ref.txt; the drop-in build must print the
   identical text (std::vector<int> + predicate, ArrayView + StaticFuncs::useNW/bridgeNW, batch,
   SmithWaterman member persistence on empty input).
+* tests/cpp/dropin_wide — std::vector<int> with ~2,000 distinct values (more than the 256 byte
+  codes), equality / a "within 1" predicate, all four aligners: the drop-in takes the
+  match-bitmap path and must print what the reference build printed (dropin_wide.ref.txt).
 * tests/cpp/dropin_bridge — anchor gaps of three sequence pairs bridged with NW: the reference
   build calls StaticFuncs::bridgeNW per window (tests/golden/dropin_bridge.ref.txt); the
   drop-in build sends every window through StaticFuncs::bridgeNWBatch in one GPU pass.
@@ -26,7 +29,7 @@ CPP = os.path.join(ROOT, "tests", "cpp")
 def binaries():
     subprocess.check_call(["make", "-s", "-C", CPP])
     return (os.path.join(CPP, "dropin_driver"), os.path.join(CPP, "dropin_types"),
-            os.path.join(CPP, "dropin_bridge"))
+            os.path.join(CPP, "dropin_bridge"), os.path.join(CPP, "dropin_wide"))
 
 
 def case_line(e):
@@ -68,4 +71,10 @@ def test_generic_types_match_reference_build(binaries, engine):
 def test_batched_bridging_matches_reference_bridgeNW(binaries, engine):
     ref = open(os.path.join(GOLDEN, "dropin_bridge.ref.txt")).read()
     out = subprocess.run([binaries[2]], capture_output=True, text=True, timeout=300, check=True).stdout
+    assert out == ref
+
+
+def test_wide_alphabet_matches_reference_build(binaries, engine):
+    ref = open(os.path.join(GOLDEN, "dropin_wide.ref.txt")).read()
+    out = subprocess.run([binaries[3]], capture_output=True, text=True, timeout=300, check=True).stdout
     assert out == ref

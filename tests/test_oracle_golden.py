@@ -109,3 +109,46 @@ def test_oracle_batch_matches_single():
             got = (int(res["score"][p]), int(res["end_i"][p]), int(res["end_j"][p]), int(res["start_i"][p]),
                    int(res["start_j"][p]), ops[off:off + int(res["nops"][p])].tobytes())
             assert got == (o["score"], o["end_i"], o["end_j"], o["start_i"], o["start_j"], o["ops"]), (algo, p)
+
+
+def test_oracle_matrix_form_matches_symbol_form():
+    """oracle_align_matrix (generic Ty: an m x n match matrix) equals oracle_align on byte symbols
+    whose match matrix it is, for every algorithm with a bitmap path, equality and a LUT."""
+    import numpy as np
+    from util import oracle_align_matrix
+    import seqalib_amd as sa
+    lut = named_lut("purine")
+    pairs = [(sa.synth_dna(70 + k, 30 + 17 * k), sa.synth_mutate(sa.synth_dna(70 + k, 30 + 17 * k), k)) for k in range(10)]
+    pairs += [(b"", b"ACG"), (b"A", b""), (b"A" * 314, b"C" * 288)]   # empty sides, LocalGotoh size hack
+    for algo, args in ((0, (-1, 1, -1)), (0, (-2, 1, -1, False)), (1, (-1, 2, -1)), (1, (-1, 2)),
+                       (2, (-3, -1, 1, -1)), (2, (-3, -1, 1, -1, False)), (3, (-3, -1, 1, -1))):
+        for table in (None, lut):
+            for a, b in pairs:
+                av = np.frombuffer(a, np.uint8) if a else np.zeros(0, np.uint8)
+                bv = np.frombuffer(b, np.uint8) if b else np.zeros(0, np.uint8)
+                mt = (av[:, None] == bv[None, :]) if table is None else table[av[:, None], bv[None, :]] != 0
+                got = oracle_align_matrix(algo, args, mt.reshape(len(a), len(b)))
+                exp = oracle_align(algo, args, a, b, table)
+                assert got["rc"] == 0
+                assert [got[k] for k in ("score", "end_i", "end_j", "start_i", "start_j", "ops")] == \
+                       [exp[k] for k in ("score", "end_i", "end_j", "start_i", "start_j", "ops")], (algo, args, len(a))
+
+
+def test_match_bitmaps_layout():
+    """seqalib_amd.match_bitmaps packs bit (j % 32) of word [i * ceil(n/32) + j / 32] = match."""
+    import numpy as np
+    import seqalib_amd as sa
+    rng = np.random.default_rng(1)
+    pairs = [(list(rng.integers(0, 2000, 70)), list(rng.integers(0, 2000, 45))), ([], [1, 2]), ([3], list(range(33)))]
+    near = lambda x, y: abs(int(x) - int(y)) <= 40
+    for match in (None, near):
+        off1, off2, bits, bits_off = sa.match_bitmaps(pairs, match)
+        for p, (a, b) in enumerate(pairs):
+            m, n = len(a), len(b)
+            wn = (n + 31) // 32
+            assert int(bits_off[p + 1] - bits_off[p]) == m * wn
+            w = bits[int(bits_off[p]):int(bits_off[p + 1])].reshape(m, wn) if m and wn else np.zeros((m, wn), np.uint32)
+            for i in range(m):
+                for j in range(n):
+                    exp = (a[i] == b[j]) if match is None else near(a[i], b[j])
+                    assert bool((int(w[i, j // 32]) >> (j % 32)) & 1) == bool(exp)

@@ -135,6 +135,9 @@ def oracle_lib():
         L.oracle_batch.restype = C.c_int
         L.oracle_sw_score_batch.argtypes = [C.POINTER(OracleScoring), vp, vp, vp, vp, C.c_int, C.c_int, vp]
         L.oracle_sw_score_batch.restype = C.c_int
+        L.oracle_align_matrix.argtypes = [C.c_int, C.POINTER(OracleScoring), C.c_int, C.c_int, vp,
+                                          C.POINTER(OracleResult), vp, C.c_int]
+        L.oracle_align_matrix.restype = C.c_int
         _oracle = L
     return _oracle
 
@@ -229,6 +232,21 @@ def pack_bytes(pairs):
     s1 = np.frombuffer(b"".join(a for a, _ in pairs) + b"\0", dtype=np.uint8)[:-1].copy()
     s2 = np.frombuffer(b"".join(b for _, b in pairs) + b"\0", dtype=np.uint8)[:-1].copy()
     return s1, o1, s2, o2
+
+
+def oracle_align_matrix(algo: int, args, mt: np.ndarray):
+    """The oracle driven by an m x n match matrix (generic Ty): dict(score, end_i, end_j, start_i,
+    start_j, ops, rc)."""
+    L = oracle_lib()
+    m, n = mt.shape
+    mt = np.ascontiguousarray(mt, dtype=np.uint8)
+    sc = _oracle_sc(args)
+    cap = m + n + 4
+    ops = C.create_string_buffer(cap)
+    res = OracleResult()
+    rc = L.oracle_align_matrix(algo, C.byref(sc), m, n, mt.ctypes.data if mt.size else None, C.byref(res), ops, cap)
+    return dict(rc=rc, score=res.score, end_i=res.end_i, end_j=res.end_j, start_i=res.start_i,
+                start_j=res.start_j, ops=ops.raw[: res.nops])
 
 
 def subset(s1, o1, s2, o2, idx):

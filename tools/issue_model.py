@@ -28,14 +28,14 @@ ALIAS = {"v_mov_b32_dpp": "v_mov_b32_dpp_shr", "v_readlane_b32": "readlane", "v_
          "v_lshl_add_u64": "v_lshl_add_u32", "v_max3_i32": "v_max3_i32", "v_add_co_u32": "add_co_e64"}
 
 KERNELS = {  # label -> (TU, mangled name, cells per lane in one steady block = SPP * R)
-    "sw_t16_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELb0ELb1ELb1ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
-    "sw_t16c_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELb0ELb1ELb1ELb1ELb1ELb0EEEvNS_10FillParamsE", 64),
-    "sw_t16c_r32": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi32ELb0ELb1ELb1ELb1ELb1ELb0EEEvNS_10FillParamsE", 64),
-    "sw_t16_r32": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi32ELb0ELb1ELb1ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
-    "nw_t16_r32": ("sa_fill_nw.hip", "_ZN2sa11fill_kernelILi1ELi32ELb0ELb1ELb0ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
-    "sw_int32_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELb0ELb1ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 64),
-    "nw_t16_r16": ("sa_fill_nw.hip", "_ZN2sa11fill_kernelILi1ELi16ELb0ELb1ELb0ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
-    "lg_int32_r16": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi16ELb0ELb1ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 32),
+    "sw_t16_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELi0ELb1ELb1ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
+    "sw_t16c_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELi0ELb1ELb1ELb1ELb1ELb0EEEvNS_10FillParamsE", 64),
+    "sw_t16c_r32": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi32ELi0ELb1ELb1ELb1ELb1ELb0EEEvNS_10FillParamsE", 64),
+    "sw_t16_r32": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi32ELi0ELb1ELb1ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
+    "nw_t16_r32": ("sa_fill_nw.hip", "_ZN2sa11fill_kernelILi1ELi32ELi0ELb1ELb0ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
+    "sw_int32_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELi0ELb1ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 64),
+    "nw_t16_r16": ("sa_fill_nw.hip", "_ZN2sa11fill_kernelILi1ELi16ELi0ELb1ELb0ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
+    "lg_int32_r16": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi16ELi0ELb1ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 32),
 }
 
 
