@@ -43,6 +43,41 @@ inline sa_ctx* context() {
     return c.h;
 }
 
+// $SEQALIB_DEVICES="0,1,..." (two or more ordinals): batches are spread over those GPUs through
+// one persistent sa_multi handle per host thread (contiguous pair ranges of near-equal work,
+// results in place); otherwise the single context above is used.
+struct ThreadMulti {
+    sa_multi* h = nullptr;
+    bool checked = false;
+    ~ThreadMulti() {
+        if (h) sa_multi_destroy(h);
+    }
+};
+
+inline sa_multi* multi_context() {
+    thread_local ThreadMulti m;
+    if (!m.checked) {
+        m.checked = true;
+        const char* env = std::getenv("SEQALIB_DEVICES");
+        std::vector<int> devs;
+        for (const char* q = env; q && *q;) {
+            char* end = nullptr;
+            const long d = std::strtol(q, &end, 10);
+            if (end == q) break;
+            devs.push_back((int)d);
+            q = (*end == ',') ? end + 1 : end;
+        }
+        if (devs.size() >= 2) {
+            const int rc = sa_multi_create(devs.data(), (int)devs.size(), &m.h);
+            if (rc != SA_OK) {
+                m.h = nullptr;
+                throw std::runtime_error(std::string("seqalib: cannot open SEQALIB_DEVICES: ") + sa_multi_last_error(nullptr));
+            }
+        }
+    }
+    return m.h;
+}
+
 // $SEQALIB_HOST_TIMING: print the host-side phases of each batch to stderr.
 struct PhaseTimer {
     bool on = std::getenv("SEQALIB_HOST_TIMING") != nullptr;
@@ -202,9 +237,17 @@ void align(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
     ops_off.resize(n);
     for (uint32_t p = 0; p < n; ++p) ops_off[p] = o1[p] + o2[p] + p;
     tm.lap("match table + buffers");
-    check(sa_align_batch(context(), algo, &sc, s1.data(), o1.data(), s2.data(), o2.data(), n,
-                         has_fn ? lut.data() : nullptr, res.data(), ops.data(), cap),
-          "sa_align_batch");
+    if (sa_multi* mg = (algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER) ? nullptr : multi_context()) {
+        const int rc = sa_multi_align_batch(mg, algo, &sc, s1.data(), o1.data(), s2.data(), o2.data(), n,
+                                            has_fn ? lut.data() : nullptr, res.data(), ops.data(), cap);
+        if (rc != SA_OK)
+            throw std::runtime_error(std::string("seqalib: sa_multi_align_batch: ") + sa_status_string(rc) + " (" +
+                                     sa_multi_last_error(mg) + ")");
+    } else {
+        check(sa_align_batch(context(), algo, &sc, s1.data(), o1.data(), s2.data(), o2.data(), n,
+                             has_fn ? lut.data() : nullptr, res.data(), ops.data(), cap),
+              "sa_align_batch");
+    }
     tm.lap("sa_align_batch (GPU)");
     for (auto& r : res) {
         if (r.flags & SA_FLAG_DIVERGED)

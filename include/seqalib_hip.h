@@ -149,6 +149,20 @@ int sa_align_batch_bits(sa_ctx* ctx, int algo, const sa_scoring* scoring,
                         const uint32_t* match_bits, const uint64_t* bits_off,
                         sa_result* results, uint8_t* ops, uint64_t ops_cap);
 
+/* Several GPUs of one node behind one handle.  sa_multi_create opens one persistent context per
+ * listed device (a device may be listed twice).  sa_multi_align_batch has exactly the contract of
+ * sa_align_batch: the batch is cut into contiguous pair ranges of near-equal sum of m*n, one per
+ * context, aligned concurrently (one host thread each, no collective), and every range writes its
+ * results and op streams in place in the caller's buffers. */
+typedef struct sa_multi sa_multi;
+int sa_multi_create(const int* devices, int ndevices, sa_multi** out);
+void sa_multi_destroy(sa_multi* multi);
+const char* sa_multi_last_error(const sa_multi* multi);
+int sa_multi_align_batch(sa_multi* multi, int algo, const sa_scoring* scoring,
+                         const uint8_t* seq1, const uint64_t* seq1_off,
+                         const uint8_t* seq2, const uint64_t* seq2_off, uint32_t npairs,
+                         const uint8_t* match_lut, sa_result* results, uint8_t* ops, uint64_t ops_cap);
+
 /* Device-resident batch API: every pointer is device memory (HBM) and the work is enqueued on
  * `stream` (a hipStream_t; NULL = the context's own stream).  Asynchronous: returns after
  * enqueueing.  max_m/max_n must bound every pair's lengths (pairs that exceed them are skipped

@@ -112,6 +112,13 @@ def load_library():
     L.sa_trim.argtypes = [vp]
     L.sa_align_batch.argtypes = [vp, C.c_int, C.POINTER(_Scoring), vp, vp, vp, vp, C.c_uint32, vp, vp, vp,
                                  C.c_uint64]
+    L.sa_multi_create.argtypes = [vp, C.c_int, C.POINTER(vp)]
+    L.sa_multi_destroy.argtypes = [vp]
+    L.sa_multi_destroy.restype = None
+    L.sa_multi_last_error.argtypes = [vp]
+    L.sa_multi_last_error.restype = C.c_char_p
+    L.sa_multi_align_batch.argtypes = [vp, C.c_int, C.POINTER(_Scoring), vp, vp, vp, vp, C.c_uint32, vp, vp, vp,
+                                       C.c_uint64]
     L.sa_align_batch_bits.argtypes = [vp, C.c_int, C.POINTER(_Scoring), vp, vp, C.c_uint32, vp, vp, vp, vp,
                                       C.c_uint64]
     L.sa_align_batch_device.argtypes = [vp, C.c_int, C.POINTER(_Scoring), vp, vp, vp, vp, C.c_uint32,
@@ -127,6 +134,7 @@ def load_library():
     L.sa_synth_mutate.argtypes = [vp, C.c_uint32, C.c_uint64, vp, C.c_uint32, C.POINTER(C.c_uint32)]
     L.sa_synth_dna_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_int]
     for fn in ("sa_set_workspace_limit", "sa_trim", "sa_align_batch", "sa_align_batch_bits", "sa_align_batch_device",
+               "sa_multi_create", "sa_multi_align_batch",
                "sa_last_timings", "sa_last_plan", "sa_plan_query", "sa_plan_query_ex", "sa_synth_dna", "sa_synth_mutate", "sa_synth_dna_batch",
                "sa_create", "sa_device_count", "sa_set_pipeline", "sa_wait"):
         getattr(L, fn).restype = C.c_int

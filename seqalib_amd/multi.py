@@ -4,16 +4,16 @@ collective on the data path.
 Two ways to use several GPUs of one node:
 * one process per GPU (torchrun; what bench.py does): rank r takes the contiguous slice
   :func:`shard_range` of the global batch; only the timing is reduced across ranks;
-* one process, one host thread + HIP context per GPU: :func:`align_multi_gpu`.
+* one process, persistent HIP contexts on several GPUs: :class:`MultiEngine` /
+  :func:`align_multi_gpu` (native sa_multi_*: one host thread per device, results in place).
 """
 from __future__ import annotations
 
-import threading
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import RESULT_DTYPE, Engine, ScoringSystem
+from . import RESULT_DTYPE, ScoringSystem
 
 
 def static_split(npairs: int, parts: int) -> List[Tuple[int, int]]:
@@ -48,44 +48,78 @@ def slice_batch(s1, o1, s2, o2, start: int, end: int):
             s2[c:d], (o2[start:end + 1] - o2[start]).astype(np.uint64))
 
 
-def align_multi_gpu(algo: int, scoring: ScoringSystem, s1: np.ndarray, o1: np.ndarray, s2: np.ndarray,
-                    o2: np.ndarray, devices: Sequence[int], lut: Optional[np.ndarray] = None,
-                    balance: str = "cells"):
-    """Align a batch on several GPUs (one host thread and HIP context each).  Returns
-    (results, ops) laid out exactly as a single-GPU sa_align_batch would return them."""
-    npairs = len(o1) - 1
-    if balance == "cells":
-        cells = (o1[1:] - o1[:-1]).astype(np.float64) * (o2[1:] - o2[:-1]).astype(np.float64)
-        ranges = balanced_split(cells, len(devices))
-    else:
-        ranges = static_split(npairs, len(devices))
-    results = np.zeros(npairs, dtype=RESULT_DTYPE)
-    ops = np.zeros(int(o1[-1] + o2[-1]) + npairs + 1, dtype=np.uint8)
-    errors: List[BaseException] = []
+class MultiEngine:
+    """Several GPUs behind one handle (sa_multi_*): one persistent HIP context per listed device
+    (a device may repeat), a batch cut into contiguous pair ranges of near-equal sum of m*n and
+    aligned concurrently, one native host thread per device.  Results and op streams land in
+    place, laid out exactly as a single sa_align_batch returns them -- no gather."""
 
-    def work(dev: int, start: int, end: int):
+    def __init__(self, devices: Sequence[int]):
+        from . import _Scoring, load_library  # noqa: F401
+        import ctypes as C
+        self.L = load_library()
+        self.devices = list(devices)
+        arr = (C.c_int * len(self.devices))(*self.devices)
+        h = C.c_void_p()
+        rc = self.L.sa_multi_create(arr, len(self.devices), C.byref(h))
+        if rc:
+            raise RuntimeError(f"sa_multi_create: {self.L.sa_multi_last_error(None).decode()}")
+        self.h = h
+
+    def align_packed(self, algo: int, scoring: ScoringSystem, s1, o1, s2, o2, lut: Optional[np.ndarray] = None):
+        import ctypes as C
+        from . import _ptr
+        npairs = len(o1) - 1
+        s1 = np.ascontiguousarray(s1, dtype=np.uint8)
+        s2 = np.ascontiguousarray(s2, dtype=np.uint8)
+        o1 = np.ascontiguousarray(o1, dtype=np.uint64)
+        o2 = np.ascontiguousarray(o2, dtype=np.uint64)
+        res = np.zeros(max(npairs, 1), dtype=RESULT_DTYPE)
+        cap = int(o1[-1] + o2[-1]) + npairs + 1
+        ops = np.zeros(cap, dtype=np.uint8)
+        lut_p = 0
+        if lut is not None:
+            lut = np.ascontiguousarray(lut, dtype=np.uint8).reshape(65536)
+            lut_p = _ptr(lut)
+        sc = scoring._c()
+        rc = self.L.sa_multi_align_batch(self.h, algo, C.byref(sc), _ptr(s1), _ptr(o1), _ptr(s2), _ptr(o2), npairs,
+                                         lut_p or None, _ptr(res), _ptr(ops), cap)
+        if rc:
+            raise RuntimeError(f"sa_multi_align_batch: {self.L.sa_multi_last_error(self.h).decode()}")
+        return res[:npairs], ops
+
+    def close(self):
+        if self.h:
+            self.L.sa_multi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
         try:
-            if end <= start:
-                return
-            eng = Engine(dev)
-            a, oa, b, ob = slice_batch(s1, o1, s2, o2, start, end)
-            res, sub_ops = eng.align_packed(algo, scoring, a, oa, b, ob, lut)
-            results[start:end] = res
-            for k in range(end - start):
-                p = start + k
-                src = int(oa[k] + ob[k]) + k
-                dst = int(o1[p] + o2[p]) + p
-                nops = int(res["nops"][k])
-                ops[dst:dst + nops] = sub_ops[src:src + nops]
-            eng.close()
-        except BaseException as e:  # surfaced to the caller below
-            errors.append(e)
+            self.close()
+        except Exception:
+            pass
 
-    threads = [threading.Thread(target=work, args=(d, r0, r1)) for d, (r0, r1) in zip(devices, ranges)]
-    for t in threads:
-        t.start()
-    for t in threads:
-        t.join()
-    if errors:
-        raise errors[0]
-    return results, ops
+
+_multi_cache: dict = {}
+
+
+def _close_cached():
+    for eng in _multi_cache.values():
+        eng.close()
+    _multi_cache.clear()
+
+
+import atexit  # noqa: E402
+
+atexit.register(_close_cached)
+
+
+def align_multi_gpu(algo: int, scoring: ScoringSystem, s1: np.ndarray, o1: np.ndarray, s2: np.ndarray,
+                    o2: np.ndarray, devices: Sequence[int], lut: Optional[np.ndarray] = None):
+    """Align a batch on several GPUs of this node (a cached MultiEngine per device list).  Returns
+    (results, ops) laid out exactly as a single-GPU sa_align_batch would return them."""
+    key = tuple(devices)
+    eng = _multi_cache.get(key)
+    if eng is None:
+        eng = _multi_cache[key] = MultiEngine(devices)
+    return eng.align_packed(algo, scoring, s1, o1, s2, o2, lut)

@@ -78,3 +78,12 @@ def test_wide_alphabet_matches_reference_build(binaries, engine):
     ref = open(os.path.join(GOLDEN, "dropin_wide.ref.txt")).read()
     out = subprocess.run([binaries[3]], capture_output=True, text=True, timeout=300, check=True).stdout
     assert out == ref
+
+
+def test_types_over_two_contexts_matches_reference_build(binaries, engine):
+    """SEQALIB_DEVICES=0,0: the C++ drop-in spreads its batches over two contexts (sa_multi);
+    the printed output is unchanged."""
+    ref = open(os.path.join(GOLDEN, "dropin_types.ref.txt")).read()
+    env = dict(os.environ, SEQALIB_DEVICES="0,0")
+    out = subprocess.run([binaries[1]], capture_output=True, text=True, timeout=300, check=True, env=env).stdout
+    assert out == ref

@@ -195,3 +195,27 @@ def test_device_selects_int32_for_wide_alphabet(engine):
     assert engine.last_plan()[0] == sa.SA_KERNEL_T16_ENDCELL
     o = oracle_align(0, SW, *pairs[5])
     assert (res[5].score, res[5].end_i, res[5].end_j, res[5].ops) == (o["score"], o["end_i"], o["end_j"], o["ops"])
+
+
+def test_multi_context_config5_shard_matches_single(engine):
+    """sa_multi (two contexts on GPU 0 here; one per GPU on a node) over the config-5 shard
+    returns byte for byte what one context returns; the ranges write in place, so there is no
+    host gather step at all."""
+    import time
+    from seqalib_amd.multi import MultiEngine
+    s1, o1, s2, o2 = sa.synth_dna_batch(5_000_000_000, 12500, 2048, 2048, threads=THREADS)
+    sc = sa.ScoringSystem(*SW)
+    t0 = time.perf_counter()
+    ref, ref_ops = engine.align_packed(0, sc, s1, o1, s2, o2)
+    t1 = time.perf_counter()
+    me = MultiEngine([0, 0])
+    try:
+        me.align_packed(0, sc, s1, o1, s2, o2)          # warm the second context's workspace
+        t2 = time.perf_counter()
+        res, ops = me.align_packed(0, sc, s1, o1, s2, o2)
+        t3 = time.perf_counter()
+    finally:
+        me.close()
+    assert res.tobytes() == ref.tobytes()
+    assert ops.tobytes() == ref_ops.tobytes()
+    print(f"single context {1e3 * (t1 - t0):.1f} ms, two contexts on one GPU {1e3 * (t3 - t2):.1f} ms")
