@@ -237,29 +237,55 @@ bool keyed_ok(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
     return bound < 65536;
 }
 
-// T16 kernel (sa_fill_impl.h) preconditions on the scoring and shapes: it keeps 4*H + tag in
-// int16, so every value a cell can take, and every candidate, must stay inside int16 after the
-// scaling; the profile bytes hold 4*s + 3 as int8.  Bounds (allow-mismatch, gap <= 0,
-// mismatch <= match):
-//   SW: 0 <= H <= max(match, 0) * min(m, n)
-//   NW: H[i][j] <= max(match, 0) * min(i, j); H[i][j] >= min(i,j)*mismatch + |i-j|*gap (the
-//       all-diagonal-then-straight path), minimised over the grid at its corner points.
-bool t16_ok(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
-    if (algo != SA_SW && algo != SA_NW) return false;
-    if (!sc->allow_mismatch) return false;
+// T16 kernel (sa_fill_impl.h) preconditions on the scoring and shapes.  It keeps 4*H + tag in
+// int16 and reads 4*s + 3 from an int8 profile (allow-mismatch, gap < 0 for SW / <= 0 for NW,
+// mismatch <= match, |s| small).
+//   NW: a constant offset delta is free for a global recurrence (every candidate of a cell shifts
+//       alike), so the fill keeps 4*(H - delta): T16 needs the whole range of H, bounded by paths
+//       (upper: min(i,j) best diagonals + |i-j| gaps; lower: the all-diagonal and the all-gap
+//       path), to fit 2^14 values around delta.
+//   SW: H >= 0 and the maximum S bounds every cell; a candidate can only wrap once a correct cell
+//       exceeds 8191 - match, and that cell is part of the maximum the fill reports.  When the
+//       bound match * min(m, n) does not prove S small enough, T16 still runs and flags every pair
+//       whose S exceeds retry_above; the int32 variant re-runs exactly those pairs (kFlagRetry).
+struct T16Mode {
+    bool ok = false;
+    int32_t delta = 0;                // NW offset
+    int32_t retry_above = INT_MAX;    // SW: per-pair retry threshold
+};
+T16Mode t16_mode(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
+    T16Mode t;
+    if (algo != SA_SW && algo != SA_NW) return t;
+    if (!sc->allow_mismatch) return t;
     const int64_t MA = sc->match, MI = sc->mismatch, G = sc->gap;
-    if (MA < -32 || MA > 31 || MI < -32 || MI > 31) return false;
-    if (G > 0 || MI > MA || G < -4096) return false;
-    if (algo == SA_SW && G == 0) return false;   // the clamped up term needs gap < 0 (sa_fill_impl.h)
+    if (MA < -32 || MA > 31 || MI < -32 || MI > 31) return t;
+    if (G > 0 || MI > MA || G < -4096) return t;
+    if (algo == SA_SW && G == 0) return t;   // the clamped up term needs gap < 0 (sa_fill_impl.h)
+    if (max_n >= 65535) return t;
     const int64_t m = max_m, n = max_n, k = std::min(m, n);
-    const int64_t hi = std::max<int64_t>(MA, 0) * k;
-    int64_t lo = 0;
-    if (algo == SA_NW) {
-        auto A = [&](int64_t i, int64_t j) { return std::min(i, j) * MI + (i > j ? i - j : j - i) * G; };
-        lo = std::min({A(0, n), A(m, 0), A(k, n), A(m, k), A(k, k), A(m, n), (int64_t)0});
+    if (algo == SA_SW) {
+        t.ok = true;
+        if (4 * std::max<int64_t>(MA, 0) * k + 3 > 32767) t.retry_above = (int32_t)(8191 - std::max<int64_t>(MA, 0));
+        return t;
     }
-    const int64_t cand_lo = 4 * (lo + std::min<int64_t>(std::min(MI, G), 0));
-    return 4 * hi + 3 <= 32767 && cand_lo >= -32768 && max_n < 65535;
+    auto hi_at = [&](int64_t i, int64_t j) {
+        return std::max(std::min(i, j) * MA + (i > j ? i - j : j - i) * G, (i + j) * G);
+    };
+    auto lo_at = [&](int64_t i, int64_t j) {
+        return std::max(std::min(i, j) * MI + (i > j ? i - j : j - i) * G, (i + j) * G);
+    };
+    int64_t hi = INT64_MIN, lo = INT64_MAX;
+    const int64_t pts[7][2] = {{0, 0}, {m, 0}, {0, n}, {k, k}, {m, n}, {k, n}, {m, k}};
+    for (auto& q : pts) {
+        hi = std::max(hi, hi_at(q[0], q[1]));
+        lo = std::min(lo, lo_at(q[0], q[1]));
+    }
+    const int64_t cand_lo = lo + std::min<int64_t>(std::min(MI, G), 0);   // candidates of a cell
+    const int64_t delta = (hi + cand_lo) >> 1;
+    if (4 * (hi - delta) + 3 > 32767 || 4 * (cand_lo - delta) < -32768) return t;
+    t.ok = true;
+    t.delta = (int32_t)delta;
+    return t;
 }
 
 int validate_scoring(sa_ctx* c, int algo, const sa_scoring* s) {
@@ -269,10 +295,11 @@ int validate_scoring(sa_ctx* c, int algo, const sa_scoring* s) {
 }
 
 // T16 by scoring and shape (the batch alphabet is checked on the device, decide_t16).
-bool t16_candidate(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
-    bool t16 = t16_ok(algo, sc, max_m, max_n) && (algo == SA_NW || keyed_ok(algo, sc, max_m, max_n));
-    if (const char* e16 = getenv("SEQALIB_T16")) if (e16[0] == '0') t16 = false;
-    return t16;
+T16Mode t16_candidate(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
+    T16Mode t = t16_mode(algo, sc, max_m, max_n);
+    if (algo == SA_SW && !keyed_ok(algo, sc, max_m, max_n)) t.ok = false;
+    if (const char* e16 = getenv("SEQALIB_T16")) if (e16[0] == '0') t.ok = false;
+    return t;
 }
 
 // Enqueue fill + traceback for pairs [0, npairs) whose inputs are on the device.  Nothing here
@@ -293,7 +320,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     const bool allow = sc->allow_mismatch != 0;
     const bool bits = d_mbits != nullptr;   // generic-Ty path: per-pair match bitmaps
     const bool lut = !bits && d_lutbits != nullptr;
-    const bool t16 = !bits && t16_candidate(algo, sc, max_m, max_n);
+    const T16Mode tm = bits ? T16Mode{} : t16_candidate(algo, sc, max_m, max_n);
+    const bool t16 = tm.ok;
     if (!c->aux) SA_HIP(c, hipMalloc(&c->aux, 2 * kAuxWords * 4));
     if (!c->h_sel) {
         SA_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_sel), 64, hipHostMallocDefault));
@@ -319,6 +347,14 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     }
     vars[nv++] = make_variant(algo, max_m, max_n, npairs, false, !c->no_split);
     c->nvar = nv;
+    // With both variants enqueued, the int32 one may re-run single pairs of a T16 batch
+    // (kFlagRetry) while the T16 traceback still reads its neighbours: one record stride for both.
+    uint64_t dir_stride = 0;
+    for (int k = 0; k < nv; ++k) dir_stride = std::max(dir_stride, vars[k].pl.g.dir_slot);
+    for (int k = 0; k < nv; ++k) {
+        vars[k].slot_bytes += dir_stride - vars[k].pl.g.dir_slot;
+        vars[k].pl.g.dir_slot = dir_stride;
+    }
     uint64_t slot_bytes = 0, sp_bands = 0;
     bool any_split = false;
     for (int k = 0; k < nv; ++k) {
@@ -393,6 +429,9 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         for (int k = 0; k < nv; ++k) {
             const Variant& v = vars[k];
             const Plan& pl = v.pl;
+            // a second SPLIT variant (the int32 re-run of flagged pairs) needs fresh tickets and
+            // hand-off granules
+            if (k > 0 && pl.split) SA_HIP(c, hipMemsetAsync(c->split, 0, 256 + hand_x_off * 8 * aff2, sf));
             uint8_t* dirs = wbase;
             int32_t* rowbuf = reinterpret_cast<int32_t*>(wbase + per_launch * pl.g.dir_slot);
             uint32_t* snap_h = reinterpret_cast<uint32_t*>(rowbuf + per_launch * pl.rowbuf_elems);
@@ -414,6 +453,9 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fp.stage_seq2 = max_n <= kMaxStagedSeq2 ? 1 : 0;
             fp.prof = aux + kAuxProf;
             fp.sel = sel; fp.sel_want = v.t16 ? 1u : 0u;
+            fp.redo = (nv == 2 && !v.t16) ? 1 : 0;
+            fp.t16_delta = v.t16 ? tm.delta : 0;
+            fp.retry_above = v.t16 ? tm.retry_above : INT_MAX;
             fp.snap_h = snap_h; fp.snap_p = snap_p; fp.snap_m = snap_m;
             fp.snap_h_slot = v.snap_h_slot; fp.snap_p_slot = v.snap_p_slot; fp.snap_nch = v.snap_nch;
             fp.split_bands = (uint32_t)sp_bands;
@@ -432,6 +474,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 rp.gap = sc->gap; rp.gap_open = sc->gap_open; rp.gap_extend = sc->gap_extend;
                 rp.cmax = v.cmax ? 1 : 0;
                 rp.sel = sel; rp.sel_want = fp.sel_want;
+                rp.redo = fp.redo; rp.retry_above = fp.retry_above;
                 e = launch_split_reduce(algo, rp, sf);
                 if (e != hipSuccess) return hip_fail(c, e, "split reduce kernel launch");
             }
@@ -962,7 +1005,7 @@ int sa_plan_query_ex(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t ma
                      int nsym, int* kernel, int* R, int* W, uint64_t* ws_bytes_per_pair) {
     if (algo < SA_SW || algo > SA_GLOBAL_GOTOH) return fail(nullptr, SA_ERR_ARG, "unknown algorithm");
     if (!sc) return fail(nullptr, SA_ERR_ARG, "scoring is NULL");
-    const bool cand = t16_candidate(algo, sc, max_m, max_n);
+    const bool cand = t16_candidate(algo, sc, max_m, max_n).ok;
     const Variant v16 = make_variant(algo, max_m, max_n, npairs, true, true);
     const Variant v32 = make_variant(algo, max_m, max_n, npairs, false, true);
     const Variant& v = (cand && nsym <= 4) ? v16 : v32;

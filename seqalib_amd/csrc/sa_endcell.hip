@@ -34,7 +34,7 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
     const uint32_t symp = P.prof[4];
     const uint32_t pidx = P.pair_base + slot;
     sa_result res = P.res[pidx];
-    if (res.reserved == 0 || (res.flags & SA_FLAG_BAD_SHAPE)) return;   // uniform over the wave
+    if (res.reserved == 0 || (res.flags & (SA_FLAG_BAD_SHAPE | kFlagRetry))) return;   // uniform over the wave
     const int c = (int)res.reserved - 1;
     const int S = res.score;
     const int iend = res.end_i;
@@ -129,10 +129,15 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
 // row-major maximum; global modes: H[m][n] from the band holding row m.  One thread per pair.
 template <int ALG>
 __global__ void split_reduce_kernel(SplitReduceParams P) {
-    if (sa_skip(P.sel, P.sel_want)) return;
+    bool redo = false;
+    if (sa_skip(P.sel, P.sel_want)) {
+        if (!P.redo) return;
+        redo = true;
+    }
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     if (slot >= P.count) return;
     const uint32_t pidx = P.pair_base + slot;
+    if (redo && !(P.res[pidx].flags & kFlagRetry)) return;
     const int m = (int)(P.off1[pidx + 1] - P.off1[pidx]);
     const int n = (int)(P.off2[pidx + 1] - P.off2[pidx]);
     sa_result r = {};
@@ -162,6 +167,7 @@ __global__ void split_reduce_kernel(SplitReduceParams P) {
         } else {
             r.score = h; r.end_i = bi; r.end_j = bj;
         }
+        if (B != 0 && h > P.retry_above) r.flags |= kFlagRetry;
     } else {
         r.end_i = m;
         r.end_j = n;
@@ -173,6 +179,7 @@ __global__ void split_reduce_kernel(SplitReduceParams P) {
             r.score = q[4 * (B - 1)];
         }
     }
+    if (redo) r.flags |= kFlagRedo;
     P.res[pidx] = r;
 }
 

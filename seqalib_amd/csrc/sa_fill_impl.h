@@ -126,7 +126,13 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     __shared__ int s_red[16 * 3];
     __shared__ int s_score;   // H[m][n] for the global modes, stored by the owning lane
 
-    if (sa_skip(P.sel, P.sel_want)) return;   // the batch selected the other kernel variant
+    // the batch selected the other kernel variant: leave -- except an int32 launch re-running the
+    // pairs a T16 fill flagged kFlagRetry (checked below, once the pair is known)
+    bool redo = false;
+    if (sa_skip(P.sel, P.sel_want)) {
+        if (!P.redo) return;
+        redo = true;
+    }
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
     const int W = P.waves;
@@ -145,6 +151,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
         slot = blockIdx.x;
     }
     const uint32_t pidx = P.pair_base + slot;
+    if (redo && !(P.res[pidx].flags & kFlagRetry)) return;   // uniform over the workgroup
     const uint64_t o1 = P.off1[pidx];
     const uint64_t o2 = P.off2[pidx];
     const int m = (int)(P.off1[pidx + 1] - o1);
@@ -451,7 +458,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
             else vs = T16 ? (int)t16_code8(symp, s2[c]) : (int)s2[c];
             if (band == 0) {
                 const int J = c + 1;
-                if constexpr (ALG == SA_NW) vh = SC * J * G;
+                if constexpr (ALG == SA_NW) vh = SC * (J * G - P.t16_delta);
                 else if constexpr (ALG == SA_GLOBAL_GOTOH) vh = GO + J * GE;
             } else if constexpr (SPLIT) {
                 // polled below, after the branch (the wave must poll together)
@@ -505,7 +512,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                         if constexpr (T16) a[r] = row < m ? (int)P.prof[t16_code8(symp, s1[row]) >> 3] : (CMAX ? (int)0x80808080u : 0);
                         else a[r] = row < m ? (int)s1[row] : 0;
                         const int i = row + 1;
-                        if constexpr (ALG == SA_NW) Hp[r] = SC * i * G;
+                        if constexpr (ALG == SA_NW) Hp[r] = SC * (i * G - P.t16_delta);
                         else if constexpr (ALG == SA_GLOBAL_GOTOH) Hp[r] = GO + i * GE;
                         else Hp[r] = 0;
                         Yp[r] = -10000;
@@ -515,7 +522,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                     lkey = 0;
                     cml = 0;
                     split_load(band, 0, pre_h, pre_x);
-                    if constexpr (ALG == SA_NW) prev_up = SC * row0 * G;
+                    if constexpr (ALG == SA_NW) prev_up = SC * (row0 * G - P.t16_delta);
                     else if constexpr (ALG == SA_GLOBAL_GOTOH) prev_up = row0 == 0 ? 0 : GO + row0 * GE;
                     else prev_up = 0;
                 }
@@ -615,7 +622,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                             int v = 0;
 #pragma unroll
                             for (int r = 0; r < R; ++r) v = (r == rr) ? Hp[r] : v;
-                            s_score = T16 ? ((int)(int16_t)(v & 0xffff)) / 4 : v;
+                            s_score = T16 ? ((int)(int16_t)(v & 0xffff)) / 4 + P.t16_delta : v;
                         }
                     }
                 }
@@ -672,6 +679,8 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
             } else {
                 r.score = h; r.end_i = bi; r.end_j = bjj;
             }
+            if (T16 && B != 0 && h > P.retry_above) r.flags |= kFlagRetry;
+            if (redo) r.flags |= kFlagRedo;
             P.res[pidx] = r;
         }
     } else {
@@ -686,6 +695,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
             } else {
                 r.score = s_score;
             }
+            if (redo) r.flags |= kFlagRedo;
             P.res[pidx] = r;
         }
     }

@@ -11,6 +11,12 @@ namespace sa {
 // How the fill decides match(Seq1[i-1], Seq2[j-1]) (sa_fill_impl.h).
 constexpr int kMatchEq = 0, kMatchLut = 1, kMatchBits = 2;
 
+// Internal per-pair flags (never returned: the int32 redo clears them).  kFlagRetry: a T16 SW
+// fill found a maximum above FillParams::retry_above, where a 16-bit candidate may have wrapped,
+// so the pair is re-run by the int32 variant; kFlagRedo: the int32 variant re-ran it (the T16
+// end-cell replay and traceback skip it, the int32 traceback walks it).
+constexpr uint32_t kFlagRetry = 1u << 30, kFlagRedo = 1u << 31;
+
 struct FillParams {
     const uint8_t* seq1;
     const uint64_t* off1;
@@ -36,9 +42,15 @@ struct FillParams {
     // symbol of code c) and prof[c] holds, in byte c', the tagged substitution term
     // 4*s(sym c, sym c') + 3 as int8 (written on the device by decide_t16, sa_alphabet.hip).
     const uint32_t* prof;
-    // device-side kernel selection: the launch runs only if *sel == sel_want (sel NULL: always)
+    // device-side kernel selection: the launch runs only if *sel == sel_want (sel NULL: always);
+    // redo: an int32 launch the batch did not select still re-runs the pairs flagged kFlagRetry
     const uint32_t* sel;
     uint32_t sel_want;
+    int redo;
+    // T16 only: NW keeps 4 * (H - t16_delta) (a constant offset that centres the score range in
+    // int16); SW flags pairs whose maximum exceeds retry_above (INT_MAX when proven to fit)
+    int32_t t16_delta;
+    int32_t retry_above;
     // CMAX only (see sa_fill_impl.h): per-slot snapshots [band][chunk][lane] of the R 16-bit row
     // values (R/2 words) and of the diagonal input (1 word); snap_nch = chunks per band.
     uint32_t* snap_h;
@@ -68,6 +80,8 @@ struct SplitReduceParams {
     int cmax;
     const uint32_t* sel;
     uint32_t sel_want;
+    int redo;              // as FillParams::redo
+    int32_t retry_above;   // T16 SW: flag pairs with a larger maximum (kFlagRetry)
 };
 hipError_t launch_split_reduce(int algo, const SplitReduceParams& p, hipStream_t stream);
 
@@ -141,6 +155,14 @@ hipError_t launch_decide_t16(const uint32_t* lutbits, int match, int mismatch, u
 // (uniform over the grid; sel NULL = unconditional).
 __device__ __forceinline__ bool sa_skip(const uint32_t* sel, uint32_t want) {
     return sel != nullptr && *sel != want;
+}
+// Traceback of a pair: by the launch of the variant the batch selected, except the pairs the
+// int32 variant re-ran (kFlagRedo), which its own traceback walks.
+template <typename TP>
+__device__ __forceinline__ bool tb_mine(const TP& P, uint32_t flags) {
+    if (!P.sel) return true;
+    const bool redone = (flags & kFlagRedo) != 0;
+    return *P.sel == P.sel_want ? !redone : redone;
 }
 hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
 // One wave per pair (sa_traceback_wave.hip): the few-pairs traceback.

@@ -65,20 +65,21 @@ __device__ unsigned long long g_tb_stats[8];
 #endif
 
 template <int ALG, int R, bool LUT>
-__global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {
+__global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {   // tb_mine: sa_internal.h
     constexpr int BPC = bits_per_cell(ALG), BPS = R * BPC / 8, SPP = 16 / BPS;
     static_assert(BPS <= 16 && (SPP & (SPP - 1)) == 0, "one packet per step record");
     constexpr int kTbLanes = R >= 32 ? 1 : 32 / R;
     constexpr int kTbGroups = 32 / SPP;
     static_assert(kTbLanes * kTbGroups <= kTbChunks, "flag window <= 32 packets");
     __shared__ __attribute__((aligned(16))) uint8_t s_tb[kTbLdsBytes];
-    if (sa_skip(P.sel, P.sel_want)) return;   // the batch selected the other kernel variant
     const int lane = threadIdx.x;
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     if (slot >= P.count) return;
     const uint32_t pidx = P.pair_base + slot;
     sa_result res = P.res[pidx];
     if (res.flags & SA_FLAG_BAD_SHAPE) return;
+    if (!tb_mine(P, res.flags)) return;
+    res.flags &= ~(kFlagRetry | kFlagRedo);
     const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
     const int m = (int)(P.off1[pidx + 1] - o1);
     const int n = (int)(P.off2[pidx + 1] - o2);

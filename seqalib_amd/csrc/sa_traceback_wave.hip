@@ -119,7 +119,6 @@ __global__ __launch_bounds__(64) void traceback_wave_kernel(TbParams P) {
     constexpr bool AFF = is_affine(ALG);
     constexpr uint32_t FD = AFF ? 8u : 2u;                               // fD bit of a cell byte
     __shared__ __attribute__((aligned(16))) uint8_t s_win[kTwD * kTwP];
-    if (sa_skip(P.sel, P.sel_want)) return;   // the batch selected the other kernel variant
     __shared__ __attribute__((aligned(16))) uint8_t s_seq1[kTwS1];
     __shared__ __attribute__((aligned(16))) uint8_t s_seq2[kTwS2];
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];
@@ -130,6 +129,8 @@ __global__ __launch_bounds__(64) void traceback_wave_kernel(TbParams P) {
     const uint32_t pidx = P.pair_base + slot;
     sa_result res = P.res[pidx];
     if (res.flags & SA_FLAG_BAD_SHAPE) return;
+    if (!tb_mine(P, res.flags)) return;
+    res.flags &= ~(kFlagRetry | kFlagRedo);
     const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
     const int m = (int)(P.off1[pidx + 1] - o1);
     const int n = (int)(P.off2[pidx + 1] - o2);

@@ -106,9 +106,14 @@ def test_config_plans(m, n, npairs, plan):
 
 
 def test_plan_t16_eligibility_by_scoring():
-    # NW at its default scoring (-1, 2, -1) on 4096^2: 4 * 2 * 4096 + 3 > 32767 -> int32
-    assert sa.plan_query_ex(1, sa.ScoringSystem(-1, 2, -1), 4096, 4096, 10000)[0] == sa.SA_KERNEL_INT32
+    # NW at its default scoring (-1, 2, -1): H in [-4096, 8192] on 4096^2 fits int16 as 4*(H - delta);
+    # on 8192^2 the range is 24,577 wide -> int32
+    assert sa.plan_query_ex(1, sa.ScoringSystem(-1, 2, -1), 4096, 4096, 10000)[0] == sa.SA_KERNEL_T16
+    assert sa.plan_query_ex(1, sa.ScoringSystem(-1, 2, -1), 8192, 8192, 10000)[0] == sa.SA_KERNEL_INT32
     assert sa.plan_query_ex(1, sa.ScoringSystem(-1, 1, -1), 4096, 4096, 10000)[0] == sa.SA_KERNEL_T16
+    # SW: any size with n < 65535 (pairs whose maximum passes the int16 headroom re-run on int32)
+    assert sa.plan_query_ex(0, sa.ScoringSystem(-1, 1, -1), 8192, 8192, 10000)[0] == sa.SA_KERNEL_T16_ENDCELL
+    assert sa.plan_query_ex(0, sa.ScoringSystem(-1, 1, -1), 8192, 70000, 10000)[0] == sa.SA_KERNEL_INT32
     # gap 0: the clamped up term needs gap < 0
     assert sa.plan_query_ex(0, sa.ScoringSystem(0, 1, -1), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32
     # affine: int32 flags

@@ -260,12 +260,17 @@ def test_t16_eligibility(engine, algo):
     five = dna[:-1] + [(dna[-1][0] + b"N", dna[-1][1])]
     compare_with_oracle(engine, algo, (-1, 2, -1), five)
     assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
-    # scores that would overflow 4*H in int16 -> int32 kernel
+    # scores past the int16 headroom of 4*H: SW runs T16 and re-runs the pair on int32 (per-pair
+    # retry); NW centres its score range with a constant offset, and only a range wider than
+    # 2^14 goes to the int32 kernel
     big = [(sa.synth_dna(77, 3000), sa.synth_dna(77, 3000))]
     compare_with_oracle(engine, algo, (-1, 3, -1), big)
-    assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
+    assert engine.last_plan()[0] in T16_KERNELS
     compare_with_oracle(engine, algo, (-1, 2, -1), big)
     assert engine.last_plan()[0] in T16_KERNELS
+    if algo == 1:
+        compare_with_oracle(engine, algo, (-1, 5, -1), big)
+        assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
     # !allowMismatch -> int32 kernel
     compare_with_oracle(engine, algo, (-2, 1, -1, False), dna)
     assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
@@ -274,6 +279,32 @@ def test_t16_eligibility(engine, algo):
         # gap < 0 (sa_fill_impl.h), so the int32 kernel takes it
         compare_with_oracle(engine, algo, (0, 1, -1), dna)
         assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
+
+
+def test_t16_range_extension_large_probes(engine):
+    """The reference's own 8192 x 8192 SW probe and its 4096 x 4096 NW probe at NW's default
+    scoring (-1, 2, -1) run on the T16 kernel (SW: max score proven small at run time; NW: the
+    constant offset) and equal the reference's golden vectors."""
+    big = {e["id"]: e for e in load_golden("large.jsonl")}
+    for pid in ("probe8192/sw/-1_1_-1/equal", "probe4096/nw/-1_2_-1/equal"):
+        assert check_golden(engine, [big[pid]]) == 1
+        assert engine.last_plan()[0] in T16_KERNELS, pid
+
+
+def test_t16_sw_retry_mixed_batch(engine):
+    """A T16 SW batch in which a few pairs score above the int16 headroom (identical 9,000-long
+    sequences: score 9,000): exactly those pairs are re-run on the int32 kernel, on the batch
+    plan (>= 1024 pairs) and on the few-pairs plan, and every pair equals the oracle."""
+    rng = np.random.default_rng(17)
+    pairs = [(sa.synth_dna(60_000 + k, int(rng.integers(50, 400))), sa.synth_dna(70_000 + k, int(rng.integers(50, 400))))
+             for k in range(1100)]
+    hot = sa.synth_dna(80_000, 9000)
+    pairs[3] = (hot, hot)
+    pairs[700] = (hot[:8500], sa.synth_mutate(hot, 3)[:8600])
+    compare_with_oracle(engine, 0, (-1, 1, -1), pairs)
+    assert engine.last_plan()[0] in T16_KERNELS
+    compare_with_oracle(engine, 0, (-1, 1, -1), [pairs[3], pairs[5], pairs[700]])
+    assert engine.last_plan()[0] in T16_KERNELS
 
 
 def test_endcell_replay_vs_oracle(engine):
