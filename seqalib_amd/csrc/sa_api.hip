@@ -104,10 +104,18 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t
         while (p.R < rmax && (uint64_t)kWave * p.R * p.W < max_m) p.R *= 2;
     } else if (split_ok(max_m, max_n, npairs, allow_split)) {
         // Few pairs, several bands each: every band its own single-wave workgroup (on its own
-        // SIMD, anywhere on the chip), bands of a pair chained through HBM/L2 hand-offs.  Short
-        // bands (R = 4) give the most concurrent bands; R = 8 once there are plenty.
+        // SIMD, anywhere on the chip), bands of a pair chained through HBM/L2 hand-offs.  A pair
+        // then takes about (n + 63 + (bands - 1) * lag) steps of one lone wave each, and a step
+        // costs ~40 + 36 R cycles (tools/microbench_lone.hip): short bands win while the chip has
+        // a SIMD for every band -- R = 2 (128 rows) -- then R = 4 and 8 for throughput.
         p.W = 1;
-        p.R = (uint64_t)npairs * ((max_m + 8 * kWave - 1) / (8 * kWave)) >= 2048 ? 8 : 4;
+        p.R = 8;
+        for (int r : {2, 4}) {
+            if ((uint64_t)npairs * ((max_m + (uint64_t)kWave * r - 1) / ((uint64_t)kWave * r)) <= 1024) {
+                p.R = r;
+                break;
+            }
+        }
         p.split = true;
     } else {
         // Few pairs: widen the workgroup instead (up to 16 waves) to use one CU fully.
@@ -117,10 +125,10 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t
         p.W = (int)std::max<uint64_t>(1, std::min<uint64_t>(16, w));
         while (p.R > 4 && (uint64_t)kWave * (p.R / 2) * p.W >= max_m) p.R /= 2;
     }
-    // tuning override: SEQALIB_PLAN="R,W" (W = 0: SPLIT plan with R in {4, 8})
+    // tuning override: SEQALIB_PLAN="R,W" (W = 0: SPLIT plan with R in {1, 2, 4, 8})
     if (const char* ov = getenv("SEQALIB_PLAN")) {
         int r = 0, w = 0;
-        if (sscanf(ov, "%d,%d", &r, &w) == 2 && w == 0 && (r == 4 || r == 8)) {
+        if (sscanf(ov, "%d,%d", &r, &w) == 2 && w == 0 && (r == 1 || r == 2 || r == 4 || r == 8)) {
             p.R = r;
             p.W = 1;
             p.split = true;
@@ -157,7 +165,7 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
     v.pl = make_plan(algo, max_m, max_n, npairs, t16, allow_split);
     // CMAX end-cell tracking (sa_fill_impl.h / sa_endcell.hip): T16 SW on one-wave plans with an
     // end-cell replay instantiation (R <= 32)
-    v.cmax = t16 && algo == SA_SW && v.pl.W == 1 && v.pl.R >= 4 && v.pl.R <= 32;
+    v.cmax = t16 && algo == SA_SW && v.pl.W == 1 && v.pl.R >= 2 && v.pl.R <= 32;
     if (const char* ec = getenv("SEQALIB_CMAX")) if (ec[0] == '0') v.cmax = false;
     if (v.cmax) {
         v.snap_nch = chunks_per_band(max_n);

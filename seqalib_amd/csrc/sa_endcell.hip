@@ -198,6 +198,7 @@ hipError_t launch_split_reduce(int algo, const SplitReduceParams& p, hipStream_t
 hipError_t launch_endcell(int R, const EndcellParams& p, hipStream_t stream) {
     const dim3 grid(p.count), block(64);
     switch (R) {
+        case 2: hipLaunchKernelGGL(endcell_kernel<2>, grid, block, 0, stream, p); break;
         case 4: hipLaunchKernelGGL(endcell_kernel<4>, grid, block, 0, stream, p); break;
         case 8: hipLaunchKernelGGL(endcell_kernel<8>, grid, block, 0, stream, p); break;
         case 16: hipLaunchKernelGGL(endcell_kernel<16>, grid, block, 0, stream, p); break;

@@ -104,7 +104,8 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     constexpr bool BITS = MM == kMatchBits;
     constexpr bool AFF = ALG >= SA_LOCAL_GOTOH;
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
-    constexpr int BPC = AFF ? 4 : 2;
+    constexpr int FBITS = AFF ? 4 : 2;            // flag bits per cell
+    constexpr int BPC = record_bpc(ALG, R);      // record bits per cell (padding above the flags)
     constexpr int RB = R * BPC;                // bits per record
     constexpr int BPS = RB / 8;                // bytes per record
     constexpr int RW = (RB + 31) / 32;         // words per record
@@ -276,12 +277,12 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     "v_add_u16 %[dn], %[hp], %[dn]\n\t"
 #define SA_T16_TAIL                                                                          \
     "v_and_b32 %[hp], -4, %[t0]\n\t"                                                         \
-    "v_alignbit_b32 %[rec], %[t0], %[rec], 2\n\t"
+    "v_alignbit_b32 %[rec], %[t0], %[rec], %[bpc]\n\t"
 #define SA_T16_KEY                                                                           \
     "v_lshl_or_b32 %[t1], %[hp], 14, %[jk]\n\t"                                              \
     "v_max_u32 %[bh], %[bh], %[t1]\n\t"
 #define SA_T16_OUT [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r]), [rec] "+v"(rw)
-#define SA_T16_IN [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL)
+#define SA_T16_IN [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL), [bpc] "i"(BPC)
 #define SA_T16_PW [tabn] "v"(tabn), [sym] "v"(sym)
                     if (r + 1 < R) {
                         uint32_t dn;
@@ -332,6 +333,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 int D;
                 if constexpr (ALLOW) D = hd + (v ? MA : MI);
                 else D = v ? hd + MA : INT_MIN;
+                if constexpr (BPC > FBITS) rw <<= BPC - FBITS;   // record padding (R <= 2)
                 if constexpr (!AFF) {
                     const int U = hu + G;
                     const int L = Hp[r] + G;
@@ -711,7 +713,7 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
     const size_t lds = lds_layout(lut, is_affine(ALG), p.waves, p.stage_seq2 ? p.max_n : 0).total;
     if (lds > kMaxLds) return hipErrorInvalidConfiguration;
     const bool split = v.split;
-    if (split && (p.waves != 1 || (R != 4 && R != 8))) return hipErrorInvalidConfiguration;
+    if (split && (p.waves != 1 || (R != 1 && R != 2 && R != 4 && R != 8))) return hipErrorInvalidConfiguration;
     if constexpr (ALG == SA_SW || ALG == SA_NW) {
         if (v.t16) {
             if (!allow || (LOCAL && !keyed)) return hipErrorInvalidValue;
@@ -735,9 +737,15 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
             SA_LAUNCH16S(16, false)
             SA_LAUNCH16S(32, false)
             SA_LAUNCH16S(64, false)
+            SA_LAUNCH16S(2, true)
             SA_LAUNCH16S(4, true)
             SA_LAUNCH16S(8, true)
 #undef SA_LAUNCH16S
+            if (R == 1 && split && !v.cmax) {   // R = 1: the per-cell key (CMAX pairs rows)
+                hipLaunchKernelGGL((fill_kernel<ALG, 1, kMatchEq, true, LOCAL, true, false, true>), dim3(grid), block,
+                                   lds, stream, p);
+                return hipGetLastError();
+            }
             return hipErrorInvalidValue;
         }
     }
@@ -770,6 +778,27 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
     SA_LAUNCH_R(8)
     SA_LAUNCH_R(16)
 #undef SA_LAUNCH_R
+    // R = 1, 2: the few-pairs (SPLIT) plans only
+#define SA_LAUNCH_S(RR, MMV, AA, KK)                                                            \
+    if (split && R == RR && mm == MMV && allow == AA && keyed == KK) {                          \
+        hipLaunchKernelGGL((fill_kernel<ALG, RR, MMV, AA, KK, false, false, true>), dim3(grid), block, lds, stream, p); \
+        return hipGetLastError();                                                               \
+    }
+#define SA_LAUNCH_SK(RR, MMV, AA) \
+    SA_LAUNCH_S(RR, MMV, AA, false) \
+    if constexpr (LOCAL) { SA_LAUNCH_S(RR, MMV, AA, true) }
+#define SA_LAUNCH_SR(RR)                 \
+    SA_LAUNCH_SK(RR, kMatchEq, true)     \
+    SA_LAUNCH_SK(RR, kMatchEq, false)    \
+    SA_LAUNCH_SK(RR, kMatchLut, true)    \
+    SA_LAUNCH_SK(RR, kMatchLut, false)   \
+    SA_LAUNCH_SK(RR, kMatchBits, true)   \
+    SA_LAUNCH_SK(RR, kMatchBits, false)
+    SA_LAUNCH_SR(1)
+    SA_LAUNCH_SR(2)
+#undef SA_LAUNCH_SR
+#undef SA_LAUNCH_SK
+#undef SA_LAUNCH_S
 #undef SA_LAUNCH_K
 #undef SA_LAUNCH
     return hipErrorInvalidValue;

@@ -66,6 +66,11 @@ constexpr uint32_t kMaxStagedSeq2 = 48 * 1024;
 
 SA_HD constexpr bool is_affine(int algo) { return algo >= 2; }
 SA_HD constexpr int bits_per_cell(int algo) { return is_affine(algo) ? 4 : 2; }
+// Record bits per cell in HBM: the flag bits, padded (above them) to 4 bits at R = 2 and 8 bits at
+// R = 1, so that one lane's record of one step is always at least a byte.  R = 1 and 2 are the
+// few-pairs (SPLIT) plans: their bands are short so that a lone wave's critical-path step stays
+// cheap, and their records are a negligible share of the HBM traffic.
+SA_HD constexpr int record_bpc(int algo, int R) { return R == 1 ? 8 : (R == 2 ? 4 : bits_per_cell(algo)); }
 
 struct Geom {
     int R;              // rows per lane
@@ -86,7 +91,7 @@ SA_HD Geom make_geom(int algo, int R, uint32_t max_m, uint32_t max_n, bool tagge
     Geom g;
     g.R = R;
     g.tagged = tagged;
-    g.bpc = bits_per_cell(algo);
+    g.bpc = record_bpc(algo, R);
     g.bps = R * g.bpc / 8;
     g.spp = g.bps >= 16 ? 1 : 16 / g.bps;
     g.pps = g.bps > 16 ? g.bps / 16 : 1;

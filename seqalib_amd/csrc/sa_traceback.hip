@@ -66,10 +66,10 @@ __device__ unsigned long long g_tb_stats[8];
 
 template <int ALG, int R, bool LUT>
 __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {   // tb_mine: sa_internal.h
-    constexpr int BPC = bits_per_cell(ALG), BPS = R * BPC / 8, SPP = 16 / BPS;
-    static_assert(BPS <= 16 && (SPP & (SPP - 1)) == 0, "one packet per step record");
-    constexpr int kTbLanes = R >= 32 ? 1 : 32 / R;
+    constexpr int BPC = record_bpc(ALG, R), BPS = R * BPC / 8, SPP = 16 / BPS;
+    static_assert(BPS >= 1 && BPS <= 16 && (SPP & (SPP - 1)) == 0, "one packet per step record");
     constexpr int kTbGroups = 32 / SPP;
+    constexpr int kTbLanes = R >= 32 ? 1 : (32 / R < kTbChunks / kTbGroups ? 32 / R : kTbChunks / kTbGroups);
     static_assert(kTbLanes * kTbGroups <= kTbChunks, "flag window <= 32 packets");
     __shared__ __attribute__((aligned(16))) uint8_t s_tb[kTbLdsBytes];
     const int lane = threadIdx.x;
@@ -331,7 +331,8 @@ hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStr
         return hipGetLastError();                                                          \
     }
 #define SA_TB_A(AA) SA_TB(AA, 4, false) SA_TB(AA, 8, false) SA_TB(AA, 16, false) \
-                    SA_TB(AA, 4, true) SA_TB(AA, 8, true) SA_TB(AA, 16, true)
+                    SA_TB(AA, 4, true) SA_TB(AA, 8, true) SA_TB(AA, 16, true)   \
+                    SA_TB(AA, 1, false) SA_TB(AA, 2, false) SA_TB(AA, 1, true) SA_TB(AA, 2, true)
     SA_TB_A(SA_SW)
     SA_TB_A(SA_NW)
     SA_TB(SA_SW, 32, false) SA_TB(SA_SW, 32, true) SA_TB(SA_NW, 32, false) SA_TB(SA_NW, 32, true)

@@ -60,7 +60,7 @@ __device__ __attribute__((noinline)) void tw_decode(const uint8_t* dir, const ui
                                                     int n, uint32_t max_m, uint32_t max_n, bool tagged, bool vrec, int i0,
                                                     int j0, tw_u8* win, tw_u8* sq1, tw_u8* sq2,
                                                     const tw_u32* lut) {
-    constexpr int BPC = bits_per_cell(ALG);
+    constexpr int BPC = bits_per_cell(ALG);   // flag bits (records may pad above them: record_bpc)
     constexpr uint32_t FMASK = (1u << BPC) - 1u;
     constexpr int NS1 = (kTwS1 + 63) / 64, NS2 = (kTwS2 + 63) / 64;
     const int lane = threadIdx.x;
@@ -315,7 +315,8 @@ hipError_t launch_traceback_wave(int algo, int R, bool lut, const TbParams& p, h
         return hipGetLastError();                                                             \
     }
 #define SA_TBW_A(AA) SA_TBW(AA, 4, false) SA_TBW(AA, 8, false) SA_TBW(AA, 16, false) \
-                     SA_TBW(AA, 4, true) SA_TBW(AA, 8, true) SA_TBW(AA, 16, true)
+                     SA_TBW(AA, 4, true) SA_TBW(AA, 8, true) SA_TBW(AA, 16, true)   \
+                     SA_TBW(AA, 1, false) SA_TBW(AA, 2, false) SA_TBW(AA, 1, true) SA_TBW(AA, 2, true)
     SA_TBW_A(SA_SW)
     SA_TBW_A(SA_NW)
     SA_TBW(SA_SW, 32, false) SA_TBW(SA_SW, 32, true) SA_TBW(SA_NW, 32, false) SA_TBW(SA_NW, 32, true)

@@ -64,10 +64,12 @@ def test_scoring_overloads_mirror_reference():
 def test_plan_and_layout(algo, shape):
     m, n, npairs = shape
     R, W, dir_bytes, row_bytes = sa.plan_query(algo, m, n, npairs)
-    assert R in (4, 8, 16) and 1 <= W <= 16
+    assert R in (2, 4, 8, 16) and 1 <= W <= 16
     bands = -(-m // (64 * R))
     assert W <= max(bands, 1)
-    bpc = 4 if algo >= 2 else 2
+    bpc = 4 if (algo >= 2 or R <= 2) else 2   # sa_layout.h record_bpc: padded at R <= 2
+    if R == 1:
+        bpc = 8
     steps_pad = -(-(n + 63) // 32) * 32
     assert dir_bytes == bands * steps_pad * 64 * R * bpc // 8
     assert row_bytes == (2 if algo >= 2 else 1) * max(n, 1) * 4
@@ -144,7 +146,8 @@ def cell_byte(R, bpc, max_n, i, j, tagged=False):
 
 @pytest.mark.parametrize("R,bpc,tagged", [(4, 2, False), (8, 2, False), (16, 2, False), (4, 4, False),
                                           (8, 4, False), (16, 4, False), (4, 2, True), (8, 2, True),
-                                          (16, 2, True)])
+                                          (16, 2, True), (1, 8, False), (1, 8, True), (2, 4, False),
+                                          (2, 4, True)])
 def test_flag_layout_is_a_bijection(R, bpc, tagged):
     """Every cell of a band gets its own bits, records pack exactly R*bpc bits per lane-step."""
     max_n = 70

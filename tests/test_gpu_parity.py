@@ -204,19 +204,28 @@ def test_split_plan_vs_oracle(engine, algo, monkeypatch):
     """Few pairs take the multi-workgroup plan: one single-wave workgroup per (pair, band), band
     b+1 polling band b's last row through write-through {tag, value} granules (sa_fill_impl.h,
     SPLIT).  Every scoring of the algorithm (T16 + end-cell replay for DNA SW/NW with
-    allow-mismatch, int32 otherwise), R = 4 and R = 8, and a custom match table, against the
-    oracle; the result must not depend on the plan."""
+    allow-mismatch, int32 otherwise), R = 2 (the default: padded records, sa_layout.h
+    record_bpc), R = 1, 4 and 8 forced, and a custom match table, against the oracle; the result
+    must not depend on the plan."""
     pairs = split_pairs(40 + algo)
+    max_m = max(len(a) for a, _ in pairs)
+    # sa_api.hip make_plan: the shortest bands (R = 2, then 4) while every band has a SIMD
+    R0 = next((r for r in (2, 4) if len(pairs) * -(-max_m // (64 * r)) <= 1024), 8)
     for args in SCORINGS[algo]:
         compare_with_oracle(engine, algo, args, pairs)
-        assert engine.last_plan()[1:] == (4, 0), args
+        assert engine.last_plan()[1:] == (R0, 0), args
         assert all(r.flags & sa.SA_FLAG_TIMEOUT == 0 for r in engine.align(algo, sc_obj(args), pairs[:2]))
-    monkeypatch.setenv("SEQALIB_PLAN", "8,0")
-    compare_with_oracle(engine, algo, SCORINGS[algo][0], pairs)
-    assert engine.last_plan()[1:] == (8, 0)
+    for r in (1, 2, 4, 8):
+        monkeypatch.setenv("SEQALIB_PLAN", f"{r},0")
+        for args in SCORINGS[algo][:2]:
+            compare_with_oracle(engine, algo, args, pairs)
+            assert engine.last_plan()[1:] == (r, 0), (r, args)
     monkeypatch.delenv("SEQALIB_PLAN")
     compare_with_oracle(engine, algo, SCORINGS[algo][0], pairs, "purine")
-    assert engine.last_plan()[1:] == (4, 0)
+    assert engine.last_plan()[1:] == (R0, 0)
+    # one long pair (configs 2 and 4): R = 2
+    compare_with_oracle(engine, algo, SCORINGS[algo][0], pairs[1:2])
+    assert engine.last_plan()[1:] == (2, 0)
 
 
 T16_KERNELS = (sa.SA_KERNEL_T16, sa.SA_KERNEL_T16_ENDCELL)

@@ -61,7 +61,7 @@ def rate_of(op, R):
 
 def steady_block(asm, name):
     st = asm.find(name + ":")
-    en = asm.find("s_endpgm", st)
+    en = asm.find(".Lfunc_end", st)   # not the first s_endpgm: the variant guard returns early
     blocks, cur = [], []
     for line in asm[st:en].split("\n"):
         if re.match(r"^\.LBB|^_Z|^; %bb\.", line):
