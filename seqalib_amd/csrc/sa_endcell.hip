@@ -20,6 +20,7 @@
 
 namespace sa {
 
+
 __device__ __forceinline__ uint32_t ec_code8(uint32_t sp, uint32_t b) {
     return (b == ((sp >> 8) & 255u) ? 8u : 0u) | (b == ((sp >> 16) & 255u) ? 16u : 0u) |
            (b == (sp >> 24) ? 24u : 0u);

@@ -95,6 +95,26 @@ constexpr int fill_max_threads() { return R >= 32 ? 256 : 1024; }
 // one expiry the workgroup stops waiting altogether (the pair is flagged SA_FLAG_TIMEOUT).
 constexpr uint64_t kSplitWaitTicks = 20000000ull;
 
+#ifdef SA_TB_STATS
+// Debug build only (-DSA_TB_STATS, tools/split_stats.py): per SPLIT ticket {slot * bands + band,
+// start, end, ticks spent polling for the producer} in s_memrealtime ticks (100 MHz, chip-wide).
+// One copy per fill translation unit (no relocatable device code), read with
+// sa_debug_split_stats_<algo> (SA_SPLIT_STATS_ACCESSOR in sa_fill_{sw,nw,lg,gg}.hip).
+static __device__ unsigned long long g_split_stats[4096][4];
+#define SA_SPLIT_STATS_ACCESSOR(NAME)                                                               \
+    extern "C" int NAME(unsigned long long* out, int reset) {                                       \
+        if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_split_stats), sizeof(g_split_stats)) != hipSuccess) \
+            return 1;                                                                               \
+        if (reset) {                                                                                \
+            static unsigned long long z[4096][4];                                                   \
+            if (hipMemcpyToSymbol(HIP_SYMBOL(g_split_stats), z, sizeof(z)) != hipSuccess) return 1; \
+        }                                                                                           \
+        return 0;                                                                                   \
+    }
+#else
+#define SA_SPLIT_STATS_ACCESSOR(NAME)
+#endif
+
 // MM: how a cell learns whether its two symbols match -- kMatchEq (byte equality), kMatchLut (the
 // 256 x 256 table of the user's match fn, LDS) or kMatchBits (a per-pair m x n match bitmap, the
 // generic-Ty path: any symbol type and count, the reference's cacheAllMatches packed to bits).
@@ -153,6 +173,10 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     }
     const uint32_t pidx = P.pair_base + slot;
     if (redo && !(P.res[pidx].flags & kFlagRetry)) return;   // uniform over the workgroup
+#ifdef SA_TB_STATS
+    const unsigned long long st_t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long st_wait = 0;
+#endif
     const uint64_t o1 = P.off1[pidx];
     const uint64_t o2 = P.off2[pidx];
     const int m = (int)(P.off1[pidx + 1] - o1);
@@ -170,6 +194,12 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     uint32_t* const s_lut = smem;
     int32_t* const s_ring = reinterpret_cast<int32_t*>(smem + lay.ring_off / 4);
     uint8_t* const s_seq2 = reinterpret_cast<uint8_t*>(smem) + lay.seq_off;
+    // LDS-fed steps: a chunk's lane-0 inputs and column symbols are read per step as LDS
+    // broadcasts straight into the DPP shift's old operand, and the band's last row is parked per
+    // step by an LDS write of lane 63 (lanes 0..62 write a discard slot, so the address is a
+    // per-lane constant and the step offset an immediate): no v_readlane / v_writelane / v_mov.
+    int32_t* const s_step = reinterpret_cast<int32_t*>(smem + lay.step_off / 4) + w * kStepBufWords;
+    int32_t* const s_park = s_step + (lane == 63 ? 96 : 160);
     const uint8_t* s1 = P.seq1 + o1;
     const uint8_t* s2 = P.seq2 + o2;
     if constexpr (LUT) {
@@ -232,10 +262,10 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                     auto odd) {
         constexpr bool STEADY = decltype(steady)::value;
         constexpr bool ODD = decltype(odd)::value;
-        const int up_h = shr1(__builtin_amdgcn_readlane(bch, q), hl);
+        const int up_h = shr1(s_step[q], hl);
         int up_x = 0;
-        if constexpr (AFF) up_x = shr1(__builtin_amdgcn_readlane(bcx, q), xl);
-        sym = shr1(__builtin_amdgcn_readlane(symc, q), sym);
+        if constexpr (AFF) up_x = shr1(s_step[32 + q], xl);
+        sym = shr1(s_step[64 + q], sym);
         const int j = s - lane;
 #pragma unroll
         for (int e = 0; e < RW; ++e) rec[e] = 0;
@@ -412,13 +442,9 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 } else {
                     pk[(g * BPS) / 4] |= rec[0] << (((g * BPS) % 4) * 8);
                 }
-                // lane 63 holds the band's last row at column kC + q - 63: park it in lane q
-                const int lh = __builtin_amdgcn_readlane(hl, 63);
-                acc_h = sa_writelane(lh, q, acc_h);
-                if constexpr (AFF) {
-                    const int lx = __builtin_amdgcn_readlane(xl, 63);
-                    acc_x = (lane == q) ? lx : acc_x;
-                }
+                // lane 63 holds the band's last row at column kC + q - 63: park it in LDS
+                s_park[q] = hl;
+                if constexpr (AFF) s_park[32 + q] = xl;
             }
             const uint64_t pkt0 = (uint64_t)((kC + q0) / SPP) * PPS;
 #pragma unroll
@@ -428,6 +454,9 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 __builtin_nontemporal_store(v4, dst);
             }
         }
+        // lane q < kChunk: the band's last row at column kC + q - 63
+        acc_h = s_step[96 + (lane & 31)];
+        if constexpr (AFF) acc_x = s_step[128 + (lane & 31)];
     };
 
     // Band -> band hand-off.  The last row of band b (H and, affine, Ix) goes to band b+1 through
@@ -480,7 +509,12 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 uint64_t t0 = 0;
                 for (;;) {
                     const bool pend = need && ((pre_h >> 32) == 0 || (AFF && (pre_x >> 32) == 0));
-                    if (__builtin_amdgcn_ballot_w64(pend) == 0 || tmo) break;
+                    if (__builtin_amdgcn_ballot_w64(pend) == 0 || tmo) {
+#ifdef SA_TB_STATS
+                        if (t0) st_wait += __builtin_amdgcn_s_memrealtime() - t0;
+#endif
+                        break;
+                    }
                     const uint64_t now = __builtin_amdgcn_s_memrealtime();
                     if (t0 == 0) t0 = now;
                     else if (now - t0 > kSplitWaitTicks) { tmo = 1; break; }
@@ -532,6 +566,11 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 const int kC = (int)chunk * kChunk;
                 int bch, bcx, symc;
                 load_chunk(band, kC, bch, bcx, symc);
+                if (lane < kChunk) {   // the chunk's per-step broadcast inputs (LDS-fed steps)
+                    s_step[lane] = bch;
+                    if constexpr (AFF) s_step[32 + lane] = bcx;
+                    s_step[64 + lane] = symc;
+                }
                 if constexpr (BITS) {
                     // my rows' match bits at columns [kC - lane, kC - lane + 32): bit q = step q
                     const int c0 = kC - lane;
@@ -651,6 +690,15 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
         if (threadIdx.x == 0) {
             int32_t* q = P.part + ((uint64_t)slot * P.split_bands + band0) * 4;
             q[0] = best_h; q[1] = best_i; q[2] = best_j; q[3] = (int32_t)tmo;
+#ifdef SA_TB_STATS
+            const uint64_t id = (uint64_t)slot * P.split_bands + band0;
+            if (id < 4096) {
+                g_split_stats[id][0] = id + 1;
+                g_split_stats[id][1] = st_t0;
+                g_split_stats[id][2] = __builtin_amdgcn_s_memrealtime();
+                g_split_stats[id][3] = st_wait;
+            }
+#endif
         }
     } else if constexpr (LOCAL) {
         // lexicographic max over (score, i, j): the reference's last row-major maximum

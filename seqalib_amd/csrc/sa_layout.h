@@ -47,14 +47,20 @@ constexpr int kLagPhases = (kChunk + 62) / kChunk + 1;
 constexpr int kRing = 128;
 static_assert(kLagPhases == 3 && kRing >= 4 * kChunk, "re-derive the ring bound");
 
-// Dynamic LDS of the fill kernel: [match bits (LUT)][hand-off rings][staged Seq2].
+// Per-wave step buffers of the fill (sa_fill_impl.h, "LDS-fed steps"), int32 words:
+//   [0, 32) lane-0 row-above input of the chunk's steps, [32, 64) its Ix (affine),
+//   [64, 96) the column symbols, [96, 128) the band's last row parked per step (H),
+//   [128, 160) the same for Ix, [160, 224) the discard target of lanes 0..62's parking writes.
+constexpr int kStepBufWords = 224;
+// Dynamic LDS of the fill kernel: [match bits (LUT)][hand-off rings][step buffers][staged Seq2].
 struct LdsLayout {
-    uint32_t ring_off, seq_off, total;
+    uint32_t ring_off, step_off, seq_off, total;
 };
 SA_HD LdsLayout lds_layout(bool lut, bool affine, int W, uint32_t staged_n) {
     LdsLayout L;
     L.ring_off = lut ? 2048 * 4 : 0;
-    L.seq_off = L.ring_off + (uint32_t)W * (affine ? 2 : 1) * kRing * 4;
+    L.step_off = L.ring_off + (uint32_t)W * (affine ? 2 : 1) * kRing * 4;
+    L.seq_off = L.step_off + (uint32_t)W * kStepBufWords * 4;
     L.total = L.seq_off + ((staged_n + 15) / 16) * 16;
     return L;
 }
