@@ -58,9 +58,10 @@ __global__ __launch_bounds__(256) void alphabet_scan(const uint8_t* d1, const ui
 
 // The T16 decision, on the device (so the host never waits for the scan): with <= 4 distinct
 // symbols, sym_pack = the symbols padded with absent byte values (codes stay distinct),
-// prof[c] byte c' = (int8)(4 * s(sym c, sym c') + 3), s = match ? match : mismatch; sel = 1.
+// prof[c] byte c' = (int8)(4 * s(sym c, sym c') + 3) -- (8 * s + 6) for the affine kernel --,
+// s = match ? match : mismatch; sel = 1.
 // More symbols: sel = 0 (the int32 kernel's launches run, the T16 ones return at once).
-__global__ void decide_t16(const uint32_t* lutbits, int match, int mismatch, uint32_t* aux) {
+__global__ void decide_t16(const uint32_t* lutbits, int match, int mismatch, int affine, uint32_t* aux) {
     if (threadIdx.x != 0) return;
     uint32_t syms[4] = {0, 0, 0, 0};
     int nsym = 0;
@@ -83,7 +84,8 @@ __global__ void decide_t16(const uint32_t* lutbits, int match, int mismatch, uin
         for (int c2 = 0; c2 < 4; ++c2) {
             const uint32_t a = syms[c], b = syms[c2];
             const bool v = lutbits ? ((lutbits[(a << 3) | (b >> 5)] >> (b & 31u)) & 1u) : (a == b);
-            const int t = 4 * (v ? match : mismatch) + 3;
+            const int s = v ? match : mismatch;
+            const int t = affine ? 8 * s + 6 : 4 * s + 3;
             w |= ((uint32_t)t & 255u) << (8 * c2);
         }
         aux[kAuxProf + c] = w;
@@ -100,8 +102,9 @@ hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uin
     return hipGetLastError();
 }
 
-hipError_t launch_decide_t16(const uint32_t* lutbits, int match, int mismatch, uint32_t* aux, hipStream_t s) {
-    hipLaunchKernelGGL(decide_t16, dim3(1), dim3(64), 0, s, lutbits, match, mismatch, aux);
+hipError_t launch_decide_t16(const uint32_t* lutbits, int match, int mismatch, int affine, uint32_t* aux,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(decide_t16, dim3(1), dim3(64), 0, s, lutbits, match, mismatch, affine, aux);
     return hipGetLastError();
 }
 

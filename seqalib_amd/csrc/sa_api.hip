@@ -96,7 +96,8 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t
         // skew between bands; hand-off through the row buffer), R up to 32 rows per lane.
         p.W = 1;
         p.R = 4;
-        while (p.R < 32 && (uint64_t)kWave * p.R < max_m) p.R *= 2;
+        const int rcap = aff ? 16 : 32;   // T16 affine: 4 rows of state per lane row
+        while (p.R < rcap && (uint64_t)kWave * p.R < max_m) p.R *= 2;
     } else if (npairs >= 1024) {
         // Many pairs: 4 waves (one band each when possible) per workgroup.
         p.W = 4;
@@ -132,14 +133,14 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t
             p.R = r;
             p.W = 1;
             p.split = true;
-        } else if (sscanf(ov, "%d,%d", &r, &w) == 2 && (r == 4 || r == 8 || r == 16 || ((r == 32 || r == 64) && t16)) &&
+        } else if (sscanf(ov, "%d,%d", &r, &w) == 2 && (r == 4 || r == 8 || r == 16 || ((r == 32 || r == 64) && t16 && !aff)) &&
             w >= 1 && w <= 16) {
             p.R = r;
             p.W = w;
             p.split = false;
         }
     }
-    if (p.R >= 32 && p.W > 4) p.W = 4;   // fill_max_threads<32>
+    if ((p.R >= 32 || (t16 && aff && p.R >= 16)) && p.W > 4) p.W = 4;   // fill_max_threads (sa_fill_impl.h)
     // never more waves than bands
     const uint64_t bands = (max_m + (uint64_t)kWave * p.R - 1) / ((uint64_t)kWave * p.R);
     if ((uint64_t)p.W > bands) p.W = (int)std::max<uint64_t>(1, bands);
@@ -256,15 +257,61 @@ bool keyed_ok(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
 //       exceeds 8191 - match, and that cell is part of the maximum the fill reports.  When the
 //       bound match * min(m, n) does not prove S small enough, T16 still runs and flags every pair
 //       whose S exceeds retry_above; the int32 variant re-runs exactly those pairs (kFlagRetry).
+//   Gotoh (T16 affine, 8*V + class/extend bits, int8 profile 8*s + 6): gap_extend < 0,
+//       gap_open <= 0.  LocalGotoh is bounded like SW (M >= 0, Iy >= GO + GE, the clamped Ix >= 0;
+//       retry above 4095 - match); GlobalGotoh like NW, with the affine path bounds, a delta
+//       offset, and the reference's -10000 Ix/Iy border provably never winning (else int32).
+//       The border becomes `sent`, below every candidate of the range.
 struct T16Mode {
     bool ok = false;
-    int32_t delta = 0;                // NW offset
-    int32_t retry_above = INT_MAX;    // SW: per-pair retry threshold
+    int32_t delta = 0;                // NW / GlobalGotoh offset
+    int32_t retry_above = INT_MAX;    // SW / LocalGotoh: per-pair retry threshold
+    int32_t sent = -10000;            // T16 affine: encoded Ix / Iy border
 };
+T16Mode t16_mode_affine(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
+    T16Mode t;
+    const int64_t MA = sc->match, MI = sc->mismatch, GO = sc->gap_open, GE = sc->gap_extend, GOE = GO + GE;
+    if (MA < -16 || MA > 15 || MI < -16 || MI > 15 || MI > MA) return t;   // 8s + 6 in int8
+    if (GE >= 0 || GO > 0 || GE < -512 || GO < -2048) return t;
+    if (max_n >= 65535) return t;
+    const int64_t m = max_m, n = max_n, k = std::min(m, n);
+    const int64_t sent = -32768 + 8 * (-GE) + 16;   // sent + 8GE + 1 cannot wrap
+    const int64_t floor_ext = sent + 8 * GE + 1;    // the border's extend candidate
+    if (algo == SA_LOCAL_GOTOH) {
+        // every candidate is >= 8 * min(MI, GOE + GE) + 1 (M >= 0, Iy >= GOE)
+        if (8 * std::min(MI, GOE + GE) + 1 <= floor_ext) return t;
+        t.ok = true;
+        t.sent = (int32_t)sent;
+        if (8 * std::max<int64_t>(MA, 0) * k + 7 > 32767) t.retry_above = (int32_t)(4095 - std::max<int64_t>(MA, 0));
+        return t;
+    }
+    if (MA < 0) return t;
+    // GlobalGotoh: the reference's border wins nowhere (SAGlobalGotoh.h: Ix[0][j] = Iy[i][0] = -10000)
+    if (GO + std::max(m, n) * GE + GOE <= -10000 + GE) return t;
+    auto gapc = [&](int64_t L) { return L > 0 ? GO + L * GE : 0; };
+    auto hi_at = [&](int64_t i, int64_t j) { return std::min(i, j) * MA + gapc(i > j ? i - j : j - i); };
+    auto lo_at = [&](int64_t i, int64_t j) {
+        return std::max(std::min(i, j) * MI + GO + (i > j ? i - j : j - i) * GE, 2 * GO + (i + j) * GE);
+    };
+    int64_t hi = INT64_MIN, lo = INT64_MAX;
+    const int64_t pts[7][2] = {{0, 0}, {m, 0}, {0, n}, {k, k}, {m, n}, {k, n}, {m, k}};
+    for (auto& q : pts) {
+        hi = std::max(hi, hi_at(q[0], q[1]));
+        lo = std::min(lo, lo_at(q[0], q[1]));
+    }
+    const int64_t cand_lo = lo + std::min<int64_t>(std::min(MI, GOE + GE), 0);
+    const int64_t delta = (hi + cand_lo) >> 1;
+    if (8 * (hi - delta) + 7 > 32767 || 8 * (cand_lo - delta) <= floor_ext) return t;
+    t.ok = true;
+    t.delta = (int32_t)delta;
+    t.sent = (int32_t)sent;
+    return t;
+}
 T16Mode t16_mode(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
     T16Mode t;
-    if (algo != SA_SW && algo != SA_NW) return t;
     if (!sc->allow_mismatch) return t;
+    if (algo == SA_LOCAL_GOTOH || algo == SA_GLOBAL_GOTOH) return t16_mode_affine(algo, sc, max_m, max_n);
+    if (algo != SA_SW && algo != SA_NW) return t;
     const int64_t MA = sc->match, MI = sc->mismatch, G = sc->gap;
     if (MA < -32 || MA > 31 || MI < -32 || MI > 31) return t;
     if (G > 0 || MI > MA || G < -4096) return t;
@@ -305,7 +352,7 @@ int validate_scoring(sa_ctx* c, int algo, const sa_scoring* s) {
 // T16 by scoring and shape (the batch alphabet is checked on the device, decide_t16).
 T16Mode t16_candidate(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
     T16Mode t = t16_mode(algo, sc, max_m, max_n);
-    if (algo == SA_SW && !keyed_ok(algo, sc, max_m, max_n)) t.ok = false;
+    if ((algo == SA_SW || algo == SA_LOCAL_GOTOH) && !keyed_ok(algo, sc, max_m, max_n)) t.ok = false;
     if (const char* e16 = getenv("SEQALIB_T16")) if (e16[0] == '0') t.ok = false;
     return t;
 }
@@ -347,7 +394,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     const uint32_t* sel = nullptr;
     if (t16) {
         SA_HIP(c, launch_alphabet_scan(d1, o1, d2, o2, npairs, aux, stream));
-        SA_HIP(c, launch_decide_t16(d_lutbits, sc->match, sc->mismatch, aux, stream));
+        SA_HIP(c, launch_decide_t16(d_lutbits, sc->match, sc->mismatch, is_affine(algo) ? 1 : 0, aux, stream));
         SA_HIP(c, hipMemcpyAsync(c->h_sel, aux + kAuxSel, 4, hipMemcpyDeviceToHost, stream));
         SA_HIP(c, hipEventRecord(c->ev_sel, stream));
         sel = aux + kAuxSel;
@@ -464,6 +511,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fp.redo = (nv == 2 && !v.t16) ? 1 : 0;
             fp.t16_delta = v.t16 ? tm.delta : 0;
             fp.retry_above = v.t16 ? tm.retry_above : INT_MAX;
+            fp.t16_sent = v.t16 ? tm.sent : -10000;
             fp.snap_h = snap_h; fp.snap_p = snap_p; fp.snap_m = snap_m;
             fp.snap_h_slot = v.snap_h_slot; fp.snap_p_slot = v.snap_p_slot; fp.snap_nch = v.snap_nch;
             fp.split_bands = (uint32_t)sp_bands;

@@ -38,6 +38,18 @@
 //     stripped from the value with one v_and_b32.
 // Cell = bfe + 3 add_u16 + 2-3 max_i16 + and + alignbit (+ lshl_or + max_u32 for the key).
 //
+// T16 affine (LocalGotoh / GlobalGotoh with allow-mismatch, same alphabet and profile rules).
+// Scores are kept as 8*V: bits 1-2 of a candidate carry its class in M's max (3 = diag, 2 = Ix,
+// 1 = Iy, 0 = the zero clamp) and bit 0 says, inside Ix's / Iy's own max, extend (1) over open
+// (0) -- the reference's tie orders (SALocalGotoh.h:304-468, SAGlobalGotoh.h:245-421).  Per cell:
+//   Ix = max(Mu + 8GOE + 4, Xu + 8GE + 1)   LocalGotoh takes the open term as max(., 0) with one
+//        saturating v_sub_u16, which also supplies M's zero clamp (max(Ix, 0) is exact wherever the
+//        traceback reads Ix, and max(D, max(Ix, 0), Iy) == max(D, Ix, Iy, 0), class bits included);
+//   Iy = max(Ml + 8GOE + 2, Yl + 8GE + 1);  M = max(D, Ix, Iy) with D = Md + (8s + 6) (profile);
+//   one v_alignbit each pushes Ix's and Iy's extend bit and M's class into the record (one byte per
+//   cell, sa_layout.h), one v_and each strips them (Ix/Iy keep their class bits).
+// 16 VALU per cell (+2 for the LocalGotoh (M, column) key) against the int32 kernel's 21.
+//
 // CMAX (T16 SW, one-wave plans): instead of a (score, column) key per cell, each row keeps its
 // maximum over the current 32-step chunk with one more v_max_i16 (fast class); at the chunk end
 // the row's (max, chunk) pair joins its key and the lane stores a snapshot of its state (R
@@ -87,9 +99,10 @@ __device__ __forceinline__ bool match_bit(const uint32_t* s_lut, int a, int b) {
     }
 }
 
-// Max workgroup size: 16 waves, except R = 32 (T16 only) which needs > 128 VGPRs per lane.
-template <int R>
-constexpr int fill_max_threads() { return R >= 32 ? 256 : 1024; }
+// Max workgroup size: 16 waves, except R = 32 (T16 only) and the T16 affine kernel at R = 16,
+// which need > 128 VGPRs per lane.
+template <int R, bool WIDE = false>
+constexpr int fill_max_threads() { return (R >= 32 || (WIDE && R >= 16)) ? 256 : 1024; }
 
 // Bounded wait of a SPLIT band for its producer, in s_memrealtime ticks (100 MHz): 0.2 s.  After
 // one expiry the workgroup stops waiting altogether (the pair is flagged SA_FLAG_TIMEOUT).
@@ -119,13 +132,13 @@ static __device__ unsigned long long g_split_stats[4096][4];
 // 256 x 256 table of the user's match fn, LDS) or kMatchBits (a per-pair m x n match bitmap, the
 // generic-Ty path: any symbol type and count, the reference's cacheAllMatches packed to bits).
 template <int ALG, int R, int MM, bool ALLOW, bool KEYED, bool T16, bool CMAX, bool SPLIT>
-__global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams P) {
+__global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)>())) void fill_kernel(FillParams P) {
     constexpr bool LUT = MM == kMatchLut;
     constexpr bool BITS = MM == kMatchBits;
     constexpr bool AFF = ALG >= SA_LOCAL_GOTOH;
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
     constexpr int FBITS = AFF ? 4 : 2;            // flag bits per cell
-    constexpr int BPC = record_bpc(ALG, R);      // record bits per cell (padding above the flags)
+    constexpr int BPC = record_bpc(ALG, R, T16);  // record bits per cell (padding above the flags)
     constexpr int RB = R * BPC;                // bits per record
     constexpr int BPS = RB / 8;                // bytes per record
     constexpr int RW = (RB + 31) / 32;         // words per record
@@ -135,10 +148,10 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     constexpr int BAND = kWave * R;
     static_assert(kChunk % SPP == 0, "chunk must hold whole packets");
     static_assert(BPS >= 1, "record must be at least a byte");
-    static_assert(!T16 || (!AFF && ALLOW && MM == kMatchEq && (RB <= 32 || RB % 32 == 0)),
-                  "T16: linear, allow-mismatch, profile");
+    static_assert(!T16 || (ALLOW && MM == kMatchEq && (RB <= 32 || RB % 32 == 0)),
+                  "T16: allow-mismatch, profile");
     static_assert(!T16 || !LOCAL || KEYED, "T16 local mode tracks its maximum with keys");
-    constexpr int SC = T16 ? 4 : 1;            // score scale of the register values
+    constexpr int SC = T16 ? (AFF ? 8 : 4) : 1;   // score scale of the register values
     static_assert(!CMAX || (T16 && ALG == SA_SW && R % 2 == 0), "CMAX: T16 Smith-Waterman");
 
     // Dynamic LDS (sizes from lds_layout(), host and device agree):
@@ -218,6 +231,14 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     // which also applies the zero clamp of the cell: max(D, max(U, 0), L) == max(D, U, L, 0).
     const uint32_t CU = LOCAL ? ((uint32_t)(-(4 * G + 2)) & 0xffffu) : (uint32_t)(4 * G + 2);
     const uint32_t CL = (uint32_t)(4 * G + 1);
+    // T16 affine: class / extend tagged gap terms (u16 arithmetic, sa_fill_impl.h header).  The
+    // LocalGotoh Ix open term is max(Mu + 8GOE + 4, 0) = Mu - CXO with unsigned saturation (Mu >= 0,
+    // CXO = -(8GOE + 4) > 0 since t16_mode demands GOE < 0).
+    const uint32_t CXO = (uint32_t)(LOCAL ? -(8 * GOE + 4) : 8 * GOE + 4) & 0xffffu;
+    const uint32_t CXE = (uint32_t)(8 * GE + 1) & 0xffffu;
+    const uint32_t CYO = (uint32_t)(8 * GOE + 2) & 0xffffu;
+    // Ix / Iy borders (the reference's -10000): T16 affine uses a value below every candidate
+    const int XB = (T16 && AFF) ? P.t16_sent : -10000;
 
     const int B = (m > 0 && n > 0) ? (m + BAND - 1) / BAND : 0;
     if (SPLIT && (int)band0 >= B) return;   // uniform: this pair has fewer bands
@@ -283,7 +304,70 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
             for (int r = 0; r < R; ++r) {
                 uint32_t& rw = rec[r / RPW];
                 int Hc;
-                if constexpr (T16) {
+                if constexpr (T16 && AFF) {
+                    // One asm block per cell (see the header): Ix and Iy terms, M's max, the three
+                    // record pushes and strips, the next row's diagonal candidate from Hp[r] before
+                    // Hp[r] is updated, and (LocalGotoh) the (M, column) key: Hp = 8M, so
+                    // Hp << 13 == M << 16.
+                    uint32_t t0, t1, xr, yr, xs;
+                    const uint32_t jk = (uint32_t)jkey;
+#define SA_T16A_HEAD_L "v_sub_u16_e64 %[t0], %[hu], %[cxo] clamp\n\t"
+#define SA_T16A_HEAD_G "v_add_u16 %[t0], %[cxo], %[hu]\n\t"
+#define SA_T16A_GAPS                                                                          \
+    "v_add_u16 %[t1], %[cyo], %[hp]\n\t"                                                       \
+    "v_add_u16 %[xr], %[cxe], %[xu]\n\t"                                                       \
+    "v_add_u16 %[yr], %[cxe], %[yp]\n\t"                                                       \
+    "v_max_i16 %[xr], %[t0], %[xr]\n\t"                                                        \
+    "v_max_i16 %[yr], %[t1], %[yr]\n\t"
+#define SA_T16A_MN                                                                            \
+    "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\t"                                                  \
+    "v_max_i16 %[t0], %[dr], %[xr]\n\t"                                                        \
+    "v_add_u16 %[dn], %[hp], %[dn]\n\t"                                                        \
+    "v_max_i16 %[t0], %[yr], %[t0]\n\t"
+#define SA_T16A_M "v_max_i16 %[t0], %[dr], %[xr]\n\tv_max_i16 %[t0], %[yr], %[t0]\n\t"
+#define SA_T16A_TAIL                                                                          \
+    "v_alignbit_b32 %[rec], %[xr], %[rec], 1\n\t"                                              \
+    "v_and_b32 %[xs], -2, %[xr]\n\t"                                                           \
+    "v_alignbit_b32 %[rec], %[yr], %[rec], 1\n\t"                                              \
+    "v_and_b32 %[yp], -2, %[yr]\n\t"                                                           \
+    "v_alignbit_b32 %[rec], %[t0], %[rec], 6\n\t"                                              \
+    "v_and_b32 %[hp], -8, %[t0]\n\t"
+#define SA_T16A_KEY "v_lshl_or_b32 %[t1], %[hp], 13, %[jk]\n\tv_max_u32 %[bh], %[bh], %[t1]\n\t"
+#define SA_T16A_OUT [t0] "=&v"(t0), [t1] "=&v"(t1), [xr] "=&v"(xr), [yr] "=&v"(yr), [xs] "=&v"(xs), \
+                    [hp] "+v"(Hp[r]), [yp] "+v"(Yp[r]), [rec] "+v"(rw)
+#define SA_T16A_IN [dr] "v"(dcur), [hu] "v"(hu), [xu] "v"(xu), [cxo] "s"(CXO), [cxe] "s"(CXE), [cyo] "s"(CYO)
+                    if (r + 1 < R) {
+                        uint32_t dn;
+                        const uint32_t tabn = (uint32_t)a[r + 1 < R ? r + 1 : r];
+                        if constexpr (LOCAL)
+                            asm(SA_T16A_HEAD_L SA_T16A_GAPS SA_T16A_MN SA_T16A_TAIL SA_T16A_KEY
+                                : SA_T16A_OUT, [dn] "=&v"(dn), [bh] "+v"(bh[r])
+                                : SA_T16A_IN, [tabn] "v"(tabn), [sym] "v"(sym), [jk] "v"(jk));
+                        else
+                            asm(SA_T16A_HEAD_G SA_T16A_GAPS SA_T16A_MN SA_T16A_TAIL
+                                : SA_T16A_OUT, [dn] "=&v"(dn)
+                                : SA_T16A_IN, [tabn] "v"(tabn), [sym] "v"(sym));
+                        dcur = dn;
+                    } else {
+                        if constexpr (LOCAL)
+                            asm(SA_T16A_HEAD_L SA_T16A_GAPS SA_T16A_M SA_T16A_TAIL SA_T16A_KEY
+                                : SA_T16A_OUT, [bh] "+v"(bh[r])
+                                : SA_T16A_IN, [jk] "v"(jk));
+                        else
+                            asm(SA_T16A_HEAD_G SA_T16A_GAPS SA_T16A_M SA_T16A_TAIL : SA_T16A_OUT : SA_T16A_IN);
+                    }
+#undef SA_T16A_HEAD_L
+#undef SA_T16A_HEAD_G
+#undef SA_T16A_GAPS
+#undef SA_T16A_MN
+#undef SA_T16A_M
+#undef SA_T16A_TAIL
+#undef SA_T16A_KEY
+#undef SA_T16A_OUT
+#undef SA_T16A_IN
+                    xu = (int)xs;
+                    Hc = Hp[r];
+                } else if constexpr (T16) {
                     // One asm block per cell (plain VALU->VALU dependences need no wait
                     // states; the compiler pads s_nop between separate asm statements).  The
                     // block also forms the NEXT row's diagonal candidate from Hp[r] before
@@ -393,7 +477,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                 }
                 }
                 if constexpr (LOCAL) {
-                    if constexpr (CMAX || (T16 && R >= 32)) {
+                    if constexpr (CMAX || (T16 && (R >= 32 || AFF))) {
                         // chunk max / key already updated by the cell's asm block
                     } else if constexpr (T16 && STEADY) {
                         // Hc = 4H with clear tag bits, so Hc << 14 == H << 16.  Two steps' keys
@@ -429,7 +513,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
             uint32_t pk[4 * PPS];
 #pragma unroll
             for (int e = 0; e < 4 * PPS; ++e) pk[e] = 0;
-            static_assert(SPP % 2 == 0 || !T16 || R >= 32, "steps pair up for the key max3");
+            static_assert(SPP % 2 == 0 || !T16 || R >= 32 || AFF, "steps pair up for the key max3");
 #pragma unroll
             for (int g = 0; g < SPP; ++g) {
                 const int q = q0 + g;
@@ -483,14 +567,14 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
     // lane 0 (top border, or the previous band's last row) and Seq2[c].
     auto load_chunk = [&](int band, int c0, int& vh, int& vx, int& vs) {
         const int c = c0 + lane;
-        vh = 0; vx = -10000; vs = 0;
+        vh = 0; vx = XB; vs = 0;
         if (lane < kChunk && c < n) {
             if (P.stage_seq2) vs = (int)s_seq2[c];
             else vs = T16 ? (int)t16_code8(symp, s2[c]) : (int)s2[c];
             if (band == 0) {
                 const int J = c + 1;
                 if constexpr (ALG == SA_NW) vh = SC * (J * G - P.t16_delta);
-                else if constexpr (ALG == SA_GLOBAL_GOTOH) vh = GO + J * GE;
+                else if constexpr (ALG == SA_GLOBAL_GOTOH) vh = SC * (GO + J * GE - P.t16_delta);
             } else if constexpr (SPLIT) {
                 // polled below, after the branch (the wave must poll together)
             } else if (band % W != 0) {
@@ -549,9 +633,9 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                         else a[r] = row < m ? (int)s1[row] : 0;
                         const int i = row + 1;
                         if constexpr (ALG == SA_NW) Hp[r] = SC * (i * G - P.t16_delta);
-                        else if constexpr (ALG == SA_GLOBAL_GOTOH) Hp[r] = GO + i * GE;
+                        else if constexpr (ALG == SA_GLOBAL_GOTOH) Hp[r] = SC * (GO + i * GE - P.t16_delta);
                         else Hp[r] = 0;
-                        Yp[r] = -10000;
+                        Yp[r] = XB;
                         bh[r] = KEYED ? 0 : INT_MIN;
                         bj[r] = 0;
                     }
@@ -559,7 +643,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                     cml = 0;
                     split_load(band, 0, pre_h, pre_x);
                     if constexpr (ALG == SA_NW) prev_up = SC * (row0 * G - P.t16_delta);
-                    else if constexpr (ALG == SA_GLOBAL_GOTOH) prev_up = row0 == 0 ? 0 : GO + row0 * GE;
+                    else if constexpr (ALG == SA_GLOBAL_GOTOH) prev_up = SC * ((row0 == 0 ? 0 : GO + row0 * GE) - P.t16_delta);
                     else prev_up = 0;
                 }
                 // ---------------------------------------------------------------- one chunk
@@ -663,7 +747,7 @@ __global__ __launch_bounds__(fill_max_threads<R>()) void fill_kernel(FillParams 
                             int v = 0;
 #pragma unroll
                             for (int r = 0; r < R; ++r) v = (r == rr) ? Hp[r] : v;
-                            s_score = T16 ? ((int)(int16_t)(v & 0xffff)) / 4 + P.t16_delta : v;
+                            s_score = T16 ? ((int)(int16_t)(v & 0xffff)) / SC + P.t16_delta : v;
                         }
                     }
                 }
@@ -794,6 +878,28 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
                                    lds, stream, p);
                 return hipGetLastError();
             }
+            return hipErrorInvalidValue;
+        }
+    }
+    if constexpr (ALG == SA_LOCAL_GOTOH || ALG == SA_GLOBAL_GOTOH) {
+        if (v.t16) {   // T16 affine: one-wave plans (R <= 16) and SPLIT bands (R <= 8)
+            if (!allow || v.cmax || (LOCAL && !keyed)) return hipErrorInvalidValue;
+            if ((int)block.x > (R >= 16 ? fill_max_threads<16, true>() : fill_max_threads<8>()))
+                return hipErrorInvalidConfiguration;
+#define SA_LAUNCH16A(RR, SP)                                                                           \
+    if (R == RR && split == SP) {                                                                      \
+        hipLaunchKernelGGL((fill_kernel<ALG, RR, kMatchEq, true, LOCAL, true, false, SP>), dim3(grid), block, \
+                           lds, stream, p);                                                            \
+        return hipGetLastError();                                                                      \
+    }
+            SA_LAUNCH16A(4, false)
+            SA_LAUNCH16A(8, false)
+            SA_LAUNCH16A(16, false)
+            SA_LAUNCH16A(1, true)
+            SA_LAUNCH16A(2, true)
+            SA_LAUNCH16A(4, true)
+            SA_LAUNCH16A(8, true)
+#undef SA_LAUNCH16A
             return hipErrorInvalidValue;
         }
     }

@@ -40,7 +40,8 @@ struct FillParams {
     int stage_seq2;            // 1: Seq2 of the pair is copied to LDS (max_n <= kMaxStagedSeq2)
     // T16 kernel only: the batch alphabet is <= 4 symbols, prof[4] = sym_pack (byte c = the
     // symbol of code c) and prof[c] holds, in byte c', the tagged substitution term
-    // 4*s(sym c, sym c') + 3 as int8 (written on the device by decide_t16, sa_alphabet.hip).
+    // 4*s(sym c, sym c') + 3 as int8, 8*s + 6 for the affine kernel (written on the device by
+    // decide_t16, sa_alphabet.hip).
     const uint32_t* prof;
     // device-side kernel selection: the launch runs only if *sel == sel_want (sel NULL: always);
     // redo: an int32 launch the batch did not select still re-runs the pairs flagged kFlagRetry
@@ -51,6 +52,9 @@ struct FillParams {
     // int16); SW flags pairs whose maximum exceeds retry_above (INT_MAX when proven to fit)
     int32_t t16_delta;
     int32_t retry_above;
+    // T16 affine only: the Ix / Iy border value (the reference's -10000), encoded below every
+    // candidate of the batch's score range (t16_mode, sa_api.hip)
+    int32_t t16_sent;
     // CMAX only (see sa_fill_impl.h): per-slot snapshots [band][chunk][lane] of the R 16-bit row
     // values (R/2 words) and of the diagonal input (1 word); snap_nch = chunks per band.
     uint32_t* snap_h;
@@ -149,7 +153,8 @@ hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uin
                                 const uint64_t* o2, uint32_t npairs, uint32_t* aux, hipStream_t s);
 // decide_t16: from the bitmap, aux[kAuxSel] = 1 if the batch has <= 4 distinct symbols (then the
 // profile and sym_pack are written), else 0.
-hipError_t launch_decide_t16(const uint32_t* lutbits, int match, int mismatch, uint32_t* aux, hipStream_t s);
+hipError_t launch_decide_t16(const uint32_t* lutbits, int match, int mismatch, int affine, uint32_t* aux,
+                             hipStream_t s);
 
 // Device-side kernel selection: a launch whose variant the batch did not select returns at once
 // (uniform over the grid; sel NULL = unconditional).

@@ -14,7 +14,9 @@
 //   affine (Gotoh), BPC = 4:  fD = (M == diag term), fX = (M == Ix),
 //                             fXe = (Ix == Ix_up + GE), fYe = (Iy == Iy_left + GE)
 // or, for the tagged 16-bit linear kernel (TAGGED records, BPC = 2), the 2-bit tag that won the
-// cell's max: 3 = diag, 2 = up, 1 = left, 0 = zero clamp (sa_fill_impl.h, "T16").
+// cell's max: 3 = diag, 2 = up, 1 = left, 0 = zero clamp (sa_fill_impl.h, "T16"); for the tagged
+// affine kernel (BPC = 8, one byte per cell): bit 0 = Ix extends, bit 1 = Iy extends, bits 3-4 =
+// the class that won M's max: 3 = diag, 2 = Ix, 1 = Iy, 0 = zero clamp (bits 2, 5-7: don't care).
 // The traceback re-derives the cell scores along its path from the end score (every move is an
 // exact equality), so zero tests and gap-open clamps need no stored bits.
 //
@@ -76,7 +78,16 @@ SA_HD constexpr int bits_per_cell(int algo) { return is_affine(algo) ? 4 : 2; }
 // R = 1, so that one lane's record of one step is always at least a byte.  R = 1 and 2 are the
 // few-pairs (SPLIT) plans: their bands are short so that a lone wave's critical-path step stays
 // cheap, and their records are a negligible share of the HBM traffic.
-SA_HD constexpr int record_bpc(int algo, int R) { return R == 1 ? 8 : (R == 2 ? 4 : bits_per_cell(algo)); }
+// Tagged affine records (T16 Gotoh) are one byte per cell at every R.
+SA_HD constexpr int record_bpc(int algo, int R, bool tagged = false) {
+    return (tagged && is_affine(algo)) ? 8 : (R == 1 ? 8 : (R == 2 ? 4 : bits_per_cell(algo)));
+}
+// The equality flags of the int32 affine records (bit 3 fD, bit 2 fX, bit 1 fXe, bit 0 fYe) from a
+// tagged affine record byte: the class that won M's max, taken in the reference's order (diag,
+// then Ix, then Iy: SALocalGotoh.h:304-468), says the same thing as the first flag that holds.
+SA_HD constexpr uint32_t t16a_flags(uint32_t b) {
+    return (((b >> 3) & 3u) == 3u ? 8u : 0u) | (((b >> 3) & 3u) == 2u ? 4u : 0u) | ((b & 1u) << 1) | ((b >> 1) & 1u);
+}
 
 struct Geom {
     int R;              // rows per lane
@@ -88,7 +99,7 @@ struct Geom {
     uint32_t bands;     // bands for max_m
     uint64_t band_stride;  // bytes per band
     uint64_t dir_slot;     // bytes per pair
-    bool tagged;           // 2-bit max tags (T16 kernel) instead of equality flags
+    bool tagged;           // max tags (T16 kernels) instead of equality flags
 };
 
 SA_HD uint32_t round_up(uint32_t x, uint32_t a) { return (x + a - 1) / a * a; }
@@ -97,7 +108,7 @@ SA_HD Geom make_geom(int algo, int R, uint32_t max_m, uint32_t max_n, bool tagge
     Geom g;
     g.R = R;
     g.tagged = tagged;
-    g.bpc = record_bpc(algo, R);
+    g.bpc = record_bpc(algo, R, tagged);
     g.bps = R * g.bpc / 8;
     g.spp = g.bps >= 16 ? 1 : 16 / g.bps;
     g.pps = g.bps > 16 ? g.bps / 16 : 1;

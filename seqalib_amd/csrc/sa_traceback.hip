@@ -64,9 +64,10 @@ typedef uint8_t __attribute__((address_space(1))) tb_glb_u8;
 __device__ unsigned long long g_tb_stats[8];
 #endif
 
-template <int ALG, int R, bool LUT>
+// TAG: tagged affine records (T16 Gotoh fills, one byte per cell; sa_layout.h t16a_flags).
+template <int ALG, int R, bool LUT, bool TAG = false>
 __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {   // tb_mine: sa_internal.h
-    constexpr int BPC = record_bpc(ALG, R), BPS = R * BPC / 8, SPP = 16 / BPS;
+    constexpr int BPC = record_bpc(ALG, R, TAG), BPS = R * BPC / 8, SPP = 16 / BPS;
     static_assert(BPS >= 1 && BPS <= 16 && (SPP & (SPP - 1)) == 0, "one packet per step record");
     constexpr int kTbGroups = 32 / SPP;
     constexpr int kTbLanes = R >= 32 ? 1 : (32 / R < kTbChunks / kTbGroups ? 32 / R : kTbChunks / kTbGroups);
@@ -257,7 +258,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {   // tb_min
                     } else if constexpr (ALG == SA_LOCAL_GOTOH) {
                         // flags: bit3 = fD (M == diag), bit2 = fX (M == Ix), bit1 = Ix extends, bit0 = Iy extends
                         if (!(i > 0 && j > 0)) { fin = true; break; }
-                        const uint32_t f = cell();
+                        const uint32_t f = TAG ? t16a_flags(cell()) : cell();
                         if (st == 0) {
                             if (V <= 0) { fin = true; break; }    // M == max(D, 0) <= 0
                             if (f & 8u) { V -= diag(i, j, f); --i; --j; }
@@ -277,7 +278,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {   // tb_min
                         if (!(i > 0 || j > 0)) { fin = true; break; }
                         if (j == 0) { emit('U'); --i; break; }   // edge rules hold in any state
                         if (i == 0) { emit('L'); --j; break; }
-                        const uint32_t f = cell();
+                        const uint32_t f = TAG ? t16a_flags(cell()) : cell();
                         if (st == 0) {
                             if (f & 8u) { diag(i, j, f); --i; --j; }
                             else st = (f & 4u) ? 1 : 2;
@@ -325,11 +326,24 @@ extern "C" int sa_debug_tb_stats(unsigned long long* out, int reset) {
 hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStream_t stream) {
     const dim3 block(64);
     const dim3 grid((p.count + 63) / 64);
+    const bool tag = p.tagged != 0 && is_affine(algo);
 #define SA_TB(AA, RR, LL)                                                                  \
-    if (algo == AA && R == RR && lut == LL) {                                              \
+    if (algo == AA && R == RR && lut == LL && !tag) {                                      \
         hipLaunchKernelGGL((traceback_kernel<AA, RR, LL>), grid, block, 0, stream, p);     \
         return hipGetLastError();                                                          \
     }
+#define SA_TBT(AA, RR, LL)                                                                 \
+    if (algo == AA && R == RR && lut == LL && tag) {                                       \
+        hipLaunchKernelGGL((traceback_kernel<AA, RR, LL, true>), grid, block, 0, stream, p); \
+        return hipGetLastError();                                                          \
+    }
+#define SA_TBT_A(AA) SA_TBT(AA, 1, false) SA_TBT(AA, 2, false) SA_TBT(AA, 4, false) SA_TBT(AA, 8, false) \
+                     SA_TBT(AA, 16, false) SA_TBT(AA, 1, true) SA_TBT(AA, 2, true) SA_TBT(AA, 4, true)    \
+                     SA_TBT(AA, 8, true) SA_TBT(AA, 16, true)
+    SA_TBT_A(SA_LOCAL_GOTOH)
+    SA_TBT_A(SA_GLOBAL_GOTOH)
+#undef SA_TBT_A
+#undef SA_TBT
 #define SA_TB_A(AA) SA_TB(AA, 4, false) SA_TB(AA, 8, false) SA_TB(AA, 16, false) \
                     SA_TB(AA, 4, true) SA_TB(AA, 8, true) SA_TB(AA, 16, true)   \
                     SA_TB(AA, 1, false) SA_TB(AA, 2, false) SA_TB(AA, 1, true) SA_TB(AA, 2, true)

@@ -100,6 +100,7 @@ __device__ __attribute__((noinline)) void tw_decode(const uint8_t* dir, const ui
         const uint32_t ok = (uint32_t)(i >= 1) & (uint32_t)(j >= 1) & (uint32_t)(j <= n);
         uint32_t f = raw[q] & FMASK;
         if (BPC == 2 && tagged) f = (f == 3u) ? 2u : (uint32_t)(f == 2u);
+        if (BPC == 4 && tagged) f = t16a_flags(raw[q] & 0xffu);   // tagged affine byte
         const int jq = min(max(j - 1 - jb, 0), kTwS2 - 1);
         const uint32_t a = sq1[p], b = sq2[jq];
         uint32_t mt;

@@ -118,8 +118,16 @@ def test_plan_t16_eligibility_by_scoring():
     assert sa.plan_query_ex(0, sa.ScoringSystem(-1, 1, -1), 8192, 70000, 10000)[0] == sa.SA_KERNEL_INT32
     # gap 0: the clamped up term needs gap < 0
     assert sa.plan_query_ex(0, sa.ScoringSystem(0, 1, -1), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32
-    # affine: int32 flags
-    assert sa.plan_query_ex(2, sa.ScoringSystem(-3, -1, 1, -1), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32
+    # affine (T16 affine kernel): LocalGotoh at any size (retry above the int16 headroom),
+    # GlobalGotoh while the affine path bounds fit 8*(V - delta); no mismatches allowed -> int32
+    aff = sa.ScoringSystem(-3, -1, 1, -1)
+    assert sa.plan_query_ex(2, aff, 1024, 1024, 10000)[:3] == (sa.SA_KERNEL_T16, 16, 1)
+    assert sa.plan_query_ex(2, aff, 8192, 8192, 10000)[0] == sa.SA_KERNEL_T16
+    assert sa.plan_query_ex(3, aff, 2048, 2048, 10000)[:3] == (sa.SA_KERNEL_T16, 16, 1)
+    assert sa.plan_query_ex(3, aff, 4096, 4096, 10000)[0] == sa.SA_KERNEL_INT32
+    assert sa.plan_query_ex(2, sa.ScoringSystem(-3, -1, 1, -1, False), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32
+    assert sa.plan_query_ex(2, sa.ScoringSystem(-3, 0, 1, -1), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32
+    assert sa.plan_query_ex(2, aff, 1024, 1024, 10000, nsym=5)[0] == sa.SA_KERNEL_INT32
 
 
 def cell_byte(R, bpc, max_n, i, j, tagged=False):
@@ -147,7 +155,8 @@ def cell_byte(R, bpc, max_n, i, j, tagged=False):
 @pytest.mark.parametrize("R,bpc,tagged", [(4, 2, False), (8, 2, False), (16, 2, False), (4, 4, False),
                                           (8, 4, False), (16, 4, False), (4, 2, True), (8, 2, True),
                                           (16, 2, True), (1, 8, False), (1, 8, True), (2, 4, False),
-                                          (2, 4, True)])
+                                          (2, 4, True), (2, 8, True), (4, 8, True), (8, 8, True),
+                                          (16, 8, True)])
 def test_flag_layout_is_a_bijection(R, bpc, tagged):
     """Every cell of a band gets its own bits, records pack exactly R*bpc bits per lane-step."""
     max_n = 70

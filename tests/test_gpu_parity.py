@@ -242,12 +242,14 @@ def dna_pairs(seed, count, maxlen):
     return pairs
 
 
-@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
 def test_t16_and_int32_kernels_both_exact(engine, algo, monkeypatch):
-    """DNA SW/NW with allow-mismatch run on the tagged 16-bit kernel; SEQALIB_T16=0 forces the
-    int32 kernel.  Both must equal the oracle."""
+    """DNA SW/NW/LocalGotoh/GlobalGotoh with allow-mismatch run on the tagged 16-bit kernels (the
+    affine one for Gotoh); SEQALIB_T16=0 forces the int32 kernel.  Both must equal the oracle."""
     pairs = dna_pairs(7 + algo, 40, 900)
-    allow_scorings = [a for a in SCORINGS[algo] if len(a) == 3 or (len(a) == 4 and a[3])]
+    nargs = 4 if algo >= 2 else 3
+    allow_scorings = [a for a in SCORINGS[algo] if len(a) == nargs - 1 or a[nargs - 1]]
+    assert allow_scorings
     for args in allow_scorings:
         compare_with_oracle(engine, algo, args, pairs)
         assert engine.last_plan()[0] in T16_KERNELS, args
@@ -314,6 +316,41 @@ def test_t16_sw_retry_mixed_batch(engine):
     assert engine.last_plan()[0] in T16_KERNELS
     compare_with_oracle(engine, 0, (-1, 1, -1), [pairs[3], pairs[5], pairs[700]])
     assert engine.last_plan()[0] in T16_KERNELS
+
+
+def test_t16_affine_eligibility_and_retry(engine):
+    """T16 affine kernel choice and headroom: LocalGotoh runs T16 at any size and re-runs on int32
+    exactly the pairs whose maximum passes 4095 - match (8*M in int16), on the batch plan and the
+    few-pairs plan; GlobalGotoh runs T16 while its affine path bounds fit (2048^2) and int32
+    beyond (the reference's 4096^2 GlobalGotoh probe); !allowMismatch and five symbols -> int32."""
+    lg = (-3, -1, 1, -1, True)
+    rng = np.random.default_rng(29)
+    pairs = [(sa.synth_dna(90_000 + k, int(rng.integers(50, 300))), sa.synth_dna(91_000 + k, int(rng.integers(50, 300))))
+             for k in range(1100)]
+    hot = sa.synth_dna(92_000, 5000)
+    pairs[5] = (hot, hot)                                        # score 5000 > 4094: retried
+    pairs[900] = (hot[:4600], sa.synth_mutate(hot, 5)[:4700])
+    compare_with_oracle(engine, 2, lg, pairs)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    compare_with_oracle(engine, 2, lg, [pairs[5], pairs[6], pairs[900]])
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    gg = (-3, -1, 1, -1, True)
+    two = [(sa.synth_dna(93_000, 2048), sa.synth_dna(93_001, 2048)),
+           (sa.synth_dna(93_002, 2000), sa.synth_mutate(sa.synth_dna(93_002, 2000), 4)[:2048])]
+    compare_with_oracle(engine, 3, gg, two)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    big = {e["id"]: e for e in load_golden("large.jsonl")}
+    assert check_golden(engine, [big["probe4096/gg/-3_-1_1_-1_1/equal"]]) == 1
+    assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
+    for pid in ("probe8192/lg/-3_-1_1_-1_1/equal", "mut4096/lg/-3_-1_1_-1_1/equal"):
+        assert check_golden(engine, [big[pid]]) == 1
+        assert engine.last_plan()[0] == sa.SA_KERNEL_T16, pid
+    dna = dna_pairs(31, 6, 400)
+    compare_with_oracle(engine, 2, (-3, -1, 1, -1, False), dna)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
+    five = dna[:-1] + [(dna[-1][0] + b"N", dna[-1][1])]
+    compare_with_oracle(engine, 3, gg, five)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
 
 
 def test_endcell_replay_vs_oracle(engine):

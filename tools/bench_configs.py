@@ -7,6 +7,7 @@ CPU path beside it.  One JSON line per config; tools/profile.sh-style evidence f
   config 3  10,000 x 1024^2 SW                   batch GCUPS (pipelined and serial)
   config 4  1 x 8192^2 LocalGotoh (-3,-1,1,-1,F)  single pair
   config 5  12,500 x 2048^2 SW                   the per-GPU shard of 100,000 pairs over 8 GPUs
+  gotoh     10,000 x 1024^2 LocalGotoh / GlobalGotoh (-3,-1,1,-1,true): T16 affine vs int32 kernel
   drop-in   C++ SmithWatermanSA::getAlignments, 1,000 x 4096^2, end-to-end incl. std::list build
 
 Seeds: config c uses base c x 1e9.  CPU figures come from oracle/_ref (the
@@ -190,6 +191,28 @@ def main():
                 "fill_gcups": round(cells / fill_ms / 1e6, 1), "traceback_ms": round(tb_ms, 2), "plan": r.eng.last_plan(),
                 "parity": parity(sa, 0, (-1, 1, -1), s1, o1, s2, o2, res, ops, [0, P - 1])}
         print(json.dumps(line), flush=True)
+        del d, outs
+
+    if "gotoh" in only:   # batched affine: T16 affine kernel vs the int32 kernel (SEQALIB_T16=0)
+        P = 10000
+        s1, o1, s2, o2 = sa.synth_dna_batch(6 * 10 ** 9, P, 1024, 1024, threads=16)
+        d, outs, n = r.put(s1, o1, s2, o2)
+        cells = P * 1024 * 1024
+        for algo, name in ((sa.SA_LOCAL_GOTOH, "LocalGotoh"), (sa.SA_GLOBAL_GOTOH, "GlobalGotoh")):
+            args = (-3, -1, 1, -1, True)
+            sc = sa.ScoringSystem(*args)
+            line = {"config": "gotoh", "workload": f"10,000 x 1024^2 {name} (-3,-1,1,-1,true)"}
+            for kern, env in (("t16", "1"), ("int32", "0")):
+                os.environ["SEQALIB_T16"] = env
+                dtp, k, fill_ms, tb_ms = r.time_calls(algo, sc, d, outs, n, 1024, 1024, 6, True)
+                res, ops = r.results(outs, k)
+                line[kern] = {"gcups": round(cells / dtp / 1e9, 1), "ms_per_step": round(dtp * 1e3, 2),
+                              "fill_ms": round(fill_ms, 2), "fill_gcups": round(cells / fill_ms / 1e6, 1),
+                              "traceback_ms": round(tb_ms, 2), "plan": r.eng.last_plan(),
+                              "parity": parity(sa, algo, args, s1, o1, s2, o2, res, ops, [0, P // 2, P - 1])}
+            os.environ.pop("SEQALIB_T16")
+            line["fill_speedup"] = round(line["int32"]["fill_ms"] / line["t16"]["fill_ms"], 2)
+            print(json.dumps(line), flush=True)
         del d, outs
 
     if "dropin" in only:
