@@ -166,13 +166,15 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
     v.pl = make_plan(algo, max_m, max_n, npairs, t16, allow_split);
     // CMAX end-cell tracking (sa_fill_impl.h / sa_endcell.hip): T16 SW on one-wave plans with an
     // end-cell replay instantiation (R <= 32)
-    v.cmax = t16 && algo == SA_SW && v.pl.W == 1 && v.pl.R >= 2 && v.pl.R <= 32;
+    v.cmax = t16 && v.pl.W == 1 && v.pl.R >= 2 &&
+             ((algo == SA_SW && v.pl.R <= 32) || (algo == SA_LOCAL_GOTOH && v.pl.R <= 16));
     if (const char* ec = getenv("SEQALIB_CMAX")) if (ec[0] == '0') v.cmax = false;
     if (v.cmax) {
         v.snap_nch = chunks_per_band(max_n);
         v.snap_p_slot = (uint64_t)v.pl.g.bands * v.snap_nch * kWave;
-        v.snap_h_slot = v.snap_p_slot * (v.pl.R / 2);
-        v.pl.rowbuf_elems = (uint64_t)v.pl.g.bands * std::max<uint32_t>(max_n, 1);
+        // per lane: R 16-bit values (LocalGotoh: M, then Iy, then the last row's Ix: R + 1 words)
+        v.snap_h_slot = v.snap_p_slot * (is_affine(algo) ? v.pl.R + 1 : v.pl.R / 2);
+        v.pl.rowbuf_elems = (uint64_t)(is_affine(algo) ? 2 : 1) * v.pl.g.bands * std::max<uint32_t>(max_n, 1);
     }
     if (v.pl.split) v.pl.rowbuf_elems = 0;   // hand-off granules live in c->split
     v.kernel = v.cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
@@ -544,15 +546,17 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                     ep.rowbuf = reinterpret_cast<const int32_t*>(fp.hand);
                     ep.rowbuf_slot = 2 * sp_bands * std::max<uint32_t>(max_n, 1);
                     ep.rowbuf_stride = 2;
+                    ep.rowbuf_x_off = 2 * hand_x_off;
                 } else {
                     ep.rowbuf = rowbuf; ep.rowbuf_slot = pl.rowbuf_elems; ep.rowbuf_stride = 1;
+                    ep.rowbuf_x_off = pl.rowbuf_elems / 2;
                 }
                 ep.max_n = max_n;
                 ep.res = d_res; ep.pair_base = (uint32_t)base; ep.count = cnt;
-                ep.gap = sc->gap;
+                ep.gap = sc->gap; ep.gap_open = sc->gap_open; ep.gap_extend = sc->gap_extend;
                 // on the fill stream, right after the fill: run beside the next call's fill (on the
                 // traceback stream) its 10,000 short waves slowed that fill by 4 % (measured)
-                e = launch_endcell(pl.R, ep, sf);
+                e = launch_endcell(algo, pl.R, ep, sf);
                 if (e != hipSuccess) return hip_fail(c, e, "end-cell kernel launch");
             }
         }

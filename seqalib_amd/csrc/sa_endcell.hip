@@ -125,6 +125,123 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
     }
 }
 
+// LocalGotoh (T16 affine CMAX fill): the same replay on the three-state recurrence
+// (SALocalGotoh.h:108-130).  The fill's snapshot of a lane holds its R values of M (8M), then its
+// R values of Iy (8Iy + 2) and the Ix of its last row (8Ix + 4, or 0 where the fill's clamped Ix
+// open term floored it); the band's top row holds M and Ix.  Replayed Ix values may differ from
+// the reference's below 0 (the fill keeps max(Ix, 0) there), which leaves every M unchanged:
+// M = max(D, Ix, Iy, 0) and max(max(Ix, 0) + GE, GE) keeps max(., 0) of the chain (GE < 0).
+template <int R>
+__global__ __launch_bounds__(64) void endcell_lg_kernel(EndcellParams P) {
+    if (sa_skip(P.sel, P.sel_want)) return;
+    const int lane = threadIdx.x;
+    const uint32_t slot = blockIdx.x;
+    if (slot >= P.count) return;
+    const uint32_t symp = P.prof[4];
+    const uint32_t pidx = P.pair_base + slot;
+    sa_result res = P.res[pidx];
+    if (res.reserved == 0 || (res.flags & (SA_FLAG_BAD_SHAPE | kFlagRetry))) return;   // uniform over the wave
+    const int c = (int)res.reserved - 1;
+    const int S = res.score;
+    const int iend = res.end_i;
+    const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
+    const int m = (int)(P.off1[pidx + 1] - o1);
+    const int n = (int)(P.off2[pidx + 1] - o2);
+    const uint8_t* s1 = P.seq1 + o1;
+    const uint8_t* s2 = P.seq2 + o2;
+    constexpr int BAND = kWave * R;
+    const int b = (iend - 1) / BAND;
+    const int tstar = ((iend - 1) % BAND) / R;
+    const int row0 = b * BAND + lane * R;
+    const int GE = P.gap_extend, GOE = P.gap_open + P.gap_extend;
+    constexpr int kNeg = INT_MIN / 4;   // the Ix / Iy borders: below every candidate
+
+    if (S == 0) {   // every M is 0: the last cell is the reference's maximum (MaxScore from INT_MIN)
+        if (lane == 0) {
+            res.end_i = m;
+            res.end_j = n;
+            res.reserved = 0;
+            P.res[pidx] = res;
+        }
+        return;
+    }
+    uint32_t tab[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int row = row0 + r;
+        tab[r] = row < m ? P.prof[ec_code8(symp, s1[row]) >> 3] : 0u;
+    }
+    const uint32_t rs = P.rowbuf_stride;
+    const int32_t* top = b > 0 ? P.rowbuf + (uint64_t)slot * P.rowbuf_slot + (uint64_t)(b - 1) * P.max_n * rs : nullptr;
+    const int32_t* topx = top ? top + P.rowbuf_x_off : nullptr;
+    const int32_t* lmax = P.snap_m + (uint64_t)slot * P.snap_p_slot + (uint64_t)b * P.snap_nch * kWave + tstar;
+    int rbest = -1, jbest = -1;
+    for (int cc = 0; cc <= c; ++cc) {
+        if (lmax[(uint64_t)cc * kWave] != 8 * S) continue;   // uniform: lane tstar never reached S here
+        int Mp[R], Yp[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) { Mp[r] = 0; Yp[r] = kNeg; }
+        int prev_up = 0, xl = kNeg;
+        if (cc > 0) {
+            const uint64_t e = (uint64_t)b * P.snap_nch + (cc - 1);
+            const uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + (e * kWave + lane) * (R + 1);
+#pragma unroll
+            for (int q = 0; q < R / 2; ++q) {
+                const uint32_t w = sh[q], y = sh[R / 2 + q];
+                Mp[2 * q] = (int)(w & 0xffffu) >> 3;   // 8M, non-negative
+                Mp[2 * q + 1] = (int)(w >> 16) >> 3;
+                Yp[2 * q] = (int)(int16_t)(y & 0xffffu) >> 3;   // 8Iy + 2 (the border: far below)
+                Yp[2 * q + 1] = (int)(int16_t)(y >> 16) >> 3;
+            }
+            xl = (int)(int16_t)(sh[R] & 0xffffu) >> 3;
+            prev_up = P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] >> 3;
+        }
+        int hl = Mp[R - 1];
+        for (int q = 0; q < kChunk; ++q) {
+            const int s = cc * kChunk + q;
+            const int j0 = s - lane;
+            int up_h = __shfl_up(hl, 1);
+            int up_x = __shfl_up(xl, 1);
+            if (lane == 0) {
+                const bool t = top && s < n;
+                up_h = t ? (top[(uint64_t)s * rs] >> 3) : 0;
+                up_x = t ? ((int)(int16_t)(topx[(uint64_t)s * rs] & 0xffff) >> 3) : kNeg;
+            }
+            if (j0 >= 0 && j0 < n) {
+                const uint32_t sym = ec_code8(symp, s2[j0]);
+                int hd = prev_up, hu = up_h, xu = up_x;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    // profile byte = 8s+6 (signed); the builtin returns unsigned: shift as int
+                    const int sub = ((int)__builtin_amdgcn_sbfe(tab[r], sym, 8) - 6) >> 3;
+                    const int X = max(hu + GOE, xu + GE);
+                    const int Y = max(Mp[r] + GOE, Yp[r] + GE);
+                    const int M = max(max(hd + sub, X), max(Y, 0));
+                    hd = Mp[r];
+                    Mp[r] = M;
+                    Yp[r] = Y;
+                    hu = M;
+                    xu = X;
+                    // last row of the lane holding S, then its last column (chunks ascend)
+                    if (lane == tstar && row0 + r < m && M == S && (r > rbest || (r == rbest && j0 > jbest))) {
+                        rbest = r;
+                        jbest = j0;
+                    }
+                }
+                prev_up = up_h;
+                hl = Mp[R - 1];
+                xl = xu;
+            }
+        }
+    }
+    if (lane == tstar) {
+        res.end_i = row0 + rbest + 1;
+        res.end_j = jbest + 1;
+        res.reserved = 0;
+        P.res[pidx] = res;
+    }
+}
+
 // SPLIT fills (sa_fill_impl.h): fold each pair's per-band partials {score, i, j, timeout} into
 // its result — local modes: the lexicographic max over (score, i, j), i.e. the reference's last
 // row-major maximum; global modes: H[m][n] from the band holding row m.  One thread per pair.
@@ -196,8 +313,19 @@ hipError_t launch_split_reduce(int algo, const SplitReduceParams& p, hipStream_t
     return hipGetLastError();
 }
 
-hipError_t launch_endcell(int R, const EndcellParams& p, hipStream_t stream) {
+hipError_t launch_endcell(int algo, int R, const EndcellParams& p, hipStream_t stream) {
     const dim3 grid(p.count), block(64);
+    if (algo == SA_LOCAL_GOTOH) {
+        switch (R) {
+            case 2: hipLaunchKernelGGL(endcell_lg_kernel<2>, grid, block, 0, stream, p); break;
+            case 4: hipLaunchKernelGGL(endcell_lg_kernel<4>, grid, block, 0, stream, p); break;
+            case 8: hipLaunchKernelGGL(endcell_lg_kernel<8>, grid, block, 0, stream, p); break;
+            case 16: hipLaunchKernelGGL(endcell_lg_kernel<16>, grid, block, 0, stream, p); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    if (algo != SA_SW) return hipErrorInvalidValue;
     switch (R) {
         case 2: hipLaunchKernelGGL(endcell_kernel<2>, grid, block, 0, stream, p); break;
         case 4: hipLaunchKernelGGL(endcell_kernel<4>, grid, block, 0, stream, p); break;

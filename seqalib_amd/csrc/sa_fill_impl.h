@@ -50,7 +50,7 @@
 //   cell, sa_layout.h), one v_and each strips them (Ix/Iy keep their class bits).
 // 16 VALU per cell (+2 for the LocalGotoh (M, column) key) against the int32 kernel's 21.
 //
-// CMAX (T16 SW, one-wave plans): instead of a (score, column) key per cell, each row keeps its
+// CMAX (T16 SW and LocalGotoh, one-wave plans): instead of a (score, column) key per cell, each row keeps its
 // maximum over the current 32-step chunk with one more v_max_i16 (fast class); at the chunk end
 // the row's (max, chunk) pair joins its key and the lane stores a snapshot of its state (R
 // 16-bit values + the diagonal input), and each band's top row is kept.  The fill then reports
@@ -152,7 +152,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                   "T16: allow-mismatch, profile");
     static_assert(!T16 || !LOCAL || KEYED, "T16 local mode tracks its maximum with keys");
     constexpr int SC = T16 ? (AFF ? 8 : 4) : 1;   // score scale of the register values
-    static_assert(!CMAX || (T16 && ALG == SA_SW && R % 2 == 0), "CMAX: T16 Smith-Waterman");
+    static_assert(!CMAX || (T16 && LOCAL && R % 2 == 0), "CMAX: T16 Smith-Waterman / LocalGotoh");
 
     // Dynamic LDS (sizes from lds_layout(), host and device agree):
     //   [match bits: 2048 words, LUT only][hand-off rings: W x kRing x (1|2) ints][Seq2 bytes, staged]
@@ -254,8 +254,10 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
 
     uint8_t* const dslot = P.dirs + (uint64_t)slot * P.dir_slot;
     int32_t* const rb_h = P.rowbuf + (uint64_t)slot * P.rowbuf_slot;
-    int32_t* const rb_x = rb_h + P.max_n;
-    // CMAX keeps every band's top row (row buffer = bands x max_n); otherwise one row is reused
+    // affine: [M rows][Ix rows], the halves of the slot
+    int32_t* const rb_x = rb_h + P.rowbuf_slot / 2;
+    // CMAX keeps every band's top row (row buffer = bands x max_n per component); otherwise one
+    // row is reused
     const uint64_t rbs = CMAX ? P.max_n : 0;
 
     // Per-lane state for the current band.
@@ -339,7 +341,11 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     if (r + 1 < R) {
                         uint32_t dn;
                         const uint32_t tabn = (uint32_t)a[r + 1 < R ? r + 1 : r];
-                        if constexpr (LOCAL)
+                        if constexpr (LOCAL && CMAX)
+                            asm(SA_T16A_HEAD_L SA_T16A_GAPS SA_T16A_MN SA_T16A_TAIL
+                                : SA_T16A_OUT, [dn] "=&v"(dn)
+                                : SA_T16A_IN, [tabn] "v"(tabn), [sym] "v"(sym));
+                        else if constexpr (LOCAL)
                             asm(SA_T16A_HEAD_L SA_T16A_GAPS SA_T16A_MN SA_T16A_TAIL SA_T16A_KEY
                                 : SA_T16A_OUT, [dn] "=&v"(dn), [bh] "+v"(bh[r])
                                 : SA_T16A_IN, [tabn] "v"(tabn), [sym] "v"(sym), [jk] "v"(jk));
@@ -349,7 +355,9 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                                 : SA_T16A_IN, [tabn] "v"(tabn), [sym] "v"(sym));
                         dcur = dn;
                     } else {
-                        if constexpr (LOCAL)
+                        if constexpr (LOCAL && CMAX)
+                            asm(SA_T16A_HEAD_L SA_T16A_GAPS SA_T16A_M SA_T16A_TAIL : SA_T16A_OUT : SA_T16A_IN);
+                        else if constexpr (LOCAL)
                             asm(SA_T16A_HEAD_L SA_T16A_GAPS SA_T16A_M SA_T16A_TAIL SA_T16A_KEY
                                 : SA_T16A_OUT, [bh] "+v"(bh[r])
                                 : SA_T16A_IN, [jk] "v"(jk));
@@ -365,6 +373,10 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
 #undef SA_T16A_KEY
 #undef SA_T16A_OUT
 #undef SA_T16A_IN
+                    if constexpr (CMAX) {   // the lane's chunk maximum (8M >= 0), as for SW below
+                        if (r & 1)
+                            asm("v_max3_u32 %0, %0, %1, %2" : "+v"(cml) : "v"(Hp[r >= 1 ? r - 1 : 0]), "v"(Hp[r]));
+                    }
                     xu = (int)xs;
                     Hc = Hp[r];
                 } else if constexpr (T16) {
@@ -582,7 +594,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                 if constexpr (AFF) vx = ring(band % W, 1)[c % kRing];
             } else {
                 vh = rb_h[(uint64_t)(band - 1) * rbs + c];
-                if constexpr (AFF) vx = rb_x[c];
+                if constexpr (AFF) vx = rb_x[(uint64_t)(band - 1) * rbs + c];
             }
         }
         if constexpr (SPLIT) {
@@ -698,7 +710,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                             if constexpr (AFF) ring(nw, 1)[cc % kRing] = acc_x;
                         } else {
                             rb_h[(uint64_t)band * rbs + cc] = acc_h;
-                            if constexpr (AFF) rb_x[cc] = acc_x;
+                            if constexpr (AFF) rb_x[(uint64_t)band * rbs + cc] = acc_x;
                         }
                     }
                 }
@@ -707,13 +719,21 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     const uint32_t ck = chunk + 1;
                     const uint64_t e = (uint64_t)band * P.snap_nch + chunk;
                     P.snap_m[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = (int32_t)cml;
-                    lkey = max(lkey, (cml >> 2) << 12 | ck);
+                    lkey = max(lkey, (cml >> (AFF ? 3 : 2)) << 12 | ck);
                     cml = 0;
                     if (chunk + 1 < nch) {   // state entering chunk + 1, for the end-cell replay
-                        uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + (e * kWave + lane) * (R / 2);
+                        // R 16-bit values (affine: then the R Iy values and the last row's Ix)
+                        constexpr int SW = AFF ? R + 1 : R / 2;
+                        uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + (e * kWave + lane) * SW;
 #pragma unroll
                         for (int q = 0; q < R / 2; ++q)
                             sh[q] = ((uint32_t)Hp[2 * q] & 0xffffu) | ((uint32_t)Hp[2 * q + 1] << 16);
+                        if constexpr (AFF) {
+#pragma unroll
+                            for (int q = 0; q < R / 2; ++q)
+                                sh[R / 2 + q] = ((uint32_t)Yp[2 * q] & 0xffffu) | ((uint32_t)Yp[2 * q + 1] << 16);
+                            sh[R] = (uint32_t)xl;
+                        }
                         P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = prev_up;
                     }
                 }
@@ -883,11 +903,19 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
     }
     if constexpr (ALG == SA_LOCAL_GOTOH || ALG == SA_GLOBAL_GOTOH) {
         if (v.t16) {   // T16 affine: one-wave plans (R <= 16) and SPLIT bands (R <= 8)
-            if (!allow || v.cmax || (LOCAL && !keyed)) return hipErrorInvalidValue;
+            if (!allow || (v.cmax && !LOCAL) || (LOCAL && !keyed)) return hipErrorInvalidValue;
             if ((int)block.x > (R >= 16 ? fill_max_threads<16, true>() : fill_max_threads<8>()))
                 return hipErrorInvalidConfiguration;
 #define SA_LAUNCH16A(RR, SP)                                                                           \
     if (R == RR && split == SP) {                                                                      \
+        if constexpr (LOCAL && RR % 2 == 0) {                                                          \
+            if (v.cmax) {                                                                              \
+                hipLaunchKernelGGL((fill_kernel<ALG, RR, kMatchEq, true, true, true, true, SP>), dim3(grid), block, \
+                                   lds, stream, p);                                                    \
+                return hipGetLastError();                                                              \
+            }                                                                                          \
+        }                                                                                              \
+        if (v.cmax) return hipErrorInvalidValue;                                                       \
         hipLaunchKernelGGL((fill_kernel<ALG, RR, kMatchEq, true, LOCAL, true, false, SP>), dim3(grid), block, \
                            lds, stream, p);                                                            \
         return hipGetLastError();                                                                      \

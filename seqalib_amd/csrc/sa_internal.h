@@ -57,7 +57,7 @@ struct FillParams {
     int32_t t16_sent;
     // CMAX only (see sa_fill_impl.h): per-slot snapshots [band][chunk][lane] of the R 16-bit row
     // values (R/2 words) and of the diagonal input (1 word); snap_nch = chunks per band.
-    uint32_t* snap_h;
+    uint32_t* snap_h;   // LocalGotoh: R values of M, then R of Iy, then the last row's Ix (R + 1 words)
     int32_t* snap_p;
     int32_t* snap_m;   // per [band][chunk][lane]: the lane's maximum over the chunk (4H)
     uint64_t snap_h_slot, snap_p_slot;   // snap_m slots are snap_p_slot words too
@@ -106,10 +106,11 @@ struct EndcellParams {
     const int32_t* rowbuf;
     uint64_t rowbuf_slot;
     uint32_t rowbuf_stride;    // int32 per column: 1 (row buffer) or 2 (SPLIT {value, tag} granules)
+    uint64_t rowbuf_x_off;     // LocalGotoh: int32 offset of the Ix rows from the M rows
     uint32_t max_n;
     sa_result* res;
     uint32_t pair_base, count;
-    int32_t gap;
+    int32_t gap, gap_open, gap_extend;
 };
 
 struct TbParams {
@@ -172,7 +173,7 @@ __device__ __forceinline__ bool tb_mine(const TP& P, uint32_t flags) {
 hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
 // One wave per pair (sa_traceback_wave.hip): the few-pairs traceback.
 hipError_t launch_traceback_wave(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
-hipError_t launch_endcell(int R, const EndcellParams& p, hipStream_t stream);
+hipError_t launch_endcell(int algo, int R, const EndcellParams& p, hipStream_t stream);
 }  // namespace sa
 #include <string>
 #include <vector>

@@ -121,8 +121,8 @@ def test_plan_t16_eligibility_by_scoring():
     # affine (T16 affine kernel): LocalGotoh at any size (retry above the int16 headroom),
     # GlobalGotoh while the affine path bounds fit 8*(V - delta); no mismatches allowed -> int32
     aff = sa.ScoringSystem(-3, -1, 1, -1)
-    assert sa.plan_query_ex(2, aff, 1024, 1024, 10000)[:3] == (sa.SA_KERNEL_T16, 16, 1)
-    assert sa.plan_query_ex(2, aff, 8192, 8192, 10000)[0] == sa.SA_KERNEL_T16
+    assert sa.plan_query_ex(2, aff, 1024, 1024, 10000)[:3] == (sa.SA_KERNEL_T16_ENDCELL, 16, 1)
+    assert sa.plan_query_ex(2, aff, 8192, 8192, 10000)[0] == sa.SA_KERNEL_T16_ENDCELL
     assert sa.plan_query_ex(3, aff, 2048, 2048, 10000)[:3] == (sa.SA_KERNEL_T16, 16, 1)
     assert sa.plan_query_ex(3, aff, 4096, 4096, 10000)[0] == sa.SA_KERNEL_INT32
     assert sa.plan_query_ex(2, sa.ScoringSystem(-3, -1, 1, -1, False), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32

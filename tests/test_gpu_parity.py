@@ -331,9 +331,9 @@ def test_t16_affine_eligibility_and_retry(engine):
     pairs[5] = (hot, hot)                                        # score 5000 > 4094: retried
     pairs[900] = (hot[:4600], sa.synth_mutate(hot, 5)[:4700])
     compare_with_oracle(engine, 2, lg, pairs)
-    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16_ENDCELL
     compare_with_oracle(engine, 2, lg, [pairs[5], pairs[6], pairs[900]])
-    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16_ENDCELL
     gg = (-3, -1, 1, -1, True)
     two = [(sa.synth_dna(93_000, 2048), sa.synth_dna(93_001, 2048)),
            (sa.synth_dna(93_002, 2000), sa.synth_mutate(sa.synth_dna(93_002, 2000), 4)[:2048])]
@@ -344,7 +344,7 @@ def test_t16_affine_eligibility_and_retry(engine):
     assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
     for pid in ("probe8192/lg/-3_-1_1_-1_1/equal", "mut4096/lg/-3_-1_1_-1_1/equal"):
         assert check_golden(engine, [big[pid]]) == 1
-        assert engine.last_plan()[0] == sa.SA_KERNEL_T16, pid
+        assert engine.last_plan()[0] == sa.SA_KERNEL_T16_ENDCELL, pid
     dna = dna_pairs(31, 6, 400)
     compare_with_oracle(engine, 2, (-3, -1, 1, -1, False), dna)
     assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
@@ -379,6 +379,14 @@ def test_endcell_replay_vs_oracle(engine):
     for args in [(-1, 1, -1), (-3, 2, -2), (-1, 2, -1)]:
         compare_with_oracle(engine, 0, args, pairs)
         assert engine.last_plan()[:2] == (sa.SA_KERNEL_T16_ENDCELL, 32), args
+    # LocalGotoh: the affine end-cell replay (M, Iy and the last row's Ix per lane; the band's top
+    # M and Ix rows), R = 16 (max_m 4200 -> 5 bands); the SPLIT plan's R = 2, 4, 8 replays below
+    for args in [(-3, -1, 1, -1, True), (-2, -1, 2, -1, True), (-1, -1, 3, -2, True)]:
+        compare_with_oracle(engine, 2, args, pairs)
+        assert engine.last_plan()[:2] == (sa.SA_KERNEL_T16_ENDCELL, 16), args
+    few = [pairs[7], pairs[11], pairs[13], pairs[1], pairs[2], pairs[0]]
+    compare_with_oracle(engine, 2, (-3, -1, 1, -1, True), few)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16_ENDCELL
 
 
 @pytest.mark.parametrize("match", ["purine", "nwild", "caseless"])
