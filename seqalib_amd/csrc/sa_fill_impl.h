@@ -290,8 +290,12 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
         if constexpr (AFF) up_x = shr1(s_step[32 + q], xl);
         sym = shr1(s_step[64 + q], sym);
         const int j = s - lane;
+        // T16 with whole record words: the v_alignbit pushes shift every bit a word held out of
+        // it, and a lane-step outside the matrix only fills its own (never read) record bytes
+        if constexpr (!T16 || RB % 32 != 0) {
 #pragma unroll
-        for (int e = 0; e < RW; ++e) rec[e] = 0;
+            for (int e = 0; e < RW; ++e) rec[e] = 0;
+        }
         if (STEADY || (unsigned)j < (unsigned)n) {
             const int jkey = j + 1;      // 1-based column, < 2^16 when KEYED
             int hd = prev_up;            // H[i-1][j-1] of my first row

@@ -37,6 +37,7 @@ KERNELS = {  # label -> (TU, mangled name, cells per lane in one steady block = 
     "nw_t16_r16": ("sa_fill_nw.hip", "_ZN2sa11fill_kernelILi1ELi16ELi0ELb1ELb0ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
     "lg_int32_r16": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi16ELi0ELb1ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 32),
     "lg_t16_r16": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi16ELi0ELb1ELb1ELb1ELb0ELb0EEEvNS_10FillParamsE", 16),
+    "lg_t16c_r16": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi16ELi0ELb1ELb1ELb1ELb1ELb0EEEvNS_10FillParamsE", 16),
     "lg_t16_r8": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi8ELi0ELb1ELb1ELb1ELb0ELb0EEEvNS_10FillParamsE", 16),
     "gg_t16_r16": ("sa_fill_gg.hip", "_ZN2sa11fill_kernelILi3ELi16ELi0ELb1ELb0ELb1ELb0ELb0EEEvNS_10FillParamsE", 16),
     "gg_int32_r16": ("sa_fill_gg.hip", "_ZN2sa11fill_kernelILi3ELi16ELi0ELb1ELb0ELb0ELb0ELb0EEEvNS_10FillParamsE", 32),
