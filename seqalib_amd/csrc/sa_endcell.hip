@@ -77,10 +77,10 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
         int prev_up = 0;
         if (cc > 0) {
             const uint64_t e = (uint64_t)b * P.snap_nch + (cc - 1);
-            const uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + (e * kWave + lane) * (R / 2);
+            const uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + e * (R / 2) * kWave + lane;
 #pragma unroll
             for (int q = 0; q < R / 2; ++q) {
-                const uint32_t w = sh[q];
+                const uint32_t w = sh[q * kWave];
                 Hp[2 * q] = (int)(w & 0xffffu) >> 2;        // stored as 4H (non-negative)
                 Hp[2 * q + 1] = (int)(w >> 16) >> 2;
             }
@@ -184,16 +184,16 @@ __global__ __launch_bounds__(64) void endcell_lg_kernel(EndcellParams P) {
         int prev_up = 0, xl = kNeg;
         if (cc > 0) {
             const uint64_t e = (uint64_t)b * P.snap_nch + (cc - 1);
-            const uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + (e * kWave + lane) * (R + 1);
+            const uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + e * (R + 1) * kWave + lane;
 #pragma unroll
             for (int q = 0; q < R / 2; ++q) {
-                const uint32_t w = sh[q], y = sh[R / 2 + q];
+                const uint32_t w = sh[q * kWave], y = sh[(R / 2 + q) * kWave];
                 Mp[2 * q] = (int)(w & 0xffffu) >> 3;   // 8M, non-negative
                 Mp[2 * q + 1] = (int)(w >> 16) >> 3;
                 Yp[2 * q] = (int)(int16_t)(y & 0xffffu) >> 3;   // 8Iy + 2 (the border: far below)
                 Yp[2 * q + 1] = (int)(int16_t)(y >> 16) >> 3;
             }
-            xl = (int)(int16_t)(sh[R] & 0xffffu) >> 3;
+            xl = (int)(int16_t)(sh[R * kWave] & 0xffffu) >> 3;
             prev_up = P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] >> 3;
         }
         int hl = Mp[R - 1];

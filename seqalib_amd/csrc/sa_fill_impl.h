@@ -728,15 +728,16 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     if (chunk + 1 < nch) {   // state entering chunk + 1, for the end-cell replay
                         // R 16-bit values (affine: then the R Iy values and the last row's Ix)
                         constexpr int SW = AFF ? R + 1 : R / 2;
-                        uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + (e * kWave + lane) * SW;
+                        // word-major ([chunk][word][lane]): every store is one coalesced 256 B row
+                        uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + e * SW * kWave + lane;
 #pragma unroll
                         for (int q = 0; q < R / 2; ++q)
-                            sh[q] = ((uint32_t)Hp[2 * q] & 0xffffu) | ((uint32_t)Hp[2 * q + 1] << 16);
+                            sh[q * kWave] = ((uint32_t)Hp[2 * q] & 0xffffu) | ((uint32_t)Hp[2 * q + 1] << 16);
                         if constexpr (AFF) {
 #pragma unroll
                             for (int q = 0; q < R / 2; ++q)
-                                sh[R / 2 + q] = ((uint32_t)Yp[2 * q] & 0xffffu) | ((uint32_t)Yp[2 * q + 1] << 16);
-                            sh[R] = (uint32_t)xl;
+                                sh[(R / 2 + q) * kWave] = ((uint32_t)Yp[2 * q] & 0xffffu) | ((uint32_t)Yp[2 * q + 1] << 16);
+                            sh[R * kWave] = (uint32_t)xl;
                         }
                         P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = prev_up;
                     }

@@ -55,7 +55,7 @@ struct FillParams {
     // T16 affine only: the Ix / Iy border value (the reference's -10000), encoded below every
     // candidate of the batch's score range (t16_mode, sa_api.hip)
     int32_t t16_sent;
-    // CMAX only (see sa_fill_impl.h): per-slot snapshots [band][chunk][lane] of the R 16-bit row
+    // CMAX only (see sa_fill_impl.h): per-slot snapshots [band][chunk][word][lane] of the R 16-bit row
     // values (R/2 words) and of the diagonal input (1 word); snap_nch = chunks per band.
     uint32_t* snap_h;   // LocalGotoh: R values of M, then R of Iy, then the last row's Ix (R + 1 words)
     int32_t* snap_p;
