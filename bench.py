@@ -39,7 +39,7 @@ SCORING = (-1, 1, -1)         # SmithWatermanSA::getDefaultScoring (SASmithWater
 # The fill kernel is VALU-issue bound.  Its roofline peak is the issue ceiling of the steady
 # loop's own instruction mix, every opcode priced at its measured gfx950 issue rate
 # (tools/issue_model.py -> ISSUE_MODEL, rates from profiles/microbench_valu_issue_r01.txt).
-ISSUE_MODEL = os.path.join(ROOT, "profiles", "issue_model_r03.json")
+ISSUE_MODEL = os.path.join(ROOT, "profiles", "issue_model_r04.json")
 # Register-only cell-level measurement of the same instruction mix (tools/microbench_cellmix.hip,
 # variant V8 = the shipped T16 end-cell cell): what the mix really issues at, no memory traffic.
 CELL_MIX_CEILING = {"sw_t16c_r32": (5677.8, "profiles/microbench_cellmix_r01.txt (V8, 3 waves/SIMD as the fill runs)")}
@@ -284,7 +284,7 @@ def main():
                  "issue_ceiling_gcups": model["peak_gcups"] if model else None,
                  "issue_ceiling_frac": round(fill_gcups / model["peak_gcups"], 4) if model else None,
                  "issue_ceiling_basis": "steady-loop VALU mix x measured per-opcode issue rates (tools/issue_model.py, "
-                                        "profiles/issue_model_r03.json)",
+                                        "profiles/issue_model_r04.json)",
                  "cell_mix_ceiling_gcups": CELL_MIX_CEILING.get(label, (None,))[0],
                  "cell_mix_frac": (round(fill_gcups / CELL_MIX_CEILING[label][0], 4) if label in CELL_MIX_CEILING else None),
                  "cell_mix_source": CELL_MIX_CEILING.get(label, (None, None))[1],
