@@ -181,12 +181,13 @@ int sa_align_batch_device(sa_ctx* ctx, int algo, const sa_scoring* scoring,
 int sa_last_timings(sa_ctx* ctx, float* fill_ms, float* traceback_ms, int* fill_launches);
 
 /* Fill kernel of the last sa_align_batch[_device] call: SA_KERNEL_INT32 (int32 scores, equality
- * flags; any alphabet, LUT, scoring) or SA_KERNEL_T16 (tagged 16-bit profile kernel: SW/NW with
- * allow-mismatch, <= 4 distinct symbols in the batch, scores proven to fit).  Also R and W.
- * Environment: SEQALIB_T16=0 forces the int32 kernel. */
+ * flags; any alphabet, LUT, scoring) or SA_KERNEL_T16 (tagged 16-bit profile kernels: SW/NW and,
+ * with the affine cell, LocalGotoh/GlobalGotoh, all with allow-mismatch, <= 4 distinct symbols in
+ * the batch, score range checked).  Also R and W.  Environment: SEQALIB_T16=0 forces the int32
+ * kernel. */
 #define SA_KERNEL_INT32 0
 #define SA_KERNEL_T16 1
-#define SA_KERNEL_T16_ENDCELL 2   /* T16 SW with per-chunk maxima + end-cell replay */
+#define SA_KERNEL_T16_ENDCELL 2   /* T16 SW / LocalGotoh with per-chunk maxima + end-cell replay */
 int sa_last_plan(sa_ctx* ctx, int* kernel, int* rows_per_lane, int* waves);
 
 /* Plan of the int32 kernel for a batch (host-only query, no device needed): rows per lane R,

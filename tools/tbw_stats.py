@@ -1,8 +1,8 @@
-"""Wave-traceback statistics (debug build: `make stats` -> build/libstats.so).
+"""Wave-traceback statistics (debug build: `make stats`, copied to tools/bin/libstats.so).
     python3 tools/tbw_stats.py [pairs=1] [len=4096]"""
 import ctypes as C, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["SEQALIB_HIP_LIB"] = os.path.join(ROOT, "build", "libstats.so")
+os.environ["SEQALIB_HIP_LIB"] = os.path.join(ROOT, "tools", "bin", "libstats.so")
 sys.path.insert(0, ROOT)
 import numpy as np, torch
 import seqalib_amd as sa
