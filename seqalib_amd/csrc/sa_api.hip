@@ -154,6 +154,7 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t
 struct Variant {
     Plan pl;
     bool t16 = false, cmax = false;
+    bool x2 = false;   // two pairs per wave (sa_fill_x2.hip)
     uint32_t snap_nch = 0;
     uint64_t snap_h_slot = 0, snap_p_slot = 0;   // 32-bit words per pair
     uint64_t slot_bytes = 0;
@@ -169,6 +170,14 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
     v.cmax = t16 && v.pl.W == 1 && v.pl.R >= 2 &&
              ((algo == SA_SW && v.pl.R <= 32) || (algo == SA_LOCAL_GOTOH && v.pl.R <= 16));
     if (const char* ec = getenv("SEQALIB_CMAX")) if (ec[0] == '0') v.cmax = false;
+    // Many long SW pairs: two pairs per wave on packed 16-bit halves (sa_fill_x2.hip), bands of
+    // 1024 rows (R = 16: 96 VGPRs, 5 waves per SIMD).  SEQALIB_X2=0 keeps one pair per wave.
+    v.x2 = v.cmax && algo == SA_SW && !v.pl.split && v.pl.W == 1 && v.pl.R >= 16 && npairs >= 1024;
+    if (const char* e2 = getenv("SEQALIB_X2")) if (e2[0] == '0') v.x2 = false;
+    if (v.x2) {
+        v.pl.R = 16;
+        v.pl.g = make_geom(algo, 16, max_m, max_n, 2);
+    }
     if (v.cmax) {
         v.snap_nch = chunks_per_band(max_n);
         v.snap_p_slot = (uint64_t)v.pl.g.bands * v.snap_nch * kWave;
@@ -177,7 +186,7 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
         v.pl.rowbuf_elems = (uint64_t)(is_affine(algo) ? 2 : 1) * v.pl.g.bands * std::max<uint32_t>(max_n, 1);
     }
     if (v.pl.split) v.pl.rowbuf_elems = 0;   // hand-off granules live in c->split
-    v.kernel = v.cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
+    v.kernel = v.x2 ? SA_KERNEL_T16_X2 : v.cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
     v.slot_bytes = v.pl.g.dir_slot + v.pl.rowbuf_elems * 4 + (v.snap_h_slot + 2 * v.snap_p_slot) * 4;
     return v;
 }
@@ -507,6 +516,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fp.gap = sc->gap; fp.match = sc->match; fp.mismatch = allow ? sc->mismatch : INT_MIN;
             fp.gap_open = sc->gap_open; fp.gap_extend = sc->gap_extend;
             fp.waves = pl.W;
+            fp.count = cnt;
             fp.stage_seq2 = max_n <= kMaxStagedSeq2 ? 1 : 0;
             fp.prof = aux + kAuxProf;
             fp.sel = sel; fp.sel_want = v.t16 ? 1u : 0u;
@@ -522,7 +532,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fp.hand_x_off = pl.split ? hand_x_off : 0;
             fp.part = pl.split ? reinterpret_cast<int32_t*>(c->split + sp_zero) : nullptr;
             const FillVariant fv = {pl.R, lut, allow, keyed, v.t16, v.cmax, pl.split, bits};
-            hipError_t e = launch_fill(algo, fv, fp, pl.split ? (uint32_t)(cnt * sp_bands) : cnt, sf);
+            hipError_t e = v.x2 ? launch_fill_sw_x2(pl.R, fp, cnt, sf)
+                                : launch_fill(algo, fv, fp, pl.split ? (uint32_t)(cnt * sp_bands) : cnt, sf);
             if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
             if (pl.split) {
                 SplitReduceParams rp;
@@ -575,7 +586,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             tp.gap = fps[k].gap; tp.match = fps[k].match; tp.mismatch = fps[k].mismatch;
             tp.gap_open = fps[k].gap_open; tp.gap_extend = fps[k].gap_extend;
             tp.allow = allow ? 1 : 0;
-            tp.tagged = v.t16 ? 1 : 0;
+            tp.tagged = v.x2 ? 2 : (v.t16 ? 1 : 0);
             tp.sel = sel; tp.sel_want = fps[k].sel_want;
             hipError_t e = tb_wave(cnt) ? launch_traceback_wave(algo, v.pl.R, lut, tp, stb)
                                         : launch_traceback(algo, v.pl.R, lut, tp, stb);

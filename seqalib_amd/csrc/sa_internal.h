@@ -37,6 +37,7 @@ struct FillParams {
     uint32_t max_m, max_n;
     int32_t gap, match, mismatch, gap_open, gap_extend;
     int waves;                 // waves per workgroup (blockDim.x / 64)
+    uint32_t count;            // pairs of this launch (the two-pair kernel's odd tail)
     int stage_seq2;            // 1: Seq2 of the pair is copied to LDS (max_n <= kMaxStagedSeq2)
     // T16 kernel only: the batch alphabet is <= 4 symbols, prof[4] = sym_pack (byte c = the
     // symbol of code c) and prof[c] holds, in byte c', the tagged substitution term
@@ -127,7 +128,7 @@ struct TbParams {
     uint32_t max_m, max_n;
     int32_t gap, match, mismatch, gap_open, gap_extend;
     int allow;
-    int tagged;                // records hold T16 max tags (sa_layout.h)
+    int tagged;                // record layout: 0 flags, 1 T16 max tags, 2 two-pair tags (sa_layout.h)
     int vrec;                  // kMatchBits fills: under fD the second flag bit is the match bit
     const uint32_t* sel;
     uint32_t sel_want;
@@ -140,6 +141,7 @@ struct TbParams {
 struct FillVariant {
     int R;
     bool lut, allow, keyed, t16, cmax, split;
+    bool x2 = false;     // T16 SW chunk-max fill, two pairs per wave (sa_fill_x2.hip)
     bool bits = false;   // kMatchBits (then lut is ignored)
 };
 hipError_t launch_fill(int algo, const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream);
@@ -147,6 +149,8 @@ hipError_t launch_fill_sw(const FillVariant& v, const FillParams& p, uint32_t gr
 hipError_t launch_fill_nw(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_fill_lg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_fill_gg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
+// T16 SW chunk-max fill, two pairs per wave (sa_fill_x2.hip), R in {16, 32}
+hipError_t launch_fill_sw_x2(int R, const FillParams& p, uint32_t pairs, hipStream_t stream);
 // Batch alphabet scan (presence bitmap of every byte of both sequence sets, 8 words) and the
 // device-side T16 decision.  aux layout (kAux* below): [bitmap 8][profile 4][sym_pack][sel].
 constexpr int kAuxProf = 8, kAuxSel = 13, kAuxWords = 64;

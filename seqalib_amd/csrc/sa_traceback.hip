@@ -86,7 +86,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {   // tb_min
     const int n = (int)(P.off2[pidx + 1] - o2);
     const uint8_t* s1 = P.seq1 + o1;
     const uint8_t* s2 = P.seq2 + o2;
-    const bool tagged = P.tagged != 0;
+    const int tagged = P.tagged;   // record layout (sa_layout.h Geom::tagged)
     // Locals only below: lambdas capturing P or a Geom by reference keep them on the stack.
     const uint64_t band_stride = make_geom(ALG, R, P.max_m, P.max_n, tagged).band_stride;
     const uint32_t* const lutbits = P.lutbits;

@@ -57,7 +57,7 @@ typedef uint32_t __attribute__((address_space(3))) tw_u32;
 // matrix masked to 0 afterwards), so the wave waits once for all of them.
 template <int ALG, int R, bool LUT>
 __device__ __attribute__((noinline)) void tw_decode(const uint8_t* dir, const uint8_t* s1, const uint8_t* s2, int m,
-                                                    int n, uint32_t max_m, uint32_t max_n, bool tagged, bool vrec, int i0,
+                                                    int n, uint32_t max_m, uint32_t max_n, int tagged, bool vrec, int i0,
                                                     int j0, tw_u8* win, tw_u8* sq1, tw_u8* sq2,
                                                     const tw_u32* lut) {
     constexpr int BPC = bits_per_cell(ALG);   // flag bits (records may pad above them: record_bpc)
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(64) void traceback_wave_kernel(TbParams P) {
     const int n = (int)(P.off2[pidx + 1] - o2);
     const uint8_t* s1 = P.seq1 + o1;
     const uint8_t* s2 = P.seq2 + o2;
-    const bool tagged = P.tagged != 0;
+    const int tagged = P.tagged;   // record layout (sa_layout.h Geom::tagged)
     const uint8_t* dir = P.dirs + (uint64_t)slot * P.dir_slot;
     uint8_t* ops = P.ops + o1 + o2 + pidx;
     const bool allow = P.allow != 0;

@@ -228,7 +228,7 @@ def test_split_plan_vs_oracle(engine, algo, monkeypatch):
     assert engine.last_plan()[1:] == (2, 0)
 
 
-T16_KERNELS = (sa.SA_KERNEL_T16, sa.SA_KERNEL_T16_ENDCELL)
+T16_KERNELS = (sa.SA_KERNEL_T16, sa.SA_KERNEL_T16_ENDCELL, sa.SA_KERNEL_T16_X2)
 
 
 def dna_pairs(seed, count, maxlen):
@@ -353,11 +353,12 @@ def test_t16_affine_eligibility_and_retry(engine):
     assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
 
 
-def test_endcell_replay_vs_oracle(engine):
-    """>= 1024 DNA SW pairs take the one-wave T16 plan with per-chunk maxima and the end-cell
-    replay (sa_endcell.hip).  Cases: all-zero matrices (end cell = last cell), periodic
-    sequences (many tied maxima across rows and chunks), identical sequences, and multi-band
-    pairs at R = 32 (max_m 4200 -> 3 bands)."""
+def test_endcell_replay_vs_oracle(engine, monkeypatch):
+    """>= 1024 DNA SW pairs take the T16 plan with per-chunk maxima and the end-cell replay
+    (sa_endcell.hip): two pairs per wave at R = 16 (sa_fill_x2.hip; max_m 4200 -> 5 bands, ragged
+    shapes inside a wave, the odd last pair alone), and with SEQALIB_X2=0 one pair per wave at
+    R = 32 (3 bands).  Cases: all-zero matrices (end cell = last cell), periodic sequences (many
+    tied maxima across rows and chunks), identical sequences, multi-band pairs."""
     rng = np.random.default_rng(5)
     pairs = []
     for k in range(1030):
@@ -378,7 +379,14 @@ def test_endcell_replay_vs_oracle(engine):
     pairs[13] = (b"ACGT" * 1050, b"ACGT" * 700)
     for args in [(-1, 1, -1), (-3, 2, -2), (-1, 2, -1)]:
         compare_with_oracle(engine, 0, args, pairs)
+        assert engine.last_plan()[:2] == (sa.SA_KERNEL_T16_X2, 16), args
+    compare_with_oracle(engine, 0, (-1, 1, -1), pairs[:1029])   # odd count: the last wave has one pair
+    assert engine.last_plan()[:2] == (sa.SA_KERNEL_T16_X2, 16)
+    monkeypatch.setenv("SEQALIB_X2", "0")
+    for args in [(-1, 1, -1), (-3, 2, -2)]:
+        compare_with_oracle(engine, 0, args, pairs)
         assert engine.last_plan()[:2] == (sa.SA_KERNEL_T16_ENDCELL, 32), args
+    monkeypatch.delenv("SEQALIB_X2")
     # LocalGotoh: the affine end-cell replay (M, Iy and the last row's Ix per lane; the band's top
     # M and Ix rows), R = 16 (max_m 4200 -> 5 bands); the SPLIT plan's R = 2, 4, 8 replays below
     for args in [(-3, -1, 1, -1, True), (-2, -1, 2, -1, True), (-1, -1, 3, -2, True)]:
