@@ -122,7 +122,7 @@ __global__ __launch_bounds__(64, R == 16 ? 5 : 3) void fill_x2_kernel(FillParams
             const int row = row0 + r;
             const uint32_t ca = row < m[0] ? x2_code(symp, s1[0][row]) : 13u;
             const uint32_t cb = row < m[1] ? 4u + x2_code(symp, s1[1][row]) : 13u;
-            rs[r] = 0x0c000c00u | ca << 8 | cb << 24;
+            rs[r] = 0x000c000cu | ca << 8 | cb << 24;   // bytes 0, 2: selector 12 = 0x00
             Hp[r] = 0;
         }
         lkey[0] = lkey[1] = 0;

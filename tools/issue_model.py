@@ -35,7 +35,7 @@ KERNELS = {  # label -> (TU, mangled name, cells per lane in one steady block = 
     "nw_t16_r32": ("sa_fill_nw.hip", "_ZN2sa11fill_kernelILi1ELi32ELi0ELb1ELb0ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
     "sw_int32_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELi0ELb1ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 64),
     "nw_t16_r16": ("sa_fill_nw.hip", "_ZN2sa11fill_kernelILi1ELi16ELi0ELb1ELb0ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
-    "sw_x2_r16": ("sa_fill_x2.hip", "_ZN2sa14fill_x2_kernelILi16EEEvNS_10FillParamsE", 128),
+    "sw_x2_r16": ("sa_fill_x2.hip", "_ZN2sa14fill_x2_kernelILi16EEEvNS_10FillParamsE", 32),   # one step (exec-masked body): 16 rows x 2 pairs
     "lg_int32_r16": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi16ELi0ELb1ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 32),
     "lg_t16_r16": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi16ELi0ELb1ELb1ELb1ELb0ELb0EEEvNS_10FillParamsE", 16),
     "lg_t16c_r16": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi16ELi0ELb1ELb1ELb1ELb1ELb0EEEvNS_10FillParamsE", 16),

@@ -28,7 +28,7 @@ __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, i
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         tab[r] = in[(lane * 7 + r) & 1023];
-        sel[r] = 0x0c000c00u | ((uint32_t)(r & 3) << 8) | ((uint32_t)(4 + ((r + lane) & 3)) << 24);
+        sel[r] = 0x000c000cu | ((uint32_t)(r & 3) << 8) | ((uint32_t)(4 + ((r + lane) & 3)) << 24);
         Hp[r] = 0;
     }
     uint32_t hl = 0, sym = (lane & 3) * 8, colA = in[lane & 1023], colB = in[(lane + 5) & 1023];
