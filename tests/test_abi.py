@@ -88,10 +88,10 @@ def test_headline_plan_fits_hbm():
     assert ws >= t16_dirs
     assert 2 * 10000 * ws + 2 * 4096 < 0.5 * 288e9, ws   # one launch, both slots, well inside HBM
     R32, W32, dir_bytes, row_bytes = sa.plan_query(0, 4096, 4096, 10000)
-    assert (R32, W32) == (16, 4)
+    assert (R32, W32) == (16, 1)
     assert 10000 * (dir_bytes + row_bytes) < 64e9
     # more than four symbols: the int32 kernel
-    assert sa.plan_query_ex(0, sw, 4096, 4096, 10000, nsym=5)[:3] == (sa.SA_KERNEL_INT32, 16, 4)
+    assert sa.plan_query_ex(0, sw, 4096, 4096, 10000, nsym=5)[:3] == (sa.SA_KERNEL_INT32, 16, 1)
 
 
 @pytest.mark.parametrize("m,n,npairs,plan", [

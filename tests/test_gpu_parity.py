@@ -160,7 +160,8 @@ def test_ragged_batch_vs_oracle(engine, algo):
 
 @pytest.mark.parametrize("algo", [0, 1, 2, 3])
 def test_many_pairs_plan_vs_oracle(engine, algo):
-    """>= 1024 pairs selects the 4-wave many-pairs plan."""
+    """>= 1024 pairs selects the one-wave many-pairs plan (bands back to back through the row
+    buffer; T16 for DNA SW/NW/Gotoh with allow-mismatch, int32 otherwise)."""
     pairs = []
     for k in range(1100):
         m, n = 150 + (k % 37), 140 + (k % 53)
