@@ -173,10 +173,13 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
     v.cmax = t16 && v.pl.W == 1 && v.pl.R >= 2 &&
              ((algo == SA_SW && v.pl.R <= 32) || (algo == SA_LOCAL_GOTOH && v.pl.R <= 16));
     if (const char* ec = getenv("SEQALIB_CMAX")) if (ec[0] == '0') v.cmax = false;
-    // Many long SW pairs: two pairs per wave on packed 16-bit halves (sa_fill_x2.hip), bands of
-    // 1024 rows (R = 16: 96 VGPRs, 5 waves per SIMD).  SEQALIB_X2=0 keeps one pair per wave.
-    v.x2 = v.cmax && algo == SA_SW && !v.pl.split && v.pl.W == 1 && v.pl.R >= 16 && npairs >= 1024;
-    if (const char* e2 = getenv("SEQALIB_X2")) if (e2[0] == '0') v.x2 = false;
+    // Two pairs per wave on packed 16-bit halves (sa_fill_x2.hip, bands of 1024 rows, 5 waves per
+    // SIMD) for many long SW pairs: opt-in (SEQALIB_X2=1).  It takes the same shader cycles as
+    // the one-pair kernel on the headline batch (rocprofv3 GRBM_GUI_ACTIVE 5.34e8 vs 5.20e8,
+    // profiles/pmc_clock_r02.txt), so the default stays one pair per wave.
+    v.x2 = false;
+    if (const char* e2 = getenv("SEQALIB_X2"))
+        v.x2 = e2[0] == '1' && v.cmax && algo == SA_SW && !v.pl.split && v.pl.W == 1 && v.pl.R >= 16 && npairs >= 1024;
     if (v.x2) {
         v.pl.R = 16;
         v.pl.g = make_geom(algo, 16, max_m, max_n, 2);

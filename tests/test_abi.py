@@ -77,10 +77,10 @@ def test_plan_and_layout(algo, shape):
 
 def test_headline_plan_fits_hbm():
     # north-star batch: 10,000 pairs of 4096 x 4096 SW (DNA, default scoring).  The shipped plan is
-    # the T16 end-cell kernel with two pairs per wave, R = 16; the int32 plan is the fallback.
+    # the T16 end-cell kernel, one wave per pair, R = 32; the int32 plan is the fallback.
     sw = sa.ScoringSystem(-1, 1, -1)
     kernel, R, W, ws = sa.plan_query_ex(0, sw, 4096, 4096, 10000, nsym=4)
-    assert (kernel, R, W) == (sa.SA_KERNEL_T16_X2, 16, 1)
+    assert (kernel, R, W) == (sa.SA_KERNEL_T16_ENDCELL, 32, 1)
     # both variants are provisioned (the choice is made on the device): dirs + row buffers +
     # snapshots of the larger one; the pipelined context keeps two slots per pair of a launch
     steps_pad = -(-(4096 + 63) // 32) * 32
@@ -95,8 +95,8 @@ def test_headline_plan_fits_hbm():
 
 
 @pytest.mark.parametrize("m,n,npairs,plan", [
-    (1024, 1024, 10000, (sa.SA_KERNEL_T16_X2, 16, 1)),         # config 3
-    (2048, 2048, 12500, (sa.SA_KERNEL_T16_X2, 16, 1)),         # config 5 shard (1 of 8 GPUs)
+    (1024, 1024, 10000, (sa.SA_KERNEL_T16_ENDCELL, 16, 1)),    # config 3
+    (2048, 2048, 12500, (sa.SA_KERNEL_T16_ENDCELL, 32, 1)),    # config 5 shard (1 of 8 GPUs)
     (4096, 4096, 1, None),                                      # config 2: few pairs
 ])
 def test_config_plans(m, n, npairs, plan):
@@ -114,7 +114,7 @@ def test_plan_t16_eligibility_by_scoring():
     assert sa.plan_query_ex(1, sa.ScoringSystem(-1, 2, -1), 8192, 8192, 10000)[0] == sa.SA_KERNEL_INT32
     assert sa.plan_query_ex(1, sa.ScoringSystem(-1, 1, -1), 4096, 4096, 10000)[0] == sa.SA_KERNEL_T16
     # SW: any size with n < 65535 (pairs whose maximum passes the int16 headroom re-run on int32)
-    assert sa.plan_query_ex(0, sa.ScoringSystem(-1, 1, -1), 8192, 8192, 10000)[0] == sa.SA_KERNEL_T16_X2
+    assert sa.plan_query_ex(0, sa.ScoringSystem(-1, 1, -1), 8192, 8192, 10000)[0] == sa.SA_KERNEL_T16_ENDCELL
     assert sa.plan_query_ex(0, sa.ScoringSystem(-1, 1, -1), 8192, 70000, 10000)[0] == sa.SA_KERNEL_INT32
     # gap 0: the clamped up term needs gap < 0
     assert sa.plan_query_ex(0, sa.ScoringSystem(0, 1, -1), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32

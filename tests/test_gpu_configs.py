@@ -68,7 +68,7 @@ def test_config3_batch_1024(engine):
     R = 16 (one wave per pair, one band), every pair's score and end cell against the oracle."""
     s1, o1, s2, o2 = sa.synth_dna_batch(3_000_000_000, 10000, 1024, 1024, threads=THREADS)
     res, ops = engine.align_packed(0, sa.ScoringSystem(*SW), s1, o1, s2, o2)
-    assert engine.last_plan() == (sa.SA_KERNEL_T16_X2, 16, 1)
+    assert engine.last_plan() == (sa.SA_KERNEL_T16_ENDCELL, 16, 1)
     check_batch(engine, s1, o1, s2, o2, res, ops, score_sample=10000, ops_sample=256, seed=3)
 
 
@@ -81,16 +81,19 @@ def test_config5_shard_2048(engine):
     assert (start, stop) == (0, 12500)
     s1, o1, s2, o2 = sa.synth_dna_batch(5_000_000_000 + 2 * start, stop - start, 2048, 2048, threads=THREADS)
     res, ops = engine.align_packed(0, sa.ScoringSystem(*SW), s1, o1, s2, o2)
-    assert engine.last_plan() == (sa.SA_KERNEL_T16_X2, 16, 1)
+    assert engine.last_plan() == (sa.SA_KERNEL_T16_ENDCELL, 32, 1)
     check_batch(engine, s1, o1, s2, o2, res, ops, score_sample=2048, ops_sample=64, seed=5)
 
 
-def test_north_star_shape_1024x4096(engine):
+@pytest.mark.parametrize("x2", ["0", "1"])
+def test_north_star_shape_1024x4096(engine, x2, monkeypatch):
     """North-star pair shape (4096 x 4096), 1,024 pairs in one launch: every end cell against the
-    linear-space oracle, 128 pairs' op streams against the full-matrix oracle."""
+    linear-space oracle, 128 pairs' op streams against the full-matrix oracle -- on the shipped
+    one-pair kernel (R = 32) and on the opt-in two-pair kernel (SEQALIB_X2=1, R = 16)."""
+    monkeypatch.setenv("SEQALIB_X2", x2)
     s1, o1, s2, o2 = sa.synth_dna_batch(9_000_000_000, 1024, 4096, 4096, threads=THREADS)
     res, ops = engine.align_packed(0, sa.ScoringSystem(*SW), s1, o1, s2, o2)
-    assert engine.last_plan() == (sa.SA_KERNEL_T16_X2, 16, 1)
+    assert engine.last_plan() == ((sa.SA_KERNEL_T16_X2, 16, 1) if x2 == "1" else (sa.SA_KERNEL_T16_ENDCELL, 32, 1))
     check_batch(engine, s1, o1, s2, o2, res, ops, score_sample=1024, ops_sample=128, seed=9)
 
 
@@ -192,7 +195,7 @@ def test_device_selects_int32_for_wide_alphabet(engine):
         assert (res[p].score, res[p].end_i, res[p].end_j, res[p].ops) == (o["score"], o["end_i"], o["end_j"], o["ops"])
     pairs[5] = (sa.synth_dna(805, 700), pairs[5][1])
     res = engine.align(0, sa.ScoringSystem(*SW), pairs)
-    assert engine.last_plan()[0] == sa.SA_KERNEL_T16_X2
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16_ENDCELL
     o = oracle_align(0, SW, *pairs[5])
     assert (res[5].score, res[5].end_i, res[5].end_j, res[5].ops) == (o["score"], o["end_i"], o["end_j"], o["ops"])
 

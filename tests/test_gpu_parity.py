@@ -356,9 +356,9 @@ def test_t16_affine_eligibility_and_retry(engine):
 
 def test_endcell_replay_vs_oracle(engine, monkeypatch):
     """>= 1024 DNA SW pairs take the T16 plan with per-chunk maxima and the end-cell replay
-    (sa_endcell.hip): two pairs per wave at R = 16 (sa_fill_x2.hip; max_m 4200 -> 5 bands, ragged
-    shapes inside a wave, the odd last pair alone), and with SEQALIB_X2=0 one pair per wave at
-    R = 32 (3 bands).  Cases: all-zero matrices (end cell = last cell), periodic sequences (many
+    (sa_endcell.hip): one pair per wave at R = 32 (max_m 4200 -> 3 bands), and with SEQALIB_X2=1
+    two pairs per wave at R = 16 (sa_fill_x2.hip; 5 bands, ragged shapes inside a wave, the odd
+    last pair alone).  Cases: all-zero matrices (end cell = last cell), periodic sequences (many
     tied maxima across rows and chunks), identical sequences, multi-band pairs."""
     rng = np.random.default_rng(5)
     pairs = []
@@ -380,13 +380,13 @@ def test_endcell_replay_vs_oracle(engine, monkeypatch):
     pairs[13] = (b"ACGT" * 1050, b"ACGT" * 700)
     for args in [(-1, 1, -1), (-3, 2, -2), (-1, 2, -1)]:
         compare_with_oracle(engine, 0, args, pairs)
+        assert engine.last_plan()[:2] == (sa.SA_KERNEL_T16_ENDCELL, 32), args
+    monkeypatch.setenv("SEQALIB_X2", "1")
+    for args in [(-1, 1, -1), (-3, 2, -2)]:
+        compare_with_oracle(engine, 0, args, pairs)
         assert engine.last_plan()[:2] == (sa.SA_KERNEL_T16_X2, 16), args
     compare_with_oracle(engine, 0, (-1, 1, -1), pairs[:1029])   # odd count: the last wave has one pair
     assert engine.last_plan()[:2] == (sa.SA_KERNEL_T16_X2, 16)
-    monkeypatch.setenv("SEQALIB_X2", "0")
-    for args in [(-1, 1, -1), (-3, 2, -2)]:
-        compare_with_oracle(engine, 0, args, pairs)
-        assert engine.last_plan()[:2] == (sa.SA_KERNEL_T16_ENDCELL, 32), args
     monkeypatch.delenv("SEQALIB_X2")
     # LocalGotoh: the affine end-cell replay (M, Iy and the last row's Ix per lane; the band's top
     # M and Ix rows), R = 16 (max_m 4200 -> 5 bands); the SPLIT plan's R = 2, 4, 8 replays below
