@@ -141,8 +141,9 @@ struct TbParams {
 struct FillVariant {
     int R;
     bool lut, allow, keyed, t16, cmax, split;
-    bool x2 = false;     // T16 SW chunk-max fill, two pairs per wave (sa_fill_x2.hip)
     bool bits = false;   // kMatchBits (then lut is ignored)
+    bool x2 = false;     // T16 SW chunk-max fill, two pairs per wave (sa_fill_x2.hip); keep it
+                         // last: launch sites brace-initialise the members above in order
 };
 hipError_t launch_fill(int algo, const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream);
 hipError_t launch_fill_sw(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
