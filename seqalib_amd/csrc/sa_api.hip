@@ -210,10 +210,23 @@ __global__ void lut_to_bits(const uint8_t* lut, uint32_t* bits) {
 // per pair (sa_traceback.hip) for batches.  SEQALIB_TB=wave|lane overrides.
 bool tb_wave(uint32_t count) {
     if (const char* e = getenv("SEQALIB_TB")) {
-        if (!strcmp(e, "wave")) return true;
+        if (!strcmp(e, "wave") || !strcmp(e, "seg")) return true;
         if (!strcmp(e, "lane")) return false;
     }
     return count < 1024;
+}
+
+// Segmented traceback (sa_traceback_seg.hip) of SPLIT launches with the wave walker: 1 for the
+// pairs whose walk is long (seg_take), 2 for every pair (SEQALIB_TB=seg, tests), 0 off
+// (SEQALIB_TB=wave|lane).  It needs per pair and band NST * (n + 1) + 1 exit records, so it is
+// offered to launches of at most kSegMaxBands (pair, band) slots (16,384 when forced).
+constexpr uint64_t kSegMaxBands = 512;
+int tb_seg_mode() {
+    if (const char* e = getenv("SEQALIB_TB")) {
+        if (!strcmp(e, "seg")) return 2;
+        if (!strcmp(e, "wave") || !strcmp(e, "lane")) return 0;
+    }
+    return 1;
 }
 
 int ensure_ws(sa_ctx* c, uint64_t need) {
@@ -449,15 +462,25 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                                          " bytes of workspace, above the limit");
     int rc = ensure_ws(c, std::max<uint64_t>(pipe ? 2 * need : need, 4096));
     if (rc) return rc;
-    // SPLIT scratch (the fills of all calls run on one stream, so one copy serves the pipeline)
+    // SPLIT scratch, per variant: [ticket][hand-off granules] (zeroed before its fill; the
+    // segmented traceback reads the granules after both variants' fills), then the per-band
+    // partials and the segmented traceback's exit records.  Pipelined calls alternate two copies
+    // (the traceback of call k reads its granules beside the fill of call k + 1).
     const uint64_t aff2 = is_affine(algo) ? 2 : 1;
     const uint64_t sp_gran = any_split ? per_launch * sp_bands * std::max<uint32_t>(max_n, 1) * aff2 : 0;
-    const uint64_t sp_zero = 256 + sp_gran * 8;   // ticket + granules: zeroed before every launch
-    const uint64_t sp_need = any_split ? sp_zero + per_launch * sp_bands * 16 : 0;
+    const uint64_t sp_vblk = (256 + sp_gran * 8 + 255) & ~(uint64_t)255;
+    const uint64_t sp_part = (uint64_t)nv * sp_vblk;
+    const int seg_mode = any_split && tb_wave((uint32_t)per_launch) ? tb_seg_mode() : 0;
+    const bool seg_on = seg_mode != 0 && per_launch * sp_bands <= (seg_mode == 2 ? 16384 : kSegMaxBands);
+    const uint64_t seg_rs = (uint64_t)aff2 * ((uint64_t)max_n + 1) + 1;
+    const uint64_t sp_seg = (sp_part + per_launch * sp_bands * 16 + 255) & ~(uint64_t)255;
+    const uint64_t sp_slot = sp_seg + (seg_on ? (per_launch * sp_bands * seg_rs + per_launch) * 16 : 0);
+    const uint64_t sp_need = any_split ? sp_slot * (pipe ? 2 : 1) : 0;
     if (any_split && c->split_bytes < sp_need) {
         if (c->split) {
             SA_HIP(c, hipStreamSynchronize(c->stream));
             if (c->s_fill) SA_HIP(c, hipStreamSynchronize(c->s_fill));
+            if (c->s_tb) SA_HIP(c, hipStreamSynchronize(c->s_tb));
             (void)hipFree(c->split);
             c->split = nullptr;
             c->split_bytes = 0;
@@ -471,6 +494,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     // A pipeline slot is one contiguous half of the workspace holding everything its calls
     // write (dirs, row buffers, snapshots), so calls on the other slot never touch it.
     uint8_t* const wbase = c->ws + (pipe ? slot * ((c->ws_bytes / 2) & ~(uint64_t)255) : 0);
+    // (fixed halves of the scratch, as the workspace: a slot's block never moves with the shape)
+    uint8_t* const spbase = any_split ? c->split + (pipe ? slot * ((c->split_bytes / 2) & ~(uint64_t)255) : 0) : nullptr;
 
     // reset timing
     c->launches = 0;
@@ -496,14 +521,14 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         if (pipe && c->launches > 0) SA_HIP(c, hipStreamWaitEvent(sf, c->events[3 * c->launches - 1], 0));
         SA_HIP(c, hipEventRecord(ev[0], sf));
         const uint64_t hand_x_off = any_split ? (uint64_t)cnt * sp_bands * std::max<uint32_t>(max_n, 1) : 0;
-        if (any_split) SA_HIP(c, hipMemsetAsync(c->split, 0, 256 + hand_x_off * 8 * aff2, sf));
         FillParams fps[2];
         for (int k = 0; k < nv; ++k) {
             const Variant& v = vars[k];
             const Plan& pl = v.pl;
-            // a second SPLIT variant (the int32 re-run of flagged pairs) needs fresh tickets and
+            // each SPLIT variant (the int32 one re-runs flagged pairs) has its own tickets and
             // hand-off granules
-            if (k > 0 && pl.split) SA_HIP(c, hipMemsetAsync(c->split, 0, 256 + hand_x_off * 8 * aff2, sf));
+            uint8_t* const vblk = pl.split ? spbase + (uint64_t)k * sp_vblk : nullptr;
+            if (pl.split) SA_HIP(c, hipMemsetAsync(vblk, 0, 256 + hand_x_off * 8 * aff2, sf));
             uint8_t* dirs = wbase;
             int32_t* rowbuf = reinterpret_cast<int32_t*>(wbase + per_launch * pl.g.dir_slot);
             uint32_t* snap_h = reinterpret_cast<uint32_t*>(rowbuf + per_launch * pl.rowbuf_elems);
@@ -533,10 +558,10 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fp.snap_h = snap_h; fp.snap_p = snap_p; fp.snap_m = snap_m;
             fp.snap_h_slot = v.snap_h_slot; fp.snap_p_slot = v.snap_p_slot; fp.snap_nch = v.snap_nch;
             fp.split_bands = (uint32_t)sp_bands;
-            fp.ticket = pl.split ? reinterpret_cast<uint32_t*>(c->split) : nullptr;
-            fp.hand = pl.split ? reinterpret_cast<unsigned long long*>(c->split + 256) : nullptr;
+            fp.ticket = pl.split ? reinterpret_cast<uint32_t*>(vblk) : nullptr;
+            fp.hand = pl.split ? reinterpret_cast<unsigned long long*>(vblk + 256) : nullptr;
             fp.hand_x_off = pl.split ? hand_x_off : 0;
-            fp.part = pl.split ? reinterpret_cast<int32_t*>(c->split + sp_zero) : nullptr;
+            fp.part = pl.split ? reinterpret_cast<int32_t*>(spbase + sp_part) : nullptr;
             const FillVariant fv = {pl.R, lut, allow, keyed, v.t16, v.cmax, pl.split, bits};
             hipError_t e = v.x2 ? launch_fill_sw_x2(pl.R, fp, cnt, sf)
                                 : launch_fill(algo, fv, fp, pl.split ? (uint32_t)(cnt * sp_bands) : cnt, sf);
@@ -581,7 +606,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         if (pipe) SA_HIP(c, hipStreamWaitEvent(stb, ev[1], 0));
         for (int k = 0; k < nv; ++k) {
             const Variant& v = vars[k];
-            TbParams tp;
+            TbParams tp{};
             tp.seq1 = d1; tp.off1 = o1; tp.seq2 = d2; tp.off2 = o2;
             tp.lutbits = lut ? d_lutbits : nullptr;
             tp.vrec = bits ? 1 : 0;
@@ -594,6 +619,31 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             tp.allow = allow ? 1 : 0;
             tp.tagged = v.x2 ? 2 : (v.t16 ? 1 : 0);
             tp.sel = sel; tp.sel_want = fps[k].sel_want;
+            if (seg_on && v.pl.split && tb_wave(cnt)) {
+                tp.seg_mode = seg_mode;
+                tp.hand = fps[k].hand;
+                tp.hand_x_off = fps[k].hand_x_off;
+                tp.split_bands = (uint32_t)sp_bands;
+                tp.hand_shift = v.t16 ? (is_affine(algo) ? 3 : 2) : 0;
+                tp.seg_rec = reinterpret_cast<int4*>(spbase + sp_seg);
+                tp.seg_fin = tp.seg_rec + per_launch * sp_bands * seg_rs;
+                SA_HIP(c, hipMemsetAsync(tp.seg_fin, 0xff, (uint64_t)cnt * 16, stb));
+                hipError_t e = launch_traceback_seg(algo, v.pl.R, lut, tp, stb);
+                if (e != hipSuccess) return hip_fail(c, e, "segmented traceback kernel launch");
+                if (const char* dump = getenv("SEQALIB_SEG_DUMP")) {   // debugging aid: exit records
+                    const uint64_t nrec = (uint64_t)cnt * sp_bands * seg_rs;
+                    std::vector<int4> h(nrec + cnt);
+                    SA_HIP(c, hipStreamSynchronize(stb));
+                    SA_HIP(c, hipMemcpy(h.data(), tp.seg_rec, nrec * 16, hipMemcpyDeviceToHost));
+                    SA_HIP(c, hipMemcpy(h.data() + nrec, tp.seg_fin, (uint64_t)cnt * 16, hipMemcpyDeviceToHost));
+                    if (FILE* f = fopen(dump, "wb")) {
+                        const uint64_t hdr[4] = {cnt, sp_bands, seg_rs, (uint64_t)v.pl.R};
+                        fwrite(hdr, 8, 4, f);
+                        fwrite(h.data(), 16, h.size(), f);
+                        fclose(f);
+                    }
+                }
+            }
             hipError_t e = tb_wave(cnt) ? launch_traceback_wave(algo, v.pl.R, lut, tp, stb)
                                         : launch_traceback(algo, v.pl.R, lut, tp, stb);
             if (e != hipSuccess) return hip_fail(c, e, "traceback kernel launch");

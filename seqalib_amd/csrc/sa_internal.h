@@ -132,8 +132,21 @@ struct TbParams {
     int vrec;                  // kMatchBits fills: under fD the second flag bit is the match bit
     const uint32_t* sel;
     uint32_t sel_want;
+    // Segmented traceback of SPLIT fills (sa_traceback_seg.hip); seg_mode 0 off, 1 long walks,
+    // 2 every pair (tests).  hand / hand_x_off / split_bands: the fill's hand-off granules
+    // (FillParams), hand_shift: 0 int32 values, 2 / 3 T16 4H / 8V; seg_rec: per slot and band
+    // NST * (max_n + 1) + 1 exit records {i, j, nops, flags}; seg_fin: per slot {start_i,
+    // start_j, nops, flags} of the band where the walk stopped.
+    int seg_mode;
+    const unsigned long long* hand;
+    uint64_t hand_x_off;
+    uint32_t split_bands;
+    int hand_shift;
+    int4* seg_rec;
+    int4* seg_fin;
 };
 // SA_FLAG_TIMEOUT: a SPLIT band's bounded wait for its producer expired (results invalid)
+
 
 // R in {4, 8, 16}; keyed: 16-bit (score, column) max keys (local modes only); t16: the tagged
 // 16-bit profile kernel (SW/NW with allow-mismatch, see sa_fill_impl.h).
@@ -175,6 +188,29 @@ __device__ __forceinline__ bool tb_mine(const TP& P, uint32_t flags) {
     const bool redone = (flags & kFlagRedo) != 0;
     return *P.sel == P.sel_want ? !redone : redone;
 }
+// Does a pair take the segmented traceback?  The seg kernels and the wave walker evaluate it on
+// the same (unchanged) sa_result, so they agree.  *b_e: the band of the walk's first cell.  Long
+// walks only: a local path of score S has >= S / match diagonal moves, a global one >= max(m, n).
+constexpr int kSegMinMoves = 64;
+template <int ALG, int R>
+__device__ __forceinline__ bool seg_take(const TbParams& P, const sa_result& res, int m, int n, int* b_e) {
+    if (!P.seg_mode || !P.hand) return false;
+    if (res.flags & (SA_FLAG_BAD_SHAPE | SA_FLAG_TIMEOUT)) return false;
+    if (!tb_mine(P, res.flags)) return false;
+    if (m <= 0 || n <= 0) return false;
+    constexpr bool SCORED = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
+    int ie = m;
+    if (SCORED) {
+        ie = res.end_i;
+        if (ie < 1 || ie > m || res.end_j < 1 || res.end_j > n) return false;
+    }
+    *b_e = (ie - 1) / (kWave * R);
+    if (P.seg_mode == 2) return true;
+    if (*b_e < 1) return false;
+    if (SCORED) return P.match > 0 && (int64_t)res.score >= (int64_t)kSegMinMoves * P.match;
+    return m + n >= 16 * kSegMinMoves;
+}
+hipError_t launch_traceback_seg(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
 hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
 // One wave per pair (sa_traceback_wave.hip): the few-pairs traceback.
 hipError_t launch_traceback_wave(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);

@@ -131,10 +131,29 @@ __global__ __launch_bounds__(64) void traceback_wave_kernel(TbParams P) {
     sa_result res = P.res[pidx];
     if (res.flags & SA_FLAG_BAD_SHAPE) return;
     if (!tb_mine(P, res.flags)) return;
-    res.flags &= ~(kFlagRetry | kFlagRedo);
     const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
     const int m = (int)(P.off1[pidx + 1] - o1);
     const int n = (int)(P.off2[pidx + 1] - o2);
+    int seg_b = 0;
+    if (seg_take<ALG, R>(P, res, m, n, &seg_b)) {
+        // walked band-parallel by sa_traceback_seg.hip: apply the band where the walk stopped
+        if (lane == 0) {
+            const int4 f = P.seg_fin[slot];   // preset to -1 by the host
+            res.flags &= ~(kFlagRetry | kFlagRedo);
+            res.start_i = f.x;
+            res.start_j = f.y;
+            res.nops = (uint32_t)f.z;
+            if (f.w & 2) res.flags |= SA_FLAG_DIVERGED;
+            if (f.z < 0 || (f.w & 16)) {   // no band recorded the end, or a guard fired
+                res.start_i = -1;
+                res.start_j = -1;
+                res.nops = 0;
+            }
+            P.res[pidx] = res;
+        }
+        return;
+    }
+    res.flags &= ~(kFlagRetry | kFlagRedo);
     const uint8_t* s1 = P.seq1 + o1;
     const uint8_t* s2 = P.seq2 + o2;
     const int tagged = P.tagged;   // record layout (sa_layout.h Geom::tagged)

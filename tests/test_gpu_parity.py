@@ -556,10 +556,11 @@ def test_multi_gpu_threads_match_single(engine):
 
 
 @pytest.mark.parametrize("algo", [0, 1, 2, 3])
-@pytest.mark.parametrize("tb", ["wave", "lane"])
+@pytest.mark.parametrize("tb", ["wave", "lane", "seg"])
 def test_traceback_flavours_vs_oracle(engine, algo, tb, monkeypatch):
-    """Both traceback kernels on both plans: one wave per pair (sa_traceback_wave.hip, default
-    below 1024 pairs) and one lane per pair (sa_traceback.hip, default for batches), forced with
+    """The traceback kernels on both plans: one wave per pair (sa_traceback_wave.hip, default
+    below 1024 pairs), one lane per pair (sa_traceback.hip, default for batches) and the
+    band-parallel walk of SPLIT fills (sa_traceback_seg.hip, "seg": every pair), forced with
     SEQALIB_TB.  Long related pairs cross many decode windows (128 rows x 16 diagonals) and drift
     across diagonals through gaps; the many-pairs batch takes the one-wave-per-pair fill."""
     monkeypatch.setenv("SEQALIB_TB", tb)
@@ -572,3 +573,36 @@ def test_traceback_flavours_vs_oracle(engine, algo, tb, monkeypatch):
         b = sa.synth_mutate(a, k)[: 90 + k % 250] if k % 2 else sa.synth_dna(90_001 + 2 * k, 80 + k % 200)
         many.append((a, b))
     compare_with_oracle(engine, algo, SCORINGS[algo][0], many, "purine" if algo == 3 else None)
+
+
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+def test_segmented_traceback_vs_oracle(engine, algo, monkeypatch):
+    """Band-parallel traceback of SPLIT fills (sa_traceback_seg.hip): per band, walkers from every
+    cell of its last row (score from the fill's hand-off granules) record where they leave the
+    band; the path is then chained from the end cell and each band's segment re-walked at its op
+    offset.  Forced for every pair (SEQALIB_TB=seg) on every SPLIT R, T16 and int32 kernels,
+    related pairs (long paths over many bands, gaps across band edges) and a custom match table;
+    and the default (long walks only) on one long related pair per algorithm."""
+    rng = np.random.default_rng(300 + algo)
+    pairs = []
+    for k in range(6):
+        m = int(rng.integers(300, 2300))
+        a = sa.synth_dna(40_000 + 2 * k, m)
+        b = sa.synth_mutate(a, 7 + k) if k % 3 else sa.synth_dna(40_001 + 2 * k, int(rng.integers(200, 2400)))
+        pairs.append((a, b))
+    pairs.append((sa.synth_dna(41_000, 700), sa.synth_dna(41_001, 1)))
+    pairs.append((sa.synth_dna(41_002, 1), sa.synth_dna(41_003, 900)))
+    monkeypatch.setenv("SEQALIB_TB", "seg")
+    for r in (1, 2, 4, 8):
+        monkeypatch.setenv("SEQALIB_PLAN", f"{r},0")
+        for args in SCORINGS[algo]:
+            compare_with_oracle(engine, algo, args, pairs)
+            assert engine.last_plan()[1:] == (r, 0), (r, args)
+    monkeypatch.setenv("SEQALIB_PLAN", "2,0")
+    compare_with_oracle(engine, algo, SCORINGS[algo][0], pairs, "purine")
+    monkeypatch.delenv("SEQALIB_PLAN")
+    monkeypatch.delenv("SEQALIB_TB")
+    a = sa.synth_dna(42_000 + algo, 3000)
+    long_pairs = [(a, sa.synth_mutate(a, 99)), (sa.synth_dna(42_100, 2900), sa.synth_dna(42_101, 3100))]
+    for args in SCORINGS[algo][:2]:
+        compare_with_oracle(engine, algo, args, long_pairs)
