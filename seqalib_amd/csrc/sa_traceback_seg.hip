@@ -49,6 +49,7 @@ struct SegBand {
     const uint8_t* s2;
     uint64_t stage_base;     // slot offset of the first staged record byte
     uint32_t stage_bytes;
+    uint32_t pk_lo;          // first staged packet group of the band
     int s1_lo, s1_cnt;       // staged Seq1 [s1_lo, s1_lo + s1_cnt)
     int s2_lo, s2_cnt;       // staged Seq2 [s2_lo, s2_lo + s2_cnt)
     int m, n;
@@ -76,6 +77,7 @@ __device__ SegBand seg_stage(const TbParams& P, const Geom& g, const uint8_t* di
     S.m = m; S.n = n;
     S.cap = 0;
     S.stage_base = (uint64_t)b * g.band_stride + (uint64_t)pk_lo * pk_bytes;
+    S.pk_lo = pk_lo;
     S.stage_bytes = (pk_hi - pk_lo) * pk_bytes;
     const int BR = kWave * R;
     S.s1_lo = b * BR;
@@ -107,12 +109,12 @@ __device__ SegBand seg_stage(const TbParams& P, const Geom& g, const uint8_t* di
 // One segment of the walk: from (i, j) in state st with score V, until the walk stops or reaches
 // row itop (> 0: the last row of band b - 1).  EMIT writes the op bytes at ops[k...].
 // Returns true if the walk stopped (fin) inside the band.
-template <int ALG, int R, bool LUT, bool EMIT>
+template <int ALG, int R, bool LUT, bool TAG, bool EMIT>
 __device__ bool seg_walk(const TbParams& P, const Geom& g, const SegBand& S, int itop, int& i, int& j, int& st,
                          int& V, uint32_t& k, uint32_t& fl, uint8_t* ops) {
     constexpr int BPC = bits_per_cell(ALG);
     constexpr uint32_t FMASK = (1u << BPC) - 1u;
-    const bool tagged = P.tagged != 0, vrec = P.vrec != 0, allow = P.allow != 0;
+    const bool vrec = P.vrec != 0, allow = P.allow != 0;
     const int G = P.gap, MA = P.match, MI = P.mismatch, GE = P.gap_extend;
     const int GOE = P.gap_open + P.gap_extend;
     const uint32_t obase = allow ? 'S' : 'X';
@@ -123,21 +125,40 @@ __device__ bool seg_walk(const TbParams& P, const Geom& g, const SegBand& S, int
         }
         ++k;
     };
-    // flags of cell (i, j) in the int32 layout (fD/fU, or fD/fX/fXe/fYe) and its match bit
+    // flags of cell (i, j) in the int32 layout (fD/fU, or fD/fX/fXe/fYe) and its match bit.  The
+    // record geometry is compile-time (R, TAG), so the staged offset is a few 32-bit shifts and
+    // adds (sa_layout.h cell_byte restated); cells outside the staged window read HBM.
+    constexpr int RBPC = record_bpc(ALG, R, TAG);
+    constexpr int BPS = R * RBPC / 8, SPP = 16 / BPS;
+    static_assert(BPS >= 1 && BPS <= 16 && 16 % BPS == 0, "SPLIT records: one packet per step group");
+    constexpr int RPW = (R * RBPC < 32 ? R * RBPC : 32) / RBPC;   // rows per record word
+    const uint32_t ib0 = (uint32_t)(itop);   // first row of the band, 0-based = b * BR
     auto cell = [&](int ci, int cj, uint32_t& mt) -> uint32_t {
-        int sh;
-        const uint64_t off = cell_byte(g, (uint32_t)ci, (uint32_t)cj, &sh);
-        const uint64_t rel = off - S.stage_base;
-        const uint32_t raw = (uint32_t)(rel < S.stage_bytes ? S.l_rec[rel] : S.dir[off]) >> sh;
+        const uint32_t ii = (uint32_t)ci - 1u - ib0;
+        const uint32_t t = ii / R, r = ii % R;
+        const uint32_t sst = (uint32_t)cj - 1u + t;
+        const uint32_t word = r / RPW, rr = r % RPW;
+        const uint32_t lowbit = TAG ? RBPC * rr : (uint32_t)((R * RBPC < 32 ? R * RBPC : 32) - RBPC * (rr + 1));
+        const uint32_t bir = word * 4 + lowbit / 8;
+        const uint32_t rel = (sst / SPP - S.pk_lo) * 1024u + t * 16u + (sst % SPP) * BPS + bir;
+        // the LDS reads are issued unconditionally (clamped index), HBM only off the window (rare)
+        uint32_t raw = S.l_rec[min(rel, S.stage_bytes - 1u)];
+        if (rel >= S.stage_bytes) {
+            int sh;
+            raw = S.dir[cell_byte(g, (uint32_t)ci, (uint32_t)cj, &sh)];
+        }
+        raw >>= (lowbit % 8);
         uint32_t f = raw & FMASK;
-        if (BPC == 2 && tagged) f = (f == 3u) ? 2u : (uint32_t)(f == 2u);
-        if (BPC == 4 && tagged) f = t16a_flags(raw & 0xffu);
+        if (BPC == 2 && TAG) f = (f == 3u) ? 2u : (uint32_t)(f == 2u);
+        if (BPC == 4 && TAG) f = t16a_flags(raw & 0xffu);
         if (vrec) {
             mt = BPC == 2 ? ((f >> 1) & f & 1u) : ((f >> 3) & (f >> 2) & 1u);
         } else {
-            const int x1 = ci - 1 - S.s1_lo, x2 = cj - 1 - S.s2_lo;
-            const uint32_t a = (unsigned)x1 < (unsigned)S.s1_cnt ? S.l_s1[x1] : S.s1[ci - 1];
-            const uint32_t bb = (unsigned)x2 < (unsigned)S.s2_cnt ? S.l_s2[x2] : S.s2[cj - 1];
+            // Seq1: the band's rows are all staged; Seq2: a window, HBM beyond it
+            const uint32_t x2 = (uint32_t)(cj - 1 - S.s2_lo);
+            const uint32_t a = S.l_s1[ii];
+            uint32_t bb = S.l_s2[min(x2, (uint32_t)S.s2_cnt - 1u)];
+            if (x2 >= (uint32_t)S.s2_cnt) bb = S.s2[cj - 1];
             if constexpr (LUT) mt = (S.l_lut[(a << 3) | (bb >> 5)] >> (bb & 31)) & 1u;
             else mt = (uint32_t)(a == bb);
         }
@@ -148,7 +169,7 @@ __device__ bool seg_walk(const TbParams& P, const Geom& g, const SegBand& S, int
     bool stop = false;
     for (;;) {
         if (i == itop && itop > 0) break;   // entered band b - 1
-        if (i < 0 || j < 0 || i > S.m || j > S.n) { fl |= kSegErr; stop = true; break; }
+        if ((uint32_t)i > (uint32_t)S.m || (uint32_t)j > (uint32_t)S.n) { fl |= kSegErr; stop = true; break; }
         const bool inner = i > 0 && j > 0;
         uint32_t op = 0, f = 0, v = 0;
         int di = 0, dj = 0, dv = 0, nst = st;
@@ -226,7 +247,7 @@ __device__ __forceinline__ int seg_hand(const TbParams& P, uint32_t slot, int b,
     return P.hand_shift ? ((int)(int16_t)(v & 0xffff) >> P.hand_shift) : v;
 }
 
-template <int ALG, int R, bool LUT>
+template <int ALG, int R, bool LUT, bool TAG>
 __global__ __launch_bounds__(512) void seg_exit_kernel(TbParams P) {
     constexpr int NST = is_affine(ALG) ? 2 : 1;
     __shared__ __attribute__((aligned(16))) uint8_t s_lds[kSegStageBytes + kWave * 8 + kSegS2 + (LUT ? 8192 : 0)];
@@ -246,7 +267,7 @@ __global__ __launch_bounds__(512) void seg_exit_kernel(TbParams P) {
     const bool endw = (tile == ntile);   // the end cell's own segment
     if (endw != (b == b_e)) return;
     if (tile > ntile) return;
-    const Geom g = make_geom(ALG, R, P.max_m, P.max_n, P.tagged);
+    const Geom g = make_geom(ALG, R, P.max_m, P.max_n, TAG ? 1 : 0);
     const int BR = kWave * R;
     const uint8_t* dir = P.dirs + (uint64_t)slot * P.dir_slot;
     const uint8_t* s1 = P.seq1 + o1;
@@ -282,14 +303,14 @@ __global__ __launch_bounds__(512) void seg_exit_kernel(TbParams P) {
     __syncthreads();
     if (out == nullptr) return;
     uint32_t k = 0, fl = 0;
-    const bool stop = seg_walk<ALG, R, LUT, false>(P, g, S, b * BR, i, j, st, V, k, fl, nullptr);
+    const bool stop = seg_walk<ALG, R, LUT, TAG, false>(P, g, S, b * BR, i, j, st, V, k, fl, nullptr);
     int4 r;
     r.x = i; r.y = j; r.z = (int)k;
     r.w = (int)((stop ? kSegStop : 0u) | fl | ((uint32_t)st << 2));
     *out = r;
 }
 
-template <int ALG, int R, bool LUT>
+template <int ALG, int R, bool LUT, bool TAG>
 __global__ __launch_bounds__(256) void seg_emit_kernel(TbParams P) {
     constexpr int NST = is_affine(ALG) ? 2 : 1;
     __shared__ __attribute__((aligned(16))) uint8_t s_lds[kSegStageBytes + kWave * 8 + kSegS2 + (LUT ? 8192 : 0)];
@@ -329,7 +350,7 @@ __global__ __launch_bounds__(256) void seg_emit_kernel(TbParams P) {
     }
     __syncthreads();
     if (!s_entry[3]) return;
-    const Geom g = make_geom(ALG, R, P.max_m, P.max_n, P.tagged);
+    const Geom g = make_geom(ALG, R, P.max_m, P.max_n, TAG ? 1 : 0);
     const int BR = kWave * R;
     const uint8_t* dir = P.dirs + (uint64_t)slot * P.dir_slot;
     const uint8_t* s1 = P.seq1 + o1;
@@ -352,7 +373,7 @@ __global__ __launch_bounds__(256) void seg_emit_kernel(TbParams P) {
     uint32_t k = 0, fl = 0;
     SegBand Sc = S;
     Sc.cap = (uint32_t)(m + n + 1) - min(off, (uint32_t)(m + n + 1));
-    const bool stop = seg_walk<ALG, R, LUT, true>(P, g, Sc, b * BR, i, j, st, V, k, fl, ops);
+    const bool stop = seg_walk<ALG, R, LUT, TAG, true>(P, g, Sc, b * BR, i, j, st, V, k, fl, ops);
     if (stop) {
         // the walk ends in this band: the pair's traceback result (applied by the wave kernel)
         int4 f;
@@ -366,21 +387,24 @@ hipError_t launch_traceback_seg(int algo, int R, bool lut, const TbParams& p, hi
     const uint32_t ntile = (p.max_n + 1 + kSegTW - 1) / kSegTW;
     const dim3 gx(ntile + 1, p.split_bands, p.count), bx(kSegTW * nst);
     const dim3 ge(1, p.split_bands, p.count), be(256);
-#define SA_SEG(AA, RR, LL)                                                                  \
-    if (algo == AA && R == RR && lut == LL) {                                               \
-        hipLaunchKernelGGL((seg_exit_kernel<AA, RR, LL>), gx, bx, 0, stream, p);            \
+    const bool tag = p.tagged != 0;
+    if (p.tagged > 1) return hipErrorInvalidValue;   // two-pair records never come from SPLIT fills
+#define SA_SEG(AA, RR, LL, TT)                                                              \
+    if (algo == AA && R == RR && lut == LL && tag == TT) {                                  \
+        hipLaunchKernelGGL((seg_exit_kernel<AA, RR, LL, TT>), gx, bx, 0, stream, p);        \
         hipError_t e = hipGetLastError();                                                   \
         if (e != hipSuccess) return e;                                                      \
-        hipLaunchKernelGGL((seg_emit_kernel<AA, RR, LL>), ge, be, 0, stream, p);            \
+        hipLaunchKernelGGL((seg_emit_kernel<AA, RR, LL, TT>), ge, be, 0, stream, p);        \
         return hipGetLastError();                                                           \
     }
-#define SA_SEG_A(AA) SA_SEG(AA, 1, false) SA_SEG(AA, 2, false) SA_SEG(AA, 4, false) SA_SEG(AA, 8, false) \
-                     SA_SEG(AA, 1, true) SA_SEG(AA, 2, true) SA_SEG(AA, 4, true) SA_SEG(AA, 8, true)
+#define SA_SEG_R(AA, LL, TT) SA_SEG(AA, 1, LL, TT) SA_SEG(AA, 2, LL, TT) SA_SEG(AA, 4, LL, TT) SA_SEG(AA, 8, LL, TT)
+#define SA_SEG_A(AA) SA_SEG_R(AA, false, false) SA_SEG_R(AA, true, false) SA_SEG_R(AA, false, true) SA_SEG_R(AA, true, true)
     SA_SEG_A(SA_SW)
     SA_SEG_A(SA_NW)
     SA_SEG_A(SA_LOCAL_GOTOH)
     SA_SEG_A(SA_GLOBAL_GOTOH)
 #undef SA_SEG_A
+#undef SA_SEG_R
 #undef SA_SEG
     return hipErrorInvalidValue;
 }

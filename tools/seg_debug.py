@@ -42,6 +42,13 @@ def main():
     rec = rec[:cnt * bands * rs].reshape(cnt, bands, rs, 4)
     print("dump: cnt", cnt, "bands", bands, "rs", rs, "R", RR, "fin", fin[0])
     BR = 64 * R
+    nst0 = 2 if algo >= 2 else 1
+    W0 = int(rs - 1) // nst0
+    body = rec[0, :-1, :W0 * nst0].reshape(int(bands) - 1, nst0, W0, 4)[:, :, :n + 1]
+    nops = body[..., 2].astype(np.int64)
+    waves = nops[..., : (n + 1) // 64 * 64].reshape(nops.shape[0], nst0, -1, 64)
+    print(f"walk lengths: mean {nops.mean():.1f}, p99 {np.percentile(nops, 99):.0f}, max {nops.max()}; "
+          f"per-wave max: mean {waves.max(axis=-1).mean():.1f}, max {waves.max()}")
     nst = 2 if algo >= 2 else 1
     W = int(rs - 1) // nst
     for bb in range(min(3, int(bands))):
