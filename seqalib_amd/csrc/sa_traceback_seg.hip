@@ -106,6 +106,13 @@ __device__ SegBand seg_stage(const TbParams& P, const Geom& g, const uint8_t* di
     return S;
 }
 
+// Off-window reads, out of line so that the walk loop keeps its few registers and branches.
+__device__ __attribute__((noinline)) uint32_t seg_slow_rec(const Geom& g, const uint8_t* dir, int ci, int cj) {
+    int sh;
+    return dir[cell_byte(g, (uint32_t)ci, (uint32_t)cj, &sh)];
+}
+__device__ __attribute__((noinline)) uint32_t seg_slow_byte(const uint8_t* p) { return *p; }
+
 // One segment of the walk: from (i, j) in state st with score V, until the walk stops or reaches
 // row itop (> 0: the last row of band b - 1).  EMIT writes the op bytes at ops[k...].
 // Returns true if the walk stopped (fin) inside the band.
@@ -141,27 +148,23 @@ __device__ bool seg_walk(const TbParams& P, const Geom& g, const SegBand& S, int
         const uint32_t lowbit = TAG ? RBPC * rr : (uint32_t)((R * RBPC < 32 ? R * RBPC : 32) - RBPC * (rr + 1));
         const uint32_t bir = word * 4 + lowbit / 8;
         const uint32_t rel = (sst / SPP - S.pk_lo) * 1024u + t * 16u + (sst % SPP) * BPS + bir;
-        // the LDS reads are issued unconditionally (clamped index), HBM only off the window (rare)
+        // The three LDS reads (record byte, Seq1 and Seq2 symbols) are issued together and
+        // unconditionally (clamped indices); HBM is read only off the staged window (rare).
+        // Seq1: the band's rows are all staged; Seq2: a window.
+        const uint32_t x2 = (uint32_t)(cj - 1 - S.s2_lo);
+        const uint32_t a = S.l_s1[ii];
+        uint32_t bb = S.l_s2[min(x2, (uint32_t)S.s2_cnt - 1u)];
         uint32_t raw = S.l_rec[min(rel, S.stage_bytes - 1u)];
-        if (rel >= S.stage_bytes) {
-            int sh;
-            raw = S.dir[cell_byte(g, (uint32_t)ci, (uint32_t)cj, &sh)];
-        }
+        if (rel >= S.stage_bytes) raw = seg_slow_rec(g, S.dir, ci, cj);
+        if (!vrec && x2 >= (uint32_t)S.s2_cnt) bb = seg_slow_byte(S.s2 + (cj - 1));
         raw >>= (lowbit % 8);
         uint32_t f = raw & FMASK;
         if (BPC == 2 && TAG) f = (f == 3u) ? 2u : (uint32_t)(f == 2u);
         if (BPC == 4 && TAG) f = t16a_flags(raw & 0xffu);
-        if (vrec) {
-            mt = BPC == 2 ? ((f >> 1) & f & 1u) : ((f >> 3) & (f >> 2) & 1u);
-        } else {
-            // Seq1: the band's rows are all staged; Seq2: a window, HBM beyond it
-            const uint32_t x2 = (uint32_t)(cj - 1 - S.s2_lo);
-            const uint32_t a = S.l_s1[ii];
-            uint32_t bb = S.l_s2[min(x2, (uint32_t)S.s2_cnt - 1u)];
-            if (x2 >= (uint32_t)S.s2_cnt) bb = S.s2[cj - 1];
-            if constexpr (LUT) mt = (S.l_lut[(a << 3) | (bb >> 5)] >> (bb & 31)) & 1u;
-            else mt = (uint32_t)(a == bb);
-        }
+        uint32_t me;
+        if constexpr (LUT) me = (S.l_lut[(a << 3) | (bb >> 5)] >> (bb & 31)) & 1u;
+        else me = (uint32_t)(a == bb);
+        mt = vrec ? (BPC == 2 ? ((f >> 1) & f & 1u) : ((f >> 3) & (f >> 2) & 1u)) : me;
         return f;
     };
     // Branch-light move selection: every iteration computes (op, di, dj, dv, next state) and
