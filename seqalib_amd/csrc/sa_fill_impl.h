@@ -522,12 +522,28 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
         }
     };
 
+    // SPLIT: granules of the producer band for the chunk at column c0 (lane q: column c0 + q,
+    // clamped to the row, so every lane loads and no value is conditionally defined -- that keeps
+    // the prefetched registers in place instead of a copy that would wait for the load).
+    unsigned long long pre_h = 0, pre_x = 0;
+    auto split_load = [&](int band, int c0, unsigned long long& x, unsigned long long& y) {
+        if constexpr (SPLIT) {
+            const int cl = min(c0 + lane, n - 1);
+            gu64* const gh = hand_pair + (uint64_t)(band > 0 ? band - 1 : 0) * P.max_n + cl;
+            x = __hip_atomic_load(gh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if constexpr (AFF) y = __hip_atomic_load(gh + P.hand_x_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
     // One chunk of kChunk steps of one band.
     auto run_chunk = [&](auto steady, int band, int kC, int bch, int bcx, int symc, int& acc_h,
                          int& acc_x) {
         uint8_t* const dband = dslot + (uint64_t)band * P.band_stride;
 #pragma unroll 1
         for (int q0 = 0; q0 < kChunk; q0 += SPP) {
+            // SPLIT: the next chunk's hand-off granules are fetched mid-chunk rather than at the
+            // chunk start: the producer is then 16 steps further along, so the load finds them
+            // ready at a smaller band lag (each failed poll costs a memory round trip)
+            if (SPLIT && q0 == kChunk / 2 && band > 0) split_load(band, kC + kChunk, pre_h, pre_x);
             uint32_t pk[4 * PPS];
 #pragma unroll
             for (int e = 0; e < 4 * PPS; ++e) pk[e] = 0;
@@ -568,18 +584,6 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     // flag stores (no s_waitcnt vmcnt behind them).
     auto ring = [&](int wave, int comp) -> int32_t* {
         return s_ring + (wave * (AFF ? 2 : 1) + comp) * kRing;
-    };
-    // SPLIT: granules of the producer band for the chunk at column c0 (lane q: column c0 + q,
-    // clamped to the row, so every lane loads and no value is conditionally defined -- that keeps
-    // the prefetched registers in place instead of a copy that would wait for the load).
-    unsigned long long pre_h = 0, pre_x = 0;
-    auto split_load = [&](int band, int c0, unsigned long long& x, unsigned long long& y) {
-        if constexpr (SPLIT) {
-            const int cl = min(c0 + lane, n - 1);
-            gu64* const gh = hand_pair + (uint64_t)(band > 0 ? band - 1 : 0) * P.max_n + cl;
-            x = __hip_atomic_load(gh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if constexpr (AFF) y = __hip_atomic_load(gh + P.hand_x_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     };
     // Lane q < kChunk of the returned registers holds column c0 + q: the row-above value for
     // lane 0 (top border, or the previous band's last row) and Seq2[c].
@@ -627,7 +631,6 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     vh = (int)(uint32_t)pre_h;
                     if constexpr (AFF) vx = (int)(uint32_t)pre_x;
                 }
-                split_load(band, c0 + kChunk, pre_h, pre_x);   // next chunk's, in flight meanwhile
             }
         }
     };
