@@ -772,16 +772,14 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         SA_HIP(c, hipGetLastError());
     }
     if (npairs && dc) {
-        std::vector<sa_result> hres;
-        const uint8_t* hops = nullptr;
-        uint64_t hops_bytes = 0;
         std::string e;
         c->launches = 0;
         const auto run = algo == SA_HIRSCHBERG ? hirschberg_run : myersmiller_run;
-        if (run(sc, d1, do1, d2, do2, npairs, use_lut ? dbits : nullptr, st, hres, &hops, &hops_bytes, &e))
+        if (run(sc, d1, do1, d2, do2, npairs, use_lut ? dbits : nullptr, st, dres, dops, &e))
             return fail(c, SA_ERR_HIP, (algo == SA_HIRSCHBERG ? "hirschberg: " : "myers-miller: ") + e);
-        memcpy(results, hres.data(), sizeof(sa_result) * npairs);
-        memcpy(ops, hops, std::min<uint64_t>(ops_total, ops_cap));
+        SA_HIP(c, hipMemcpyAsync(results, dres, sizeof(sa_result) * npairs, hipMemcpyDeviceToHost, st));
+        SA_HIP(c, hipMemcpyAsync(ops, dops, ops_total, hipMemcpyDeviceToHost, st));
+        SA_HIP(c, hipStreamSynchronize(st));
         return SA_OK;
     }
     if (npairs) {
@@ -1037,25 +1035,11 @@ int sa_align_batch_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8
         SA_HIP(c, hipGetLastError());
     }
     if (algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER) {
-        std::vector<sa_result> hres;
-        const uint8_t* hops = nullptr;
-        uint64_t hops_bytes = 0;
         std::string e;
         c->launches = 0;
         const auto run = algo == SA_HIRSCHBERG ? hirschberg_run : myersmiller_run;
-        const auto t_run = std::chrono::steady_clock::now();
-        if (run(sc, d1, o1, d2, o2, npairs, bits, st, hres, &hops, &hops_bytes, &e))
+        if (run(sc, d1, o1, d2, o2, npairs, bits, st, d_res, d_ops, &e))
             return fail(c, SA_ERR_HIP, (algo == SA_HIRSCHBERG ? "hirschberg: " : "myers-miller: ") + e);
-        // results go back through pinned staging, and the wait polls (see dc_sync)
-        static thread_local HostBuf<sa_result> pres;
-        SA_HIP(c, pres.alloc(npairs));
-        memcpy(pres.data(), hres.data(), sizeof(sa_result) * npairs);
-        SA_HIP(c, hipMemcpyAsync(d_res, pres.data(), sizeof(sa_result) * npairs, hipMemcpyHostToDevice, st));
-        if (hops_bytes) SA_HIP(c, hipMemcpyAsync(d_ops, hops, hops_bytes, hipMemcpyHostToDevice, st));
-        SA_HIP(c, dc_sync(st));
-        if (getenv("SEQALIB_MM_TIMING"))
-            fprintf(stderr, "[api] after runner: %8.2f ms\n",
-                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_run).count());
         return SA_OK;
     }
     return run_device(c, algo, sc, d1, o1, d2, o2, npairs, max_m, max_n, bits, d_res, d_ops, st, c->pipeline != 0);

@@ -1,12 +1,11 @@
 // sa_dc.h — host and device pieces shared by the linear-space divide-and-conquer aligners
 // (sa_hirschberg.hip: HirschbergSA, sa_myersmiller.hip: MyersMillerSA).
 //
-// Both run their recursion breadth-first over all pairs: device levels split subproblems with
-// batched last-row sweeps, and what is left ("leaves") is finished one GPU thread per leaf,
-// each writing its forward-order op list.  A pair's leaves tile its alignment path: leaf k
-// starts at (a0, b0) where leaf k-1 ended, so sorting the leaves of a pair by (a0, b0) puts
-// them in path order (a leaf that is empty in both sequences emits nothing and may land
-// anywhere).  dc_assemble concatenates them and reverses the result into the engine's
+// Both run their recursion breadth-first over all pairs, entirely on the device (sa_dc.hip):
+// device levels split subproblems with batched last-row sweeps, and what is left ("leaves") is
+// finished one GPU thread per leaf, each writing its forward-order op list at its key
+// a0 + b0.  A pair's leaves tile its alignment path in Seq1 order, so dc_assemble_kernel walks
+// the pair's key range, concatenates them and reverses the result into the engine's
 // traceback-order op stream (include/seqalib_hip.h: pair p's ops at off1[p] + off2[p] + p).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -29,6 +28,10 @@ template <typename T>
 struct DevBuf {
     T* p = nullptr;
     size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;              // owning: a copy's destructor would free p
+    DevBuf& operator=(const DevBuf&) = delete;
+    void swap(DevBuf& o) { std::swap(p, o.p); std::swap(n, o.n); }
     hipError_t alloc(size_t count) {
         if (count <= n && p) return hipSuccess;
         if (p) (void)hipFree(p);
@@ -47,6 +50,9 @@ template <typename T>
 struct HostBuf {
     T* p = nullptr;
     size_t n = 0;
+    HostBuf() = default;
+    HostBuf(const HostBuf&) = delete;
+    HostBuf& operator=(const HostBuf&) = delete;
     hipError_t alloc(size_t count) {
         if (count <= n && p) return hipSuccess;
         if (p) (void)hipHostFree(p);
@@ -99,74 +105,90 @@ inline hipError_t dc_sync(hipStream_t st) {
     return e;
 }
 
-// Host vector -> device through a pinned staging buffer, so the copy is a plain async DMA.
-// The stage may be reused once the stream has passed the copy (the drivers wait every level).
-template <typename T>
-hipError_t dc_put(T* dst, const std::vector<T>& v, HostBuf<T>& stage, hipStream_t st) {
-    if (v.empty()) return hipSuccess;
-    if (hipError_t e = stage.alloc(v.size())) return e;
-    memcpy(stage.data(), v.data(), v.size() * sizeof(T));
-    return hipMemcpyAsync(dst, stage.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st);
-}
-
 #define SA_DC_HIP(call)                                                                              \
     do {                                                                                             \
         hipError_t e_ = (call);                                                                      \
         if (e_ != hipSuccess) { *err = std::string(#call) + ": " + hipGetErrorString(e_); return -1; } \
     } while (0)
 
-struct DcLeafRef {
+// One subproblem of a level (or a leaf).  m < 0 marks an empty slot.  tb / te: Myers–Miller's
+// boundary gap opens (unused by Hirschberg).
+struct DcSub {
+    uint64_t a0, b0;   // absolute start in seq1 / seq2; key = a0 + b0
+    int32_t m, n;
+    int32_t tb, te;
     uint32_t pair;
-    uint64_t a0, b0;   // absolute start in seq1 / seq2
-    uint64_t out;      // byte offset of the leaf's forward ops in the leaf op buffer
-    bool top;          // the leaf is the pair's whole problem: its score is the pair's
+    int32_t top;       // the pair's whole problem: its score is the pair's
 };
 
-// Fill res[p] (end cell (m, n), nops, score of a top leaf) and ops for every pair.
-inline hipError_t dc_assemble(uint32_t npairs, const uint64_t* o1, const uint64_t* o2, const std::vector<DcLeafRef>& leaves,
-                        const int32_t* nout, const int32_t* lscore, const uint8_t* lops, std::vector<sa_result>& res,
-                        HostBuf<uint8_t>& ops) {
-    if (hipError_t e = ops.alloc(o1[npairs] + o2[npairs] + npairs)) return e;
-    memset(ops.data(), 0, o1[npairs] + o2[npairs] + npairs);
-    // bucket leaves by pair (counting sort), then assemble pairs independently on host threads
-    std::vector<uint32_t> start(npairs + 1, 0), order(leaves.size());
-    for (const DcLeafRef& s : leaves) ++start[s.pair + 1];
-    for (uint32_t p = 0; p < npairs; ++p) start[p + 1] += start[p];
-    {
-        std::vector<uint32_t> pos(start.begin(), start.end() - 1);
-        for (uint32_t k = 0; k < leaves.size(); ++k) order[pos[leaves[k].pair]++] = k;
-    }
-    auto assemble = [&](uint32_t p0, uint32_t p1) {
-        for (uint32_t p = p0; p < p1; ++p) {
-            uint32_t* b0 = order.data() + start[p];
-            uint32_t* b1 = order.data() + start[p + 1];
-            std::sort(b0, b1, [&](uint32_t x, uint32_t y) {
-                return leaves[x].a0 != leaves[y].a0 ? leaves[x].a0 < leaves[y].a0 : leaves[x].b0 < leaves[y].b0;
-            });
-            uint32_t total = 0;
-            for (uint32_t* q = b0; q < b1; ++q) total += (uint32_t)nout[*q];
-            sa_result& r = res[p];
-            r.end_i = (int32_t)(o1[p + 1] - o1[p]);
-            r.end_j = (int32_t)(o2[p + 1] - o2[p]);
-            r.nops = total;
-            // forward op f lands at traceback index total - 1 - f
-            uint8_t* dst = ops.data() + o1[p] + o2[p] + p + total;
-            for (uint32_t* q = b0; q < b1; ++q) {
-                const uint32_t k = *q;
-                if (leaves[k].top) r.score = lscore[k];
-                const uint8_t* src = lops + leaves[k].out;
-                for (int32_t c = 0; c < nout[k]; ++c) *--dst = src[c];
-            }
-        }
-    };
-    uint32_t cap = 16;   // host threads for assembly: SEQALIB_DC_THREADS overrides
-    if (const char* t = getenv("SEQALIB_DC_THREADS")) cap = std::max(1, atoi(t));
-    const uint32_t nth = std::max<uint32_t>(1, std::min<uint32_t>(cap, npairs / 64));
-    std::vector<std::thread> pool;
-    for (uint32_t t = 0; t < nth; ++t)
-        pool.emplace_back(assemble, (uint32_t)((uint64_t)npairs * t / nth), (uint32_t)((uint64_t)npairs * (t + 1) / nth));
-    for (auto& th : pool) th.join();
+struct DcLevel {
+    uint32_t nsplit;   // subproblems split at this level (the next level has mult * nsplit slots)
+    uint32_t pad;
+};
+
+// sa_dc.hip
+hipError_t dc_launch_init(const uint64_t* o1, const uint64_t* o2, uint32_t npairs, int32_t t0, DcSub* subs,
+                          hipStream_t st);
+hipError_t dc_launch_classify(const DcSub* cur, uint32_t cap, uint32_t fixed, const DcLevel* prev, uint32_t mult,
+                              int leaf_rows, int min_n, DcLevel* lvl, DcSub* split, DcSub* leaves, uint32_t* nleaf,
+                              hipStream_t st);
+hipError_t dc_launch_assemble(const uint64_t* o1, const uint64_t* o2, uint32_t npairs, const int32_t* mark,
+                              const uint8_t* stage, sa_result* res, uint8_t* ops, hipStream_t st);
+
+// Host-side sizes of a batch (one read of the device offsets): grid bounds of the level loop.
+struct DcBounds {
+    uint64_t t1 = 0, t2 = 0;   // total Seq1 / Seq2 symbols
+    int max_m = 0;             // longest Seq1
+};
+
+inline hipError_t dc_bounds(const uint64_t* d_o1, const uint64_t* d_o2, uint32_t npairs, hipStream_t st, DcBounds* b) {
+    static thread_local HostBuf<uint64_t> o1, o2;
+    if (hipError_t e = o1.alloc(npairs + 1)) return e;
+    if (hipError_t e = o2.alloc(npairs + 1)) return e;
+    if (hipError_t e = hipMemcpyAsync(o1.data(), d_o1, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st)) return e;
+    if (hipError_t e = hipMemcpyAsync(o2.data(), d_o2, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st)) return e;
+    if (hipError_t e = dc_sync(st)) return e;
+    b->max_m = 0;
+    for (uint32_t p = 0; p < npairs; ++p) b->max_m = std::max<int>(b->max_m, (int)(o1[p + 1] - o1[p]));
+    // key-addressed buffers are indexed by absolute a0 + b0
+    b->t1 = o1[npairs];
+    b->t2 = o2[npairs];
     return hipSuccess;
 }
+
+// Device work buffers of one level loop (grow-only, per host thread).  Bounds: a split
+// subproblem has > leaf_rows rows and the subproblems of a level have disjoint Seq1 ranges, so
+// a level splits at most t1 / (leaf_rows + 1) + 1 of them; leaves have >= 1 row (or are a whole
+// empty pair), so there are at most t1 + npairs of them.
+struct DcWork {
+    DevBuf<DcSub> cur, next, split, leaves;
+    DevBuf<DcLevel> lvl;
+    DevBuf<int32_t> rows, scratch, mark;
+    DevBuf<uint8_t> stage;
+    uint64_t max_splits = 0, leaf_cap = 0;
+    int levels = 0;
+    uint32_t* nleaf() { return &lvl.p[levels + 1].nsplit; }   // lvl[0..levels]: the levels
+    hipError_t prepare(const DcBounds& b, uint32_t npairs, int leaf_rows, uint32_t mult, uint32_t rows_per_key,
+                       uint32_t scratch_per_key, hipStream_t st) {
+        max_splits = b.t1 / (uint64_t)(leaf_rows + 1) + 1;
+        uint64_t cap = npairs, total = npairs;
+        levels = 0;
+        for (int m = b.max_m; m > leaf_rows; m = (m + 1) / 2) {
+            cap = mult * std::min<uint64_t>(cap, max_splits);
+            total += cap;
+            ++levels;
+        }
+        leaf_cap = std::min<uint64_t>(total, b.t1 + npairs);
+        const uint64_t sub_cap = std::max<uint64_t>(npairs, mult * max_splits);
+        const uint64_t keys = b.t1 + b.t2 + 1;
+        hipError_t e;
+        if ((e = cur.alloc(sub_cap)) || (e = next.alloc(sub_cap)) || (e = split.alloc(std::min(sub_cap, max_splits))) ||
+            (e = leaves.alloc(leaf_cap)) || (e = lvl.alloc(levels + 2)) || (e = rows.alloc(rows_per_key * keys)) ||
+            (e = scratch.alloc(scratch_per_key * keys)) || (e = mark.alloc(keys)) || (e = stage.alloc(keys)))
+            return e;
+        if ((e = hipMemsetAsync(lvl.p, 0, sizeof(DcLevel) * (levels + 2), st))) return e;
+        return hipMemsetAsync(mark.p, 0, sizeof(int32_t) * keys, st);
+    }
+};
 
 }  // namespace sa

@@ -1,0 +1,125 @@
+// sa_dc.hip — the device-resident level loop shared by HirschbergSA (sa_hirschberg.hip) and
+// MyersMillerSA (sa_myersmiller.hip).
+//
+// Both recursions run breadth-first over all pairs of a batch.  Every buffer they touch is
+// addressed by a subproblem's KEY = a0 + b0 (its first Seq1 index plus its first Seq2 index,
+// both absolute in the concatenated inputs): the subproblems of one pair at one level, and the
+// leaves of one pair, cover disjoint increasing ranges of Seq1 and of Seq2, so the key spans
+// [a0 + b0, a0 + b0 + m + n) are disjoint across the whole batch.  A subproblem's sweep rows,
+// a leaf's scratch and a leaf's forward op list therefore live at fixed multiples of its key,
+// and no prefix sum or host round trip is needed between levels:
+//   dc_init_kernel      pairs -> level-0 subproblems
+//   dc_classify_kernel  per level: split / leaf, appended with one atomic per wave
+//   (per algorithm)     sweeps + split write the next level's subproblems; leaves write their
+//                       forward ops at stage[key] and their op count at mark[key]
+//   dc_assemble_kernel  one wave per pair: walks its key range in order (= Seq1 order of the
+//                       leaves), prefix-sums the counts and writes the traceback-order stream.
+#include <hip/hip_runtime.h>
+
+#include "sa_dc.h"
+
+namespace sa {
+
+__global__ __launch_bounds__(64) void dc_init_kernel(const uint64_t* o1, const uint64_t* o2, uint32_t npairs,
+                                                     int32_t t0, DcSub* subs) {
+    const uint32_t p = blockIdx.x * 64 + threadIdx.x;
+    if (p >= npairs) return;
+    DcSub s;
+    s.a0 = o1[p];
+    s.b0 = o2[p];
+    s.m = (int32_t)(o1[p + 1] - o1[p]);
+    s.n = (int32_t)(o2[p + 1] - o2[p]);
+    s.tb = t0;
+    s.te = t0;
+    s.pair = p;
+    s.top = 1;
+    subs[p] = s;
+}
+
+// count = fixed (level 0) or mult * prev->nsplit; slots with m < 0 are empty (Myers–Miller's
+// type-1 midpoints leave their third child slot empty).
+__global__ __launch_bounds__(64) void dc_classify_kernel(const DcSub* cur, uint32_t fixed, const DcLevel* prev,
+                                                         uint32_t mult, int leaf_rows, int min_n, DcLevel* lvl,
+                                                         DcSub* split, DcSub* leaves, uint32_t* nleaf) {
+    const int lane = threadIdx.x;
+    const uint32_t count = prev ? mult * prev->nsplit : fixed;
+    const uint32_t k = blockIdx.x * 64 + lane;
+    DcSub s{};
+    bool valid = k < count;
+    if (valid) {
+        s = cur[k];
+        valid = s.m >= 0;
+    }
+    const bool is_split = valid && s.m > leaf_rows && s.n >= min_n;
+    const bool is_leaf = valid && !is_split;
+    const uint64_t bs = __ballot(is_split), bl = __ballot(is_leaf);
+    uint32_t base_s = 0, base_l = 0;
+    if (lane == 0) {
+        if (bs) base_s = atomicAdd(&lvl->nsplit, (uint32_t)__popcll(bs));
+        if (bl) base_l = atomicAdd(nleaf, (uint32_t)__popcll(bl));
+    }
+    base_s = __shfl(base_s, 0);
+    base_l = __shfl(base_l, 0);
+    const uint64_t below = (1ull << lane) - 1;
+    if (is_split) split[base_s + __popcll(bs & below)] = s;
+    if (is_leaf) leaves[base_l + __popcll(bl & below)] = s;
+}
+
+__global__ __launch_bounds__(64) void dc_assemble_kernel(const uint64_t* o1, const uint64_t* o2, const int32_t* mark,
+                                                         const uint8_t* stage, sa_result* res, uint8_t* ops) {
+    const int lane = threadIdx.x;
+    const uint32_t p = blockIdx.x;
+    const uint64_t key0 = o1[p] + o2[p];
+    const int32_t m = (int32_t)(o1[p + 1] - o1[p]), n = (int32_t)(o2[p + 1] - o2[p]);
+    const int32_t len = m + n;
+    int32_t total = 0;
+    for (int32_t i = lane; i < len; i += 64) total += mark[key0 + i];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) total += __shfl_xor(total, off);
+    uint8_t* dst = ops + key0 + p;   // this pair's stream (m + n + 1 bytes)
+    int32_t base = 0;
+    for (int32_t c0 = 0; c0 < len; c0 += 64) {
+        const int32_t i = c0 + lane;
+        const int32_t cnt = i < len ? mark[key0 + i] : 0;
+        int32_t incl = cnt;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int32_t v = __shfl_up(incl, off);
+            if (lane >= off) incl += v;
+        }
+        // forward op f of the pair lands at traceback index total - 1 - f
+        const int32_t f0 = base + incl - cnt;
+        const uint8_t* src = stage + key0 + i;
+        for (int32_t q = 0; q < cnt; ++q) dst[total - 1 - (f0 + q)] = src[q];
+        base += __shfl(incl, 63);
+    }
+    for (int32_t i = total + lane; i <= len; i += 64) dst[i] = 0;
+    if (lane == 0) {
+        res[p].end_i = m;
+        res[p].end_j = n;
+        res[p].nops = (uint32_t)total;
+    }
+}
+
+hipError_t dc_launch_init(const uint64_t* o1, const uint64_t* o2, uint32_t npairs, int32_t t0, DcSub* subs,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(dc_init_kernel, dim3((npairs + 63) / 64), dim3(64), 0, st, o1, o2, npairs, t0, subs);
+    return hipGetLastError();
+}
+
+hipError_t dc_launch_classify(const DcSub* cur, uint32_t cap, uint32_t fixed, const DcLevel* prev, uint32_t mult,
+                              int leaf_rows, int min_n, DcLevel* lvl, DcSub* split, DcSub* leaves, uint32_t* nleaf,
+                              hipStream_t st) {
+    if (!cap) return hipSuccess;
+    hipLaunchKernelGGL(dc_classify_kernel, dim3((cap + 63) / 64), dim3(64), 0, st, cur, fixed, prev, mult, leaf_rows,
+                       min_n, lvl, split, leaves, nleaf);
+    return hipGetLastError();
+}
+
+hipError_t dc_launch_assemble(const uint64_t* o1, const uint64_t* o2, uint32_t npairs, const int32_t* mark,
+                              const uint8_t* stage, sa_result* res, uint8_t* ops, hipStream_t st) {
+    hipLaunchKernelGGL(dc_assemble_kernel, dim3(npairs), dim3(64), 0, st, o1, o2, mark, stage, res, ops);
+    return hipGetLastError();
+}
+
+}  // namespace sa

@@ -8,14 +8,17 @@
 //     bottom half and reversed Seq2) become two rows of one batched launch of hb_sweep_kernel
 //     (score-only NW, one wave per sweep, anti-diagonal wavefront as in the fill kernel, the
 //     last DP row written out); hb_split_kernel then takes, per subproblem, the LAST i in
-//     [0, |Seq2|) maximising Fwd[i] + Rev[|Seq2|-i] (:138-149; i never reaches |Seq2|) and the
-//     host forms the two children (:151-161).
+//     [0, |Seq2|) maximising Fwd[i] + Rev[|Seq2|-i] (:138-149; i never reaches |Seq2|) and
+//     writes the two children (:151-161) as the next level's subproblems.
 //   * leaves: everything smaller (and every base case) is finished by hb_leaf_kernel, one
 //     thread per subproblem running the same recursion iteratively (explicit stack, left child
 //     first), including the NW base case of :119-126 with the reference's NW traceback rules.
 //   * assembly: a pair's leaves cover disjoint, increasing ranges of Seq1, so its alignment is
-//     the concatenation of its leaves' forward op lists in Seq1 order; the host reverses it into
-//     the engine's traceback-order op stream (include/seqalib_hip.h).
+//     the concatenation of its leaves' forward op lists in Seq1 order; dc_assemble_kernel
+//     (sa_dc.hip) reverses it into the engine's traceback-order op stream (include/seqalib_hip.h).
+// The level loop never returns to the host: subproblems are classified on the device and every
+// buffer is addressed by the subproblem's key a0 + b0 (sa_dc.hip); the host only launches, with
+// grid sizes from upper bounds (the largest subproblem halves per level).
 // Score reported: NW H[m][n] (the reference exposes none): max over i in [0, n] of the level-0
 // split sums, or the leaf's own full NWScore.
 #include <hip/hip_runtime.h>
@@ -45,18 +48,14 @@ struct HbSweep {       // NWScore over A (alen) x B (blen) -> rows[out .. out+bl
     uint64_t out;      // int32 index into the row buffer
 };
 
-struct HbSplit {
-    uint64_t fwd, rev; // row indices of the forward / reverse last rows (blen + 1 each)
-    int32_t n, top;    // |Seq2| of the subproblem; top: also report the NW score
-};
-
-struct HbLeaf {
-    uint64_t a0, b0;   // Seq1 / Seq2 start (indices into seq1 / seq2)
-    int32_t alen, blen;
-    uint64_t scratch;  // int32 index into the leaf scratch
-    uint64_t out;      // byte index into the leaf op buffer (capacity alen + blen)
-    int32_t top, pad;
-};
+// Sweep rows of a split subproblem live at 2 * key (forward) and 2 * key + n + 1 (reverse):
+// 2 (n + 1) <= 2 (m + n) ints, inside its key span.
+__device__ __forceinline__ HbSweep hb_sweep_of(const DcSub& s, int rev) {
+    const int mid = s.m / 2;
+    const uint64_t key = s.a0 + s.b0;
+    if (!rev) return HbSweep{s.a0, s.b0, mid, s.n, 0, 0, 2 * key};
+    return HbSweep{s.a0 + (uint64_t)s.m - 1, s.b0 + (uint64_t)s.n - 1, s.m - mid, s.n, 1, 0, 2 * key + s.n + 1};
+}
 
 struct HbScore {
     int32_t gap, match, mismatch, allow;
@@ -83,11 +82,13 @@ __device__ __forceinline__ int32_t hb_cell_t(int32_t hd, int32_t hu, int32_t hl,
 
 // ------------------------------------------------------------------ batched NWScore sweeps
 template <int R, bool LUT, bool ALLOW>
-__global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const uint8_t* s2, const HbSweep* sweeps,
-                                                      int32_t* rows, const uint32_t* lutbits, HbScore sc) {
+__global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* split,
+                                                      const DcLevel* lvl, int32_t* rows, const uint32_t* lutbits,
+                                                      HbScore sc) {
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];
     const int lane = threadIdx.x;
-    const HbSweep d = sweeps[blockIdx.x];
+    if (blockIdx.x / 2 >= lvl->nsplit) return;   // grid sized from an upper bound
+    const HbSweep d = hb_sweep_of(split[blockIdx.x / 2], blockIdx.x & 1);
     if constexpr (LUT) {
         for (int k = lane; k < 2048; k += 64) s_lut[k] = lutbits[k];
         __syncthreads();
@@ -163,13 +164,14 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
 }
 
 // ---------------------------------------------------------------------------- split
-__global__ __launch_bounds__(64) void hb_split_kernel(const HbSplit* splits, const int32_t* rows, int32_t* mid2,
-                                                      int32_t* score) {
+__global__ __launch_bounds__(64) void hb_split_kernel(const DcSub* split, const DcLevel* lvl, const int32_t* rows,
+                                                      DcSub* next, sa_result* res) {
     const int lane = threadIdx.x;
-    const HbSplit d = splits[blockIdx.x];
-    const int32_t* F = rows + d.fwd;
-    const int32_t* B = rows + d.rev;
+    if (blockIdx.x >= lvl->nsplit) return;
+    const DcSub d = split[blockIdx.x];
+    const int32_t* F = rows + 2 * (d.a0 + d.b0);
     const int n = d.n;
+    const int32_t* B = F + n + 1;
     int32_t best = INT_MIN;
     int idx = 0;
     for (int i = lane; i < n; i += 64) {
@@ -184,8 +186,10 @@ __global__ __launch_bounds__(64) void hb_split_kernel(const HbSplit* splits, con
         if (ob > best || (ob == best && oi > idx)) { best = ob; idx = oi; }
     }
     if (lane == 0) {
-        mid2[blockIdx.x] = idx;
-        if (d.top) score[blockIdx.x] = max(best, F[n] + B[0]);   // NW H[m][n] over i in [0, n]
+        if (d.top) res[d.pair].score = max(best, F[n] + B[0]);   // NW H[m][n] over i in [0, n]
+        const int mid = d.m / 2;
+        next[2 * blockIdx.x] = DcSub{d.a0, d.b0, mid, idx, 0, 0, d.pair, 0};
+        next[2 * blockIdx.x + 1] = DcSub{d.a0 + (uint64_t)mid, d.b0 + (uint64_t)idx, d.m - mid, n - idx, 0, 0, d.pair, 0};
     }
 }
 
@@ -287,93 +291,80 @@ __device__ int hb_leaf_solve(Seq S1, Seq S2, const uint8_t* g1, const uint8_t* g
 
 constexpr int kHbLdsCols = 64;   // leaves with |Seq1|, |Seq2| <= this run with LDS rows + symbols
 
-__global__ __launch_bounds__(64) void hb_leaf_kernel(const uint8_t* s1, const uint8_t* s2, const HbLeaf* leaves,
-                                                     uint32_t nleaves, int32_t* scratch, uint8_t* outops,
-                                                     int32_t* nout, int32_t* score, const uint32_t* lut,
+// A leaf's global scratch lives at 6 * key (F, X, Cc: 3 (blen + 1); base-case matrix:
+// 2 (max(alen, blen) + 1); together <= 6 (alen + blen) whenever alen, blen >= 1, the only
+// leaves that use scratch), its forward ops at stage[key], its op count at mark[key].
+__global__ __launch_bounds__(64) void hb_leaf_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* leaves,
+                                                     const uint32_t* nleaves, int32_t* scratch, uint8_t* stage,
+                                                     int32_t* mark, sa_result* res, const uint32_t* lut,
                                                      HbScore sc) {
     __shared__ int32_t s_rows[3 * (kHbLdsCols + 1) * 64];
     __shared__ uint8_t s_seq[2 * kHbLdsCols * 64];
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
-    if (id >= nleaves) return;
+    if (id >= *nleaves) return;
     const int t = threadIdx.x;
-    const HbLeaf L = leaves[id];
+    const DcSub L = leaves[id];
+    const uint64_t key = L.a0 + L.b0;
     const uint8_t* g1 = s1 + L.a0;
     const uint8_t* g2 = s2 + L.b0;
-    int32_t* Fg = scratch + L.scratch;
-    int32_t* Hs = Fg + 3 * (L.blen + 1);        // 2 * (max(alen, blen) + 1): base-case matrix
-    uint8_t* out = outops + L.out;
+    int32_t* Fg = scratch + 6 * key;
+    int32_t* Hs = Fg + 3 * (L.n + 1);
+    uint8_t* out = stage + key;
+    int32_t* score = &res[L.pair].score;   // written only for a top leaf
     int k;
-    if (L.alen <= kHbLdsCols && L.blen <= kHbLdsCols) {
+    if (L.m <= kHbLdsCols && L.n <= kHbLdsCols) {
         dc_lds_u8* q1 = (dc_lds_u8*)s_seq + t;
         dc_lds_u8* q2 = q1 + kHbLdsCols * 64;
-        for (int c = 0; c < L.alen; ++c) q1[c * 64] = g1[c];
-        for (int c = 0; c < L.blen; ++c) q2[c * 64] = g2[c];
+        for (int c = 0; c < L.m; ++c) q1[c * 64] = g1[c];
+        for (int c = 0; c < L.n; ++c) q2[c * 64] = g2[c];
         dc_lds_i32* r0 = (dc_lds_i32*)s_rows + t;
         const LRow F{r0}, X{r0 + (kHbLdsCols + 1) * 64}, Cc{r0 + 2 * (kHbLdsCols + 1) * 64};
-        k = hb_leaf_solve(LSeq{q1}, LSeq{q2}, g1, g2, L.alen, L.blen, L.top != 0, F, X, Cc, Hs, out, score + id,
-                          lut, sc);
+        k = hb_leaf_solve(LSeq{q1}, LSeq{q2}, g1, g2, L.m, L.n, L.top != 0, F, X, Cc, Hs, out, score, lut, sc);
     } else {
-        const GRow F{Fg}, X{Fg + (L.blen + 1)}, Cc{Fg + 2 * (L.blen + 1)};
-        k = hb_leaf_solve(GSeq{g1}, GSeq{g2}, g1, g2, L.alen, L.blen, L.top != 0, F, X, Cc, Hs, out, score + id,
-                          lut, sc);
+        const GRow F{Fg}, X{Fg + (L.n + 1)}, Cc{Fg + 2 * (L.n + 1)};
+        k = hb_leaf_solve(GSeq{g1}, GSeq{g2}, g1, g2, L.m, L.n, L.top != 0, F, X, Cc, Hs, out, score, lut, sc);
     }
-    nout[id] = k;
+    if (k) mark[key] = k;
 }
 
 // ---------------------------------------------------------------------------- host driver
 namespace {
 
-struct Sub {
-    uint32_t pair;
-    uint64_t a0, b0;   // absolute indices into seq1 / seq2
-    int32_t m, n;
-    bool top;
-};
-
 template <bool LUT, bool ALLOW>
-void launch_sweeps_t(int R, dim3 grid, const uint8_t* d1, const uint8_t* d2, const HbSweep* sw, int32_t* rows,
-                     const uint32_t* lut, const HbScore& sc, hipStream_t st) {
+void launch_sweeps_t(int R, dim3 grid, const uint8_t* d1, const uint8_t* d2, const DcSub* split, const DcLevel* lvl,
+                     int32_t* rows, const uint32_t* lut, const HbScore& sc, hipStream_t st) {
     const dim3 block(64);
     switch (R) {
-        case 1: hipLaunchKernelGGL((hb_sweep_kernel<1, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 2: hipLaunchKernelGGL((hb_sweep_kernel<2, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 4: hipLaunchKernelGGL((hb_sweep_kernel<4, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 8: hipLaunchKernelGGL((hb_sweep_kernel<8, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 16: hipLaunchKernelGGL((hb_sweep_kernel<16, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        default: hipLaunchKernelGGL((hb_sweep_kernel<32, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 1: hipLaunchKernelGGL((hb_sweep_kernel<1, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
+        case 2: hipLaunchKernelGGL((hb_sweep_kernel<2, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
+        case 4: hipLaunchKernelGGL((hb_sweep_kernel<4, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
+        case 8: hipLaunchKernelGGL((hb_sweep_kernel<8, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
+        case 16: hipLaunchKernelGGL((hb_sweep_kernel<16, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
+        default: hipLaunchKernelGGL((hb_sweep_kernel<32, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
     }
 }
 
-hipError_t launch_sweeps(int R, uint32_t count, const uint8_t* d1, const uint8_t* d2, const HbSweep* sw,
-                         int32_t* rows, const uint32_t* lut, const HbScore& sc, hipStream_t st) {
+hipError_t launch_sweeps(int R, uint32_t count, const uint8_t* d1, const uint8_t* d2, const DcSub* split,
+                         const DcLevel* lvl, int32_t* rows, const uint32_t* lut, const HbScore& sc, hipStream_t st) {
     const dim3 grid(count);
     if (lut) {
-        if (sc.allow) launch_sweeps_t<true, true>(R, grid, d1, d2, sw, rows, lut, sc, st);
-        else launch_sweeps_t<true, false>(R, grid, d1, d2, sw, rows, lut, sc, st);
+        if (sc.allow) launch_sweeps_t<true, true>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
+        else launch_sweeps_t<true, false>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
     } else {
-        if (sc.allow) launch_sweeps_t<false, true>(R, grid, d1, d2, sw, rows, lut, sc, st);
-        else launch_sweeps_t<false, false>(R, grid, d1, d2, sw, rows, lut, sc, st);
+        if (sc.allow) launch_sweeps_t<false, true>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
+        else launch_sweeps_t<false, false>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
     }
     return hipGetLastError();
 }
 
 }  // namespace
 
-// Host driver: inputs on the device (offsets too), results and the traceback-order op streams
-// returned in host memory (res[npairs], ops laid out at off1[p] + off2[p] + p).
+// Host driver: inputs, results and the traceback-order op streams (pair p's at
+// off1[p] + off2[p] + p) all on the device; enqueued on st without waiting for it, apart from
+// one read of the offsets (grid bounds).
 int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
                    const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
-                   std::vector<sa_result>& res, const uint8_t** ops, uint64_t* ops_bytes,
-                   std::string* err) {
-    const bool timing = getenv("SEQALIB_HB_TIMING") != nullptr;
-    auto now = [] { return std::chrono::steady_clock::now(); };
-    auto t_start = now(), t_mark = t_start;
-    auto lap = [&](const char* what) {
-        if (!timing) return;
-        const auto t = now();
-        fprintf(stderr, "[hb] %-28s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_mark).count());
-        t_mark = t;
-    };
+                   sa_result* d_res, uint8_t* d_ops, std::string* err) {
     int leaf_rows = kHbLeafRows;   // tuning override: SEQALIB_HB_LEAF
     if (const char* lr = getenv("SEQALIB_HB_LEAF")) leaf_rows = std::max(2, atoi(lr));
     HbScore sc;
@@ -381,127 +372,34 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
     sc.match = scoring->match;
     sc.allow = scoring->allow_mismatch != 0;
     sc.mismatch = sc.allow ? scoring->mismatch : INT_MIN;
-    static thread_local HostBuf<uint64_t> o1, o2;
-    SA_DC_HIP(o1.alloc(npairs + 1));
-    SA_DC_HIP(o2.alloc(npairs + 1));
-    static thread_local HostBuf<uint8_t> hops;   // traceback-order op streams, returned in *ops
-    SA_DC_HIP(hipMemcpyAsync(o1.data(), d_o1, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
-    SA_DC_HIP(hipMemcpyAsync(o2.data(), d_o2, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
-    SA_DC_HIP(dc_sync(st));
-    lap("setup (offsets D2H)");
-    res.assign(npairs, sa_result{});
-    std::vector<Sub> cur, leaves;
-    cur.reserve(npairs);
-    for (uint32_t p = 0; p < npairs; ++p)
-        cur.push_back(Sub{p, o1[p], o2[p], (int32_t)(o1[p + 1] - o1[p]), (int32_t)(o2[p + 1] - o2[p]), true});
-
-    // device buffers persist per host thread (hipMalloc/hipFree per call would serialise)
-    static thread_local DevBuf<HbSweep> dsw;
-    static thread_local DevBuf<HbSplit> dsp;
-    static thread_local DevBuf<int32_t> drows, dmid, dscore;
-    std::vector<HbSweep> sw;
-    std::vector<HbSplit> sp;
-    std::vector<Sub> split, next;
-    static thread_local HostBuf<int32_t> mid2, tops;
-    while (!cur.empty()) {
-        split.clear();
-        for (const Sub& s : cur) (s.m > leaf_rows && s.n >= 2 ? split : leaves).push_back(s);
-        if (split.empty()) break;
-        sw.clear();
-        sp.clear();
-        uint64_t rowpos = 0;
-        int maxa = 0;
-        for (const Sub& s : split) {
-            const int mid = s.m / 2;
-            HbSplit d;
-            d.n = s.n;
-            d.top = s.top ? 1 : 0;
-            d.fwd = rowpos;
-            sw.push_back(HbSweep{s.a0, s.b0, mid, s.n, 0, 0, rowpos});
-            rowpos += (uint64_t)s.n + 1;
-            d.rev = rowpos;
-            sw.push_back(HbSweep{s.a0 + (uint64_t)s.m - 1, s.b0 + (uint64_t)s.n - 1, s.m - mid, s.n, 1, 0, rowpos});
-            rowpos += (uint64_t)s.n + 1;
-            sp.push_back(d);
-            maxa = std::max(maxa, s.m - mid);
-        }
-        SA_DC_HIP(dsw.alloc(sw.size()));
-        SA_DC_HIP(dsp.alloc(sp.size()));
-        SA_DC_HIP(drows.alloc(rowpos));
-        SA_DC_HIP(dmid.alloc(sp.size()));
-        SA_DC_HIP(dscore.alloc(sp.size()));
-        static thread_local HostBuf<HbSweep> ssw;
-        static thread_local HostBuf<HbSplit> ssp;
-        SA_DC_HIP(dc_put(dsw.p, sw, ssw, st));
-        lap("level: descriptors + H2D");
-        SA_DC_HIP(dc_put(dsp.p, sp, ssp, st));
+    DcBounds b;
+    SA_DC_HIP(dc_bounds(d_o1, d_o2, npairs, st, &b));
+    static thread_local DcWork w;
+    SA_DC_HIP(w.prepare(b, npairs, leaf_rows, 2, 2, 6, st));
+    SA_DC_HIP(hipMemsetAsync(d_res, 0, sizeof(sa_result) * npairs, st));
+    SA_DC_HIP(dc_launch_init(d_o1, d_o2, npairs, 0, w.cur.p, st));
+    uint32_t cap = npairs;     // upper bound on this level's subproblems
+    int maxm = b.max_m;        // upper bound on their Seq1 length
+    for (int l = 0;; ++l) {
+        SA_DC_HIP(dc_launch_classify(w.cur.p, cap, npairs, l ? w.lvl.p + l - 1 : nullptr, 2, leaf_rows, 2,
+                                     w.lvl.p + l, w.split.p, w.leaves.p, w.nleaf(), st));
+        if (maxm <= leaf_rows) break;
+        const uint32_t splits = std::min<uint64_t>(cap, w.max_splits);
+        const int maxa = (maxm + 1) / 2;
         int R = 1;
         while (R < 32 && 64 * R < maxa) R *= 2;
-        SA_DC_HIP(launch_sweeps(R, (uint32_t)sw.size(), d1, d2, dsw.p, drows.p, d_lutbits, sc, st));
-        hipLaunchKernelGGL(hb_split_kernel, dim3((uint32_t)sp.size()), dim3(64), 0, st, dsp.p, drows.p, dmid.p,
-                           dscore.p);
+        SA_DC_HIP(launch_sweeps(R, 2 * splits, d1, d2, w.split.p, w.lvl.p + l, w.rows.p, d_lutbits, sc, st));
+        hipLaunchKernelGGL(hb_split_kernel, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p, w.next.p,
+                           d_res);
         SA_DC_HIP(hipGetLastError());
-        SA_DC_HIP(mid2.alloc(sp.size()));
-        SA_DC_HIP(tops.alloc(sp.size()));
-        SA_DC_HIP(hipMemcpyAsync(mid2.data(), dmid.p, sp.size() * 4, hipMemcpyDeviceToHost, st));
-        SA_DC_HIP(hipMemcpyAsync(tops.data(), dscore.p, sp.size() * 4, hipMemcpyDeviceToHost, st));
-        SA_DC_HIP(dc_sync(st));
-        next.clear();
-        for (size_t k = 0; k < split.size(); ++k) {
-            const Sub& s = split[k];
-            if (s.top) res[s.pair].score = tops[k];
-            const int mid = s.m / 2, j = mid2[k];
-            next.push_back(Sub{s.pair, s.a0, s.b0, mid, j, false});
-            next.push_back(Sub{s.pair, s.a0 + (uint64_t)mid, s.b0 + (uint64_t)j, s.m - mid, s.n - j, false});
-        }
-        cur.swap(next);
-        lap("level (sweeps + split)");
+        w.cur.swap(w.next);
+        cap = 2 * splits;
+        maxm = maxa;
     }
-
-    // leaves: one thread each
-    std::vector<HbLeaf> lv(leaves.size());
-    uint64_t scr = 0, outpos = 0;
-    for (size_t k = 0; k < leaves.size(); ++k) {
-        const Sub& s = leaves[k];
-        lv[k] = HbLeaf{s.a0, s.b0, s.m, s.n, scr, outpos, s.top ? 1 : 0, 0};
-        scr += 3ull * ((uint64_t)s.n + 1) + 2ull * ((uint64_t)std::max(s.m, s.n) + 1);
-        outpos += (uint64_t)s.m + (uint64_t)s.n;
-    }
-    if (!lv.empty()) {
-        static thread_local DevBuf<HbLeaf> dlv;
-        static thread_local DevBuf<int32_t> dscr, dnout, dlscore;
-        static thread_local DevBuf<uint8_t> dout;
-        SA_DC_HIP(dlv.alloc(lv.size()));
-        SA_DC_HIP(dscr.alloc(scr));
-        SA_DC_HIP(dnout.alloc(lv.size()));
-        SA_DC_HIP(dlscore.alloc(lv.size()));
-        SA_DC_HIP(dout.alloc(outpos));
-        static thread_local HostBuf<HbLeaf> slv;
-        SA_DC_HIP(dc_put(dlv.p, lv, slv, st));
-        hipLaunchKernelGGL(hb_leaf_kernel, dim3((uint32_t)((lv.size() + 63) / 64)), dim3(64), 0, st, d1, d2, dlv.p,
-                           (uint32_t)lv.size(), dscr.p, dout.p, dnout.p, dlscore.p, d_lutbits, sc);
-        SA_DC_HIP(hipGetLastError());
-        static thread_local HostBuf<int32_t> nout, lscore;
-        static thread_local HostBuf<uint8_t> lops;
-        SA_DC_HIP(nout.alloc(lv.size()));
-        SA_DC_HIP(lscore.alloc(lv.size()));
-        SA_DC_HIP(lops.alloc(outpos));
-        SA_DC_HIP(hipMemcpyAsync(nout.data(), dnout.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
-        SA_DC_HIP(hipMemcpyAsync(lscore.data(), dlscore.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
-        if (outpos) SA_DC_HIP(hipMemcpyAsync(lops.data(), dout.p, outpos, hipMemcpyDeviceToHost, st));
-        SA_DC_HIP(dc_sync(st));
-        lap("leaves (kernel + D2H)");
-        std::vector<DcLeafRef> refs(lv.size());
-        for (size_t k = 0; k < lv.size(); ++k)
-            refs[k] = DcLeafRef{leaves[k].pair, leaves[k].a0, leaves[k].b0, lv[k].out, leaves[k].top};
-        SA_DC_HIP(dc_assemble(npairs, o1.data(), o2.data(), refs, nout.data(), lscore.data(), lops.data(), res, hops));
-        lap("assembly (host)");
-    } else {
-        SA_DC_HIP(hops.alloc(o1[npairs] + o2[npairs] + npairs));
-        memset(hops.data(), 0, o1[npairs] + o2[npairs] + npairs);
-    }
-    *ops = hops.data();
-    *ops_bytes = o1[npairs] + o2[npairs] + npairs;
+    hipLaunchKernelGGL(hb_leaf_kernel, dim3((w.leaf_cap + 63) / 64), dim3(64), 0, st, d1, d2, w.leaves.p, w.nleaf(),
+                       w.scratch.p, w.stage.p, w.mark.p, d_res, d_lutbits, sc);
+    SA_DC_HIP(hipGetLastError());
+    SA_DC_HIP(dc_launch_assemble(d_o1, d_o2, npairs, w.mark.p, w.stage.p, d_res, d_ops, st));
     return 0;
 }
 

@@ -219,18 +219,14 @@ hipError_t launch_endcell(int algo, int R, const EndcellParams& p, hipStream_t s
 #include <string>
 #include <vector>
 namespace sa {
-// HirschbergSA driver (sa_hirschberg.hip): device inputs, host outputs (results, op streams at
-// off1[p] + off2[p] + p).  Returns 0 or -1 with *err set.
+// HirschbergSA / MyersMillerSA drivers (sa_hirschberg.hip, sa_myersmiller.hip): device inputs,
+// device outputs (results, op streams at off1[p] + off2[p] + p), enqueued on st; the only host
+// wait is one read of the offsets.  Return 0, or -1 with *err set.
 int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
                    const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
-                   std::vector<sa_result>& res, const uint8_t** ops, uint64_t* ops_bytes,
-                   std::string* err);
-// MyersMillerSA (sa_myersmiller.hip): same contract as hirschberg_run.  *ops is set to a pinned
-// host buffer owned by the calling thread (valid until its next call) holding
-// off1[npairs] + off2[npairs] + npairs bytes.
+                   sa_result* d_res, uint8_t* d_ops, std::string* err);
 int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
                     const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
-                    std::vector<sa_result>& res, const uint8_t** ops, uint64_t* ops_bytes,
-                   std::string* err);
+                    sa_result* d_res, uint8_t* d_ops, std::string* err);
 
 }  // namespace sa

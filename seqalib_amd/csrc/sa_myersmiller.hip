@@ -9,13 +9,15 @@
 //     mm_sweep_kernel (score-only affine DP, one wave per sweep, anti-diagonal wavefront; each
 //     sweep writes its last C and D rows); mm_split_kernel then takes, per subproblem, the FIRST
 //     j in [0, N] maximising max(CC[j] + RR[j], DD[j] + SS[j] - g) and the midpoint type
-//     (type 2 iff the gap term is not strictly smaller, :320-340); the host forms the children
-//     with their tb/te (:358-395).  A type-2 midpoint's two deletions (:390-392) become a leaf
+//     (type 2 iff the gap term is not strictly smaller, :320-340) and writes the children with
+//     their tb/te (:358-395) as the next level's subproblems (three slots per split; a type-1
+//     midpoint leaves the third empty).  A type-2 midpoint's two deletions (:390-392) become a leaf
 //     of 2 rows and 0 columns, which emits exactly those.
 //   * leaves: mm_leaf_kernel, one thread per subproblem, runs the same recursion iteratively
 //     (explicit stack, left child first) including the base cases N == 0, M == 0 and M == 1
 //     (:57-160, with its "failsafe" pair of gap entries).
-//   * assembly: dc_assemble (sa_dc.h).
+//   * assembly: dc_assemble_kernel (sa_dc.hip).  The level loop stays on the device (sa_dc.hip:
+//     key-addressed buffers, device-side classification).
 // Score reported (the reference exposes none): the top call's optimum — its midpoint maximum,
 // the M == 1 maximum, or the boundary value of an empty side (oracle: align_myers_miller).
 //
@@ -46,23 +48,19 @@ struct MmSweep {       // affine sweep over A (alen) x B (blen) -> C row at out,
     uint64_t out;      // int32 index into the row buffer
 };
 
-struct MmSplit {
-    uint64_t fwd, rev; // row indices of the forward / reverse C rows (D follows at + n + 1)
-    int32_t n, pad;
-};
-
-struct MmLeaf {
-    uint64_t a0, b0;   // Seq1 / Seq2 start (indices into seq1 / seq2)
-    int32_t alen, blen;
-    int32_t tb, te;
-    uint64_t scratch;  // int32 index into the leaf scratch (4 * (blen + 1))
-    uint64_t out;      // byte index into the leaf op buffer (capacity alen + blen)
-    int32_t top, pad;
-};
-
 struct MmScore {
     int32_t g, h, match, mismatch, allow;   // mismatch = INT_MIN when !allow (:15)
 };
+
+// Sweep rows of a split subproblem live at 4 * key: forward C, D, reverse C, D, n + 1 ints
+// each (4 (n + 1) <= 4 (m + n), inside its key span).
+__device__ __forceinline__ MmSweep mm_sweep_of(const DcSub& s, int rev) {
+    const int mid = s.m / 2;
+    const uint64_t base = 4 * (s.a0 + s.b0);
+    if (!rev) return MmSweep{s.a0, s.b0, mid, s.n, 0, s.tb, base};
+    return MmSweep{s.a0 + (uint64_t)s.m - 1, s.b0 + (uint64_t)s.n - 1, s.m - mid, s.n, 1, s.te,
+                   base + 2ull * ((uint64_t)s.n + 1)};
+}
 
 // diagonal candidate of c = max({DD, e, s + Similarity}) (:218-232); INT_MIN drops out of the max
 __device__ __forceinline__ int32_t mm_diag(int32_t s, bool v, const MmScore& sc) {
@@ -173,11 +171,13 @@ __device__ __forceinline__ void mm_band(const MmSweep& d, const uint8_t* s1, con
 }
 
 template <int R, bool LUT, bool ALLOW>
-__global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const uint8_t* s2, const MmSweep* sweeps,
-                                                      int32_t* rows, const uint32_t* lutbits, MmScore sc) {
+__global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* split,
+                                                      const DcLevel* lvl, int32_t* rows, const uint32_t* lutbits,
+                                                      MmScore sc) {
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];
     const int lane = threadIdx.x;
-    const MmSweep d = sweeps[blockIdx.x];
+    if (blockIdx.x / 2 >= lvl->nsplit) return;   // grid sized from an upper bound
+    const MmSweep d = mm_sweep_of(split[blockIdx.x / 2], blockIdx.x & 1);
     if constexpr (LUT) {
         for (int k = lane; k < 2048; k += 64) s_lut[k] = lutbits[k];
         __syncthreads();
@@ -204,15 +204,15 @@ __global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const u
 }
 
 // ---------------------------------------------------------------------------- split
-// out3[3k] = index, out3[3k+1] = type (1: type 2), out3[3k+2] = the maximum (:320-340)
-__global__ __launch_bounds__(64) void mm_split_kernel(const MmSplit* splits, const int32_t* rows, int32_t* out3,
-                                                      int32_t g) {
+__global__ __launch_bounds__(64) void mm_split_kernel(const DcSub* split, const DcLevel* lvl, const int32_t* rows,
+                                                      DcSub* next, sa_result* res, int32_t g) {
     const int lane = threadIdx.x;
-    const MmSplit d = splits[blockIdx.x];
+    if (blockIdx.x >= lvl->nsplit) return;
+    const DcSub d = split[blockIdx.x];
     const int n = d.n;
-    const int32_t* C = rows + d.fwd;
+    const int32_t* C = rows + 4 * (d.a0 + d.b0);
     const int32_t* D = C + n + 1;
-    const int32_t* Cr = rows + d.rev;
+    const int32_t* Cr = D + n + 1;
     const int32_t* Dr = Cr + n + 1;
     int32_t best = INT_MIN;
     int idx = 0, ty = 0;
@@ -231,9 +231,18 @@ __global__ __launch_bounds__(64) void mm_split_kernel(const MmSplit* splits, con
         if (ob > best || (ob == best && oi < idx)) { best = ob; idx = oi; ty = ot; }
     }
     if (lane == 0) {
-        out3[3 * blockIdx.x] = idx;
-        out3[3 * blockIdx.x + 1] = ty;
-        out3[3 * blockIdx.x + 2] = best;
+        if (d.top) res[d.pair].score = best;
+        const int mid = d.m / 2, j = idx;
+        DcSub* c = next + 3 * blockIdx.x;
+        if (!ty) {   // type 1 (:358-374)
+            c[0] = DcSub{d.a0, d.b0, mid, j, d.tb, g, d.pair, 0};
+            c[1] = DcSub{d.a0 + (uint64_t)mid, d.b0 + (uint64_t)j, d.m - mid, n - j, g, d.te, d.pair, 0};
+            c[2] = DcSub{0, 0, -1, 0, 0, 0, d.pair, 0};
+        } else {     // type 2 (:375-395): the two deletions of :390-392 as a 2-row, 0-column leaf
+            c[0] = DcSub{d.a0, d.b0, mid - 1, j, d.tb, 0, d.pair, 0};
+            c[1] = DcSub{d.a0 + (uint64_t)mid - 1, d.b0 + (uint64_t)j, 2, 0, 0, 0, d.pair, 0};
+            c[2] = DcSub{d.a0 + (uint64_t)mid + 1, d.b0 + (uint64_t)j, d.m - mid - 1, n - j, 0, d.te, d.pair, 0};
+        }
     }
 }
 
@@ -350,97 +359,78 @@ __device__ int mm_leaf_solve(Seq S1, Seq S2, int alen, int blen, int32_t tb0, in
 
 constexpr int kMmLdsCols = 64;   // leaves with |Seq1|, |Seq2| <= this run with LDS rows + symbols
 
-__global__ __launch_bounds__(64) void mm_leaf_kernel(const uint8_t* s1, const uint8_t* s2, const MmLeaf* leaves,
-                                                     uint32_t nleaves, int32_t* scratch, uint8_t* outops,
-                                                     int32_t* nout, int32_t* score, const uint32_t* lut,
+// Leaves beyond the LDS size keep their four rows at 6 * key (4 (blen + 1) <= 6 (alen + blen));
+// forward ops at stage[key], op count at mark[key].
+__global__ __launch_bounds__(64) void mm_leaf_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* leaves,
+                                                     const uint32_t* nleaves, int32_t* scratch, uint8_t* stage,
+                                                     int32_t* mark, sa_result* res, const uint32_t* lut,
                                                      MmScore sc) {
     __shared__ int32_t s_rows[4 * (kMmLdsCols + 1) * 64];
     __shared__ uint8_t s_seq[2 * kMmLdsCols * 64];
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
-    if (id >= nleaves) return;
+    if (id >= *nleaves) return;
     const int t = threadIdx.x;
-    const MmLeaf L = leaves[id];
+    const DcSub L = leaves[id];
+    const uint64_t key = L.a0 + L.b0;
     const uint8_t* g1 = s1 + L.a0;
     const uint8_t* g2 = s2 + L.b0;
-    uint8_t* out = outops + L.out;
+    uint8_t* out = stage + key;
+    int32_t* score = &res[L.pair].score;   // written only for a top leaf
     int k;
-    if (L.alen <= kMmLdsCols && L.blen <= kMmLdsCols) {
+    if (L.m <= kMmLdsCols && L.n <= kMmLdsCols) {
         dc_lds_u8* q1 = (dc_lds_u8*)s_seq + t;
         dc_lds_u8* q2 = q1 + kMmLdsCols * 64;
-        for (int c = 0; c < L.alen; ++c) q1[c * 64] = g1[c];
-        for (int c = 0; c < L.blen; ++c) q2[c * 64] = g2[c];
+        for (int c = 0; c < L.m; ++c) q1[c * 64] = g1[c];
+        for (int c = 0; c < L.n; ++c) q2[c * 64] = g2[c];
         dc_lds_i32* r0 = (dc_lds_i32*)s_rows + t;
         constexpr int W = (kMmLdsCols + 1) * 64;
-        k = mm_leaf_solve(LSeq{q1}, LSeq{q2}, L.alen, L.blen, L.tb, L.te, L.top != 0, LRow{r0}, LRow{r0 + W},
-                          LRow{r0 + 2 * W}, LRow{r0 + 3 * W}, out, score + id, lut, sc);
+        k = mm_leaf_solve(LSeq{q1}, LSeq{q2}, L.m, L.n, L.tb, L.te, L.top != 0, LRow{r0}, LRow{r0 + W},
+                          LRow{r0 + 2 * W}, LRow{r0 + 3 * W}, out, score, lut, sc);
     } else {
-        int32_t* F = scratch + L.scratch;
-        const int W = L.blen + 1;
-        k = mm_leaf_solve(GSeq{g1}, GSeq{g2}, L.alen, L.blen, L.tb, L.te, L.top != 0, GRow{F}, GRow{F + W},
-                          GRow{F + 2 * W}, GRow{F + 3 * W}, out, score + id, lut, sc);
+        int32_t* F = scratch + 6 * key;
+        const int W = L.n + 1;
+        k = mm_leaf_solve(GSeq{g1}, GSeq{g2}, L.m, L.n, L.tb, L.te, L.top != 0, GRow{F}, GRow{F + W},
+                          GRow{F + 2 * W}, GRow{F + 3 * W}, out, score, lut, sc);
     }
-    nout[id] = k;
+    if (k) mark[key] = k;
 }
 
 // ---------------------------------------------------------------------------- host driver
 namespace {
 
-struct Sub {
-    uint32_t pair;
-    uint64_t a0, b0;   // absolute indices into seq1 / seq2
-    int32_t m, n;
-    int32_t tb, te;
-    bool top;
-};
-
 template <bool LUT, bool ALLOW>
-void launch_mm_sweeps_t(int R, dim3 grid, const uint8_t* d1, const uint8_t* d2, const MmSweep* sw, int32_t* rows,
-                        const uint32_t* lut, const MmScore& sc, hipStream_t st) {
+void launch_mm_sweeps_t(int R, dim3 grid, const uint8_t* d1, const uint8_t* d2, const DcSub* split,
+                        const DcLevel* lvl, int32_t* rows, const uint32_t* lut, const MmScore& sc, hipStream_t st) {
     const dim3 block(64);
     switch (R) {
-        case 1: hipLaunchKernelGGL((mm_sweep_kernel<1, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 2: hipLaunchKernelGGL((mm_sweep_kernel<2, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 4: hipLaunchKernelGGL((mm_sweep_kernel<4, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 8: hipLaunchKernelGGL((mm_sweep_kernel<8, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        case 16: hipLaunchKernelGGL((mm_sweep_kernel<16, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
-        default: hipLaunchKernelGGL((mm_sweep_kernel<32, LUT, ALLOW>), grid, block, 0, st, d1, d2, sw, rows, lut, sc); break;
+        case 1: hipLaunchKernelGGL((mm_sweep_kernel<1, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
+        case 2: hipLaunchKernelGGL((mm_sweep_kernel<2, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
+        case 4: hipLaunchKernelGGL((mm_sweep_kernel<4, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
+        case 8: hipLaunchKernelGGL((mm_sweep_kernel<8, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
+        case 16: hipLaunchKernelGGL((mm_sweep_kernel<16, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
+        default: hipLaunchKernelGGL((mm_sweep_kernel<32, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
     }
 }
 
-hipError_t launch_mm_sweeps(int R, uint32_t count, const uint8_t* d1, const uint8_t* d2, const MmSweep* sw,
-                            int32_t* rows, const uint32_t* lut, const MmScore& sc, hipStream_t st) {
+hipError_t launch_mm_sweeps(int R, uint32_t count, const uint8_t* d1, const uint8_t* d2, const DcSub* split,
+                            const DcLevel* lvl, int32_t* rows, const uint32_t* lut, const MmScore& sc, hipStream_t st) {
     const dim3 grid(count);
     if (lut) {
-        if (sc.allow) launch_mm_sweeps_t<true, true>(R, grid, d1, d2, sw, rows, lut, sc, st);
-        else launch_mm_sweeps_t<true, false>(R, grid, d1, d2, sw, rows, lut, sc, st);
+        if (sc.allow) launch_mm_sweeps_t<true, true>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
+        else launch_mm_sweeps_t<true, false>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
     } else {
-        if (sc.allow) launch_mm_sweeps_t<false, true>(R, grid, d1, d2, sw, rows, lut, sc, st);
-        else launch_mm_sweeps_t<false, false>(R, grid, d1, d2, sw, rows, lut, sc, st);
+        if (sc.allow) launch_mm_sweeps_t<false, true>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
+        else launch_mm_sweeps_t<false, false>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
     }
     return hipGetLastError();
 }
 
 }  // namespace
 
-// Host driver: inputs on the device (offsets too), results and the traceback-order op streams
-// returned in host memory (res[npairs], ops laid out at off1[p] + off2[p] + p).
+// Host driver: same contract as hirschberg_run (device results and op streams, enqueued on st).
 int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
                     const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
-                    std::vector<sa_result>& res, const uint8_t** ops, uint64_t* ops_bytes,
-                   std::string* err) {
-    const bool timing = getenv("SEQALIB_MM_TIMING") != nullptr;
-    auto now = [] { return std::chrono::steady_clock::now(); };
-    auto t_mark = now();
-    auto lap = [&](const char* what) {
-        if (!timing) return;
-        const auto t = now();
-        fprintf(stderr, "[mm] %-28s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_mark).count());
-        t_mark = t;
-    };
-    if (timing) {
-        (void)hipDeviceSynchronize();
-        lap("entry: device idle");
-    }
+                    sa_result* d_res, uint8_t* d_ops, std::string* err) {
     int leaf_rows = kMmLeafRows;   // tuning override: SEQALIB_MM_LEAF (the leaf stack bounds it)
     if (const char* lr = getenv("SEQALIB_MM_LEAF")) leaf_rows = std::min(4096, std::max(2, atoi(lr)));
     MmScore sc;
@@ -449,132 +439,35 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
     sc.match = scoring->match;
     sc.allow = scoring->allow_mismatch != 0;
     sc.mismatch = sc.allow ? scoring->mismatch : INT_MIN;
-    static thread_local HostBuf<uint64_t> o1, o2;
-    SA_DC_HIP(o1.alloc(npairs + 1));
-    SA_DC_HIP(o2.alloc(npairs + 1));
-    static thread_local HostBuf<uint8_t> hops;   // traceback-order op streams, returned in *ops
-    SA_DC_HIP(hipMemcpyAsync(o1.data(), d_o1, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
-    SA_DC_HIP(hipMemcpyAsync(o2.data(), d_o2, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st));
-    SA_DC_HIP(dc_sync(st));
-    lap("setup (offsets D2H)");
-    res.assign(npairs, sa_result{});
-    std::vector<Sub> cur, leaves;
-    cur.reserve(npairs);
-    for (uint32_t p = 0; p < npairs; ++p)
-        cur.push_back(Sub{p, o1[p], o2[p], (int32_t)(o1[p + 1] - o1[p]), (int32_t)(o2[p + 1] - o2[p]), sc.g, sc.g,
-                          true});   // getAlignment: buildResultRec(.., GapOpen, GapOpen) (:417)
-
-    static thread_local DevBuf<MmSweep> dsw;
-    static thread_local DevBuf<MmSplit> dsp;
-    static thread_local DevBuf<int32_t> drows, dout3;
-    std::vector<MmSweep> sw;
-    std::vector<MmSplit> sp;
-    std::vector<Sub> split, next;
-    static thread_local HostBuf<int32_t> out3;
-    while (!cur.empty()) {
-        split.clear();
-        for (const Sub& s : cur) (s.m > leaf_rows && s.n >= 1 ? split : leaves).push_back(s);
-        if (split.empty()) break;
-        sw.clear();
-        sp.clear();
-        uint64_t rowpos = 0;
-        int maxa = 0;
-        for (const Sub& s : split) {
-            const int mid = s.m / 2;
-            MmSplit d;
-            d.n = s.n;
-            d.pad = 0;
-            d.fwd = rowpos;
-            sw.push_back(MmSweep{s.a0, s.b0, mid, s.n, 0, s.tb, rowpos});
-            rowpos += 2ull * ((uint64_t)s.n + 1);
-            d.rev = rowpos;
-            sw.push_back(MmSweep{s.a0 + (uint64_t)s.m - 1, s.b0 + (uint64_t)s.n - 1, s.m - mid, s.n, 1, s.te, rowpos});
-            rowpos += 2ull * ((uint64_t)s.n + 1);
-            sp.push_back(d);
-            maxa = std::max(maxa, s.m - mid);
-        }
-        SA_DC_HIP(dsw.alloc(sw.size()));
-        SA_DC_HIP(dsp.alloc(sp.size()));
-        SA_DC_HIP(drows.alloc(rowpos));
-        SA_DC_HIP(dout3.alloc(3 * sp.size()));
-        static thread_local HostBuf<MmSweep> ssw;
-        static thread_local HostBuf<MmSplit> ssp;
-        SA_DC_HIP(dc_put(dsw.p, sw, ssw, st));
-        lap("level: descriptors + H2D");
-        SA_DC_HIP(dc_put(dsp.p, sp, ssp, st));
+    DcBounds b;
+    SA_DC_HIP(dc_bounds(d_o1, d_o2, npairs, st, &b));
+    static thread_local DcWork w;
+    SA_DC_HIP(w.prepare(b, npairs, leaf_rows, 3, 4, 6, st));
+    SA_DC_HIP(hipMemsetAsync(d_res, 0, sizeof(sa_result) * npairs, st));
+    // getAlignment: buildResultRec(.., GapOpen, GapOpen) (:417)
+    SA_DC_HIP(dc_launch_init(d_o1, d_o2, npairs, sc.g, w.cur.p, st));
+    uint32_t cap = npairs;
+    int maxm = b.max_m;
+    for (int l = 0;; ++l) {
+        SA_DC_HIP(dc_launch_classify(w.cur.p, cap, npairs, l ? w.lvl.p + l - 1 : nullptr, 3, leaf_rows, 1,
+                                     w.lvl.p + l, w.split.p, w.leaves.p, w.nleaf(), st));
+        if (maxm <= leaf_rows) break;
+        const uint32_t splits = std::min<uint64_t>(cap, w.max_splits);
+        const int maxa = (maxm + 1) / 2;
         int R = 1;
         while (R < 32 && 64 * R < maxa) R *= 2;
-        SA_DC_HIP(launch_mm_sweeps(R, (uint32_t)sw.size(), d1, d2, dsw.p, drows.p, d_lutbits, sc, st));
-        hipLaunchKernelGGL(mm_split_kernel, dim3((uint32_t)sp.size()), dim3(64), 0, st, dsp.p, drows.p, dout3.p, sc.g);
+        SA_DC_HIP(launch_mm_sweeps(R, 2 * splits, d1, d2, w.split.p, w.lvl.p + l, w.rows.p, d_lutbits, sc, st));
+        hipLaunchKernelGGL(mm_split_kernel, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p, w.next.p,
+                           d_res, sc.g);
         SA_DC_HIP(hipGetLastError());
-        SA_DC_HIP(out3.alloc(3 * sp.size()));
-        SA_DC_HIP(hipMemcpyAsync(out3.data(), dout3.p, 3 * sp.size() * 4, hipMemcpyDeviceToHost, st));
-        SA_DC_HIP(dc_sync(st));
-        next.clear();
-        for (size_t k = 0; k < split.size(); ++k) {
-            const Sub& s = split[k];
-            if (s.top) res[s.pair].score = out3[3 * k + 2];
-            const int mid = s.m / 2, j = out3[3 * k];
-            if (!out3[3 * k + 1]) {   // type 1 (:358-374)
-                next.push_back(Sub{s.pair, s.a0, s.b0, mid, j, s.tb, sc.g, false});
-                next.push_back(Sub{s.pair, s.a0 + (uint64_t)mid, s.b0 + (uint64_t)j, s.m - mid, s.n - j, sc.g, s.te, false});
-            } else {                  // type 2 (:375-395)
-                next.push_back(Sub{s.pair, s.a0, s.b0, mid - 1, j, s.tb, 0, false});
-                next.push_back(Sub{s.pair, s.a0 + (uint64_t)mid - 1, s.b0 + (uint64_t)j, 2, 0, 0, 0, false});
-                next.push_back(Sub{s.pair, s.a0 + (uint64_t)mid + 1, s.b0 + (uint64_t)j, s.m - mid - 1, s.n - j, 0, s.te,
-                                   false});
-            }
-        }
-        cur.swap(next);
-        lap("level (sweeps + split)");
+        w.cur.swap(w.next);
+        cap = 3 * splits;
+        maxm = maxa;
     }
-
-    // leaves: one thread each
-    std::vector<MmLeaf> lv(leaves.size());
-    uint64_t scr = 0, outpos = 0;
-    for (size_t k = 0; k < leaves.size(); ++k) {
-        const Sub& s = leaves[k];
-        lv[k] = MmLeaf{s.a0, s.b0, s.m, s.n, s.tb, s.te, scr, outpos, s.top ? 1 : 0, 0};
-        if (s.m > kMmLdsCols || s.n > kMmLdsCols) scr += 4ull * ((uint64_t)s.n + 1);
-        outpos += (uint64_t)s.m + (uint64_t)s.n;
-    }
-    if (lv.empty()) {
-        SA_DC_HIP(hops.alloc(o1[npairs] + o2[npairs] + npairs));
-        memset(hops.data(), 0, o1[npairs] + o2[npairs] + npairs);
-        *ops = hops.data();
-    *ops_bytes = o1[npairs] + o2[npairs] + npairs;
-        return 0;
-    }
-    static thread_local DevBuf<MmLeaf> dlv;
-    static thread_local DevBuf<int32_t> dscr, dnout, dlscore;
-    static thread_local DevBuf<uint8_t> dout;
-    SA_DC_HIP(dlv.alloc(lv.size()));
-    SA_DC_HIP(dscr.alloc(scr));
-    SA_DC_HIP(dnout.alloc(lv.size()));
-    SA_DC_HIP(dlscore.alloc(lv.size()));
-    SA_DC_HIP(dout.alloc(outpos));
-    static thread_local HostBuf<MmLeaf> slv;
-    SA_DC_HIP(dc_put(dlv.p, lv, slv, st));
-    hipLaunchKernelGGL(mm_leaf_kernel, dim3((uint32_t)((lv.size() + 63) / 64)), dim3(64), 0, st, d1, d2, dlv.p,
-                       (uint32_t)lv.size(), dscr.p, dout.p, dnout.p, dlscore.p, d_lutbits, sc);
+    hipLaunchKernelGGL(mm_leaf_kernel, dim3((w.leaf_cap + 63) / 64), dim3(64), 0, st, d1, d2, w.leaves.p, w.nleaf(),
+                       w.scratch.p, w.stage.p, w.mark.p, d_res, d_lutbits, sc);
     SA_DC_HIP(hipGetLastError());
-    static thread_local HostBuf<int32_t> nout, lscore;
-    static thread_local HostBuf<uint8_t> lops;
-    SA_DC_HIP(nout.alloc(lv.size()));
-    SA_DC_HIP(lscore.alloc(lv.size()));
-    SA_DC_HIP(lops.alloc(outpos));
-    SA_DC_HIP(hipMemcpyAsync(nout.data(), dnout.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
-    SA_DC_HIP(hipMemcpyAsync(lscore.data(), dlscore.p, lv.size() * 4, hipMemcpyDeviceToHost, st));
-    if (outpos) SA_DC_HIP(hipMemcpyAsync(lops.data(), dout.p, outpos, hipMemcpyDeviceToHost, st));
-    SA_DC_HIP(dc_sync(st));
-    lap("leaves (kernel + D2H)");
-    std::vector<DcLeafRef> refs(lv.size());
-    for (size_t k = 0; k < lv.size(); ++k)
-        refs[k] = DcLeafRef{leaves[k].pair, leaves[k].a0, leaves[k].b0, lv[k].out, leaves[k].top};
-    SA_DC_HIP(dc_assemble(npairs, o1.data(), o2.data(), refs, nout.data(), lscore.data(), lops.data(), res, hops));
-    lap("assembly (host)");
-    *ops = hops.data();
-    *ops_bytes = o1[npairs] + o2[npairs] + npairs;
+    SA_DC_HIP(dc_launch_assemble(d_o1, d_o2, npairs, w.mark.p, w.stage.p, d_res, d_ops, st));
     return 0;
 }
 
