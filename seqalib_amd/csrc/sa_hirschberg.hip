@@ -38,7 +38,7 @@
 
 namespace sa {
 
-constexpr int kHbLeafRows = 48;   // subproblems with <= this many Seq1 rows are leaves (tuned)
+constexpr int kHbLeafRows = 24;   // subproblems with <= this many Seq1 rows are leaves (tuned, tools/ab_dc.sh)
 
 struct HbSweep {       // NWScore over A (alen) x B (blen) -> rows[out .. out+blen]
     uint64_t a, b;     // index of A[0] / B[0] in seq1 / seq2 (rev: of the LAST element read first)
@@ -194,30 +194,33 @@ __global__ __launch_bounds__(64) void hb_split_kernel(const DcSub* split, const 
 }
 
 // ---------------------------------------------------------------------------- leaves
+// NWScore's last row (:31-66) into F[0..blen], one row updated in place (the cell above is read
+// before it is overwritten; its old value is the next column's diagonal).
 template <typename Row, typename Seq>
 __device__ void hb_nwscore(Seq A, int alen, int arev, Seq B, int blen, int brev,
-                           const uint32_t* lut, const HbScore& sc, Row& F, Row& X) {
+                           const uint32_t* lut, const HbScore& sc, Row F) {
     F[0] = 0;
     for (int j = 1; j <= blen; ++j) F[j] = F[j - 1] + sc.gap;
     for (int i = 1; i <= alen; ++i) {
         const uint32_t ai = arev ? A[alen - i] : A[i - 1];
-        int32_t left = F[0] + sc.gap, diag = F[0];
-        X[0] = left;
+        int32_t diag = F[0];
+        int32_t left = diag + sc.gap;
+        F[0] = left;
         for (int j = 1; j <= blen; ++j) {
             const uint32_t bj = brev ? B[blen - j] : B[j - 1];
             const int32_t up = F[j];
             left = hb_cell(diag, up, left, dc_match(lut, ai, bj), sc);
-            X[j] = left;
+            F[j] = left;
             diag = up;
         }
-        Row t = F; F = X; X = t;
     }
 }
 
 // NeedlemanWunschSA::getAlignment on a 1 x k or k x 1 view (:119-126): full matrix + the
 // reference NW traceback (SANeedlemanWunsch.h:167-230); writes forward-order ops at out.
+template <typename Row>
 __device__ int hb_nw_small(const uint8_t* A, int m, const uint8_t* B, int n, const uint32_t* lut,
-                           const HbScore& sc, int32_t* H, uint8_t* out) {
+                           const HbScore& sc, Row H, uint8_t* out) {
     const int w = n + 1;
     for (int i = 0; i <= m; ++i) H[i * w] = i * sc.gap;
     for (int j = 0; j <= n; ++j) H[j] = j * sc.gap;
@@ -247,13 +250,13 @@ __device__ int hb_nw_small(const uint8_t* A, int m, const uint8_t* B, int n, con
 // One leaf: the whole HirschbergRec below it (explicit stack, left child first), forward ops.
 template <typename Row, typename Seq>
 __device__ int hb_leaf_solve(Seq S1, Seq S2, const uint8_t* g1, const uint8_t* g2, int alen, int blen, bool top,
-                             Row F, Row X, Row Cc, int32_t* Hs, uint8_t* out, int32_t* score,
+                             Row F, Row Cc, Row Hs, uint8_t* out, int32_t* score,
                              const uint32_t* lut, const HbScore& sc) {
     if (top) {
         int32_t s;
         if (alen == 0) s = blen * sc.gap;
         else if (blen == 0) s = alen * sc.gap;
-        else { hb_nwscore(S1, alen, 0, S2, blen, 0, lut, sc, F, X); s = F[blen]; }
+        else { hb_nwscore(S1, alen, 0, S2, blen, 0, lut, sc, F); s = F[blen]; }
         *score = s;
     }
     int k = 0;
@@ -272,9 +275,9 @@ __device__ int hb_leaf_solve(Seq S1, Seq S2, const uint8_t* g1, const uint8_t* g
         } else {
             const int mid = xl / 2;
             const Seq A0 = S1.shifted(x0), B0 = S2.shifted(y0), A1 = S1.shifted(x0 + mid);
-            hb_nwscore(A0, mid, 0, B0, yl, 0, lut, sc, F, X);
+            hb_nwscore(A0, mid, 0, B0, yl, 0, lut, sc, F);
             for (int q = 0; q <= yl; ++q) Cc[q] = F[q];
-            hb_nwscore(A1, xl - mid, 1, B0, yl, 1, lut, sc, F, X);
+            hb_nwscore(A1, xl - mid, 1, B0, yl, 1, lut, sc, F);
             int mid2 = 0;
             int32_t best = INT_MIN;
             for (int i = 0; i < yl; ++i) {
@@ -289,16 +292,24 @@ __device__ int hb_leaf_solve(Seq S1, Seq S2, const uint8_t* g1, const uint8_t* g
     return k;
 }
 
-constexpr int kHbLdsCols = 64;   // leaves with |Seq1|, |Seq2| <= this run with LDS rows + symbols
+// Leaves with |Seq1|, |Seq2| <= kHbLdsCols run with LDS rows + symbols: 2 rows + 2 symbol
+// strings per thread, 21 KiB per 64-thread block at 32 (at 64 with a third row it was 58 KiB:
+// 2 blocks per CU).  Leaves have <= kHbLeafRows rows; on DNA their columns rarely pass 32;
+// wider leaves take the global-scratch path.  Measured (tools/ab_dc.sh, 10,000 x 1024^2):
+// 64 cols / 48-row leaves 21.3 ms, 48 / 48 17.1 ms, 48 / 24 13.0 ms, 32 / 24 12.6 ms.
+#ifndef SA_HB_LDS_COLS
+#define SA_HB_LDS_COLS 32
+#endif
+constexpr int kHbLdsCols = SA_HB_LDS_COLS;
 
-// A leaf's global scratch lives at 6 * key (F, X, Cc: 3 (blen + 1); base-case matrix:
+// A leaf's global scratch lives at 6 * key (F, -, Cc: 3 (blen + 1); base-case matrix:
 // 2 (max(alen, blen) + 1); together <= 6 (alen + blen) whenever alen, blen >= 1, the only
 // leaves that use scratch), its forward ops at stage[key], its op count at mark[key].
 __global__ __launch_bounds__(64) void hb_leaf_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* leaves,
                                                      const uint32_t* nleaves, int32_t* scratch, uint8_t* stage,
                                                      int32_t* mark, sa_result* res, const uint32_t* lut,
                                                      HbScore sc) {
-    __shared__ int32_t s_rows[3 * (kHbLdsCols + 1) * 64];
+    __shared__ int32_t s_rows[2 * (kHbLdsCols + 1) * 64];
     __shared__ uint8_t s_seq[2 * kHbLdsCols * 64];
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= *nleaves) return;
@@ -318,11 +329,12 @@ __global__ __launch_bounds__(64) void hb_leaf_kernel(const uint8_t* s1, const ui
         for (int c = 0; c < L.m; ++c) q1[c * 64] = g1[c];
         for (int c = 0; c < L.n; ++c) q2[c * 64] = g2[c];
         dc_lds_i32* r0 = (dc_lds_i32*)s_rows + t;
-        const LRow F{r0}, X{r0 + (kHbLdsCols + 1) * 64}, Cc{r0 + 2 * (kHbLdsCols + 1) * 64};
-        k = hb_leaf_solve(LSeq{q1}, LSeq{q2}, g1, g2, L.m, L.n, L.top != 0, F, X, Cc, Hs, out, score, lut, sc);
+        const LRow F{r0}, Cc{r0 + (kHbLdsCols + 1) * 64};
+        // a base case's (<= 2 x (kHbLdsCols + 1)) matrix reuses F and Cc, both dead by then
+        k = hb_leaf_solve(LSeq{q1}, LSeq{q2}, g1, g2, L.m, L.n, L.top != 0, F, Cc, F, out, score, lut, sc);
     } else {
-        const GRow F{Fg}, X{Fg + (L.n + 1)}, Cc{Fg + 2 * (L.n + 1)};
-        k = hb_leaf_solve(GSeq{g1}, GSeq{g2}, g1, g2, L.m, L.n, L.top != 0, F, X, Cc, Hs, out, score, lut, sc);
+        const GRow F{Fg}, Cc{Fg + 2 * (L.n + 1)};
+        k = hb_leaf_solve(GSeq{g1}, GSeq{g2}, g1, g2, L.m, L.n, L.top != 0, F, Cc, GRow{Hs}, out, score, lut, sc);
     }
     if (k) mark[key] = k;
 }

@@ -38,7 +38,7 @@
 
 namespace sa {
 
-constexpr int kMmLeafRows = 48;   // subproblems with <= this many Seq1 rows are leaves
+constexpr int kMmLeafRows = 24;   // subproblems with <= this many Seq1 rows are leaves (tuned, tools/ab_dc.sh)
 
 struct MmSweep {       // affine sweep over A (alen) x B (blen) -> C row at out, D row at out + blen + 1
     uint64_t a, b;     // index of A[0] / B[0] in seq1 / seq2 (rev: of the LAST element, read first)
@@ -357,7 +357,11 @@ __device__ int mm_leaf_solve(Seq S1, Seq S2, int alen, int blen, int32_t tb0, in
     return k;
 }
 
-constexpr int kMmLdsCols = 64;   // leaves with |Seq1|, |Seq2| <= this run with LDS rows + symbols
+// Leaves with |Seq1|, |Seq2| <= kMmLdsCols run with LDS rows (C, D, Cr, Dr) + symbols.
+#ifndef SA_MM_LDS_COLS
+#define SA_MM_LDS_COLS 32
+#endif
+constexpr int kMmLdsCols = SA_MM_LDS_COLS;
 
 // Leaves beyond the LDS size keep their four rows at 6 * key (4 (blen + 1) <= 6 (alen + blen));
 // forward ops at stage[key], op count at mark[key].
