@@ -163,6 +163,67 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
     if (lane == 0) out[0] = m * G;
 }
 
+// Packed sweeps for the deep levels (every sweep of the level has alen <= G rows): 64 / G sweeps
+// per wave, G lanes each, one row per lane, so a sweep takes n + G - 1 steps on G lanes instead
+// of n + 63 steps on a whole wave.  The row-above value and column symbol still arrive by DPP
+// wave_shr:1; a segment's first lane takes the top border (H[0][j] = j * gap) and its column
+// symbol (one ds_bpermute from the segment's chunk of Seq2, loaded a chunk ahead) instead.
+template <int G, bool LUT, bool ALLOW>
+__global__ __launch_bounds__(64) void hb_sweep_seg_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* split,
+                                                          const DcLevel* lvl, int32_t* rows, const uint32_t* lutbits,
+                                                          HbScore sc) {
+    constexpr int P = 64 / G;
+    __shared__ uint32_t s_lut[LUT ? 2048 : 1];
+    const int lane = threadIdx.x;
+    const uint32_t nsw = 2 * lvl->nsplit;
+    if (blockIdx.x * P >= nsw) return;   // grid sized from an upper bound (uniform exit)
+    if constexpr (LUT) {
+        for (int k = lane; k < 2048; k += 64) s_lut[k] = lutbits[k];
+        __syncthreads();
+    }
+    const uint32_t* lut = s_lut;
+    const int seg = lane / G, ls = lane % G;
+    const uint32_t swi = blockIdx.x * P + seg;
+    const bool active = swi < nsw;
+    HbSweep d{};
+    if (active) d = hb_sweep_of(split[swi / 2], swi & 1);
+    const int m = d.alen, n = d.blen, Gp = sc.gap;
+    int32_t* out = rows + d.out;
+    int steps = n + G - 1;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) steps = max(steps, __shfl_xor(steps, off));
+    auto symB = [&](int k) -> uint32_t { return d.rev ? s2[d.b - k] : s2[d.b + k]; };
+    const uint32_t a = ls < m ? (d.rev ? s1[d.a - ls] : s1[d.a + ls]) : 0u;
+    int32_t Hp = (ls + 1) * Gp;          // H[ls + 1][0]
+    int32_t prev_up = ls * Gp;           // H[ls][0]: the diagonal of column 1
+    int32_t hl = Hp;
+    uint32_t sym = 0;
+    const bool last_row = ls == m - 1;
+    uint32_t vs = ls < n ? symB(ls) : 0u, nvs;
+    for (int c0 = 0; c0 < steps; c0 += G) {
+        nvs = c0 + G + ls < n ? symB(c0 + G + ls) : 0u;
+        const int qn = min(G, steps - c0);
+        for (int q = 0; q < qn; ++q) {
+            const int s = c0 + q;
+            const uint32_t b0 = __shfl(vs, seg * G + q);
+            const int32_t up_d = __builtin_amdgcn_update_dpp(0, hl, 0x138, 0xf, 0xf, false);
+            const uint32_t sy_d = __builtin_amdgcn_update_dpp(0u, sym, 0x138, 0xf, 0xf, false);
+            const int32_t up_h = ls == 0 ? (s + 1) * Gp : up_d;
+            sym = ls == 0 ? b0 : sy_d;
+            const int j0 = s - ls;
+            if (j0 >= 0 && j0 < n && ls < m) {
+                const int32_t h = hb_cell_t<LUT, ALLOW>(prev_up, up_h, Hp, a, sym, lut, sc);
+                Hp = h;
+                prev_up = up_h;
+                hl = h;
+                if (last_row) out[j0 + 1] = h;   // row m of the sweep
+            }
+        }
+        vs = nvs;
+    }
+    if (active && ls == 0) out[0] = m * Gp;
+}
+
 // ---------------------------------------------------------------------------- split
 __global__ __launch_bounds__(64) void hb_split_kernel(const DcSub* split, const DcLevel* lvl, const int32_t* rows,
                                                       DcSub* next, sa_result* res) {
@@ -356,8 +417,31 @@ void launch_sweeps_t(int R, dim3 grid, const uint8_t* d1, const uint8_t* d2, con
     }
 }
 
-hipError_t launch_sweeps(int R, uint32_t count, const uint8_t* d1, const uint8_t* d2, const DcSub* split,
+template <bool LUT, bool ALLOW>
+void launch_seg_t(int G, uint32_t count, const uint8_t* d1, const uint8_t* d2, const DcSub* split, const DcLevel* lvl,
+                  int32_t* rows, const uint32_t* lut, const HbScore& sc, hipStream_t st) {
+    const dim3 block(64);
+    if (G == 16)
+        hipLaunchKernelGGL((hb_sweep_seg_kernel<16, LUT, ALLOW>), dim3((count + 3) / 4), block, 0, st, d1, d2, split,
+                           lvl, rows, lut, sc);
+    else
+        hipLaunchKernelGGL((hb_sweep_seg_kernel<32, LUT, ALLOW>), dim3((count + 1) / 2), block, 0, st, d1, d2, split,
+                           lvl, rows, lut, sc);
+}
+
+// R = 0: packed sweeps of G = 16 or 32 lanes (maxa <= G) instead of R rows per lane.
+hipError_t launch_sweeps(int R, int G, uint32_t count, const uint8_t* d1, const uint8_t* d2, const DcSub* split,
                          const DcLevel* lvl, int32_t* rows, const uint32_t* lut, const HbScore& sc, hipStream_t st) {
+    if (G) {
+        if (lut) {
+            if (sc.allow) launch_seg_t<true, true>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
+            else launch_seg_t<true, false>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
+        } else {
+            if (sc.allow) launch_seg_t<false, true>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
+            else launch_seg_t<false, false>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
+        }
+        return hipGetLastError();
+    }
     const dim3 grid(count);
     if (lut) {
         if (sc.allow) launch_sweeps_t<true, true>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
@@ -379,6 +463,8 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
                    sa_result* d_res, uint8_t* d_ops, std::string* err) {
     int leaf_rows = kHbLeafRows;   // tuning override: SEQALIB_HB_LEAF
     if (const char* lr = getenv("SEQALIB_HB_LEAF")) leaf_rows = std::max(2, atoi(lr));
+    const char* segenv = getenv("SEQALIB_DC_SEG");   // 0: whole-wave sweeps only (A/B, tests)
+    const bool seg_sweeps = !segenv || atoi(segenv) != 0;
     HbScore sc;
     sc.gap = scoring->gap;
     sc.match = scoring->match;
@@ -400,7 +486,8 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
         const int maxa = (maxm + 1) / 2;
         int R = 1;
         while (R < 32 && 64 * R < maxa) R *= 2;
-        SA_DC_HIP(launch_sweeps(R, 2 * splits, d1, d2, w.split.p, w.lvl.p + l, w.rows.p, d_lutbits, sc, st));
+        const int G = !seg_sweeps ? 0 : maxa <= 16 ? 16 : maxa <= 32 ? 32 : 0;
+        SA_DC_HIP(launch_sweeps(R, G, 2 * splits, d1, d2, w.split.p, w.lvl.p + l, w.rows.p, d_lutbits, sc, st));
         hipLaunchKernelGGL(hb_split_kernel, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p, w.next.p,
                            d_res);
         SA_DC_HIP(hipGetLastError());

@@ -203,6 +203,80 @@ __global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const u
     }
 }
 
+// Packed sweeps for the deep levels (every sweep has alen <= G rows): 64 / G sweeps per wave, G
+// lanes each, one row per lane (as hb_sweep_seg_kernel).  A segment's first lane takes the top
+// border (CC[j] = g + j h, DD[j] = CC[j] + g, :183-188) and its column symbol by ds_bpermute.
+template <int G, bool LUT, bool ALLOW>
+__global__ __launch_bounds__(64) void mm_sweep_seg_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* split,
+                                                          const DcLevel* lvl, int32_t* rows, const uint32_t* lutbits,
+                                                          MmScore sc) {
+    constexpr int P = 64 / G;
+    __shared__ uint32_t s_lut[LUT ? 2048 : 1];
+    const int lane = threadIdx.x;
+    const uint32_t nsw = 2 * lvl->nsplit;
+    if (blockIdx.x * P >= nsw) return;   // grid sized from an upper bound (uniform exit)
+    if constexpr (LUT) {
+        for (int k = lane; k < 2048; k += 64) s_lut[k] = lutbits[k];
+        __syncthreads();
+    }
+    const uint32_t* lut = s_lut;
+    const int seg = lane / G, ls = lane % G;
+    const uint32_t swi = blockIdx.x * P + seg;
+    const bool active = swi < nsw;
+    MmSweep d{};
+    if (active) d = mm_sweep_of(split[swi / 2], swi & 1);
+    const int m = d.alen, n = d.blen, g = sc.g, h = sc.h;
+    int32_t* outC = rows + d.out;
+    int32_t* outD = outC + n + 1;
+    int steps = n + G - 1;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) steps = max(steps, __shfl_xor(steps, off));
+    auto symB = [&](int k) -> uint32_t { return d.rev ? s2[d.b - k] : s2[d.b + k]; };
+    const uint32_t a = ls < m ? (d.rev ? s1[d.a - ls] : s1[d.a + ls]) : 0u;
+    int32_t Cp = d.t0 + h * (ls + 1);                 // C[i][0] = t0 + i h (:192-197)
+    int32_t Ep = Cp + g;                              // e = t + g (:198)
+    int32_t prev_up = ls == 0 ? 0 : d.t0 + h * ls;    // C[ls][0]; C[0][0] = 0 (:172)
+    int32_t cl = Cp, dl = 0;
+    uint32_t sym = 0;
+    const bool last_row = ls == m - 1;
+    uint32_t vs = ls < n ? symB(ls) : 0u, nvs;
+    for (int c0 = 0; c0 < steps; c0 += G) {
+        nvs = c0 + G + ls < n ? symB(c0 + G + ls) : 0u;
+        const int qn = min(G, steps - c0);
+        for (int q = 0; q < qn; ++q) {
+            const int s = c0 + q;
+            const uint32_t b0 = __shfl(vs, seg * G + q);
+            const int32_t c_d = __builtin_amdgcn_update_dpp(0, cl, 0x138, 0xf, 0xf, false);
+            const int32_t d_d = __builtin_amdgcn_update_dpp(0, dl, 0x138, 0xf, 0xf, false);
+            const uint32_t sy_d = __builtin_amdgcn_update_dpp(0u, sym, 0x138, 0xf, 0xf, false);
+            const int32_t bc = g + h * (s + 1);
+            const int32_t up_c = ls == 0 ? bc : c_d;
+            const int32_t up_d = ls == 0 ? bc + g : d_d;
+            sym = ls == 0 ? b0 : sy_d;
+            const int j0 = s - ls;
+            if (j0 >= 0 && j0 < n && ls < m) {
+                const int32_t e = max(Ep, Cp + g) + h;                  // :202
+                const int32_t dd = max(up_d, up_c + g) + h;             // :203
+                const int32_t c = max(max(dd, e), mm_diag_t<LUT, ALLOW>(prev_up, a, sym, lut, sc));
+                Cp = c;
+                Ep = e;
+                prev_up = up_c;
+                cl = c;
+                dl = dd;
+                if (last_row) {                                         // row m of the sweep
+                    outC[j0 + 1] = c;
+                    outD[j0 + 1] = dd;
+                }
+            }
+        }
+        vs = nvs;
+    }
+    if (active && ls == 0) {
+        outC[0] = d.t0 + h * m;
+        outD[0] = outC[0];                                              // DD[0] = CC[0] (:238)
+    }
+}
+
 // ---------------------------------------------------------------------------- split
 __global__ __launch_bounds__(64) void mm_split_kernel(const DcSub* split, const DcLevel* lvl, const int32_t* rows,
                                                       DcSub* next, sa_result* res, int32_t g) {
@@ -416,8 +490,31 @@ void launch_mm_sweeps_t(int R, dim3 grid, const uint8_t* d1, const uint8_t* d2, 
     }
 }
 
-hipError_t launch_mm_sweeps(int R, uint32_t count, const uint8_t* d1, const uint8_t* d2, const DcSub* split,
+template <bool LUT, bool ALLOW>
+void launch_mm_seg_t(int G, uint32_t count, const uint8_t* d1, const uint8_t* d2, const DcSub* split,
+                     const DcLevel* lvl, int32_t* rows, const uint32_t* lut, const MmScore& sc, hipStream_t st) {
+    const dim3 block(64);
+    if (G == 16)
+        hipLaunchKernelGGL((mm_sweep_seg_kernel<16, LUT, ALLOW>), dim3((count + 3) / 4), block, 0, st, d1, d2, split,
+                           lvl, rows, lut, sc);
+    else
+        hipLaunchKernelGGL((mm_sweep_seg_kernel<32, LUT, ALLOW>), dim3((count + 1) / 2), block, 0, st, d1, d2, split,
+                           lvl, rows, lut, sc);
+}
+
+// G = 16 / 32: packed sweeps (maxa <= G); G = 0: R rows per lane, one sweep per wave.
+hipError_t launch_mm_sweeps(int R, int G, uint32_t count, const uint8_t* d1, const uint8_t* d2, const DcSub* split,
                             const DcLevel* lvl, int32_t* rows, const uint32_t* lut, const MmScore& sc, hipStream_t st) {
+    if (G) {
+        if (lut) {
+            if (sc.allow) launch_mm_seg_t<true, true>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
+            else launch_mm_seg_t<true, false>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
+        } else {
+            if (sc.allow) launch_mm_seg_t<false, true>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
+            else launch_mm_seg_t<false, false>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
+        }
+        return hipGetLastError();
+    }
     const dim3 grid(count);
     if (lut) {
         if (sc.allow) launch_mm_sweeps_t<true, true>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
@@ -437,6 +534,8 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
                     sa_result* d_res, uint8_t* d_ops, std::string* err) {
     int leaf_rows = kMmLeafRows;   // tuning override: SEQALIB_MM_LEAF (the leaf stack bounds it)
     if (const char* lr = getenv("SEQALIB_MM_LEAF")) leaf_rows = std::min(4096, std::max(2, atoi(lr)));
+    const char* segenv = getenv("SEQALIB_DC_SEG");   // 0: whole-wave sweeps only (A/B, tests)
+    const bool seg_sweeps = !segenv || atoi(segenv) != 0;
     MmScore sc;
     sc.g = scoring->gap_open;
     sc.h = scoring->gap_extend;
@@ -460,7 +559,8 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
         const int maxa = (maxm + 1) / 2;
         int R = 1;
         while (R < 32 && 64 * R < maxa) R *= 2;
-        SA_DC_HIP(launch_mm_sweeps(R, 2 * splits, d1, d2, w.split.p, w.lvl.p + l, w.rows.p, d_lutbits, sc, st));
+        const int G = !seg_sweeps ? 0 : maxa <= 16 ? 16 : maxa <= 32 ? 32 : 0;
+        SA_DC_HIP(launch_mm_sweeps(R, G, 2 * splits, d1, d2, w.split.p, w.lvl.p + l, w.rows.p, d_lutbits, sc, st));
         hipLaunchKernelGGL(mm_split_kernel, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p, w.next.p,
                            d_res, sc.g);
         SA_DC_HIP(hipGetLastError());

@@ -123,6 +123,29 @@ def test_golden_large(engine):
     assert check_golden(engine, load_golden("large.jsonl")) == 10
 
 
+@pytest.mark.parametrize("algo", ["hb", "mm"])
+@pytest.mark.parametrize("leaf,seg", [(6, "1"), (24, "0"), (24, "1"), (100, "1")])
+def test_dc_level_loop_variants_vs_oracle(engine, monkeypatch, algo, leaf, seg):
+    """Device-resident level loop (sa_dc.hip) under other leaf thresholds and with the packed
+    16/32-lane sweeps on or off: more levels (leaf 6: packed sweeps of <= 16 rows, 3-row leaves),
+    fewer (leaf 100: leaves past the LDS tile, global scratch), ragged and empty pairs."""
+    monkeypatch.setenv("SEQALIB_HB_LEAF" if algo == "hb" else "SEQALIB_MM_LEAF", str(leaf))
+    monkeypatch.setenv("SEQALIB_DC_SEG", seg)
+    rng = np.random.default_rng(17 + leaf)
+    pairs = []
+    for k in range(60):
+        m = int(rng.integers(0, 700)) if k % 6 else int(rng.integers(0, 3))
+        n = int(rng.integers(0, 700)) if k % 7 else int(rng.integers(0, 3))
+        a = sa.synth_dna(90_000 + 2 * k, m)
+        b = sa.synth_mutate(a, k)[:n] if k % 2 else sa.synth_dna(90_001 + 2 * k, n)
+        pairs.append((a, b))
+    pairs.append((sa.synth_dna(13, 2000), sa.synth_dna(14, 150)))   # wide leaves / thin levels
+    if algo == "hb":
+        compare_with_oracle(engine, sa.SA_HIRSCHBERG, (-1, 2, -1), pairs)
+    else:
+        compare_with_oracle(engine, sa.SA_MYERS_MILLER, (-3, -1, 1, -1, True), pairs)
+
+
 def compare_with_oracle(engine, algo, args, pairs, match=None):
     lut = named_lut(match)
     res = engine.align(algo, sc_obj(args), pairs, lut)
