@@ -38,7 +38,7 @@
 
 namespace sa {
 
-constexpr int kHbLeafRows = 24;   // subproblems with <= this many Seq1 rows are leaves (tuned, tools/ab_dc.sh)
+constexpr int kHbLeafRows = 12;   // subproblems with <= this many Seq1 rows are leaves (tuned, tools/ab_dc.sh)
 
 struct HbSweep {       // NWScore over A (alen) x B (blen) -> rows[out .. out+blen]
     uint64_t a, b;     // index of A[0] / B[0] in seq1 / seq2 (rev: of the LAST element read first)
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
     if (lane == 0) out[0] = m * G;
 }
 
-// Packed sweeps for the deep levels (every sweep of the level has alen <= G rows): 64 / G sweeps
+// Packed sweeps for the deep levels (every sweep of the level has alen <= G = 8, 16 or 32 rows): 64 / G sweeps
 // per wave, G lanes each, one row per lane, so a sweep takes n + G - 1 steps on G lanes instead
 // of n + 63 steps on a whole wave.  The row-above value and column symbol still arrive by DPP
 // wave_shr:1; a segment's first lane takes the top border (H[0][j] = j * gap) and its column
@@ -421,7 +421,10 @@ template <bool LUT, bool ALLOW>
 void launch_seg_t(int G, uint32_t count, const uint8_t* d1, const uint8_t* d2, const DcSub* split, const DcLevel* lvl,
                   int32_t* rows, const uint32_t* lut, const HbScore& sc, hipStream_t st) {
     const dim3 block(64);
-    if (G == 16)
+    if (G == 8)
+        hipLaunchKernelGGL((hb_sweep_seg_kernel<8, LUT, ALLOW>), dim3((count + 7) / 8), block, 0, st, d1, d2, split,
+                           lvl, rows, lut, sc);
+    else if (G == 16)
         hipLaunchKernelGGL((hb_sweep_seg_kernel<16, LUT, ALLOW>), dim3((count + 3) / 4), block, 0, st, d1, d2, split,
                            lvl, rows, lut, sc);
     else
@@ -486,7 +489,7 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
         const int maxa = (maxm + 1) / 2;
         int R = 1;
         while (R < 32 && 64 * R < maxa) R *= 2;
-        const int G = !seg_sweeps ? 0 : maxa <= 16 ? 16 : maxa <= 32 ? 32 : 0;
+        const int G = !seg_sweeps ? 0 : maxa <= 8 ? 8 : maxa <= 16 ? 16 : maxa <= 32 ? 32 : 0;
         SA_DC_HIP(launch_sweeps(R, G, 2 * splits, d1, d2, w.split.p, w.lvl.p + l, w.rows.p, d_lutbits, sc, st));
         hipLaunchKernelGGL(hb_split_kernel, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p, w.next.p,
                            d_res);

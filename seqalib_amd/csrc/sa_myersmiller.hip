@@ -38,7 +38,7 @@
 
 namespace sa {
 
-constexpr int kMmLeafRows = 24;   // subproblems with <= this many Seq1 rows are leaves (tuned, tools/ab_dc.sh)
+constexpr int kMmLeafRows = 12;   // subproblems with <= this many Seq1 rows are leaves (tuned, tools/ab_dc.sh)
 
 struct MmSweep {       // affine sweep over A (alen) x B (blen) -> C row at out, D row at out + blen + 1
     uint64_t a, b;     // index of A[0] / B[0] in seq1 / seq2 (rev: of the LAST element, read first)
@@ -494,7 +494,10 @@ template <bool LUT, bool ALLOW>
 void launch_mm_seg_t(int G, uint32_t count, const uint8_t* d1, const uint8_t* d2, const DcSub* split,
                      const DcLevel* lvl, int32_t* rows, const uint32_t* lut, const MmScore& sc, hipStream_t st) {
     const dim3 block(64);
-    if (G == 16)
+    if (G == 8)
+        hipLaunchKernelGGL((mm_sweep_seg_kernel<8, LUT, ALLOW>), dim3((count + 7) / 8), block, 0, st, d1, d2, split,
+                           lvl, rows, lut, sc);
+    else if (G == 16)
         hipLaunchKernelGGL((mm_sweep_seg_kernel<16, LUT, ALLOW>), dim3((count + 3) / 4), block, 0, st, d1, d2, split,
                            lvl, rows, lut, sc);
     else
@@ -559,7 +562,7 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
         const int maxa = (maxm + 1) / 2;
         int R = 1;
         while (R < 32 && 64 * R < maxa) R *= 2;
-        const int G = !seg_sweeps ? 0 : maxa <= 16 ? 16 : maxa <= 32 ? 32 : 0;
+        const int G = !seg_sweeps ? 0 : maxa <= 8 ? 8 : maxa <= 16 ? 16 : maxa <= 32 ? 32 : 0;
         SA_DC_HIP(launch_mm_sweeps(R, G, 2 * splits, d1, d2, w.split.p, w.lvl.p + l, w.rows.p, d_lutbits, sc, st));
         hipLaunchKernelGGL(mm_split_kernel, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p, w.next.p,
                            d_res, sc.g);
