@@ -70,7 +70,8 @@ def test_golden_random(engine):
 
 def test_golden_hirschberg(engine):
     """HirschbergSA (SAHirschberg.h) vectors of the unmodified reference: device levels (pairs
-    taller than 64 rows), per-thread leaves, NW base cases, empty / length-1 edges."""
+    taller than 12 rows, packed and whole-wave sweeps), per-thread leaves, NW base cases, empty /
+    length-1 edges."""
     assert check_golden(engine, load_golden("hirschberg.jsonl")) > 800
 
 
@@ -93,7 +94,7 @@ def test_hirschberg_batch_vs_oracle(engine, args, match):
 
 def test_golden_myers_miller(engine):
     """MyersMillerSA (SAMyersMiller.h) vectors of the unmodified reference: device levels (pairs
-    taller than 48 rows), per-thread leaves, both midpoint types, M == 1 / N == 0 / M == 0 base
+    taller than 12 rows), per-thread leaves, both midpoint types, M == 1 / N == 0 / M == 0 base
     cases, empty edges."""
     assert check_golden(engine, load_golden("myersmiller.jsonl")) > 850
 

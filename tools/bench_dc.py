@@ -39,10 +39,7 @@ def main():
     run(); torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        t1 = time.perf_counter()
         run()
-        if os.environ.get("SEQALIB_MM_TIMING") or os.environ.get("SEQALIB_HB_TIMING"):
-            print(f"[bench] call {1e3 * (time.perf_counter() - t1):.2f} ms", file=sys.stderr)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
     r = np.frombuffer(res.cpu().numpy().tobytes(), dtype=sa.RESULT_DTYPE)
