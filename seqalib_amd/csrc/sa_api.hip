@@ -746,8 +746,8 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     hipStream_t st = c->stream;
     const bool dc = algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER;
     if (dc) {
-        // the divide-and-conquer drivers wait on the stream every level: upload from pinned
-        // staging so no pageable copy is in flight (see sa_dc.h)
+        // upload from pinned staging (a pageable copy inside a process that also runs PyTorch was
+        // measured to stall 10-25 ms per call)
         static thread_local HostBuf<uint8_t> stage;
         const uint64_t bo = 8ull * (npairs + 1);
         SA_HIP(c, stage.alloc(t1 + t2 + 2 * bo));
@@ -775,7 +775,12 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         std::string e;
         c->launches = 0;
         const auto run = algo == SA_HIRSCHBERG ? hirschberg_run : myersmiller_run;
-        if (run(sc, d1, do1, d2, do2, npairs, use_lut ? dbits : nullptr, st, dres, dops, &e))
+        DcBounds b;
+        b.t1 = t1;
+        b.t2 = t2;
+        b.max_m = max_m;
+        b.max_n = max_n;
+        if (run(sc, d1, do1, d2, do2, npairs, b, use_lut ? dbits : nullptr, st, dres, dops, &e))
             return fail(c, SA_ERR_HIP, (algo == SA_HIRSCHBERG ? "hirschberg: " : "myers-miller: ") + e);
         SA_HIP(c, hipMemcpyAsync(results, dres, sizeof(sa_result) * npairs, hipMemcpyDeviceToHost, st));
         SA_HIP(c, hipMemcpyAsync(ops, dops, ops_total, hipMemcpyDeviceToHost, st));
@@ -1038,7 +1043,12 @@ int sa_align_batch_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8
         std::string e;
         c->launches = 0;
         const auto run = algo == SA_HIRSCHBERG ? hirschberg_run : myersmiller_run;
-        if (run(sc, d1, o1, d2, o2, npairs, bits, st, d_res, d_ops, &e))
+        DcBounds b;   // the caller's bounds (pairs past them: SA_FLAG_BAD_SHAPE), no read of o1 / o2
+        b.t1 = (uint64_t)npairs * max_m;
+        b.t2 = (uint64_t)npairs * max_n;
+        b.max_m = max_m;
+        b.max_n = max_n;
+        if (run(sc, d1, o1, d2, o2, npairs, b, bits, st, d_res, d_ops, &e))
             return fail(c, SA_ERR_HIP, (algo == SA_HIRSCHBERG ? "hirschberg: " : "myers-miller: ") + e);
         return SA_OK;
     }

@@ -127,34 +127,22 @@ struct DcLevel {
 };
 
 // sa_dc.hip
-hipError_t dc_launch_init(const uint64_t* o1, const uint64_t* o2, uint32_t npairs, int32_t t0, DcSub* subs,
-                          hipStream_t st);
+struct DcBounds;
+hipError_t dc_launch_init(const uint64_t* o1, const uint64_t* o2, uint32_t npairs, int32_t t0, const DcBounds& b,
+                          DcSub* subs, sa_result* res, hipStream_t st);
 hipError_t dc_launch_classify(const DcSub* cur, uint32_t cap, uint32_t fixed, const DcLevel* prev, uint32_t mult,
                               int leaf_rows, int min_n, DcLevel* lvl, DcSub* split, DcSub* leaves, uint32_t* nleaf,
                               hipStream_t st);
 hipError_t dc_launch_assemble(const uint64_t* o1, const uint64_t* o2, uint32_t npairs, const int32_t* mark,
                               const uint8_t* stage, sa_result* res, uint8_t* ops, hipStream_t st);
 
-// Host-side sizes of a batch (one read of the device offsets): grid bounds of the level loop.
+// Host-side sizes of a batch: grid bounds of the level loop and the key range (keys are
+// absolute a0 + b0 < t1 + t2).  From the host offsets (host API), or from the device API's
+// max_m / max_n (t1 <= npairs * max_m): no read of the device offsets, no wait.
 struct DcBounds {
-    uint64_t t1 = 0, t2 = 0;   // total Seq1 / Seq2 symbols
-    int max_m = 0;             // longest Seq1
+    uint64_t t1 = 0, t2 = 0;   // Seq1 / Seq2 symbol totals (upper bounds)
+    uint32_t max_m = 0, max_n = 0;
 };
-
-inline hipError_t dc_bounds(const uint64_t* d_o1, const uint64_t* d_o2, uint32_t npairs, hipStream_t st, DcBounds* b) {
-    static thread_local HostBuf<uint64_t> o1, o2;
-    if (hipError_t e = o1.alloc(npairs + 1)) return e;
-    if (hipError_t e = o2.alloc(npairs + 1)) return e;
-    if (hipError_t e = hipMemcpyAsync(o1.data(), d_o1, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st)) return e;
-    if (hipError_t e = hipMemcpyAsync(o2.data(), d_o2, 8ull * (npairs + 1), hipMemcpyDeviceToHost, st)) return e;
-    if (hipError_t e = dc_sync(st)) return e;
-    b->max_m = 0;
-    for (uint32_t p = 0; p < npairs; ++p) b->max_m = std::max<int>(b->max_m, (int)(o1[p + 1] - o1[p]));
-    // key-addressed buffers are indexed by absolute a0 + b0
-    b->t1 = o1[npairs];
-    b->t2 = o2[npairs];
-    return hipSuccess;
-}
 
 // Device work buffers of one level loop (grow-only, per host thread).  Bounds: a split
 // subproblem has > leaf_rows rows and the subproblems of a level have disjoint Seq1 ranges, so
@@ -173,7 +161,7 @@ struct DcWork {
         max_splits = b.t1 / (uint64_t)(leaf_rows + 1) + 1;
         uint64_t cap = npairs, total = npairs;
         levels = 0;
-        for (int m = b.max_m; m > leaf_rows; m = (m + 1) / 2) {
+        for (int m = (int)b.max_m; m > leaf_rows; m = (m + 1) / 2) {
             cap = mult * std::min<uint64_t>(cap, max_splits);
             total += cap;
             ++levels;

@@ -20,8 +20,11 @@
 
 namespace sa {
 
+// A pair longer than the caller's bounds (device API: max_m / max_n), or any pair of a batch
+// whose key range passes key_cap, is not aligned: SA_FLAG_BAD_SHAPE, empty slot.
 __global__ __launch_bounds__(64) void dc_init_kernel(const uint64_t* o1, const uint64_t* o2, uint32_t npairs,
-                                                     int32_t t0, DcSub* subs) {
+                                                     int32_t t0, uint32_t max_m, uint32_t max_n, uint64_t key_cap,
+                                                     DcSub* subs, sa_result* res) {
     const uint32_t p = blockIdx.x * 64 + threadIdx.x;
     if (p >= npairs) return;
     DcSub s;
@@ -33,6 +36,10 @@ __global__ __launch_bounds__(64) void dc_init_kernel(const uint64_t* o1, const u
     s.te = t0;
     s.pair = p;
     s.top = 1;
+    if ((uint32_t)s.m > max_m || (uint32_t)s.n > max_n || o1[npairs] + o2[npairs] > key_cap) {
+        s.m = -1;
+        res[p].flags = SA_FLAG_BAD_SHAPE;
+    }
     subs[p] = s;
 }
 
@@ -69,6 +76,7 @@ __global__ __launch_bounds__(64) void dc_assemble_kernel(const uint64_t* o1, con
                                                          const uint8_t* stage, sa_result* res, uint8_t* ops) {
     const int lane = threadIdx.x;
     const uint32_t p = blockIdx.x;
+    if (res[p].flags & SA_FLAG_BAD_SHAPE) return;   // not aligned (dc_init_kernel)
     const uint64_t key0 = o1[p] + o2[p];
     const int32_t m = (int32_t)(o1[p + 1] - o1[p]), n = (int32_t)(o2[p + 1] - o2[p]);
     const int32_t len = m + n;
@@ -101,9 +109,10 @@ __global__ __launch_bounds__(64) void dc_assemble_kernel(const uint64_t* o1, con
     }
 }
 
-hipError_t dc_launch_init(const uint64_t* o1, const uint64_t* o2, uint32_t npairs, int32_t t0, DcSub* subs,
-                          hipStream_t st) {
-    hipLaunchKernelGGL(dc_init_kernel, dim3((npairs + 63) / 64), dim3(64), 0, st, o1, o2, npairs, t0, subs);
+hipError_t dc_launch_init(const uint64_t* o1, const uint64_t* o2, uint32_t npairs, int32_t t0, const DcBounds& b,
+                          DcSub* subs, sa_result* res, hipStream_t st) {
+    hipLaunchKernelGGL(dc_init_kernel, dim3((npairs + 63) / 64), dim3(64), 0, st, o1, o2, npairs, t0, b.max_m, b.max_n,
+                       b.t1 + b.t2, subs, res);
     return hipGetLastError();
 }
 

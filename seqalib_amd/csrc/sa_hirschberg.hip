@@ -459,11 +459,11 @@ hipError_t launch_sweeps(int R, int G, uint32_t count, const uint8_t* d1, const 
 }  // namespace
 
 // Host driver: inputs, results and the traceback-order op streams (pair p's at
-// off1[p] + off2[p] + p) all on the device; enqueued on st without waiting for it, apart from
-// one read of the offsets (grid bounds).
+// off1[p] + off2[p] + p) all on the device; enqueued on st without waiting for it (grid
+// bounds from b).
 int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
-                   const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
-                   sa_result* d_res, uint8_t* d_ops, std::string* err) {
+                   const uint64_t* d_o2, uint32_t npairs, const DcBounds& b, const uint32_t* d_lutbits,
+                   hipStream_t st, sa_result* d_res, uint8_t* d_ops, std::string* err) {
     int leaf_rows = kHbLeafRows;   // tuning override: SEQALIB_HB_LEAF
     if (const char* lr = getenv("SEQALIB_HB_LEAF")) leaf_rows = std::max(2, atoi(lr));
     const char* segenv = getenv("SEQALIB_DC_SEG");   // 0: whole-wave sweeps only (A/B, tests)
@@ -473,14 +473,12 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
     sc.match = scoring->match;
     sc.allow = scoring->allow_mismatch != 0;
     sc.mismatch = sc.allow ? scoring->mismatch : INT_MIN;
-    DcBounds b;
-    SA_DC_HIP(dc_bounds(d_o1, d_o2, npairs, st, &b));
     static thread_local DcWork w;
     SA_DC_HIP(w.prepare(b, npairs, leaf_rows, 2, 2, 6, st));
     SA_DC_HIP(hipMemsetAsync(d_res, 0, sizeof(sa_result) * npairs, st));
-    SA_DC_HIP(dc_launch_init(d_o1, d_o2, npairs, 0, w.cur.p, st));
+    SA_DC_HIP(dc_launch_init(d_o1, d_o2, npairs, 0, b, w.cur.p, d_res, st));
     uint32_t cap = npairs;     // upper bound on this level's subproblems
-    int maxm = b.max_m;        // upper bound on their Seq1 length
+    int maxm = (int)b.max_m;        // upper bound on their Seq1 length
     for (int l = 0;; ++l) {
         SA_DC_HIP(dc_launch_classify(w.cur.p, cap, npairs, l ? w.lvl.p + l - 1 : nullptr, 2, leaf_rows, 2,
                                      w.lvl.p + l, w.split.p, w.leaves.p, w.nleaf(), st));

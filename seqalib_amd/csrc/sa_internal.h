@@ -220,13 +220,14 @@ hipError_t launch_endcell(int algo, int R, const EndcellParams& p, hipStream_t s
 #include <vector>
 namespace sa {
 // HirschbergSA / MyersMillerSA drivers (sa_hirschberg.hip, sa_myersmiller.hip): device inputs,
-// device outputs (results, op streams at off1[p] + off2[p] + p), enqueued on st; the only host
-// wait is one read of the offsets.  Return 0, or -1 with *err set.
+// device outputs (results, op streams at off1[p] + off2[p] + p), enqueued on st with no host
+// wait (grid bounds from b).  Return 0, or -1 with *err set.
+struct DcBounds;   // sa_dc.h: symbol totals and longest sides (upper bounds)
 int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
-                   const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
-                   sa_result* d_res, uint8_t* d_ops, std::string* err);
+                   const uint64_t* d_o2, uint32_t npairs, const DcBounds& b, const uint32_t* d_lutbits,
+                   hipStream_t st, sa_result* d_res, uint8_t* d_ops, std::string* err);
 int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
-                    const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
-                    sa_result* d_res, uint8_t* d_ops, std::string* err);
+                    const uint64_t* d_o2, uint32_t npairs, const DcBounds& b, const uint32_t* d_lutbits,
+                    hipStream_t st, sa_result* d_res, uint8_t* d_ops, std::string* err);
 
 }  // namespace sa

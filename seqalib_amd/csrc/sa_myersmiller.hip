@@ -533,8 +533,8 @@ hipError_t launch_mm_sweeps(int R, int G, uint32_t count, const uint8_t* d1, con
 
 // Host driver: same contract as hirschberg_run (device results and op streams, enqueued on st).
 int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
-                    const uint64_t* d_o2, uint32_t npairs, const uint32_t* d_lutbits, hipStream_t st,
-                    sa_result* d_res, uint8_t* d_ops, std::string* err) {
+                    const uint64_t* d_o2, uint32_t npairs, const DcBounds& b, const uint32_t* d_lutbits,
+                    hipStream_t st, sa_result* d_res, uint8_t* d_ops, std::string* err) {
     int leaf_rows = kMmLeafRows;   // tuning override: SEQALIB_MM_LEAF (the leaf stack bounds it)
     if (const char* lr = getenv("SEQALIB_MM_LEAF")) leaf_rows = std::min(4096, std::max(2, atoi(lr)));
     const char* segenv = getenv("SEQALIB_DC_SEG");   // 0: whole-wave sweeps only (A/B, tests)
@@ -545,15 +545,13 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
     sc.match = scoring->match;
     sc.allow = scoring->allow_mismatch != 0;
     sc.mismatch = sc.allow ? scoring->mismatch : INT_MIN;
-    DcBounds b;
-    SA_DC_HIP(dc_bounds(d_o1, d_o2, npairs, st, &b));
     static thread_local DcWork w;
     SA_DC_HIP(w.prepare(b, npairs, leaf_rows, 3, 4, 6, st));
     SA_DC_HIP(hipMemsetAsync(d_res, 0, sizeof(sa_result) * npairs, st));
     // getAlignment: buildResultRec(.., GapOpen, GapOpen) (:417)
-    SA_DC_HIP(dc_launch_init(d_o1, d_o2, npairs, sc.g, w.cur.p, st));
+    SA_DC_HIP(dc_launch_init(d_o1, d_o2, npairs, sc.g, b, w.cur.p, d_res, st));
     uint32_t cap = npairs;
-    int maxm = b.max_m;
+    int maxm = (int)b.max_m;
     for (int l = 0;; ++l) {
         SA_DC_HIP(dc_launch_classify(w.cur.p, cap, npairs, l ? w.lvl.p + l - 1 : nullptr, 3, leaf_rows, 1,
                                      w.lvl.p + l, w.split.p, w.leaves.p, w.nleaf(), st));

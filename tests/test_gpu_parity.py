@@ -523,6 +523,47 @@ def test_device_api_and_timings(engine):
     assert n >= 1 and fill_ms > 0
 
 
+@pytest.mark.parametrize("algo", ["hb", "mm"])
+def test_dc_device_api_bounds(engine, algo):
+    """sa_align_batch_device for the linear-space aligners: no host wait inside the call (grid
+    bounds from max_m / max_n); two back-to-back calls on one stream equal the host API; a pair
+    longer than max_m is flagged SA_FLAG_BAD_SHAPE and the others are unaffected."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda", 0)
+    t = lambda x: torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)
+    A = sa.SA_HIRSCHBERG if algo == "hb" else sa.SA_MYERS_MILLER
+    sc = sa.ScoringSystem(*((-1, 2, -1) if algo == "hb" else (-3, -1, 1, -1, True)))
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for seed, lens in ((5, (300, 40, 0, 257)), (6, (120, 512, 33, 7))):
+        pairs = [(sa.synth_dna(seed * 100 + k, m), sa.synth_dna(seed * 100 + 50 + k, (m * 7) % 300 + 1))
+                 for k, m in enumerate(lens)]
+        s1 = np.frombuffer(b"".join(a for a, _ in pairs), dtype=np.uint8)
+        s2 = np.frombuffer(b"".join(b for _, b in pairs), dtype=np.uint8)
+        o1 = np.cumsum([0] + [len(a) for a, _ in pairs]).astype(np.uint64)
+        o2 = np.cumsum([0] + [len(b) for _, b in pairs]).astype(np.uint64)
+        d = [t(s1.copy()), t(o1), t(s2.copy()), t(o2)]
+        d_res = torch.zeros(len(pairs) * 32, dtype=torch.uint8, device=dev)
+        d_ops = torch.zeros(len(s1) + len(s2) + len(pairs), dtype=torch.uint8, device=dev)
+        max_m = 300   # the second batch's 512-row pair passes it
+        engine.align_device(A, sc, d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), len(pairs),
+                            max_m, 300, d_res.data_ptr(), d_ops.data_ptr(), stream)
+        outs.append((pairs, o1, o2, d, d_res, d_ops))
+    torch.cuda.synchronize()
+    for pairs, o1, o2, d, d_res, d_ops in outs:
+        res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=sa.RESULT_DTYPE)
+        ops = d_ops.cpu().numpy()
+        ref = engine.align(A, sc, pairs)
+        for p, ((a, b), r) in enumerate(zip(pairs, ref)):
+            if len(a) > 300:
+                assert res["flags"][p] & sa.SA_FLAG_BAD_SHAPE
+                continue
+            off = int(o1[p] + o2[p]) + p
+            got = (int(res["score"][p]), int(res["end_i"][p]), int(res["end_j"][p]),
+                   ops[off:off + int(res["nops"][p])].tobytes())
+            assert got == (r.score, r.end_i, r.end_j, r.ops), (algo, p)
+
+
 @pytest.mark.parametrize("algo", [0, 1, 2, 3])
 def test_pipelined_device_api_matches_serial(engine, algo):
     """sa_set_pipeline: consecutive device calls overlap (traceback of call k with the fill of

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 echo "[dc] tests $(date +%T)"
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "hirschberg or myers" --timeout 120 --timeout-method thread > gpurun_out/dc_tests.log 2>&1 || { echo dc tests failed; tail -30 gpurun_out/dc_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "hirschberg or myers or dc_" --timeout 120 --timeout-method thread > gpurun_out/dc_tests.log 2>&1 || { echo dc tests failed; tail -30 gpurun_out/dc_tests.log; exit 1; }
 tail -2 gpurun_out/dc_tests.log
 : > gpurun_out/dc.jsonl
 for algo in hb mm; do
