@@ -354,12 +354,12 @@ __device__ int hb_leaf_solve(Seq S1, Seq S2, const uint8_t* g1, const uint8_t* g
 }
 
 // Leaves with |Seq1|, |Seq2| <= kHbLdsCols run with LDS rows + symbols: 2 rows + 2 symbol
-// strings per thread, 21 KiB per 64-thread block at 32 (at 64 with a third row it was 58 KiB:
-// 2 blocks per CU).  Leaves have <= kHbLeafRows rows; on DNA their columns rarely pass 32;
-// wider leaves take the global-scratch path.  Measured (tools/ab_dc.sh, 10,000 x 1024^2):
-// 64 cols / 48-row leaves 21.3 ms, 48 / 48 17.1 ms, 48 / 24 13.0 ms, 32 / 24 12.6 ms.
+// strings per thread, 15.8 KiB per 64-thread block at 24 (at 64 with a third row it was 58 KiB:
+// 2 blocks per CU).  Leaves have <= kHbLeafRows rows; wider ones take the global-scratch path.
+// Measured (tools/ab_dc.sh, 10,000 x 1024^2; profiles/ab_dc_r02*.txt): 64 cols / 48-row leaves
+// 21.3 ms, 48 / 48 17.1, 32 / 24 12.6, then with packed sweeps 32 / 12 9.2, 24 / 12 9.0 ms.
 #ifndef SA_HB_LDS_COLS
-#define SA_HB_LDS_COLS 32
+#define SA_HB_LDS_COLS 24
 #endif
 constexpr int kHbLdsCols = SA_HB_LDS_COLS;
 

@@ -431,9 +431,11 @@ __device__ int mm_leaf_solve(Seq S1, Seq S2, int alen, int blen, int32_t tb0, in
     return k;
 }
 
-// Leaves with |Seq1|, |Seq2| <= kMmLdsCols run with LDS rows (C, D, Cr, Dr) + symbols.
+// Leaves with |Seq1|, |Seq2| <= kMmLdsCols run with LDS rows (C, D, Cr, Dr) + symbols: 19 KiB
+// per 64-thread block at 16 (8 blocks per CU).  Measured with 12-row leaves (tools/ab_dc.sh,
+// 10,000 x 1024^2): 32 cols 14.1 ms, 24 13.9, 16 13.6 ms; wider leaves use global scratch.
 #ifndef SA_MM_LDS_COLS
-#define SA_MM_LDS_COLS 32
+#define SA_MM_LDS_COLS 16
 #endif
 constexpr int kMmLdsCols = SA_MM_LDS_COLS;
 
