@@ -468,6 +468,8 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
     if (const char* lr = getenv("SEQALIB_HB_LEAF")) leaf_rows = std::max(2, atoi(lr));
     const char* segenv = getenv("SEQALIB_DC_SEG");   // 0: whole-wave sweeps only (A/B, tests)
     const bool seg_sweeps = !segenv || atoi(segenv) != 0;
+    int rmax = 32;                                   // tuning: SEQALIB_DC_RMAX caps the sweep's R
+    if (const char* r = getenv("SEQALIB_DC_RMAX")) rmax = std::min(32, std::max(1, atoi(r)));
     HbScore sc;
     sc.gap = scoring->gap;
     sc.match = scoring->match;
@@ -486,7 +488,7 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
         const uint32_t splits = std::min<uint64_t>(cap, w.max_splits);
         const int maxa = (maxm + 1) / 2;
         int R = 1;
-        while (R < 32 && 64 * R < maxa) R *= 2;
+        while (R < rmax && 64 * R < maxa) R *= 2;   // bands of 64 R rows
         const int G = !seg_sweeps ? 0 : maxa <= 8 ? 8 : maxa <= 16 ? 16 : maxa <= 32 ? 32 : 0;
         SA_DC_HIP(launch_sweeps(R, G, 2 * splits, d1, d2, w.split.p, w.lvl.p + l, w.rows.p, d_lutbits, sc, st));
         hipLaunchKernelGGL(hb_split_kernel, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p, w.next.p,
