@@ -223,8 +223,6 @@ void align(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
     }
     tm.lap("symbol coding");
     if (coder.overflow) {   // more than 256 distinct symbols: the generic-Ty (bitmap) path
-        if (algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER)
-            throw std::runtime_error("seqalib: more than 256 distinct symbols: not supported by the linear-space aligners");
         align_bits<Ty>(algo, sc, fn, has_fn, pairs, res, ops, ops_off);
         return;
     }
@@ -237,7 +235,7 @@ void align(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
     ops_off.resize(n);
     for (uint32_t p = 0; p < n; ++p) ops_off[p] = o1[p] + o2[p] + p;
     tm.lap("match table + buffers");
-    if (sa_multi* mg = (algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER) ? nullptr : multi_context()) {
+    if (sa_multi* mg = multi_context()) {
         const int rc = sa_multi_align_batch(mg, algo, &sc, s1.data(), o1.data(), s2.data(), o2.data(), n,
                                             has_fn ? lut.data() : nullptr, res.data(), ops.data(), cap);
         if (rc != SA_OK)

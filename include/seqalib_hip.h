@@ -59,8 +59,12 @@ enum {
                                  (only reachable with scorings whose gap terms are >= 0) */
     SA_FLAG_BAD_SHAPE = 2,    /* device API: pair longer than the max_m/max_n it was given */
     SA_FLAG_SIZE_HACK = 4,    /* LocalGotoh pair replaced by NW (SALocalGotoh.h:484-488)   */
-    SA_FLAG_TIMEOUT = 8       /* multi-workgroup plan: a band's bounded wait for the band
-                                 above it expired; the pair's result is invalid           */
+    SA_FLAG_TIMEOUT = 8,      /* internal, never returned: a multi-workgroup (SPLIT) band's
+                                 bounded wait for the band above it expired; the same call
+                                 re-runs such pairs on the single-workgroup plan         */
+    SA_FLAG_RECOVERED = 16    /* informational: a consistency guard of the band-parallel
+                                 traceback fired and the pair was re-walked serially; the
+                                 result is exact                                          */
 };
 
 /* ScoringSystem (include/SequenceAlignment.h:82-131).  Which fields are meaningful depends on

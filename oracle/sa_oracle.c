@@ -288,23 +288,41 @@ static int align_gotoh(int local, const oracle_scoring* sc, int m, int n, const 
 }
 
 /* ------------------------------------------------------- Hirschberg (SAHirschberg.h) */
+/* match(Seq1[i], Seq2[j]) by position: bytes through the LUT / equality, or (generic-Ty form)
+ * the caller's m x n match matrix mt -- what the reference's MatchFnTy returns per cell
+ * (SAHirschberg.h:74, :90; SAMyersMiller.h:24-37 caches the same per recursion). */
+typedef struct {
+    const uint8_t *s1, *s2, *lut;
+    const uint8_t* mt;       /* NULL: byte symbols */
+    int n;                   /* row length of mt */
+} pos_match;
+
+static inline int match_at(const pos_match* p, int i, int j) {
+    if (p->mt) return p->mt[(size_t)i * (size_t)p->n + (size_t)j] != 0;
+    return p->lut ? p->lut[p->s1[i] * 256 + p->s2[j]] != 0 : p->s1[i] == p->s2[j];
+}
+
+/* the match cache of the sub-block [a0, a0+m) x [b0, b0+n) */
+static uint8_t* match_block(const pos_match* p, int a0, int m, int b0, int n) {
+    uint8_t* mt = (uint8_t*)malloc((size_t)m * (size_t)n + 1);
+    if (!mt) return NULL;
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < n; ++j) mt[(size_t)i * n + j] = (uint8_t)match_at(p, a0 + i, b0 + j);
+    return mt;
+}
+
 typedef struct {
     const oracle_scoring* sc;
-    const uint8_t *s1, *s2, *lut;
+    pos_match pm;
     int32_t *F, *A, *C;      /* FinalScore, ScoreAux, ScoreCache (n+1 each), :174-178 */
     uint8_t* fwd;            /* forward-order op list of the whole alignment */
     int nf;
     int err;
 } hb_ctx;
 
-static inline int hb_match(const hb_ctx* h, uint8_t a, uint8_t b) {
-    return h->lut ? h->lut[a * 256 + b] != 0 : a == b;
-}
-
-/* NWScore (:11-100): last row of NW over a[0..alen) x b[0..blen), each read forwards or (rev)
- * backwards, into h->F[0..blen]. */
-static void hb_nwscore(hb_ctx* h, const uint8_t* a, int alen, int arev, const uint8_t* b, int blen,
-                       int brev) {
+/* NWScore (:11-100): last row of NW over Seq1[a0..a0+alen) x Seq2[b0..b0+blen), each read
+ * forwards or (rev) backwards, into h->F[0..blen]. */
+static void hb_nwscore(hb_ctx* h, int a0, int alen, int arev, int b0, int blen, int brev) {
     const int32_t G = h->sc->gap, MA = h->sc->match;
     const int allow = h->sc->allow_mismatch;
     const int32_t MI = allow ? h->sc->mismatch : INT_MIN;
@@ -312,11 +330,11 @@ static void hb_nwscore(hb_ctx* h, const uint8_t* a, int alen, int arev, const ui
     F[0] = 0;
     for (int j = 1; j <= blen; ++j) F[j] = F[j - 1] + G;
     for (int i = 1; i <= alen; ++i) {
-        const uint8_t ai = arev ? a[alen - i] : a[i - 1];
+        const int ai = arev ? a0 + alen - i : a0 + i - 1;
         A[0] = F[0] + G;
         for (int j = 1; j <= blen; ++j) {
-            const uint8_t bj = brev ? b[blen - j] : b[j - 1];
-            const int v = hb_match(h, ai, bj);
+            const int bj = brev ? b0 + blen - j : b0 + j - 1;
+            const int v = match_at(&h->pm, ai, bj);
             const int32_t sub = allow ? F[j - 1] + (v ? MA : MI) : (v ? F[j - 1] + MA : MI);
             A[j] = max3(sub, F[j] + G, A[j - 1] + G);
         }
@@ -336,19 +354,19 @@ static void hb_rec(hb_ctx* h, int a0, int alen, int b0, int blen) {
         for (int k = 0; k < alen; ++k) hb_put(h, 'U');   /* Entry(Char, Blank) */
     } else if (alen == 1 || blen == 1) {
         /* NeedlemanWunschSA::getAlignment on the two views, spliced at the end (:119-126) */
-        uint8_t* mt = match_cache(h->s1 + a0, alen, h->s2 + b0, blen, h->lut);
+        uint8_t* mt = match_block(&h->pm, a0, alen, b0, blen);
         uint8_t* tb = (uint8_t*)malloc((size_t)(alen + blen) + 1);
         if (!mt || !tb) { free(mt); free(tb); h->err = -2; return; }
         opbuf ob = {tb, alen + blen + 1, 0, 0};
         oracle_result r;
-        if (align_nw(h->sc, h->s1 + a0, alen, h->s2 + b0, blen, mt, &r, &ob)) h->err = -2;
+        if (align_nw(h->sc, NULL, alen, NULL, blen, mt, &r, &ob)) h->err = -2;
         for (int k = ob.n - 1; k >= 0; --k) hb_put(h, tb[k]);   /* traceback order -> forward */
         free(mt); free(tb);
     } else {
         const int mid = alen / 2;
-        hb_nwscore(h, h->s1 + a0, mid, 0, h->s2 + b0, blen, 0);
+        hb_nwscore(h, a0, mid, 0, b0, blen, 0);
         memcpy(h->C, h->F, sizeof(int32_t) * (size_t)(blen + 1));          /* swap into ScoreCache */
-        hb_nwscore(h, h->s1 + a0 + mid, alen - mid, 1, h->s2 + b0, blen, 1);
+        hb_nwscore(h, a0 + mid, alen - mid, 1, b0, blen, 1);
         int mid2 = 0;
         int32_t best = INT_MIN;
         for (int i = 0; i < blen; ++i) {                                  /* :138-149, i < size */
@@ -360,18 +378,18 @@ static void hb_rec(hb_ctx* h, int a0, int alen, int b0, int blen) {
     }
 }
 
-static int align_hirschberg(const oracle_scoring* sc, const uint8_t* s1, int m, const uint8_t* s2,
-                            int n, const uint8_t* lut, oracle_result* res, opbuf* ob) {
+static int align_hirschberg(const oracle_scoring* sc, const pos_match* pm, int m, int n, oracle_result* res,
+                            opbuf* ob) {
     hb_ctx h;
     memset(&h, 0, sizeof(h));
-    h.sc = sc; h.s1 = s1; h.s2 = s2; h.lut = lut;
+    h.sc = sc; h.pm = *pm;
     h.F = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n + 1) * 3);
     h.fwd = (uint8_t*)malloc((size_t)(m + n) + 1);
     if (!h.F || !h.fwd) { free(h.F); free(h.fwd); return -2; }
     h.A = h.F + (n + 1);
     h.C = h.A + (n + 1);
     int32_t* base = h.F;
-    hb_nwscore(&h, s1, m, 0, s2, n, 0);                 /* score: NW H[m][n] */
+    hb_nwscore(&h, 0, m, 0, 0, n, 0);                   /* score: NW H[m][n] */
     res->score = h.F[n];
     hb_rec(&h, 0, m, 0, n);
     for (int k = h.nf - 1; k >= 0; --k) put(ob, h.fwd[k]);   /* back to traceback order */
@@ -385,7 +403,7 @@ static int align_hirschberg(const oracle_scoring* sc, const uint8_t* s1, int m, 
 /* ----------------------------------------------------- Myers–Miller (SAMyersMiller.h) */
 typedef struct {
     const oracle_scoring* sc;
-    const uint8_t *s1, *s2, *lut;
+    pos_match pm;
     int32_t *C, *D, *Cr, *Dr;   /* CC, DD (:167-168) and RR, SS (:242-243), n+1 each */
     uint8_t* fwd;               /* forward-order op list of the whole alignment */
     int nf;
@@ -393,11 +411,10 @@ typedef struct {
     int32_t score;              /* the top call's optimum (see align_myers_miller) */
 } mm_ctx;
 
-/* The forward sweep of buildResultRec (:172-238) over a[0..alen) x b[0..blen), each read
- * forwards or (rev) backwards, with row-0 gap open t0 (tb).  Read backwards with t0 = te it is
- * the reverse sweep (:247-313) in reversed coordinates: RR[j] = C[blen-j], SS[j] = D[blen-j]. */
-static void mm_sweep(mm_ctx* h, const uint8_t* a, int alen, int rev, const uint8_t* b, int blen,
-                     int32_t t0, int32_t* C, int32_t* D) {
+/* The forward sweep of buildResultRec (:172-238) over Seq1[a0..a0+alen) x Seq2[b0..b0+blen), each
+ * read forwards or (rev) backwards, with row-0 gap open t0 (tb).  Read backwards with t0 = te it
+ * is the reverse sweep (:247-313) in reversed coordinates: RR[j] = C[blen-j], SS[j] = D[blen-j]. */
+static void mm_sweep(mm_ctx* h, int a0, int alen, int rev, int b0, int blen, int32_t t0, int32_t* C, int32_t* D) {
     const int32_t g = h->sc->gap_open, x = h->sc->gap_extend, MA = h->sc->match;
     const int allow = h->sc->allow_mismatch;
     const int32_t MI = allow ? h->sc->mismatch : INT_MIN;
@@ -406,17 +423,17 @@ static void mm_sweep(mm_ctx* h, const uint8_t* a, int alen, int rev, const uint8
     for (int j = 1; j <= blen; ++j) { t += x; C[j] = t; D[j] = t + g; }   /* :183-188 */
     t = t0;
     for (int i = 1; i <= alen; ++i) {
-        const uint8_t ai = rev ? a[alen - i] : a[i - 1];
+        const int ai = rev ? a0 + alen - i : a0 + i - 1;
         int32_t s = C[0];
         t += x;
         int32_t c = t;
         C[0] = c;
         int32_t e = t + g;
         for (int j = 1; j <= blen; ++j) {
-            const uint8_t bj = rev ? b[blen - j] : b[j - 1];
+            const int bj = rev ? b0 + blen - j : b0 + j - 1;
             e = (e > c + g ? e : c + g) + x;
             D[j] = (D[j] > C[j] + g ? D[j] : C[j] + g) + x;
-            const int v = h->lut ? h->lut[ai * 256 + bj] != 0 : ai == bj;
+            const int v = match_at(&h->pm, ai, bj);
             const int32_t diag = (allow || v) ? s + (v ? MA : MI) : INT_MIN;   /* :218-232 */
             c = max3(D[j], e, diag);
             s = C[j];
@@ -443,13 +460,11 @@ static void mm_rec(mm_ctx* h, int a0, int M, int b0, int N, int32_t tb, int32_t 
         for (int k = 0; k < N; ++k) mm_put(h, 'L');
         if (top) h->score = g + x * N;
     } else if (M == 1) {                                              /* :75-160 */
-        const uint8_t a = h->s1[a0];
         const int32_t base = (tb > te ? tb : te) + x + (g + x * N);
         int32_t best = INT_MIN;
         int index = 0;
         for (int j = 1; j <= N; ++j) {
-            const uint8_t bj = h->s2[b0 + j - 1];
-            const int v = h->lut ? h->lut[a * 256 + bj] != 0 : a == bj;
+            const int v = match_at(&h->pm, a0, b0 + j - 1);
             int32_t t = base;
             if (allow || v) {
                 const int32_t via = g + x * (j - 1) + (v ? MA : MI) + g + x * (N - j);
@@ -459,8 +474,7 @@ static void mm_rec(mm_ctx* h, int a0, int M, int b0, int N, int32_t tb, int32_t 
         }
         for (int j = 1; j <= N; ++j) {
             if (j == index) {
-                const uint8_t bj = h->s2[b0 + j - 1];
-                const int v = h->lut ? h->lut[a * 256 + bj] != 0 : a == bj;
+                const int v = match_at(&h->pm, a0, b0 + j - 1);
                 if (!allow && !v) {          /* :141-147: (a, Blank) then (Blank, b) */
                     mm_put(h, 'U');
                     mm_put(h, 'L');
@@ -474,8 +488,8 @@ static void mm_rec(mm_ctx* h, int a0, int M, int b0, int N, int32_t tb, int32_t 
         if (top) h->score = best;
     } else {
         const int mid = M / 2;
-        mm_sweep(h, h->s1 + a0, mid, 0, h->s2 + b0, N, tb, h->C, h->D);
-        mm_sweep(h, h->s1 + a0 + mid, M - mid, 1, h->s2 + b0, N, te, h->Cr, h->Dr);
+        mm_sweep(h, a0, mid, 0, b0, N, tb, h->C, h->D);
+        mm_sweep(h, a0 + mid, M - mid, 1, b0, N, te, h->Cr, h->Dr);
         int index = 0, type2 = 0;
         int32_t best = INT_MIN;
         for (int j = 0; j <= N; ++j) {                                /* :320-340 */
@@ -500,11 +514,11 @@ static void mm_rec(mm_ctx* h, int a0, int M, int b0, int N, int32_t tb, int32_t 
 /* MyersMillerSA::getAlignment (:412-420): buildResultRec(.., M, N, GapOpen, GapOpen).  The
  * reference exposes no score; res->score is the optimum the top call computes (its midpoint
  * maximum :320-340, the M == 1 maximum :81-124, or the boundary value of an empty side). */
-static int align_myers_miller(const oracle_scoring* sc, const uint8_t* s1, int m, const uint8_t* s2,
-                              int n, const uint8_t* lut, oracle_result* res, opbuf* ob) {
+static int align_myers_miller(const oracle_scoring* sc, const pos_match* pm, int m, int n, oracle_result* res,
+                              opbuf* ob) {
     mm_ctx h;
     memset(&h, 0, sizeof(h));
-    h.sc = sc; h.s1 = s1; h.s2 = s2; h.lut = lut;
+    h.sc = sc; h.pm = *pm;
     int32_t* base = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n + 1) * 4);
     h.fwd = (uint8_t*)malloc((size_t)(m + n) + 1);
     if (!base || !h.fwd) { free(base); free(h.fwd); return -2; }
@@ -532,8 +546,9 @@ int oracle_align(int algo, const oracle_scoring* sc, const uint8_t* s1, int m, c
     if (algo == OR_HIRSCHBERG || algo == OR_MYERS_MILLER) {
         opbuf hb = {ops, ops_cap, 0, 0};
         memset(res, 0, sizeof(*res));
-        int rc = algo == OR_HIRSCHBERG ? align_hirschberg(sc, s1, m, s2, n, lut, res, &hb)
-                                       : align_myers_miller(sc, s1, m, s2, n, lut, res, &hb);
+        const pos_match pm = {s1, s2, lut, NULL, n};
+        int rc = algo == OR_HIRSCHBERG ? align_hirschberg(sc, &pm, m, n, res, &hb)
+                                       : align_myers_miller(sc, &pm, m, n, res, &hb);
         res->nops = hb.n;
         if (rc) return rc;
         if (hb.overflow) return -1;
@@ -729,11 +744,20 @@ int oracle_sw_score_batch(const oracle_scoring* sc, const uint8_t* s1cat, const 
 /* Generic-Ty form (test infrastructure): the same aligners driven by a caller-supplied m x n
  * match matrix (mt[i*n + j] != 0 iff match(Seq1[i], Seq2[j]), the reference's cacheAllMatches)
  * instead of byte symbols; results and op stream only.  SW, NW, LocalGotoh (size hack included),
- * GlobalGotoh. */
+ * GlobalGotoh, HirschbergSA and MyersMillerSA. */
 int oracle_align_matrix(int algo, const oracle_scoring* sc, int m, int n, const uint8_t* mt_in,
                         oracle_result* res, uint8_t* ops, int ops_cap) {
     if (algo == OR_LOCAL_GOTOH && lg_size_hack(m, n)) algo = OR_NW;
-    if (algo == OR_HIRSCHBERG || algo == OR_MYERS_MILLER) return -3;
+    if (algo == OR_HIRSCHBERG || algo == OR_MYERS_MILLER) {
+        opbuf hb = {ops, ops_cap, 0, 0};
+        memset(res, 0, sizeof(*res));
+        const pos_match pm = {NULL, NULL, NULL, mt_in, n};
+        int rc = algo == OR_HIRSCHBERG ? align_hirschberg(sc, &pm, m, n, res, &hb)
+                                       : align_myers_miller(sc, &pm, m, n, res, &hb);
+        res->nops = hb.n;
+        if (rc) return rc;
+        return hb.overflow ? -1 : 0;
+    }
     uint8_t* mt = (uint8_t*)malloc((size_t)m * (size_t)n + 1);
     if (!mt) return -2;
     for (size_t k = 0; k < (size_t)m * (size_t)n; ++k) mt[k] = mt_in[k] != 0;

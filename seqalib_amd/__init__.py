@@ -323,7 +323,8 @@ def match_bitmaps(pairs: Sequence[Tuple[Sequence, Sequence]], match: Optional[Ca
     tuples of ints, objects, ...): length offsets and per-pair m x n match bitmaps, i.e. the
     reference's cacheAllMatches (SASmithWaterman.h:20-45) packed to bits.  match(a, b) is the
     MatchFnTy; None means equality (the reference's nullptr match fn).  Hashable symbols are coded
-    first, so the predicate runs once per distinct (a, b) pair of a pair's sequences."""
+    first (by type and value, so 1, 1.0 and True stay distinct), and the predicate runs once per
+    distinct (a, b) pair of a pair's sequences."""
     n_p = len(pairs)
     off1 = np.zeros(n_p + 1, dtype=np.uint64)
     off2 = np.zeros(n_p + 1, dtype=np.uint64)
@@ -337,10 +338,10 @@ def match_bitmaps(pairs: Sequence[Tuple[Sequence, Sequence]], match: Optional[Ca
         if m and n:
             try:
                 ua = {}
-                c1 = np.fromiter((ua.setdefault(x, len(ua)) for x in a), dtype=np.int64, count=m)
+                c1 = np.fromiter((ua.setdefault((type(x), x), len(ua)) for x in a), dtype=np.int64, count=m)
                 ub = {}
-                c2 = np.fromiter((ub.setdefault(x, len(ub)) for x in b), dtype=np.int64, count=n)
-                va, vb = list(ua), list(ub)
+                c2 = np.fromiter((ub.setdefault((type(x), x), len(ub)) for x in b), dtype=np.int64, count=n)
+                va, vb = [k[1] for k in ua], [k[1] for k in ub]
                 if match is None:
                     tab = np.array([[x == y for y in vb] for x in va], dtype=bool)
                 else:

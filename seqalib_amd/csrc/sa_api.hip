@@ -39,7 +39,6 @@ struct sa_ctx {
     int nvar = 0, var_kernel[2] = {0, 0}, var_R[2] = {0, 0}, var_W[2] = {0, 0};
     uint32_t* h_sel = nullptr;
     hipEvent_t ev_sel = nullptr;
-    bool no_split = false;   // host API re-run after a SPLIT wait expired
     // cross-call pipeline of the device API (sa_set_pipeline): fills on s_fill, tracebacks on
     // s_tb, two workspace slots; ev_slot[k] = traceback of the last call that used slot k done
     int pipeline = 0;
@@ -49,6 +48,14 @@ struct sa_ctx {
     // SPLIT plans (few pairs, one workgroup per band): [ticket, pad to 256 B][granules][partials]
     uint8_t* split = nullptr;
     uint64_t split_bytes = 0;
+    // HirschbergSA / MyersMillerSA level-loop buffers and the host API's pinned upload staging
+    sa::DcWork dc;
+    sa::HostBuf<uint8_t> stage;
+    // Calls on one context are ordered: every call's stream waits for ev_last, the end of the
+    // last un-pipelined call (whatever stream it ran on), since they share the workspace, the
+    // I/O cache and the DC buffers.
+    hipEvent_t ev_last = nullptr;
+    bool ev_last_set = false;
 };
 
 namespace {
@@ -70,6 +77,26 @@ int hip_fail(sa_ctx* c, hipError_t e, const char* what) {
         hipError_t e_ = (call);                           \
         if (e_ != hipSuccess) return hip_fail(c, e_, #call); \
     } while (0)
+
+// Order a call on stream st after the context's last call, and mark the end of this one.
+int order_after_last(sa_ctx* c, hipStream_t st) {
+    if (c->ev_last_set) SA_HIP(c, hipStreamWaitEvent(st, c->ev_last, 0));
+    return SA_OK;
+}
+int mark_last(sa_ctx* c, hipStream_t st) {
+    if (!c->ev_last) SA_HIP(c, hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming));
+    SA_HIP(c, hipEventRecord(c->ev_last, st));
+    c->ev_last_set = true;
+    return SA_OK;
+}
+// Before a context buffer is freed: every stream that may still use it has finished.
+int drain(sa_ctx* c) {
+    SA_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->s_fill) SA_HIP(c, hipStreamSynchronize(c->s_fill));
+    if (c->s_tb) SA_HIP(c, hipStreamSynchronize(c->s_tb));
+    if (c->ev_last_set) SA_HIP(c, hipEventSynchronize(c->ev_last));
+    return SA_OK;
+}
 
 // ------------------------------------------------------------------------------- planning
 struct Plan {
@@ -232,9 +259,7 @@ int tb_seg_mode() {
 int ensure_ws(sa_ctx* c, uint64_t need) {
     if (c->ws_bytes >= need) return SA_OK;
     if (c->ws) {
-        SA_HIP(c, hipStreamSynchronize(c->stream));
-        if (c->s_fill) SA_HIP(c, hipStreamSynchronize(c->s_fill));
-        if (c->s_tb) SA_HIP(c, hipStreamSynchronize(c->s_tb));
+        if (int rc = drain(c)) return rc;
         (void)hipFree(c->ws);
         c->ws = nullptr;
         c->ws_bytes = 0;
@@ -245,6 +270,24 @@ int ensure_ws(sa_ctx* c, uint64_t need) {
         return fail(c, SA_ERR_NOMEM, "hipMalloc workspace of " + std::to_string(need) + " bytes failed");
     }
     c->ws_bytes = need;
+    return SA_OK;
+}
+
+// The I/O cache of the host API (device copies of the caller's buffers; the device API keeps the
+// LUT bits in its tail): grow-only.
+int ensure_io(sa_ctx* c, uint64_t need) {
+    if (c->io_bytes >= need) return SA_OK;
+    if (c->io) {
+        if (int rc = drain(c)) return rc;
+        (void)hipFree(c->io);
+        c->io = nullptr;
+        c->io_bytes = 0;
+    }
+    if (hipMalloc(&c->io, need) != hipSuccess) {
+        c->io = nullptr;
+        return fail(c, SA_ERR_NOMEM, "hipMalloc of I/O buffers (" + std::to_string(need) + " bytes) failed");
+    }
+    c->io_bytes = need;
     return SA_OK;
 }
 
@@ -297,9 +340,11 @@ struct T16Mode {
     int32_t delta = 0;                // NW / GlobalGotoh offset
     int32_t retry_above = INT_MAX;    // SW / LocalGotoh: per-pair retry threshold
     int32_t sent = -10000;            // T16 affine: encoded Ix / Iy border
+    int32_t mismatch = 0;             // the mismatch score the T16 variant runs with (see t16_mode)
 };
 T16Mode t16_mode_affine(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
     T16Mode t;
+    t.mismatch = sc->mismatch;
     const int64_t MA = sc->match, MI = sc->mismatch, GO = sc->gap_open, GE = sc->gap_extend, GOE = GO + GE;
     if (MA < -16 || MA > 15 || MI < -16 || MI > 15 || MI > MA) return t;   // 8s + 6 in int8
     if (GE >= 0 || GO > 0 || GE < -512 || GO < -2048) return t;
@@ -337,9 +382,28 @@ T16Mode t16_mode_affine(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t
     t.sent = (int32_t)sent;
     return t;
 }
-T16Mode t16_mode(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
+// !AllowMismatch.  The reference's diagonal term of a mismatch is INT_MIN (SASmithWaterman.h:
+// 119-131, SANeedlemanWunsch.h:88-92, SALocalGotoh.h:144-170, SAGlobalGotoh.h), so it never
+// wins a max and its traceback never takes a mismatched diagonal (max(INT_MIN, 0) = 0 equals a
+// cell only where the zero test stops the walk anyway).  A finite mismatch score MI' loses just
+// as surely when MI' < 2 * Gap (linear) / 2 * (GapOpen + GapExtend) (affine): every cell has
+// H[i-1][j] >= H[i-1][j-1] + Gap (its left candidate; borders included), so the up candidate is
+// >= Hd + 2 * Gap > Hd + MI'; affine: M[i-1][j] >= Iy[i-1][j] >= M[i-1][j-1] + GOE, so
+// Ix >= Md + 2 * GOE > Md + MI'.  Strictly smaller, so no tie either: the matrices, the end cell
+// and every traceback decision are the reference's, and T16 runs the allow-mismatch kernel with
+// MI' = 2 * Gap - 1 (2 * GOE - 1), the largest such score (narrowest score range).
+T16Mode t16_mode(int algo, const sa_scoring* sc0, uint32_t max_m, uint32_t max_n) {
+    sa_scoring eff = *sc0;
+    if (!sc0->allow_mismatch) {
+        if (algo != SA_SW && algo != SA_NW && algo != SA_LOCAL_GOTOH && algo != SA_GLOBAL_GOTOH) return T16Mode{};
+        const int64_t mi = is_affine(algo) ? 2 * ((int64_t)sc0->gap_open + sc0->gap_extend) - 1 : 2 * (int64_t)sc0->gap - 1;
+        if (mi < INT_MIN / 4) return T16Mode{};
+        eff.mismatch = (int32_t)mi;
+        eff.allow_mismatch = 1;
+    }
+    const sa_scoring* sc = &eff;
     T16Mode t;
-    if (!sc->allow_mismatch) return t;
+    t.mismatch = sc->mismatch;
     if (algo == SA_LOCAL_GOTOH || algo == SA_GLOBAL_GOTOH) return t16_mode_affine(algo, sc, max_m, max_n);
     if (algo != SA_SW && algo != SA_NW) return t;
     const int64_t MA = sc->match, MI = sc->mismatch, G = sc->gap;
@@ -387,6 +451,31 @@ T16Mode t16_candidate(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t m
     return t;
 }
 
+// The kernel variants a call enqueues: T16 (when the scoring and shapes admit it; the device
+// picks it or the int32 one by the batch alphabet) and int32, plus -- when a variant uses the
+// SPLIT plan -- the int32 single-workgroup FALLBACK, whose launches re-run, inside the same call,
+// only the pairs whose SPLIT band wait expired (SA_FLAG_TIMEOUT), so no API returns one.  All
+// share one record stride (the int32 variant re-runs single pairs of a T16 batch, kFlagRetry,
+// while the T16 traceback still reads their neighbours).  Returns the number of variants;
+// vars[nv] is the fallback when *has_fb.
+int build_variants(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t16, Variant (&vars)[3],
+                   bool* has_fb) {
+    int nv = 0;
+    if (t16) vars[nv++] = make_variant(algo, max_m, max_n, npairs, true, true);
+    vars[nv++] = make_variant(algo, max_m, max_n, npairs, false, true);
+    *has_fb = false;
+    for (int k = 0; k < nv; ++k) *has_fb = *has_fb || vars[k].pl.split;
+    if (*has_fb) vars[nv] = make_variant(algo, max_m, max_n, npairs, false, false);
+    const int all = nv + (*has_fb ? 1 : 0);
+    uint64_t dir_stride = 0;
+    for (int k = 0; k < all; ++k) dir_stride = std::max(dir_stride, vars[k].pl.g.dir_slot);
+    for (int k = 0; k < all; ++k) {
+        vars[k].slot_bytes += dir_stride - vars[k].pl.g.dir_slot;
+        vars[k].pl.g.dir_slot = dir_stride;
+    }
+    return nv;
+}
+
 // Enqueue fill + traceback for pairs [0, npairs) whose inputs are on the device.  Nothing here
 // waits on the host: when the scoring and shapes admit the T16 kernel, the batch alphabet is
 // scanned on the device and BOTH variants (T16 and int32) are enqueued, each launch guarded by
@@ -419,33 +508,27 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     const int slot = pipe ? (int)(c->pipe_k & 1) : 0;
     uint32_t* aux = c->aux + kAuxWords * slot;
     if (pipe && c->ev_slot[slot]) SA_HIP(c, hipStreamWaitEvent(stream, c->ev_slot[slot], 0));   // slot free
-    Variant vars[2];
-    int nv = 0;
     const uint32_t* sel = nullptr;
     if (t16) {
         SA_HIP(c, launch_alphabet_scan(d1, o1, d2, o2, npairs, aux, stream));
-        SA_HIP(c, launch_decide_t16(d_lutbits, sc->match, sc->mismatch, is_affine(algo) ? 1 : 0, aux, stream));
+        SA_HIP(c, launch_decide_t16(d_lutbits, sc->match, tm.mismatch, is_affine(algo) ? 1 : 0, aux, stream));
         SA_HIP(c, hipMemcpyAsync(c->h_sel, aux + kAuxSel, 4, hipMemcpyDeviceToHost, stream));
         SA_HIP(c, hipEventRecord(c->ev_sel, stream));
         sel = aux + kAuxSel;
-        vars[nv++] = make_variant(algo, max_m, max_n, npairs, true, !c->no_split);
     }
-    vars[nv++] = make_variant(algo, max_m, max_n, npairs, false, !c->no_split);
+    Variant vars[3];
+    bool has_fb = false;
+    const int nv = build_variants(algo, max_m, max_n, npairs, t16, vars, &has_fb);
+    if (const char* e = getenv("SEQALIB_SPLIT_FALLBACK")) has_fb = has_fb && e[0] != '0';   // tests only
     c->nvar = nv;
-    // With both variants enqueued, the int32 one may re-run single pairs of a T16 batch
-    // (kFlagRetry) while the T16 traceback still reads its neighbours: one record stride for both.
-    uint64_t dir_stride = 0;
-    for (int k = 0; k < nv; ++k) dir_stride = std::max(dir_stride, vars[k].pl.g.dir_slot);
-    for (int k = 0; k < nv; ++k) {
-        vars[k].slot_bytes += dir_stride - vars[k].pl.g.dir_slot;
-        vars[k].pl.g.dir_slot = dir_stride;
-    }
     uint64_t slot_bytes = 0, sp_bands = 0;
     bool any_split = false;
-    for (int k = 0; k < nv; ++k) {
-        c->var_kernel[k] = vars[k].kernel;
-        c->var_R[k] = vars[k].pl.R;
-        c->var_W[k] = vars[k].pl.split ? 0 : vars[k].pl.W;   // 0: SPLIT plan (one single-wave workgroup per band)
+    for (int k = 0; k < nv + (has_fb ? 1 : 0); ++k) {
+        if (k < nv) {
+            c->var_kernel[k] = vars[k].kernel;
+            c->var_R[k] = vars[k].pl.R;
+            c->var_W[k] = vars[k].pl.split ? 0 : vars[k].pl.W;   // 0: SPLIT plan (one single-wave workgroup per band)
+        }
         slot_bytes = std::max(slot_bytes, vars[k].slot_bytes);
         if (vars[k].pl.split) {
             any_split = true;
@@ -471,6 +554,13 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     const uint64_t sp_vblk = (256 + sp_gran * 8 + 255) & ~(uint64_t)255;
     const uint64_t sp_part = (uint64_t)nv * sp_vblk;
     const int seg_mode = any_split && tb_wave((uint32_t)per_launch) ? tb_seg_mode() : 0;
+    // tests only: SEQALIB_SPLIT_WAIT_TICKS shortens the SPLIT bands' bounded wait (forces timeouts
+    // and the fallback); SEQALIB_SEG_INJECT=1 overwrites the segmented traceback's exit records
+    // between its two kernels (forces its consistency guards and the serial re-walk)
+    uint64_t wait_ticks = kSplitWaitTicksDefault;
+    if (const char* e = getenv("SEQALIB_SPLIT_WAIT_TICKS")) wait_ticks = strtoull(e, nullptr, 10);
+    const char* inj = getenv("SEQALIB_SEG_INJECT");
+    const bool seg_inject = inj && inj[0] == '1';
     const bool seg_on = seg_mode != 0 && per_launch * sp_bands <= (seg_mode == 2 ? 16384 : kSegMaxBands);
     const uint64_t seg_rs = (uint64_t)aff2 * ((uint64_t)max_n + 1) + 1;
     const uint64_t sp_seg = (sp_part + per_launch * sp_bands * 16 + 255) & ~(uint64_t)255;
@@ -478,9 +568,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     const uint64_t sp_need = any_split ? sp_slot * (pipe ? 2 : 1) : 0;
     if (any_split && c->split_bytes < sp_need) {
         if (c->split) {
-            SA_HIP(c, hipStreamSynchronize(c->stream));
-            if (c->s_fill) SA_HIP(c, hipStreamSynchronize(c->s_fill));
-            if (c->s_tb) SA_HIP(c, hipStreamSynchronize(c->s_tb));
+            if (int rc = drain(c)) return rc;
             (void)hipFree(c->split);
             c->split = nullptr;
             c->split_bytes = 0;
@@ -521,48 +609,58 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         if (pipe && c->launches > 0) SA_HIP(c, hipStreamWaitEvent(sf, c->events[3 * c->launches - 1], 0));
         SA_HIP(c, hipEventRecord(ev[0], sf));
         const uint64_t hand_x_off = any_split ? (uint64_t)cnt * sp_bands * std::max<uint32_t>(max_n, 1) : 0;
-        FillParams fps[2];
-        for (int k = 0; k < nv; ++k) {
+        // fill parameters of variant k (k == nv: the SPLIT fallback)
+        FillParams fps[3];
+        auto make_fp = [&](int k) {
             const Variant& v = vars[k];
             const Plan& pl = v.pl;
             // each SPLIT variant (the int32 one re-runs flagged pairs) has its own tickets and
             // hand-off granules
             uint8_t* const vblk = pl.split ? spbase + (uint64_t)k * sp_vblk : nullptr;
-            if (pl.split) SA_HIP(c, hipMemsetAsync(vblk, 0, 256 + hand_x_off * 8 * aff2, sf));
-            uint8_t* dirs = wbase;
             int32_t* rowbuf = reinterpret_cast<int32_t*>(wbase + per_launch * pl.g.dir_slot);
             uint32_t* snap_h = reinterpret_cast<uint32_t*>(rowbuf + per_launch * pl.rowbuf_elems);
             int32_t* snap_p = reinterpret_cast<int32_t*>(snap_h + per_launch * v.snap_h_slot);
-            int32_t* snap_m = snap_p + per_launch * v.snap_p_slot;
             FillParams& fp = fps[k];
             fp = FillParams{};
             fp.seq1 = d1; fp.off1 = o1; fp.seq2 = d2; fp.off2 = o2;
             fp.lutbits = lut ? d_lutbits : nullptr;
             fp.mbits = d_mbits; fp.mbits_off = d_mbits_off;
-            fp.dirs = dirs; fp.dir_slot = pl.g.dir_slot; fp.band_stride = pl.g.band_stride;
+            fp.dirs = wbase; fp.dir_slot = pl.g.dir_slot; fp.band_stride = pl.g.band_stride;
             fp.rowbuf = rowbuf; fp.rowbuf_slot = pl.rowbuf_elems;
             fp.res = d_res;
             fp.pair_base = (uint32_t)base;
             fp.max_m = max_m; fp.max_n = max_n;
-            fp.gap = sc->gap; fp.match = sc->match; fp.mismatch = allow ? sc->mismatch : INT_MIN;
+            // the T16 variant runs !AllowMismatch as allow-mismatch with tm.mismatch (t16_mode)
+            fp.gap = sc->gap; fp.match = sc->match;
+            fp.mismatch = v.t16 ? tm.mismatch : allow ? sc->mismatch : INT_MIN;
             fp.gap_open = sc->gap_open; fp.gap_extend = sc->gap_extend;
             fp.waves = pl.W;
             fp.count = cnt;
             fp.stage_seq2 = max_n <= kMaxStagedSeq2 ? 1 : 0;
             fp.prof = aux + kAuxProf;
-            fp.sel = sel; fp.sel_want = v.t16 ? 1u : 0u;
-            fp.redo = (nv == 2 && !v.t16) ? 1 : 0;
+            const bool fb = k == nv;
+            fp.sel = fb ? nullptr : sel; fp.sel_want = v.t16 ? 1u : 0u;
+            fp.redo = (!fb && nv == 2 && !v.t16) ? 1 : 0;
+            fp.rerun = fb ? 1 : 0;
             fp.t16_delta = v.t16 ? tm.delta : 0;
             fp.retry_above = v.t16 ? tm.retry_above : INT_MAX;
             fp.t16_sent = v.t16 ? tm.sent : -10000;
-            fp.snap_h = snap_h; fp.snap_p = snap_p; fp.snap_m = snap_m;
+            fp.snap_h = snap_h; fp.snap_p = snap_p; fp.snap_m = snap_p + per_launch * v.snap_p_slot;
             fp.snap_h_slot = v.snap_h_slot; fp.snap_p_slot = v.snap_p_slot; fp.snap_nch = v.snap_nch;
             fp.split_bands = (uint32_t)sp_bands;
             fp.ticket = pl.split ? reinterpret_cast<uint32_t*>(vblk) : nullptr;
             fp.hand = pl.split ? reinterpret_cast<unsigned long long*>(vblk + 256) : nullptr;
             fp.hand_x_off = pl.split ? hand_x_off : 0;
             fp.part = pl.split ? reinterpret_cast<int32_t*>(spbase + sp_part) : nullptr;
-            const FillVariant fv = {pl.R, lut, allow, keyed, v.t16, v.cmax, pl.split, bits};
+            fp.wait_ticks = wait_ticks;
+            return FillVariant{pl.R, lut, allow || v.t16, keyed, v.t16, v.cmax, pl.split, bits};
+        };
+        for (int k = 0; k < nv; ++k) {
+            const Variant& v = vars[k];
+            const Plan& pl = v.pl;
+            const FillVariant fv = make_fp(k);
+            const FillParams& fp = fps[k];
+            if (pl.split) SA_HIP(c, hipMemsetAsync(fp.ticket, 0, 256 + hand_x_off * 8 * aff2, sf));
             hipError_t e = v.x2 ? launch_fill_sw_x2(pl.R, fp, cnt, sf)
                                 : launch_fill(algo, fv, fp, pl.split ? (uint32_t)(cnt * sp_bands) : cnt, sf);
             if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
@@ -582,7 +680,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 EndcellParams ep{};
                 ep.seq1 = d1; ep.off1 = o1; ep.seq2 = d2; ep.off2 = o2;
                 ep.prof = fp.prof; ep.sel = sel; ep.sel_want = fp.sel_want;
-                ep.snap_h = snap_h; ep.snap_p = snap_p; ep.snap_m = snap_m;
+                ep.snap_h = fp.snap_h; ep.snap_p = fp.snap_p; ep.snap_m = fp.snap_m;
                 ep.snap_h_slot = v.snap_h_slot; ep.snap_p_slot = v.snap_p_slot; ep.snap_nch = v.snap_nch;
                 if (pl.split) {
                     ep.rowbuf = reinterpret_cast<const int32_t*>(fp.hand);
@@ -590,7 +688,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                     ep.rowbuf_stride = 2;
                     ep.rowbuf_x_off = 2 * hand_x_off;
                 } else {
-                    ep.rowbuf = rowbuf; ep.rowbuf_slot = pl.rowbuf_elems; ep.rowbuf_stride = 1;
+                    ep.rowbuf = fp.rowbuf; ep.rowbuf_slot = pl.rowbuf_elems; ep.rowbuf_stride = 1;
                     ep.rowbuf_x_off = pl.rowbuf_elems / 2;
                 }
                 ep.max_n = max_n;
@@ -604,7 +702,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         }
         SA_HIP(c, hipEventRecord(ev[1], sf));
         if (pipe) SA_HIP(c, hipStreamWaitEvent(stb, ev[1], 0));
-        for (int k = 0; k < nv; ++k) {
+        auto make_tp = [&](int k) {
             const Variant& v = vars[k];
             TbParams tp{};
             tp.seq1 = d1; tp.off1 = o1; tp.seq2 = d2; tp.off2 = o2;
@@ -616,9 +714,15 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             tp.max_m = max_m; tp.max_n = max_n;
             tp.gap = fps[k].gap; tp.match = fps[k].match; tp.mismatch = fps[k].mismatch;
             tp.gap_open = fps[k].gap_open; tp.gap_extend = fps[k].gap_extend;
-            tp.allow = allow ? 1 : 0;
+            tp.allow = (allow || v.t16) ? 1 : 0;
             tp.tagged = v.x2 ? 2 : (v.t16 ? 1 : 0);
-            tp.sel = sel; tp.sel_want = fps[k].sel_want;
+            tp.sel = fps[k].sel; tp.sel_want = fps[k].sel_want;
+            tp.rerun = fps[k].rerun;
+            return tp;
+        };
+        for (int k = 0; k < nv; ++k) {
+            const Variant& v = vars[k];
+            TbParams tp = make_tp(k);
             if (seg_on && v.pl.split && tb_wave(cnt)) {
                 tp.seg_mode = seg_mode;
                 tp.hand = fps[k].hand;
@@ -628,7 +732,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 tp.seg_rec = reinterpret_cast<int4*>(spbase + sp_seg);
                 tp.seg_fin = tp.seg_rec + per_launch * sp_bands * seg_rs;
                 SA_HIP(c, hipMemsetAsync(tp.seg_fin, 0xff, (uint64_t)cnt * 16, stb));
-                hipError_t e = launch_traceback_seg(algo, v.pl.R, lut, tp, stb);
+                hipError_t e = launch_traceback_seg(algo, v.pl.R, lut, tp, stb, seg_inject);
                 if (e != hipSuccess) return hip_fail(c, e, "segmented traceback kernel launch");
                 if (const char* dump = getenv("SEQALIB_SEG_DUMP")) {   // debugging aid: exit records
                     const uint64_t nrec = (uint64_t)cnt * sp_bands * seg_rs;
@@ -647,6 +751,18 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             hipError_t e = tb_wave(cnt) ? launch_traceback_wave(algo, v.pl.R, lut, tp, stb)
                                         : launch_traceback(algo, v.pl.R, lut, tp, stb);
             if (e != hipSuccess) return hip_fail(c, e, "traceback kernel launch");
+        }
+        if (has_fb) {
+            // SPLIT fallback, after every traceback of this launch (it rewrites the records of the
+            // pairs it re-runs): fill + traceback of exactly the pairs flagged SA_FLAG_TIMEOUT,
+            // launches that return at once when there is none
+            const FillVariant fv = make_fp(nv);
+            hipError_t e = launch_fill(algo, fv, fps[nv], cnt, stb);
+            if (e != hipSuccess) return hip_fail(c, e, "fallback fill kernel launch");
+            const TbParams tp = make_tp(nv);
+            e = tb_wave(cnt) ? launch_traceback_wave(algo, vars[nv].pl.R, lut, tp, stb)
+                             : launch_traceback(algo, vars[nv].pl.R, lut, tp, stb);
+            if (e != hipSuccess) return hip_fail(c, e, "fallback traceback kernel launch");
         }
         SA_HIP(c, hipEventRecord(ev[2], stb));
         c->launches++;
@@ -729,11 +845,7 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     const uint64_t b_res = al(sizeof(sa_result) * (uint64_t)std::max<uint32_t>(npairs, 1));
     const uint64_t b_ops = al(ops_total + 1), b_lut = al(65536), b_bits = al(8192);
     const uint64_t io_need = b_s1 + b_s2 + 2 * b_o + b_res + b_ops + b_lut + b_bits;
-    if (c->io_bytes < io_need) {
-        if (c->io) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->io); c->io = nullptr; c->io_bytes = 0; }
-        if (hipMalloc(&c->io, io_need) != hipSuccess) { c->io = nullptr; return fail(c, SA_ERR_NOMEM, "hipMalloc of I/O buffers failed"); }
-        c->io_bytes = io_need;
-    }
+    if (int rc = ensure_io(c, io_need)) return rc;
     uint8_t* p = c->io;
     uint8_t* d1 = p; p += b_s1;
     uint8_t* d2 = p; p += b_s2;
@@ -748,10 +860,9 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     if (dc) {
         // upload from pinned staging (a pageable copy inside a process that also runs PyTorch was
         // measured to stall 10-25 ms per call)
-        static thread_local HostBuf<uint8_t> stage;
         const uint64_t bo = 8ull * (npairs + 1);
-        SA_HIP(c, stage.alloc(t1 + t2 + 2 * bo));
-        uint8_t* q = stage.data();
+        SA_HIP(c, c->stage.alloc(t1 + t2 + 2 * bo));
+        uint8_t* q = c->stage.data();
         memcpy(q, seq1, t1);
         memcpy(q + t1, seq2, t2);
         memcpy(q + t1 + t2, off1, bo);
@@ -780,7 +891,8 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         b.t2 = t2;
         b.max_m = max_m;
         b.max_n = max_n;
-        if (run(sc, d1, do1, d2, do2, npairs, b, use_lut ? dbits : nullptr, st, dres, dops, &e))
+        const DcInputs in{d1, do1, d2, do2, npairs, use_lut ? dbits : nullptr, DcBits{}};
+        if (run(c->dc, c->ev_last_set ? c->ev_last : nullptr, sc, in, b, st, dres, dops, &e))
             return fail(c, SA_ERR_HIP, (algo == SA_HIRSCHBERG ? "hirschberg: " : "myers-miller: ") + e);
         SA_HIP(c, hipMemcpyAsync(results, dres, sizeof(sa_result) * npairs, hipMemcpyDeviceToHost, st));
         SA_HIP(c, hipMemcpyAsync(ops, dops, ops_total, hipMemcpyDeviceToHost, st));
@@ -795,21 +907,6 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         SA_HIP(c, hipMemcpyAsync(ops, dops, ops_total, hipMemcpyDeviceToHost, st));
     }
     SA_HIP(c, hipStreamSynchronize(st));
-    // A SPLIT band whose bounded wait for its producer expired (SA_FLAG_TIMEOUT, e.g. the GPU
-    // was time-sliced with another process) leaves an invalid pair: the host API never returns
-    // one -- it re-runs the batch on the single-workgroup plans.
-    bool tmo = false;
-    for (uint32_t p = 0; p < npairs && !tmo; ++p) tmo = (results[p].flags & SA_FLAG_TIMEOUT) != 0;
-    if (tmo && !c->no_split) {
-        c->no_split = true;
-        int rc = run_device(c, algo, sc, d1, do1, d2, do2, npairs, max_m, max_n,
-                            use_lut ? dbits : nullptr, dres, dops, st);
-        c->no_split = false;
-        if (rc) return rc;
-        SA_HIP(c, hipMemcpyAsync(results, dres, sizeof(sa_result) * npairs, hipMemcpyDeviceToHost, st));
-        SA_HIP(c, hipMemcpyAsync(ops, dops, ops_total, hipMemcpyDeviceToHost, st));
-        SA_HIP(c, hipStreamSynchronize(st));
-    }
     return SA_OK;
 }
 
@@ -835,11 +932,7 @@ int align_host_bits(sa_ctx* c, int algo, const sa_scoring* sc, const uint64_t* o
     const uint64_t b_res = al(sizeof(sa_result) * (uint64_t)npairs), b_ops = al(ops_total + 1);
     const uint64_t b_bits = al(4 * tw + 4);
     const uint64_t io_need = b_s + 3 * b_o + b_res + b_ops + b_bits;
-    if (c->io_bytes < io_need) {
-        if (c->io) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->io); c->io = nullptr; c->io_bytes = 0; }
-        if (hipMalloc(&c->io, io_need) != hipSuccess) { c->io = nullptr; return fail(c, SA_ERR_NOMEM, "hipMalloc of I/O buffers failed"); }
-        c->io_bytes = io_need;
-    }
+    if (int rc = ensure_io(c, io_need)) return rc;
     uint8_t* q = c->io;
     uint8_t* dseq = q; q += b_s;
     uint64_t* do1 = reinterpret_cast<uint64_t*>(q); q += b_o;
@@ -854,14 +947,26 @@ int align_host_bits(sa_ctx* c, int algo, const sa_scoring* sc, const uint64_t* o
     SA_HIP(c, hipMemcpyAsync(do2, off2, 8ull * (npairs + 1), hipMemcpyHostToDevice, st));
     SA_HIP(c, hipMemcpyAsync(dbo, bits_off, 8ull * (npairs + 1), hipMemcpyHostToDevice, st));
     if (tw) SA_HIP(c, hipMemcpyAsync(dbits, bits, 4 * tw, hipMemcpyHostToDevice, st));
-    int rc = run_device(c, algo, sc, dseq, do1, dseq, do2, npairs, max_m, max_n, nullptr, dres, dops, st, false,
-                        dbits, dbo);
-    if (rc) return rc;
+    if (algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER) {
+        std::string e;
+        c->launches = 0;
+        const auto run = algo == SA_HIRSCHBERG ? hirschberg_run : myersmiller_run;
+        DcBounds b;
+        b.t1 = t1;
+        b.t2 = t2;
+        b.max_m = max_m;
+        b.max_n = max_n;
+        const DcInputs in{dseq, do1, dseq, do2, npairs, nullptr, DcBits{dbits, dbo, do1, do2}};
+        if (run(c->dc, c->ev_last_set ? c->ev_last : nullptr, sc, in, b, st, dres, dops, &e))
+            return fail(c, SA_ERR_HIP, (algo == SA_HIRSCHBERG ? "hirschberg: " : "myers-miller: ") + e);
+    } else {
+        int rc = run_device(c, algo, sc, dseq, do1, dseq, do2, npairs, max_m, max_n, nullptr, dres, dops, st, false,
+                            dbits, dbo);
+        if (rc) return rc;
+    }
     SA_HIP(c, hipMemcpyAsync(results, dres, sizeof(sa_result) * npairs, hipMemcpyDeviceToHost, st));
     SA_HIP(c, hipMemcpyAsync(ops, dops, ops_total, hipMemcpyDeviceToHost, st));
     SA_HIP(c, hipStreamSynchronize(st));
-    for (uint32_t p = 0; p < npairs; ++p)
-        if (results[p].flags & SA_FLAG_TIMEOUT) return fail(c, SA_ERR_HIP, "split-plan band wait timed out");
     return SA_OK;
 }
 
@@ -913,11 +1018,9 @@ int sa_create(int device, sa_ctx** out) {
 void sa_destroy(sa_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->s_fill) (void)hipStreamSynchronize(c->s_fill);
-    if (c->s_tb) (void)hipStreamSynchronize(c->s_tb);
+    (void)drain(c);
     for (auto ev : c->events) (void)hipEventDestroy(ev);
-    for (auto ev : {c->ev_in, c->ev_slot[0], c->ev_slot[1], c->ev_sel})
+    for (auto ev : {c->ev_in, c->ev_slot[0], c->ev_slot[1], c->ev_sel, c->ev_last})
         if (ev) (void)hipEventDestroy(ev);
     if (c->s_fill) (void)hipStreamDestroy(c->s_fill);
     if (c->s_tb) (void)hipStreamDestroy(c->s_tb);
@@ -941,13 +1044,14 @@ int sa_set_workspace_limit(sa_ctx* c, uint64_t bytes) {
 int sa_trim(sa_ctx* c) {
     if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
-    if (c->s_fill) (void)hipStreamSynchronize(c->s_fill);
-    if (c->s_tb) (void)hipStreamSynchronize(c->s_tb);
+    (void)drain(c);
     if (c->ws) (void)hipFree(c->ws);
     if (c->io) (void)hipFree(c->io);
+    if (c->split) (void)hipFree(c->split);
     c->ws = nullptr; c->ws_bytes = 0;
     c->io = nullptr; c->io_bytes = 0;
+    c->split = nullptr; c->split_bytes = 0;
+    c->dc.release();
     return SA_OK;
 }
 
@@ -961,6 +1065,7 @@ int sa_align_batch(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq
     if ((off1[npairs] && !seq1) || (off2[npairs] && !seq2)) return fail(c, SA_ERR_ARG, "NULL sequence buffer");
     if (off1[0] != 0 || off2[0] != 0) return fail(c, SA_ERR_ARG, "offsets must start at 0");
     SA_HIP(c, hipSetDevice(c->device));
+    if ((rc = order_after_last(c, c->stream))) return rc;
 
     if (algo != SA_LOCAL_GOTOH)
         return align_host(c, algo, sc, seq1, off1, seq2, off2, npairs, lut, results, ops, ops_cap);
@@ -987,8 +1092,6 @@ int sa_align_batch_bits(sa_ctx* c, int algo, const sa_scoring* sc, const uint64_
     if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
     int rc = validate_scoring(c, algo, sc);
     if (rc) return rc;
-    if (algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER)
-        return fail(c, SA_ERR_UNSUPPORTED, "match bitmaps: SW, NW, LocalGotoh and GlobalGotoh only");
     if (!off1 || !off2 || !bits_off || (npairs && (!results || !ops))) return fail(c, SA_ERR_ARG, "NULL buffer");
     if (off1[0] != 0 || off2[0] != 0) return fail(c, SA_ERR_ARG, "offsets must start at 0");
     for (uint32_t p = 0; p < npairs; ++p) {
@@ -998,6 +1101,7 @@ int sa_align_batch_bits(sa_ctx* c, int algo, const sa_scoring* sc, const uint64_
     }
     if (bits_off[npairs] && !bits) return fail(c, SA_ERR_ARG, "NULL bitmap");
     SA_HIP(c, hipSetDevice(c->device));
+    if ((rc = order_after_last(c, c->stream))) return rc;
     if (algo != SA_LOCAL_GOTOH)
         return align_host_bits(c, algo, sc, off1, off2, npairs, bits, bits_off, results, ops, ops_cap);
     return lg_hack_split(c, off1, off2, npairs, results, ops, ops_cap,
@@ -1027,14 +1131,11 @@ int sa_align_batch_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8
     if (npairs == 0) return SA_OK;
     SA_HIP(c, hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if ((rc = order_after_last(c, st))) return rc;
     uint32_t* bits = nullptr;
     if (d_lut) {
         // LUT bits live in the tail of the I/O cache
-        if (c->io_bytes < 8192) {
-            if (c->io) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->io); c->io = nullptr; c->io_bytes = 0; }
-            if (hipMalloc(&c->io, 8192) != hipSuccess) { c->io = nullptr; return fail(c, SA_ERR_NOMEM, "hipMalloc LUT"); }
-            c->io_bytes = 8192;
-        }
+        if (int rc2 = ensure_io(c, 8192)) return rc2;
         bits = reinterpret_cast<uint32_t*>(c->io + c->io_bytes - 8192);
         hipLaunchKernelGGL(lut_to_bits, dim3(8), dim3(256), 0, st, d_lut, bits);
         SA_HIP(c, hipGetLastError());
@@ -1048,11 +1149,15 @@ int sa_align_batch_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8
         b.t2 = (uint64_t)npairs * max_n;
         b.max_m = max_m;
         b.max_n = max_n;
-        if (run(sc, d1, o1, d2, o2, npairs, b, bits, st, d_res, d_ops, &e))
+        const DcInputs in{d1, o1, d2, o2, npairs, bits, DcBits{}};
+        if (run(c->dc, c->ev_last_set ? c->ev_last : nullptr, sc, in, b, st, d_res, d_ops, &e))
             return fail(c, SA_ERR_HIP, (algo == SA_HIRSCHBERG ? "hirschberg: " : "myers-miller: ") + e);
-        return SA_OK;
+        return mark_last(c, st);
     }
-    return run_device(c, algo, sc, d1, o1, d2, o2, npairs, max_m, max_n, bits, d_res, d_ops, st, c->pipeline != 0);
+    const bool pipe = c->pipeline != 0;
+    rc = run_device(c, algo, sc, d1, o1, d2, o2, npairs, max_m, max_n, bits, d_res, d_ops, st, pipe);
+    if (rc || pipe) return rc;
+    return mark_last(c, st);
 }
 
 int sa_set_pipeline(sa_ctx* c, int enable) {
@@ -1127,14 +1232,17 @@ int sa_plan_query_ex(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t ma
     if (algo < SA_SW || algo > SA_GLOBAL_GOTOH) return fail(nullptr, SA_ERR_ARG, "unknown algorithm");
     if (!sc) return fail(nullptr, SA_ERR_ARG, "scoring is NULL");
     const bool cand = t16_candidate(algo, sc, max_m, max_n).ok;
-    const Variant v16 = make_variant(algo, max_m, max_n, npairs, true, true);
-    const Variant v32 = make_variant(algo, max_m, max_n, npairs, false, true);
-    const Variant& v = (cand && nsym <= 4) ? v16 : v32;
+    // exactly the variants a call enqueues (build_variants: common record stride, SPLIT fallback)
+    Variant vars[3];
+    bool has_fb = false;
+    const int nv = build_variants(algo, max_m, max_n, npairs, cand, vars, &has_fb);
+    const Variant& v = (cand && nsym <= 4) ? vars[0] : vars[nv - 1];
     if (kernel) *kernel = v.kernel;
     if (R) *R = v.pl.R;
     if (W) *W = v.pl.split ? 0 : v.pl.W;
-    // what a call allocates: both variants are enqueued when the scoring admits T16
-    if (ws_bytes_per_pair) *ws_bytes_per_pair = cand ? std::max(v16.slot_bytes, v32.slot_bytes) : v32.slot_bytes;
+    uint64_t ws = 0;
+    for (int k = 0; k < nv + (has_fb ? 1 : 0); ++k) ws = std::max(ws, vars[k].slot_bytes);
+    if (ws_bytes_per_pair) *ws_bytes_per_pair = ws;
     return SA_OK;
 }
 

@@ -104,9 +104,10 @@ __device__ __forceinline__ bool match_bit(const uint32_t* s_lut, int a, int b) {
 template <int R, bool WIDE = false>
 constexpr int fill_max_threads() { return (R >= 32 || (WIDE && R >= 16)) ? 256 : 1024; }
 
-// Bounded wait of a SPLIT band for its producer, in s_memrealtime ticks (100 MHz): 0.2 s.  After
-// one expiry the workgroup stops waiting altogether (the pair is flagged SA_FLAG_TIMEOUT).
-constexpr uint64_t kSplitWaitTicks = 20000000ull;
+// Bounded wait of a SPLIT band for its producer: FillParams::wait_ticks (kSplitWaitTicksDefault,
+// 0.2 s; SEQALIB_SPLIT_WAIT_TICKS overrides it for tests).  After one expiry the workgroup stops
+// waiting altogether: the pair is flagged SA_FLAG_TIMEOUT and re-run by the call's
+// single-workgroup fallback launch (run_device, sa_api.hip).
 
 #ifdef SA_TB_STATS
 // Debug build only (-DSA_TB_STATS, tools/split_stats.py): per SPLIT ticket {slot * bands + band,
@@ -188,6 +189,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     }
     const uint32_t pidx = P.pair_base + slot;
     if (redo && !(P.res[pidx].flags & kFlagRetry)) return;   // uniform over the workgroup
+    if (P.rerun && !(P.res[pidx].flags & SA_FLAG_TIMEOUT)) return;
 #ifdef SA_TB_STATS
     const unsigned long long st_t0 = __builtin_amdgcn_s_memrealtime();
     unsigned long long st_wait = 0;
@@ -623,7 +625,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     }
                     const uint64_t now = __builtin_amdgcn_s_memrealtime();
                     if (t0 == 0) t0 = now;
-                    else if (now - t0 > kSplitWaitTicks) { tmo = 1; break; }
+                    else if (now - t0 > P.wait_ticks) { tmo = 1; break; }
                     __builtin_amdgcn_s_sleep(2);
                     split_load(band, c0, pre_h, pre_x);
                 }
@@ -845,6 +847,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
             }
             if (T16 && B != 0 && h > P.retry_above) r.flags |= kFlagRetry;
             if (redo) r.flags |= kFlagRedo;
+            if (P.rerun) r.flags |= kFlagRerun;
             P.res[pidx] = r;
         }
     } else {
@@ -860,6 +863,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                 r.score = s_score;
             }
             if (redo) r.flags |= kFlagRedo;
+            if (P.rerun) r.flags |= kFlagRerun;
             P.res[pidx] = r;
         }
     }

@@ -67,13 +67,9 @@ __device__ __forceinline__ int32_t hb_cell(int32_t hd, int32_t hu, int32_t hl, b
     return max(max(sub, hu + s.gap), hl + s.gap);
 }
 
-// The same cell with the match source (LUT) and AllowMismatch fixed at compile time: branch-free.
-template <bool LUT, bool ALLOW>
-__device__ __forceinline__ int32_t hb_cell_t(int32_t hd, int32_t hu, int32_t hl, uint32_t a, uint32_t b,
-                                             const uint32_t* lut, const HbScore& s) {
-    bool v;
-    if constexpr (LUT) v = (lut[(a << 3) | (b >> 5)] >> (b & 31)) & 1;
-    else v = a == b;
+// The same cell with AllowMismatch fixed at compile time (branch-free), v = match(a, b).
+template <bool ALLOW>
+__device__ __forceinline__ int32_t hb_cell_v(int32_t hd, int32_t hu, int32_t hl, bool v, const HbScore& s) {
     int32_t sub;
     if constexpr (ALLOW) sub = hd + (v ? s.match : s.mismatch);
     else sub = v ? hd + s.match : INT_MIN;
@@ -81,23 +77,27 @@ __device__ __forceinline__ int32_t hb_cell_t(int32_t hd, int32_t hu, int32_t hl,
 }
 
 // ------------------------------------------------------------------ batched NWScore sweeps
-template <int R, bool LUT, bool ALLOW>
+// MM: kMatchEq / kMatchLut (byte symbols) or kMatchBits (pair-local indices + the pair's match
+// bitmap, the generic-Ty path; DcSrc in sa_dc.h).
+template <int R, int MM, bool ALLOW>
 __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* split,
                                                       const DcLevel* lvl, int32_t* rows, const uint32_t* lutbits,
-                                                      HbScore sc) {
+                                                      DcBits bits, HbScore sc) {
+    constexpr bool LUT = MM == kMatchLut;
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];
     const int lane = threadIdx.x;
     if (blockIdx.x / 2 >= lvl->nsplit) return;   // grid sized from an upper bound
-    const HbSweep d = hb_sweep_of(split[blockIdx.x / 2], blockIdx.x & 1);
+    const DcSub sub = split[blockIdx.x / 2];
+    const HbSweep d = hb_sweep_of(sub, blockIdx.x & 1);
     if constexpr (LUT) {
         for (int k = lane; k < 2048; k += 64) s_lut[k] = lutbits[k];
         __syncthreads();
     }
-    const uint32_t* lut = s_lut;
+    const DcSrc<MM> src = bits.src<MM>(s1, s2, s_lut, sub.pair, true);
     int32_t* out = rows + d.out;
     const int m = d.alen, n = d.blen, G = sc.gap;
-    auto symA = [&](int k) -> uint32_t { return d.rev ? s1[d.a - k] : s1[d.a + k]; };
-    auto symB = [&](int k) -> uint32_t { return d.rev ? s2[d.b - k] : s2[d.b + k]; };
+    auto symA = [&](int k) -> uint32_t { return src.a(d.rev ? d.a - k : d.a + k); };
+    auto symB = [&](int k) -> uint32_t { return src.b(d.rev ? d.b - k : d.b + k); };
     constexpr int BAND = 64 * R;
     const int bands = (m + BAND - 1) / BAND;
     const int lastb = bands - 1;
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
                     int32_t hd = prev_up, hu = up_h;
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
-                        const int32_t h = hb_cell_t<LUT, ALLOW>(hd, hu, Hp[r], a[r], sym, lut, sc);
+                        const int32_t h = hb_cell_v<ALLOW>(hd, hu, Hp[r], src.match(a[r], sym), sc);
                         hd = Hp[r];
                         Hp[r] = h;
                         hu = h;
@@ -168,11 +168,12 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
 // of n + 63 steps on a whole wave.  The row-above value and column symbol still arrive by DPP
 // wave_shr:1; a segment's first lane takes the top border (H[0][j] = j * gap) and its column
 // symbol (one ds_bpermute from the segment's chunk of Seq2, loaded a chunk ahead) instead.
-template <int G, bool LUT, bool ALLOW>
+template <int G, int MM, bool ALLOW>
 __global__ __launch_bounds__(64) void hb_sweep_seg_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* split,
                                                           const DcLevel* lvl, int32_t* rows, const uint32_t* lutbits,
-                                                          HbScore sc) {
+                                                          DcBits bits, HbScore sc) {
     constexpr int P = 64 / G;
+    constexpr bool LUT = MM == kMatchLut;
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];
     const int lane = threadIdx.x;
     const uint32_t nsw = 2 * lvl->nsplit;
@@ -181,19 +182,24 @@ __global__ __launch_bounds__(64) void hb_sweep_seg_kernel(const uint8_t* s1, con
         for (int k = lane; k < 2048; k += 64) s_lut[k] = lutbits[k];
         __syncthreads();
     }
-    const uint32_t* lut = s_lut;
     const int seg = lane / G, ls = lane % G;
     const uint32_t swi = blockIdx.x * P + seg;
     const bool active = swi < nsw;
     HbSweep d{};
-    if (active) d = hb_sweep_of(split[swi / 2], swi & 1);
+    uint32_t pair = 0;
+    if (active) {
+        const DcSub sub = split[swi / 2];
+        d = hb_sweep_of(sub, swi & 1);
+        pair = sub.pair;
+    }
+    const DcSrc<MM> src = bits.src<MM>(s1, s2, s_lut, pair, active);
     const int m = d.alen, n = d.blen, Gp = sc.gap;
     int32_t* out = rows + d.out;
     int steps = n + G - 1;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) steps = max(steps, __shfl_xor(steps, off));
-    auto symB = [&](int k) -> uint32_t { return d.rev ? s2[d.b - k] : s2[d.b + k]; };
-    const uint32_t a = ls < m ? (d.rev ? s1[d.a - ls] : s1[d.a + ls]) : 0u;
+    auto symB = [&](int k) -> uint32_t { return src.b(d.rev ? d.b - k : d.b + k); };
+    const uint32_t a = ls < m ? src.a(d.rev ? d.a - ls : d.a + ls) : 0u;
     int32_t Hp = (ls + 1) * Gp;          // H[ls + 1][0]
     int32_t prev_up = ls * Gp;           // H[ls][0]: the diagonal of column 1
     int32_t hl = Hp;
@@ -212,7 +218,7 @@ __global__ __launch_bounds__(64) void hb_sweep_seg_kernel(const uint8_t* s1, con
             sym = ls == 0 ? b0 : sy_d;
             const int j0 = s - ls;
             if (j0 >= 0 && j0 < n && ls < m) {
-                const int32_t h = hb_cell_t<LUT, ALLOW>(prev_up, up_h, Hp, a, sym, lut, sc);
+                const int32_t h = hb_cell_v<ALLOW>(prev_up, up_h, Hp, src.match(a, sym), sc);
                 Hp = h;
                 prev_up = up_h;
                 hl = h;
@@ -255,11 +261,13 @@ __global__ __launch_bounds__(64) void hb_split_kernel(const DcSub* split, const 
 }
 
 // ---------------------------------------------------------------------------- leaves
+// The leaf solvers take the symbols as a sequence view (Seq: GSeq / LSeq bytes, ISeq pair-local
+// indices) and the match as a functor (Match: DcLutMatch, DcBitsMatch).
 // NWScore's last row (:31-66) into F[0..blen], one row updated in place (the cell above is read
 // before it is overwritten; its old value is the next column's diagonal).
-template <typename Row, typename Seq>
+template <typename Row, typename Seq, typename Match>
 __device__ void hb_nwscore(Seq A, int alen, int arev, Seq B, int blen, int brev,
-                           const uint32_t* lut, const HbScore& sc, Row F) {
+                           const Match& mt, const HbScore& sc, Row F) {
     F[0] = 0;
     for (int j = 1; j <= blen; ++j) F[j] = F[j - 1] + sc.gap;
     for (int i = 1; i <= alen; ++i) {
@@ -270,7 +278,7 @@ __device__ void hb_nwscore(Seq A, int alen, int arev, Seq B, int blen, int brev,
         for (int j = 1; j <= blen; ++j) {
             const uint32_t bj = brev ? B[blen - j] : B[j - 1];
             const int32_t up = F[j];
-            left = hb_cell(diag, up, left, dc_match(lut, ai, bj), sc);
+            left = hb_cell(diag, up, left, mt(ai, bj), sc);
             F[j] = left;
             diag = up;
         }
@@ -279,20 +287,18 @@ __device__ void hb_nwscore(Seq A, int alen, int arev, Seq B, int blen, int brev,
 
 // NeedlemanWunschSA::getAlignment on a 1 x k or k x 1 view (:119-126): full matrix + the
 // reference NW traceback (SANeedlemanWunsch.h:167-230); writes forward-order ops at out.
-template <typename Row>
-__device__ int hb_nw_small(const uint8_t* A, int m, const uint8_t* B, int n, const uint32_t* lut,
-                           const HbScore& sc, Row H, uint8_t* out) {
+template <typename Row, typename Seq, typename Match>
+__device__ int hb_nw_small(Seq A, int m, Seq B, int n, const Match& mt, const HbScore& sc, Row H, uint8_t* out) {
     const int w = n + 1;
     for (int i = 0; i <= m; ++i) H[i * w] = i * sc.gap;
     for (int j = 0; j <= n; ++j) H[j] = j * sc.gap;
     for (int i = 1; i <= m; ++i)
         for (int j = 1; j <= n; ++j)
-            H[i * w + j] = hb_cell(H[(i - 1) * w + j - 1], H[(i - 1) * w + j], H[i * w + j - 1],
-                                   dc_match(lut, A[i - 1], B[j - 1]), sc);
+            H[i * w + j] = hb_cell(H[(i - 1) * w + j - 1], H[(i - 1) * w + j], H[i * w + j - 1], mt(A[i - 1], B[j - 1]), sc);
     int k = 0, i = m, j = n;
     while (i > 0 || j > 0) {
         if (i > 0 && j > 0) {
-            const bool v = dc_match(lut, A[i - 1], B[j - 1]);
+            const bool v = mt(A[i - 1], B[j - 1]);
             const int32_t hd = H[(i - 1) * w + j - 1];
             const int32_t dt = sc.allow ? hd + (v ? sc.match : sc.mismatch) : (v ? hd + sc.match : INT_MIN);
             if (H[i * w + j] == dt) {
@@ -309,15 +315,14 @@ __device__ int hb_nw_small(const uint8_t* A, int m, const uint8_t* B, int n, con
 }
 
 // One leaf: the whole HirschbergRec below it (explicit stack, left child first), forward ops.
-template <typename Row, typename Seq>
-__device__ int hb_leaf_solve(Seq S1, Seq S2, const uint8_t* g1, const uint8_t* g2, int alen, int blen, bool top,
-                             Row F, Row Cc, Row Hs, uint8_t* out, int32_t* score,
-                             const uint32_t* lut, const HbScore& sc) {
+template <typename Row, typename Seq, typename Match>
+__device__ int hb_leaf_solve(Seq S1, Seq S2, int alen, int blen, bool top, Row F, Row Cc, Row Hs, uint8_t* out,
+                             int32_t* score, const Match& mt, const HbScore& sc) {
     if (top) {
         int32_t s;
         if (alen == 0) s = blen * sc.gap;
         else if (blen == 0) s = alen * sc.gap;
-        else { hb_nwscore(S1, alen, 0, S2, blen, 0, lut, sc, F); s = F[blen]; }
+        else { hb_nwscore(S1, alen, 0, S2, blen, 0, mt, sc, F); s = F[blen]; }
         *score = s;
     }
     int k = 0;
@@ -332,13 +337,13 @@ __device__ int hb_leaf_solve(Seq S1, Seq S2, const uint8_t* g1, const uint8_t* g
         } else if (yl == 0) {
             for (int q = 0; q < xl; ++q) out[k++] = 'U';
         } else if (xl == 1 || yl == 1) {
-            k += hb_nw_small(g1 + x0, xl, g2 + y0, yl, lut, sc, Hs, out + k);
+            k += hb_nw_small(S1.shifted(x0), xl, S2.shifted(y0), yl, mt, sc, Hs, out + k);
         } else {
             const int mid = xl / 2;
             const Seq A0 = S1.shifted(x0), B0 = S2.shifted(y0), A1 = S1.shifted(x0 + mid);
-            hb_nwscore(A0, mid, 0, B0, yl, 0, lut, sc, F);
+            hb_nwscore(A0, mid, 0, B0, yl, 0, mt, sc, F);
             for (int q = 0; q <= yl; ++q) Cc[q] = F[q];
-            hb_nwscore(A1, xl - mid, 1, B0, yl, 1, lut, sc, F);
+            hb_nwscore(A1, xl - mid, 1, B0, yl, 1, mt, sc, F);
             int mid2 = 0;
             int32_t best = INT_MIN;
             for (int i = 0; i < yl; ++i) {
@@ -366,36 +371,48 @@ constexpr int kHbLdsCols = SA_HB_LDS_COLS;
 // A leaf's global scratch lives at 6 * key (F, -, Cc: 3 (blen + 1); base-case matrix:
 // 2 (max(alen, blen) + 1); together <= 6 (alen + blen) whenever alen, blen >= 1, the only
 // leaves that use scratch), its forward ops at stage[key], its op count at mark[key].
+// BITS: the generic-Ty path (symbols = pair-local indices, match = the pair's bitmap).
+template <bool BITS>
 __global__ __launch_bounds__(64) void hb_leaf_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* leaves,
                                                      const uint32_t* nleaves, int32_t* scratch, uint8_t* stage,
                                                      int32_t* mark, sa_result* res, const uint32_t* lut,
-                                                     HbScore sc) {
+                                                     DcBits bits, HbScore sc) {
     __shared__ int32_t s_rows[2 * (kHbLdsCols + 1) * 64];
-    __shared__ uint8_t s_seq[2 * kHbLdsCols * 64];
+    __shared__ uint8_t s_seq[BITS ? 1 : 2 * kHbLdsCols * 64];
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= *nleaves) return;
     const int t = threadIdx.x;
     const DcSub L = leaves[id];
     const uint64_t key = L.a0 + L.b0;
-    const uint8_t* g1 = s1 + L.a0;
-    const uint8_t* g2 = s2 + L.b0;
     int32_t* Fg = scratch + 6 * key;
     int32_t* Hs = Fg + 3 * (L.n + 1);
     uint8_t* out = stage + key;
     int32_t* score = &res[L.pair].score;   // written only for a top leaf
+    const bool in_lds = L.m <= kHbLdsCols && L.n <= kHbLdsCols;
+    dc_lds_i32* r0 = (dc_lds_i32*)s_rows + t;
+    const LRow F{r0}, Cc{r0 + (kHbLdsCols + 1) * 64};
     int k;
-    if (L.m <= kHbLdsCols && L.n <= kHbLdsCols) {
-        dc_lds_u8* q1 = (dc_lds_u8*)s_seq + t;
-        dc_lds_u8* q2 = q1 + kHbLdsCols * 64;
-        for (int c = 0; c < L.m; ++c) q1[c * 64] = g1[c];
-        for (int c = 0; c < L.n; ++c) q2[c * 64] = g2[c];
-        dc_lds_i32* r0 = (dc_lds_i32*)s_rows + t;
-        const LRow F{r0}, Cc{r0 + (kHbLdsCols + 1) * 64};
-        // a base case's (<= 2 x (kHbLdsCols + 1)) matrix reuses F and Cc, both dead by then
-        k = hb_leaf_solve(LSeq{q1}, LSeq{q2}, g1, g2, L.m, L.n, L.top != 0, F, Cc, F, out, score, lut, sc);
+    if constexpr (BITS) {
+        uint64_t b1, b2;
+        const DcBitsMatch mt = bits.of(L.pair, &b1, &b2);
+        const ISeq S1{(uint32_t)(L.a0 - b1)}, S2{(uint32_t)(L.b0 - b2)};
+        if (in_lds) k = hb_leaf_solve(S1, S2, L.m, L.n, L.top != 0, F, Cc, F, out, score, mt, sc);
+        else k = hb_leaf_solve(S1, S2, L.m, L.n, L.top != 0, GRow{Fg}, GRow{Fg + 2 * (L.n + 1)}, GRow{Hs}, out, score, mt, sc);
     } else {
-        const GRow F{Fg}, Cc{Fg + 2 * (L.n + 1)};
-        k = hb_leaf_solve(GSeq{g1}, GSeq{g2}, g1, g2, L.m, L.n, L.top != 0, F, Cc, GRow{Hs}, out, score, lut, sc);
+        const uint8_t* g1 = s1 + L.a0;
+        const uint8_t* g2 = s2 + L.b0;
+        const DcLutMatch mt{lut};
+        if (in_lds) {
+            dc_lds_u8* q1 = (dc_lds_u8*)s_seq + t;
+            dc_lds_u8* q2 = q1 + kHbLdsCols * 64;
+            for (int c = 0; c < L.m; ++c) q1[c * 64] = g1[c];
+            for (int c = 0; c < L.n; ++c) q2[c * 64] = g2[c];
+            // a base case's (<= 2 x (kHbLdsCols + 1)) matrix reuses F and Cc, both dead by then
+            k = hb_leaf_solve(LSeq{q1}, LSeq{q2}, L.m, L.n, L.top != 0, F, Cc, F, out, score, mt, sc);
+        } else {
+            k = hb_leaf_solve(GSeq{g1}, GSeq{g2}, L.m, L.n, L.top != 0, GRow{Fg}, GRow{Fg + 2 * (L.n + 1)}, GRow{Hs},
+                              out, score, mt, sc);
+        }
     }
     if (k) mark[key] = k;
 }
@@ -403,66 +420,55 @@ __global__ __launch_bounds__(64) void hb_leaf_kernel(const uint8_t* s1, const ui
 // ---------------------------------------------------------------------------- host driver
 namespace {
 
-template <bool LUT, bool ALLOW>
-void launch_sweeps_t(int R, dim3 grid, const uint8_t* d1, const uint8_t* d2, const DcSub* split, const DcLevel* lvl,
-                     int32_t* rows, const uint32_t* lut, const HbScore& sc, hipStream_t st) {
+struct HbLaunch {
+    const uint8_t* d1;
+    const uint8_t* d2;
+    const DcSub* split;
+    const DcLevel* lvl;
+    int32_t* rows;
+    const uint32_t* lut;
+    DcBits bits;
+    HbScore sc;
+};
+
+template <int MM, bool ALLOW>
+void launch_sweeps_t(int R, int G, uint32_t count, const HbLaunch& a, hipStream_t st) {
     const dim3 block(64);
-    switch (R) {
-        case 1: hipLaunchKernelGGL((hb_sweep_kernel<1, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
-        case 2: hipLaunchKernelGGL((hb_sweep_kernel<2, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
-        case 4: hipLaunchKernelGGL((hb_sweep_kernel<4, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
-        case 8: hipLaunchKernelGGL((hb_sweep_kernel<8, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
-        case 16: hipLaunchKernelGGL((hb_sweep_kernel<16, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
-        default: hipLaunchKernelGGL((hb_sweep_kernel<32, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
-    }
+#define SA_HB_SEG(GG)                                                                                           \
+    hipLaunchKernelGGL((hb_sweep_seg_kernel<GG, MM, ALLOW>), dim3((count + 64 / GG - 1) / (64 / GG)), block, 0, st, \
+                       a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc)
+#define SA_HB_SW(RR) \
+    hipLaunchKernelGGL((hb_sweep_kernel<RR, MM, ALLOW>), dim3(count), block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc)
+    if (G == 8) SA_HB_SEG(8);
+    else if (G == 16) SA_HB_SEG(16);
+    else if (G == 32) SA_HB_SEG(32);
+    else if (R == 1) SA_HB_SW(1);
+    else if (R == 2) SA_HB_SW(2);
+    else if (R == 4) SA_HB_SW(4);
+    else if (R == 8) SA_HB_SW(8);
+    else if (R == 16) SA_HB_SW(16);
+    else SA_HB_SW(32);
+#undef SA_HB_SEG
+#undef SA_HB_SW
 }
 
-template <bool LUT, bool ALLOW>
-void launch_seg_t(int G, uint32_t count, const uint8_t* d1, const uint8_t* d2, const DcSub* split, const DcLevel* lvl,
-                  int32_t* rows, const uint32_t* lut, const HbScore& sc, hipStream_t st) {
-    const dim3 block(64);
-    if (G == 8)
-        hipLaunchKernelGGL((hb_sweep_seg_kernel<8, LUT, ALLOW>), dim3((count + 7) / 8), block, 0, st, d1, d2, split,
-                           lvl, rows, lut, sc);
-    else if (G == 16)
-        hipLaunchKernelGGL((hb_sweep_seg_kernel<16, LUT, ALLOW>), dim3((count + 3) / 4), block, 0, st, d1, d2, split,
-                           lvl, rows, lut, sc);
-    else
-        hipLaunchKernelGGL((hb_sweep_seg_kernel<32, LUT, ALLOW>), dim3((count + 1) / 2), block, 0, st, d1, d2, split,
-                           lvl, rows, lut, sc);
-}
-
-// R = 0: packed sweeps of G = 16 or 32 lanes (maxa <= G) instead of R rows per lane.
-hipError_t launch_sweeps(int R, int G, uint32_t count, const uint8_t* d1, const uint8_t* d2, const DcSub* split,
-                         const DcLevel* lvl, int32_t* rows, const uint32_t* lut, const HbScore& sc, hipStream_t st) {
-    if (G) {
-        if (lut) {
-            if (sc.allow) launch_seg_t<true, true>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
-            else launch_seg_t<true, false>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
-        } else {
-            if (sc.allow) launch_seg_t<false, true>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
-            else launch_seg_t<false, false>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
-        }
-        return hipGetLastError();
-    }
-    const dim3 grid(count);
-    if (lut) {
-        if (sc.allow) launch_sweeps_t<true, true>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
-        else launch_sweeps_t<true, false>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
-    } else {
-        if (sc.allow) launch_sweeps_t<false, true>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
-        else launch_sweeps_t<false, false>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
-    }
+// G = 8 / 16 / 32: packed sweeps (maxa <= G); G = 0: R rows per lane, one sweep per wave.
+hipError_t launch_sweeps(int R, int G, uint32_t count, const HbLaunch& a, hipStream_t st) {
+    const int mm = a.bits.mbits ? kMatchBits : a.lut ? kMatchLut : kMatchEq;
+    if (mm == kMatchBits) a.sc.allow ? launch_sweeps_t<kMatchBits, true>(R, G, count, a, st)
+                                     : launch_sweeps_t<kMatchBits, false>(R, G, count, a, st);
+    else if (mm == kMatchLut) a.sc.allow ? launch_sweeps_t<kMatchLut, true>(R, G, count, a, st)
+                                         : launch_sweeps_t<kMatchLut, false>(R, G, count, a, st);
+    else a.sc.allow ? launch_sweeps_t<kMatchEq, true>(R, G, count, a, st) : launch_sweeps_t<kMatchEq, false>(R, G, count, a, st);
     return hipGetLastError();
 }
 
 }  // namespace
 
 // Host driver: inputs, results and the traceback-order op streams (pair p's at
-// off1[p] + off2[p] + p) all on the device; enqueued on st without waiting for it (grid
+// o1[p] + o2[p] + p) all on the device; enqueued on st without waiting for it (grid
 // bounds from b).
-int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
-                   const uint64_t* d_o2, uint32_t npairs, const DcBounds& b, const uint32_t* d_lutbits,
+int hirschberg_run(DcWork& w, hipEvent_t prev, const sa_scoring* scoring, const DcInputs& in, const DcBounds& b,
                    hipStream_t st, sa_result* d_res, uint8_t* d_ops, std::string* err) {
     int leaf_rows = kHbLeafRows;   // tuning override: SEQALIB_HB_LEAF
     if (const char* lr = getenv("SEQALIB_HB_LEAF")) leaf_rows = std::max(2, atoi(lr));
@@ -470,15 +476,16 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
     const bool seg_sweeps = !segenv || atoi(segenv) != 0;
     int rmax = 32;                                   // tuning: SEQALIB_DC_RMAX caps the sweep's R
     if (const char* r = getenv("SEQALIB_DC_RMAX")) rmax = std::min(32, std::max(1, atoi(r)));
+    const uint32_t npairs = in.npairs;
     HbScore sc;
     sc.gap = scoring->gap;
     sc.match = scoring->match;
     sc.allow = scoring->allow_mismatch != 0;
     sc.mismatch = sc.allow ? scoring->mismatch : INT_MIN;
-    static thread_local DcWork w;
-    SA_DC_HIP(w.prepare(b, npairs, leaf_rows, 2, 2, 6, st));
+    const bool bits = in.bits.mbits != nullptr;
+    SA_DC_HIP(w.prepare(b, npairs, leaf_rows, 2, 2, 6, st, prev));
     SA_DC_HIP(hipMemsetAsync(d_res, 0, sizeof(sa_result) * npairs, st));
-    SA_DC_HIP(dc_launch_init(d_o1, d_o2, npairs, 0, b, w.cur.p, d_res, st));
+    SA_DC_HIP(dc_launch_init(in.o1, in.o2, npairs, 0, b, w.cur.p, d_res, st));
     uint32_t cap = npairs;     // upper bound on this level's subproblems
     int maxm = (int)b.max_m;        // upper bound on their Seq1 length
     for (int l = 0;; ++l) {
@@ -490,7 +497,8 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
         int R = 1;
         while (R < rmax && 64 * R < maxa) R *= 2;   // bands of 64 R rows
         const int G = !seg_sweeps ? 0 : maxa <= 8 ? 8 : maxa <= 16 ? 16 : maxa <= 32 ? 32 : 0;
-        SA_DC_HIP(launch_sweeps(R, G, 2 * splits, d1, d2, w.split.p, w.lvl.p + l, w.rows.p, d_lutbits, sc, st));
+        const HbLaunch a{in.d1, in.d2, w.split.p, w.lvl.p + l, w.rows.p, in.lutbits, in.bits, sc};
+        SA_DC_HIP(launch_sweeps(R, G, 2 * splits, a, st));
         hipLaunchKernelGGL(hb_split_kernel, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p, w.next.p,
                            d_res);
         SA_DC_HIP(hipGetLastError());
@@ -498,10 +506,14 @@ int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t*
         cap = 2 * splits;
         maxm = maxa;
     }
-    hipLaunchKernelGGL(hb_leaf_kernel, dim3((w.leaf_cap + 63) / 64), dim3(64), 0, st, d1, d2, w.leaves.p, w.nleaf(),
-                       w.scratch.p, w.stage.p, w.mark.p, d_res, d_lutbits, sc);
+    if (bits)
+        hipLaunchKernelGGL(hb_leaf_kernel<true>, dim3((w.leaf_cap + 63) / 64), dim3(64), 0, st, in.d1, in.d2, w.leaves.p,
+                           w.nleaf(), w.scratch.p, w.stage.p, w.mark.p, d_res, in.lutbits, in.bits, sc);
+    else
+        hipLaunchKernelGGL(hb_leaf_kernel<false>, dim3((w.leaf_cap + 63) / 64), dim3(64), 0, st, in.d1, in.d2, w.leaves.p,
+                           w.nleaf(), w.scratch.p, w.stage.p, w.mark.p, d_res, in.lutbits, in.bits, sc);
     SA_DC_HIP(hipGetLastError());
-    SA_DC_HIP(dc_launch_assemble(d_o1, d_o2, npairs, w.mark.p, w.stage.p, d_res, d_ops, st));
+    SA_DC_HIP(dc_launch_assemble(in.o1, in.o2, npairs, w.mark.p, w.stage.p, d_res, d_ops, st));
     return 0;
 }
 

@@ -16,6 +16,11 @@ constexpr int kMatchEq = 0, kMatchLut = 1, kMatchBits = 2;
 // so the pair is re-run by the int32 variant; kFlagRedo: the int32 variant re-ran it (the T16
 // end-cell replay and traceback skip it, the int32 traceback walks it).
 constexpr uint32_t kFlagRetry = 1u << 30, kFlagRedo = 1u << 31;
+// kFlagRerun: a SPLIT pair whose band wait expired (SA_FLAG_TIMEOUT) was re-run by the
+// single-workgroup fallback plan of the same call (run_device, sa_api.hip); its traceback walks it.
+constexpr uint32_t kFlagRerun = 1u << 29;
+// Bounded wait of a SPLIT band for its producer, in s_memrealtime ticks (100 MHz): 0.2 s.
+constexpr uint64_t kSplitWaitTicksDefault = 20000000ull;
 
 struct FillParams {
     const uint8_t* seq1;
@@ -71,6 +76,9 @@ struct FillParams {
     uint32_t* ticket;
     int32_t* part;
     uint32_t split_bands;
+    uint64_t wait_ticks;       // SPLIT: bounded wait for the producer band (s_memrealtime ticks)
+    // the fallback launch: re-runs only the pairs a SPLIT fill flagged SA_FLAG_TIMEOUT
+    int rerun;
 };
 
 // SPLIT fills: per-pair fold of the per-band partials into sa_result (split_reduce_kernel).
@@ -144,6 +152,7 @@ struct TbParams {
     int hand_shift;
     int4* seg_rec;
     int4* seg_fin;
+    int rerun;                 // the fallback launch: walks only the pairs flagged kFlagRerun
 };
 // SA_FLAG_TIMEOUT: a SPLIT band's bounded wait for its producer expired (results invalid)
 
@@ -182,8 +191,11 @@ __device__ __forceinline__ bool sa_skip(const uint32_t* sel, uint32_t want) {
 }
 // Traceback of a pair: by the launch of the variant the batch selected, except the pairs the
 // int32 variant re-ran (kFlagRedo), which its own traceback walks.
+// A pair whose SPLIT band wait expired is walked by the fallback launch that re-ran it.
 template <typename TP>
 __device__ __forceinline__ bool tb_mine(const TP& P, uint32_t flags) {
+    if (P.rerun) return (flags & kFlagRerun) != 0;
+    if (flags & SA_FLAG_TIMEOUT) return false;
     if (!P.sel) return true;
     const bool redone = (flags & kFlagRedo) != 0;
     return *P.sel == P.sel_want ? !redone : redone;
@@ -210,24 +222,10 @@ __device__ __forceinline__ bool seg_take(const TbParams& P, const sa_result& res
     if (SCORED) return P.match > 0 && (int64_t)res.score >= (int64_t)kSegMinMoves * P.match;
     return m + n >= 16 * kSegMinMoves;
 }
-hipError_t launch_traceback_seg(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
+// inject (tests only): overwrite the exit records between the two kernels
+hipError_t launch_traceback_seg(int algo, int R, bool lut, const TbParams& p, hipStream_t stream, bool inject = false);
 hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
 // One wave per pair (sa_traceback_wave.hip): the few-pairs traceback.
 hipError_t launch_traceback_wave(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
 hipError_t launch_endcell(int algo, int R, const EndcellParams& p, hipStream_t stream);
-}  // namespace sa
-#include <string>
-#include <vector>
-namespace sa {
-// HirschbergSA / MyersMillerSA drivers (sa_hirschberg.hip, sa_myersmiller.hip): device inputs,
-// device outputs (results, op streams at off1[p] + off2[p] + p), enqueued on st with no host
-// wait (grid bounds from b).  Return 0, or -1 with *err set.
-struct DcBounds;   // sa_dc.h: symbol totals and longest sides (upper bounds)
-int hirschberg_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
-                   const uint64_t* d_o2, uint32_t npairs, const DcBounds& b, const uint32_t* d_lutbits,
-                   hipStream_t st, sa_result* d_res, uint8_t* d_ops, std::string* err);
-int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
-                    const uint64_t* d_o2, uint32_t npairs, const DcBounds& b, const uint32_t* d_lutbits,
-                    hipStream_t st, sa_result* d_res, uint8_t* d_ops, std::string* err);
-
 }  // namespace sa

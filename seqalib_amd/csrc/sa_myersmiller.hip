@@ -71,22 +71,18 @@ __device__ __forceinline__ int32_t mm_diag(int32_t s, bool v, const MmScore& sc)
 // Lane t owns R consecutive rows of a 64R-row band and computes column s - t at step s.  Per
 // row it keeps C and e (the horizontal-gap state) of the previous column; (C, D) of the row
 // above come from the lane above via DPP wave_shr:1 (lane 0: the previous band's last row,
-// written in place to the output rows, or the top boundary).  LUT / ALLOW are compile-time so
-// the cell is branch-free; LAST (the band holding row m) also captures D of row m.
-template <bool LUT, bool ALLOW>
-__device__ __forceinline__ int32_t mm_diag_t(int32_t cd, uint32_t a, uint32_t b, const uint32_t* lut,
-                                             const MmScore& sc) {
-    bool v;
-    if constexpr (LUT) v = (lut[(a << 3) | (b >> 5)] >> (b & 31)) & 1;
-    else v = a == b;
+// written in place to the output rows, or the top boundary).  The match source (MM: DcSrc in
+// sa_dc.h) and ALLOW are compile-time so the cell is branch-free; LAST (the band holding row m)
+// also captures D of row m.
+template <bool ALLOW>
+__device__ __forceinline__ int32_t mm_diag_v(int32_t cd, bool v, const MmScore& sc) {
     if constexpr (ALLOW) return cd + (v ? sc.match : sc.mismatch);
     else return v ? cd + sc.match : INT_MIN;
 }
 
-template <int R, bool LUT, bool ALLOW, bool LAST>
-__device__ __forceinline__ void mm_band(const MmSweep& d, const uint8_t* s1, const uint8_t* s2, const uint32_t* lut,
-                                        const MmScore& sc, int band, int32_t* outC, int32_t* outD, int tl, int rl,
-                                        int32_t& cl, int32_t& dl) {
+template <int R, int MM, bool ALLOW, bool LAST>
+__device__ __forceinline__ void mm_band(const MmSweep& d, const DcSrc<MM>& src, const MmScore& sc, int band,
+                                        int32_t* outC, int32_t* outD, int tl, int rl, int32_t& cl, int32_t& dl) {
     const int lane = threadIdx.x;
     const int m = d.alen, n = d.blen, g = sc.g, h = sc.h;
     constexpr int BAND = 64 * R;
@@ -95,7 +91,7 @@ __device__ __forceinline__ void mm_band(const MmSweep& d, const uint8_t* s1, con
     int32_t Cp[R], Ep[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        a[r] = row0 + r < m ? (d.rev ? s1[d.a - (row0 + r)] : s1[d.a + (row0 + r)]) : 0u;
+        a[r] = row0 + r < m ? src.a(d.rev ? d.a - (row0 + r) : d.a + (row0 + r)) : 0u;
         Cp[r] = d.t0 + h * (row0 + r + 1);                   // C[i][0] = t0 + i h (:192-197)
         Ep[r] = Cp[r] + g;                                   // e = t + g (:198)
     }
@@ -115,7 +111,7 @@ __device__ __forceinline__ void mm_band(const MmSweep& d, const uint8_t* s1, con
                 vc = outC[j + 1];
                 vd = outD[j + 1];
             }
-            vs = d.rev ? s2[d.b - j] : s2[d.b + j];
+            vs = src.b(d.rev ? d.b - j : d.b + j);
         }
     };
     int32_t vc, vd, nvc, nvd;
@@ -136,7 +132,7 @@ __device__ __forceinline__ void mm_band(const MmSweep& d, const uint8_t* s1, con
                 for (int r = 0; r < R; ++r) {
                     const int32_t e = max(Ep[r], Cp[r] + g) + h;   // :202
                     const int32_t dd = max(du, cu + g) + h;        // :203
-                    const int32_t c = max(max(dd, e), mm_diag_t<LUT, ALLOW>(cd, a[r], sym, lut, sc));
+                    const int32_t c = max(max(dd, e), mm_diag_v<ALLOW>(cd, src.match(a[r], sym), sc));
                     cd = Cp[r];
                     Cp[r] = c;
                     Ep[r] = e;
@@ -170,18 +166,21 @@ __device__ __forceinline__ void mm_band(const MmSweep& d, const uint8_t* s1, con
     }
 }
 
-template <int R, bool LUT, bool ALLOW>
+template <int R, int MM, bool ALLOW>
 __global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* split,
                                                       const DcLevel* lvl, int32_t* rows, const uint32_t* lutbits,
-                                                      MmScore sc) {
+                                                      DcBits bits, MmScore sc) {
+    constexpr bool LUT = MM == kMatchLut;
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];
     const int lane = threadIdx.x;
     if (blockIdx.x / 2 >= lvl->nsplit) return;   // grid sized from an upper bound
-    const MmSweep d = mm_sweep_of(split[blockIdx.x / 2], blockIdx.x & 1);
+    const DcSub sub = split[blockIdx.x / 2];
+    const MmSweep d = mm_sweep_of(sub, blockIdx.x & 1);
     if constexpr (LUT) {
         for (int k = lane; k < 2048; k += 64) s_lut[k] = lutbits[k];
         __syncthreads();
     }
+    const DcSrc<MM> src = bits.src<MM>(s1, s2, s_lut, sub.pair, true);
     const int m = d.alen, n = d.blen;
     int32_t* outC = rows + d.out;
     int32_t* outD = outC + n + 1;
@@ -191,9 +190,9 @@ __global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const u
     int32_t cl = 0, dl = 0;                                   // this lane's last row: C, D
     for (int band = 0; band < bands; ++band) {
         if (band < bands - 1)
-            mm_band<R, LUT, ALLOW, false>(d, s1, s2, s_lut, sc, band, outC, outD, tl, rl, cl, dl);
+            mm_band<R, MM, ALLOW, false>(d, src, sc, band, outC, outD, tl, rl, cl, dl);
         else
-            mm_band<R, LUT, ALLOW, true>(d, s1, s2, s_lut, sc, band, outC, outD, tl, rl, cl, dl);
+            mm_band<R, MM, ALLOW, true>(d, src, sc, band, outC, outD, tl, rl, cl, dl);
         __threadfence_block();
         __syncthreads();
     }
@@ -206,11 +205,12 @@ __global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const u
 // Packed sweeps for the deep levels (every sweep has alen <= G rows): 64 / G sweeps per wave, G
 // lanes each, one row per lane (as hb_sweep_seg_kernel).  A segment's first lane takes the top
 // border (CC[j] = g + j h, DD[j] = CC[j] + g, :183-188) and its column symbol by ds_bpermute.
-template <int G, bool LUT, bool ALLOW>
+template <int G, int MM, bool ALLOW>
 __global__ __launch_bounds__(64) void mm_sweep_seg_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* split,
                                                           const DcLevel* lvl, int32_t* rows, const uint32_t* lutbits,
-                                                          MmScore sc) {
+                                                          DcBits bits, MmScore sc) {
     constexpr int P = 64 / G;
+    constexpr bool LUT = MM == kMatchLut;
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];
     const int lane = threadIdx.x;
     const uint32_t nsw = 2 * lvl->nsplit;
@@ -219,20 +219,25 @@ __global__ __launch_bounds__(64) void mm_sweep_seg_kernel(const uint8_t* s1, con
         for (int k = lane; k < 2048; k += 64) s_lut[k] = lutbits[k];
         __syncthreads();
     }
-    const uint32_t* lut = s_lut;
     const int seg = lane / G, ls = lane % G;
     const uint32_t swi = blockIdx.x * P + seg;
     const bool active = swi < nsw;
     MmSweep d{};
-    if (active) d = mm_sweep_of(split[swi / 2], swi & 1);
+    uint32_t pair = 0;
+    if (active) {
+        const DcSub sub = split[swi / 2];
+        d = mm_sweep_of(sub, swi & 1);
+        pair = sub.pair;
+    }
+    const DcSrc<MM> src = bits.src<MM>(s1, s2, s_lut, pair, active);
     const int m = d.alen, n = d.blen, g = sc.g, h = sc.h;
     int32_t* outC = rows + d.out;
     int32_t* outD = outC + n + 1;
     int steps = n + G - 1;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) steps = max(steps, __shfl_xor(steps, off));
-    auto symB = [&](int k) -> uint32_t { return d.rev ? s2[d.b - k] : s2[d.b + k]; };
-    const uint32_t a = ls < m ? (d.rev ? s1[d.a - ls] : s1[d.a + ls]) : 0u;
+    auto symB = [&](int k) -> uint32_t { return src.b(d.rev ? d.b - k : d.b + k); };
+    const uint32_t a = ls < m ? src.a(d.rev ? d.a - ls : d.a + ls) : 0u;
     int32_t Cp = d.t0 + h * (ls + 1);                 // C[i][0] = t0 + i h (:192-197)
     int32_t Ep = Cp + g;                              // e = t + g (:198)
     int32_t prev_up = ls == 0 ? 0 : d.t0 + h * ls;    // C[ls][0]; C[0][0] = 0 (:172)
@@ -257,7 +262,7 @@ __global__ __launch_bounds__(64) void mm_sweep_seg_kernel(const uint8_t* s1, con
             if (j0 >= 0 && j0 < n && ls < m) {
                 const int32_t e = max(Ep, Cp + g) + h;                  // :202
                 const int32_t dd = max(up_d, up_c + g) + h;             // :203
-                const int32_t c = max(max(dd, e), mm_diag_t<LUT, ALLOW>(prev_up, a, sym, lut, sc));
+                const int32_t c = max(max(dd, e), mm_diag_v<ALLOW>(prev_up, src.match(a, sym), sc));
                 Cp = c;
                 Ep = e;
                 prev_up = up_c;
@@ -322,8 +327,9 @@ __global__ __launch_bounds__(64) void mm_split_kernel(const DcSub* split, const 
 
 // ---------------------------------------------------------------------------- leaves
 // One sweep of buildResultRec (forward :172-238, or reversed = :247-313) into C, D [0..blen].
-template <typename Row, typename Seq>
-__device__ void mm_sweep_thread(Seq A, int alen, int rev, Seq B, int blen, int32_t t0, const uint32_t* lut,
+// (Seq / Match: as hb_leaf_solve, sa_hirschberg.hip.)
+template <typename Row, typename Seq, typename Match>
+__device__ void mm_sweep_thread(Seq A, int alen, int rev, Seq B, int blen, int32_t t0, const Match& mt,
                                 const MmScore& sc, Row C, Row D) {
     const int32_t g = sc.g, h = sc.h;
     int32_t t = g;
@@ -347,7 +353,7 @@ __device__ void mm_sweep_thread(Seq A, int alen, int rev, Seq B, int blen, int32
             const int32_t cj = C[j];
             const int32_t dj = max(D[j], cj + g) + h;
             D[j] = dj;
-            c = max(max(dj, e), mm_diag(s, dc_match(lut, ai, bj), sc));
+            c = max(max(dj, e), mm_diag(s, mt(ai, bj), sc));
             s = cj;
             C[j] = c;
         }
@@ -355,9 +361,9 @@ __device__ void mm_sweep_thread(Seq A, int alen, int rev, Seq B, int blen, int32
     D[0] = C[0];
 }
 
-template <typename Row, typename Seq>
+template <typename Row, typename Seq, typename Match>
 __device__ int mm_leaf_solve(Seq S1, Seq S2, int alen, int blen, int32_t tb0, int32_t te0, bool top, Row C, Row D,
-                             Row Cr, Row Dr, uint8_t* out, int32_t* score, const uint32_t* lut, const MmScore& sc) {
+                             Row Cr, Row Dr, uint8_t* out, int32_t* score, const Match& mt, const MmScore& sc) {
     const int32_t g = sc.g, h = sc.h;
     int k = 0;
     int stk[48][6];   // pending subproblems (x0, xl, y0, yl, tb, te); <= 3 per level of a leaf
@@ -385,14 +391,14 @@ __device__ int mm_leaf_solve(Seq S1, Seq S2, int alen, int blen, int32_t tb0, in
             int32_t best = INT_MIN;
             int index = 0;
             for (int j = 1; j <= N; ++j) {
-                const bool v = dc_match(lut, a, S2[y0 + j - 1]);
+                const bool v = mt(a, S2[y0 + j - 1]);
                 int32_t t = base;
                 if (sc.allow || v) t = max(t, g + h * (j - 1) + (v ? sc.match : sc.mismatch) + g + h * (N - j));
                 if (t > best) { best = t; index = j; }
             }
             for (int j = 1; j <= N; ++j) {
                 if (j == index) {
-                    const bool v = dc_match(lut, a, S2[y0 + j - 1]);
+                    const bool v = mt(a, S2[y0 + j - 1]);
                     if (!sc.allow && !v) { out[k++] = 'U'; out[k++] = 'L'; }   // :141-147
                     else out[k++] = v ? 'M' : 'S';
                 } else {
@@ -402,8 +408,8 @@ __device__ int mm_leaf_solve(Seq S1, Seq S2, int alen, int blen, int32_t tb0, in
             sval = best;
         } else {
             const int mid = M / 2;
-            mm_sweep_thread(S1.shifted(x0), mid, 0, S2.shifted(y0), N, tb, lut, sc, C, D);
-            mm_sweep_thread(S1.shifted(x0 + mid), M - mid, 1, S2.shifted(y0), N, te, lut, sc, Cr, Dr);
+            mm_sweep_thread(S1.shifted(x0), mid, 0, S2.shifted(y0), N, tb, mt, sc, C, D);
+            mm_sweep_thread(S1.shifted(x0 + mid), M - mid, 1, S2.shifted(y0), N, te, mt, sc, Cr, Dr);
             int index = 0, type2 = 0;
             int32_t best = INT_MIN;
             for (int j = 0; j <= N; ++j) {                          // :320-340
@@ -440,37 +446,53 @@ __device__ int mm_leaf_solve(Seq S1, Seq S2, int alen, int blen, int32_t tb0, in
 constexpr int kMmLdsCols = SA_MM_LDS_COLS;
 
 // Leaves beyond the LDS size keep their four rows at 6 * key (4 (blen + 1) <= 6 (alen + blen));
-// forward ops at stage[key], op count at mark[key].
+// forward ops at stage[key], op count at mark[key].  BITS: the generic-Ty path (symbols =
+// pair-local indices, match = the pair's bitmap).
+template <bool BITS>
 __global__ __launch_bounds__(64) void mm_leaf_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* leaves,
                                                      const uint32_t* nleaves, int32_t* scratch, uint8_t* stage,
                                                      int32_t* mark, sa_result* res, const uint32_t* lut,
-                                                     MmScore sc) {
+                                                     DcBits bits, MmScore sc) {
     __shared__ int32_t s_rows[4 * (kMmLdsCols + 1) * 64];
-    __shared__ uint8_t s_seq[2 * kMmLdsCols * 64];
+    __shared__ uint8_t s_seq[BITS ? 1 : 2 * kMmLdsCols * 64];
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= *nleaves) return;
     const int t = threadIdx.x;
     const DcSub L = leaves[id];
     const uint64_t key = L.a0 + L.b0;
-    const uint8_t* g1 = s1 + L.a0;
-    const uint8_t* g2 = s2 + L.b0;
     uint8_t* out = stage + key;
     int32_t* score = &res[L.pair].score;   // written only for a top leaf
+    const bool in_lds = L.m <= kMmLdsCols && L.n <= kMmLdsCols;
+    dc_lds_i32* r0 = (dc_lds_i32*)s_rows + t;
+    constexpr int W = (kMmLdsCols + 1) * 64;
+    int32_t* F = scratch + 6 * key;
+    const int Wg = L.n + 1;
     int k;
-    if (L.m <= kMmLdsCols && L.n <= kMmLdsCols) {
-        dc_lds_u8* q1 = (dc_lds_u8*)s_seq + t;
-        dc_lds_u8* q2 = q1 + kMmLdsCols * 64;
-        for (int c = 0; c < L.m; ++c) q1[c * 64] = g1[c];
-        for (int c = 0; c < L.n; ++c) q2[c * 64] = g2[c];
-        dc_lds_i32* r0 = (dc_lds_i32*)s_rows + t;
-        constexpr int W = (kMmLdsCols + 1) * 64;
-        k = mm_leaf_solve(LSeq{q1}, LSeq{q2}, L.m, L.n, L.tb, L.te, L.top != 0, LRow{r0}, LRow{r0 + W},
-                          LRow{r0 + 2 * W}, LRow{r0 + 3 * W}, out, score, lut, sc);
+    if constexpr (BITS) {
+        uint64_t b1, b2;
+        const DcBitsMatch mt = bits.of(L.pair, &b1, &b2);
+        const ISeq S1{(uint32_t)(L.a0 - b1)}, S2{(uint32_t)(L.b0 - b2)};
+        if (in_lds)
+            k = mm_leaf_solve(S1, S2, L.m, L.n, L.tb, L.te, L.top != 0, LRow{r0}, LRow{r0 + W}, LRow{r0 + 2 * W},
+                              LRow{r0 + 3 * W}, out, score, mt, sc);
+        else
+            k = mm_leaf_solve(S1, S2, L.m, L.n, L.tb, L.te, L.top != 0, GRow{F}, GRow{F + Wg}, GRow{F + 2 * Wg},
+                              GRow{F + 3 * Wg}, out, score, mt, sc);
     } else {
-        int32_t* F = scratch + 6 * key;
-        const int W = L.n + 1;
-        k = mm_leaf_solve(GSeq{g1}, GSeq{g2}, L.m, L.n, L.tb, L.te, L.top != 0, GRow{F}, GRow{F + W},
-                          GRow{F + 2 * W}, GRow{F + 3 * W}, out, score, lut, sc);
+        const uint8_t* g1 = s1 + L.a0;
+        const uint8_t* g2 = s2 + L.b0;
+        const DcLutMatch mt{lut};
+        if (in_lds) {
+            dc_lds_u8* q1 = (dc_lds_u8*)s_seq + t;
+            dc_lds_u8* q2 = q1 + kMmLdsCols * 64;
+            for (int c = 0; c < L.m; ++c) q1[c * 64] = g1[c];
+            for (int c = 0; c < L.n; ++c) q2[c * 64] = g2[c];
+            k = mm_leaf_solve(LSeq{q1}, LSeq{q2}, L.m, L.n, L.tb, L.te, L.top != 0, LRow{r0}, LRow{r0 + W},
+                              LRow{r0 + 2 * W}, LRow{r0 + 3 * W}, out, score, mt, sc);
+        } else {
+            k = mm_leaf_solve(GSeq{g1}, GSeq{g2}, L.m, L.n, L.tb, L.te, L.top != 0, GRow{F}, GRow{F + Wg},
+                              GRow{F + 2 * Wg}, GRow{F + 3 * Wg}, out, score, mt, sc);
+        }
     }
     if (k) mark[key] = k;
 }
@@ -478,64 +500,54 @@ __global__ __launch_bounds__(64) void mm_leaf_kernel(const uint8_t* s1, const ui
 // ---------------------------------------------------------------------------- host driver
 namespace {
 
-template <bool LUT, bool ALLOW>
-void launch_mm_sweeps_t(int R, dim3 grid, const uint8_t* d1, const uint8_t* d2, const DcSub* split,
-                        const DcLevel* lvl, int32_t* rows, const uint32_t* lut, const MmScore& sc, hipStream_t st) {
+struct MmLaunch {
+    const uint8_t* d1;
+    const uint8_t* d2;
+    const DcSub* split;
+    const DcLevel* lvl;
+    int32_t* rows;
+    const uint32_t* lut;
+    DcBits bits;
+    MmScore sc;
+};
+
+template <int MM, bool ALLOW>
+void launch_mm_sweeps_t(int R, int G, uint32_t count, const MmLaunch& a, hipStream_t st) {
     const dim3 block(64);
-    switch (R) {
-        case 1: hipLaunchKernelGGL((mm_sweep_kernel<1, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
-        case 2: hipLaunchKernelGGL((mm_sweep_kernel<2, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
-        case 4: hipLaunchKernelGGL((mm_sweep_kernel<4, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
-        case 8: hipLaunchKernelGGL((mm_sweep_kernel<8, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
-        case 16: hipLaunchKernelGGL((mm_sweep_kernel<16, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
-        default: hipLaunchKernelGGL((mm_sweep_kernel<32, LUT, ALLOW>), grid, block, 0, st, d1, d2, split, lvl, rows, lut, sc); break;
-    }
+#define SA_MM_SEG(GG)                                                                                           \
+    hipLaunchKernelGGL((mm_sweep_seg_kernel<GG, MM, ALLOW>), dim3((count + 64 / GG - 1) / (64 / GG)), block, 0, st, \
+                       a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc)
+#define SA_MM_SW(RR) \
+    hipLaunchKernelGGL((mm_sweep_kernel<RR, MM, ALLOW>), dim3(count), block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc)
+    if (G == 8) SA_MM_SEG(8);
+    else if (G == 16) SA_MM_SEG(16);
+    else if (G == 32) SA_MM_SEG(32);
+    else if (R == 1) SA_MM_SW(1);
+    else if (R == 2) SA_MM_SW(2);
+    else if (R == 4) SA_MM_SW(4);
+    else if (R == 8) SA_MM_SW(8);
+    else if (R == 16) SA_MM_SW(16);
+    else SA_MM_SW(32);
+#undef SA_MM_SEG
+#undef SA_MM_SW
 }
 
-template <bool LUT, bool ALLOW>
-void launch_mm_seg_t(int G, uint32_t count, const uint8_t* d1, const uint8_t* d2, const DcSub* split,
-                     const DcLevel* lvl, int32_t* rows, const uint32_t* lut, const MmScore& sc, hipStream_t st) {
-    const dim3 block(64);
-    if (G == 8)
-        hipLaunchKernelGGL((mm_sweep_seg_kernel<8, LUT, ALLOW>), dim3((count + 7) / 8), block, 0, st, d1, d2, split,
-                           lvl, rows, lut, sc);
-    else if (G == 16)
-        hipLaunchKernelGGL((mm_sweep_seg_kernel<16, LUT, ALLOW>), dim3((count + 3) / 4), block, 0, st, d1, d2, split,
-                           lvl, rows, lut, sc);
-    else
-        hipLaunchKernelGGL((mm_sweep_seg_kernel<32, LUT, ALLOW>), dim3((count + 1) / 2), block, 0, st, d1, d2, split,
-                           lvl, rows, lut, sc);
-}
-
-// G = 16 / 32: packed sweeps (maxa <= G); G = 0: R rows per lane, one sweep per wave.
-hipError_t launch_mm_sweeps(int R, int G, uint32_t count, const uint8_t* d1, const uint8_t* d2, const DcSub* split,
-                            const DcLevel* lvl, int32_t* rows, const uint32_t* lut, const MmScore& sc, hipStream_t st) {
-    if (G) {
-        if (lut) {
-            if (sc.allow) launch_mm_seg_t<true, true>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
-            else launch_mm_seg_t<true, false>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
-        } else {
-            if (sc.allow) launch_mm_seg_t<false, true>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
-            else launch_mm_seg_t<false, false>(G, count, d1, d2, split, lvl, rows, lut, sc, st);
-        }
-        return hipGetLastError();
-    }
-    const dim3 grid(count);
-    if (lut) {
-        if (sc.allow) launch_mm_sweeps_t<true, true>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
-        else launch_mm_sweeps_t<true, false>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
-    } else {
-        if (sc.allow) launch_mm_sweeps_t<false, true>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
-        else launch_mm_sweeps_t<false, false>(R, grid, d1, d2, split, lvl, rows, lut, sc, st);
-    }
+// G = 8 / 16 / 32: packed sweeps (maxa <= G); G = 0: R rows per lane, one sweep per wave.
+hipError_t launch_mm_sweeps(int R, int G, uint32_t count, const MmLaunch& a, hipStream_t st) {
+    const int mm = a.bits.mbits ? kMatchBits : a.lut ? kMatchLut : kMatchEq;
+    if (mm == kMatchBits) a.sc.allow ? launch_mm_sweeps_t<kMatchBits, true>(R, G, count, a, st)
+                                     : launch_mm_sweeps_t<kMatchBits, false>(R, G, count, a, st);
+    else if (mm == kMatchLut) a.sc.allow ? launch_mm_sweeps_t<kMatchLut, true>(R, G, count, a, st)
+                                         : launch_mm_sweeps_t<kMatchLut, false>(R, G, count, a, st);
+    else a.sc.allow ? launch_mm_sweeps_t<kMatchEq, true>(R, G, count, a, st)
+                    : launch_mm_sweeps_t<kMatchEq, false>(R, G, count, a, st);
     return hipGetLastError();
 }
 
 }  // namespace
 
 // Host driver: same contract as hirschberg_run (device results and op streams, enqueued on st).
-int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t* d_o1, const uint8_t* d2,
-                    const uint64_t* d_o2, uint32_t npairs, const DcBounds& b, const uint32_t* d_lutbits,
+int myersmiller_run(DcWork& w, hipEvent_t prev, const sa_scoring* scoring, const DcInputs& in, const DcBounds& b,
                     hipStream_t st, sa_result* d_res, uint8_t* d_ops, std::string* err) {
     int leaf_rows = kMmLeafRows;   // tuning override: SEQALIB_MM_LEAF (the leaf stack bounds it)
     if (const char* lr = getenv("SEQALIB_MM_LEAF")) leaf_rows = std::min(4096, std::max(2, atoi(lr)));
@@ -543,17 +555,18 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
     const bool seg_sweeps = !segenv || atoi(segenv) != 0;
     int rmax = 32;                                   // tuning: SEQALIB_DC_RMAX caps the sweep's R
     if (const char* r = getenv("SEQALIB_DC_RMAX")) rmax = std::min(32, std::max(1, atoi(r)));
+    const uint32_t npairs = in.npairs;
     MmScore sc;
     sc.g = scoring->gap_open;
     sc.h = scoring->gap_extend;
     sc.match = scoring->match;
     sc.allow = scoring->allow_mismatch != 0;
     sc.mismatch = sc.allow ? scoring->mismatch : INT_MIN;
-    static thread_local DcWork w;
-    SA_DC_HIP(w.prepare(b, npairs, leaf_rows, 3, 4, 6, st));
+    const bool bits = in.bits.mbits != nullptr;
+    SA_DC_HIP(w.prepare(b, npairs, leaf_rows, 3, 4, 6, st, prev));
     SA_DC_HIP(hipMemsetAsync(d_res, 0, sizeof(sa_result) * npairs, st));
     // getAlignment: buildResultRec(.., GapOpen, GapOpen) (:417)
-    SA_DC_HIP(dc_launch_init(d_o1, d_o2, npairs, sc.g, b, w.cur.p, d_res, st));
+    SA_DC_HIP(dc_launch_init(in.o1, in.o2, npairs, sc.g, b, w.cur.p, d_res, st));
     uint32_t cap = npairs;
     int maxm = (int)b.max_m;
     for (int l = 0;; ++l) {
@@ -565,7 +578,8 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
         int R = 1;
         while (R < rmax && 64 * R < maxa) R *= 2;   // bands of 64 R rows
         const int G = !seg_sweeps ? 0 : maxa <= 8 ? 8 : maxa <= 16 ? 16 : maxa <= 32 ? 32 : 0;
-        SA_DC_HIP(launch_mm_sweeps(R, G, 2 * splits, d1, d2, w.split.p, w.lvl.p + l, w.rows.p, d_lutbits, sc, st));
+        const MmLaunch a{in.d1, in.d2, w.split.p, w.lvl.p + l, w.rows.p, in.lutbits, in.bits, sc};
+        SA_DC_HIP(launch_mm_sweeps(R, G, 2 * splits, a, st));
         hipLaunchKernelGGL(mm_split_kernel, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p, w.next.p,
                            d_res, sc.g);
         SA_DC_HIP(hipGetLastError());
@@ -573,10 +587,14 @@ int myersmiller_run(const sa_scoring* scoring, const uint8_t* d1, const uint64_t
         cap = 3 * splits;
         maxm = maxa;
     }
-    hipLaunchKernelGGL(mm_leaf_kernel, dim3((w.leaf_cap + 63) / 64), dim3(64), 0, st, d1, d2, w.leaves.p, w.nleaf(),
-                       w.scratch.p, w.stage.p, w.mark.p, d_res, d_lutbits, sc);
+    if (bits)
+        hipLaunchKernelGGL(mm_leaf_kernel<true>, dim3((w.leaf_cap + 63) / 64), dim3(64), 0, st, in.d1, in.d2, w.leaves.p,
+                           w.nleaf(), w.scratch.p, w.stage.p, w.mark.p, d_res, in.lutbits, in.bits, sc);
+    else
+        hipLaunchKernelGGL(mm_leaf_kernel<false>, dim3((w.leaf_cap + 63) / 64), dim3(64), 0, st, in.d1, in.d2, w.leaves.p,
+                           w.nleaf(), w.scratch.p, w.stage.p, w.mark.p, d_res, in.lutbits, in.bits, sc);
     SA_DC_HIP(hipGetLastError());
-    SA_DC_HIP(dc_launch_assemble(d_o1, d_o2, npairs, w.mark.p, w.stage.p, d_res, d_ops, st));
+    SA_DC_HIP(dc_launch_assemble(in.o1, in.o2, npairs, w.mark.p, w.stage.p, d_res, d_ops, st));
     return 0;
 }
 

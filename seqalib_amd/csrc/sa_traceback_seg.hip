@@ -385,11 +385,12 @@ __global__ __launch_bounds__(256) void seg_emit_kernel(TbParams P) {
     }
 }
 
-hipError_t launch_traceback_seg(int algo, int R, bool lut, const TbParams& p, hipStream_t stream) {
+hipError_t launch_traceback_seg(int algo, int R, bool lut, const TbParams& p, hipStream_t stream, bool inject) {
     const int nst = is_affine(algo) ? 2 : 1;
     const uint32_t ntile = (p.max_n + 1 + kSegTW - 1) / kSegTW;
     const dim3 gx(ntile + 1, p.split_bands, p.count), bx(kSegTW * nst);
     const dim3 ge(1, p.split_bands, p.count), be(256);
+    const uint64_t rs = (uint64_t)nst * ((uint64_t)p.max_n + 1) + 1;   // exit records per band
     const bool tag = p.tagged != 0;
     if (p.tagged > 1) return hipErrorInvalidValue;   // two-pair records never come from SPLIT fills
 #define SA_SEG(AA, RR, LL, TT)                                                              \
@@ -397,6 +398,10 @@ hipError_t launch_traceback_seg(int algo, int R, bool lut, const TbParams& p, hi
         hipLaunchKernelGGL((seg_exit_kernel<AA, RR, LL, TT>), gx, bx, 0, stream, p);        \
         hipError_t e = hipGetLastError();                                                   \
         if (e != hipSuccess) return e;                                                      \
+        if (inject) {                                                                       \
+            e = hipMemsetAsync(p.seg_rec, 0x40, (uint64_t)p.count * p.split_bands * rs * 16, stream); \
+            if (e != hipSuccess) return e;                                                  \
+        }                                                                                   \
         hipLaunchKernelGGL((seg_emit_kernel<AA, RR, LL, TT>), ge, be, 0, stream, p);        \
         return hipGetLastError();                                                           \
     }

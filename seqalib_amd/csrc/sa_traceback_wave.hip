@@ -135,25 +135,27 @@ __global__ __launch_bounds__(64) void traceback_wave_kernel(TbParams P) {
     const int m = (int)(P.off1[pidx + 1] - o1);
     const int n = (int)(P.off2[pidx + 1] - o2);
     int seg_b = 0;
+    bool recovered = false;
     if (seg_take<ALG, R>(P, res, m, n, &seg_b)) {
-        // walked band-parallel by sa_traceback_seg.hip: apply the band where the walk stopped
-        if (lane == 0) {
-            const int4 f = P.seg_fin[slot];   // preset to -1 by the host
-            res.flags &= ~(kFlagRetry | kFlagRedo);
-            res.start_i = f.x;
-            res.start_j = f.y;
-            res.nops = (uint32_t)f.z;
-            if (f.w & 2) res.flags |= SA_FLAG_DIVERGED;
-            if (f.z < 0 || (f.w & 16)) {   // no band recorded the end, or a guard fired
-                res.start_i = -1;
-                res.start_j = -1;
-                res.nops = 0;
+        // walked band-parallel by sa_traceback_seg.hip: apply the band where the walk stopped --
+        // unless no band recorded the end or a consistency guard fired there (kSegErr): then this
+        // wave walks the pair itself (an exact result, flagged SA_FLAG_RECOVERED), never a
+        // fabricated one
+        const int4 f = P.seg_fin[slot];   // preset to -1 by the host
+        if (f.z >= 0 && !(f.w & 16)) {
+            if (lane == 0) {
+                res.flags &= ~(kFlagRetry | kFlagRedo | kFlagRerun);
+                res.start_i = f.x;
+                res.start_j = f.y;
+                res.nops = (uint32_t)f.z;
+                if (f.w & 2) res.flags |= SA_FLAG_DIVERGED;
+                P.res[pidx] = res;
             }
-            P.res[pidx] = res;
+            return;
         }
-        return;
+        recovered = true;
     }
-    res.flags &= ~(kFlagRetry | kFlagRedo);
+    res.flags &= ~(kFlagRetry | kFlagRedo | kFlagRerun);
     const uint8_t* s1 = P.seq1 + o1;
     const uint8_t* s2 = P.seq2 + o2;
     const int tagged = P.tagged;   // record layout (sa_layout.h Geom::tagged)
@@ -322,7 +324,7 @@ __global__ __launch_bounds__(64) void traceback_wave_kernel(TbParams P) {
         res.start_i = i;
         res.start_j = j;
         res.nops = k;
-        res.flags = flags;
+        res.flags = flags | (recovered ? SA_FLAG_RECOVERED : 0u);
         P.res[pidx] = res;
     }
 }

@@ -1,6 +1,7 @@
 // Drop-in check of the generic-Ty path with a WIDE alphabet: std::vector<int> sequences holding
 // more than 256 distinct values (here ~2,000), with equality, a user predicate and a nullptr
-// match fn, through all four aligners.  The drop-in build sends these batches down the
+// match fn, through the four DP aligners and the two linear-space ones (HirschbergSA,
+// MyersMillerSA).  The drop-in build sends these batches down the
 // match-bitmap path (sa_align_batch_bits); built against the unmodified reference
 // (oracle/Makefile, target ref-dropin) the same source produced tests/golden/dropin_wide.ref.txt.
 // Prints one line per alignment: Seq1 row | match bars | Seq2 row.
@@ -82,6 +83,23 @@ int main() {
         auto r = gg.getAlignment(a, b); print(r);
         GlobalGotohSA<std::vector<int>, int, -1, Fn> gg2(ScoringSystem(-3, -1, 1, -1), near);
         auto r2 = gg2.getAlignment(c, d); print(r2);
+    }
+    {
+        // (the reference's HirschbergSA calls the match fn per cell, so it needs one)
+        HirschbergSA<std::vector<int>, int, -1, Fn> hb(ScoringSystem(-1, 2, -1), eq);
+        auto r = hb.getAlignment(a, b); print(r);
+        HirschbergSA<std::vector<int>, int, -1, Fn> hb2(ScoringSystem(-1, 2, -1, false), near);
+        auto r2 = hb2.getAlignment(c, d); print(r2);
+        HirschbergSA<std::vector<int>, int, -1, Fn> hb3(ScoringSystem(-2, 1, -1), near);
+        auto r3 = hb3.getAlignment(a, d); print(r3);
+    }
+    {
+        MyersMillerSA<std::vector<int>, int, -1, Fn> mm(ScoringSystem(-3, -1, 2, -1), eq);
+        auto r = mm.getAlignment(a, b); print(r);
+        MyersMillerSA<std::vector<int>, int, -1, Fn> mm2(ScoringSystem(-3, -1, 1, -1, false), near);
+        auto r2 = mm2.getAlignment(c, d); print(r2);
+        MyersMillerSA<std::vector<int>, int, -1, Fn> mm3(ScoringSystem(-2, -1, 2, -1));   // nullptr: ==
+        auto r3 = mm3.getAlignment(b, c); print(r3);
     }
     return 0;
 }

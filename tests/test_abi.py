@@ -119,13 +119,20 @@ def test_plan_t16_eligibility_by_scoring():
     # gap 0: the clamped up term needs gap < 0
     assert sa.plan_query_ex(0, sa.ScoringSystem(0, 1, -1), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32
     # affine (T16 affine kernel): LocalGotoh at any size (retry above the int16 headroom),
-    # GlobalGotoh while the affine path bounds fit 8*(V - delta); no mismatches allowed -> int32
+    # GlobalGotoh while the affine path bounds fit 8*(V - delta); no mismatches allowed -> T16 too
+    # (mismatch' = 2 (GO + GE) - 1 never wins, like the reference's INT_MIN), unless mismatch'
+    # leaves the int8 profile
     aff = sa.ScoringSystem(-3, -1, 1, -1)
     assert sa.plan_query_ex(2, aff, 1024, 1024, 10000)[:3] == (sa.SA_KERNEL_T16_ENDCELL, 16, 1)
     assert sa.plan_query_ex(2, aff, 8192, 8192, 10000)[0] == sa.SA_KERNEL_T16_ENDCELL
     assert sa.plan_query_ex(3, aff, 2048, 2048, 10000)[:3] == (sa.SA_KERNEL_T16, 16, 1)
     assert sa.plan_query_ex(3, aff, 4096, 4096, 10000)[0] == sa.SA_KERNEL_INT32
-    assert sa.plan_query_ex(2, sa.ScoringSystem(-3, -1, 1, -1, False), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32
+    assert sa.plan_query_ex(2, sa.ScoringSystem(-3, -1, 1, -1, False), 1024, 1024, 10000)[0] == sa.SA_KERNEL_T16_ENDCELL
+    assert sa.plan_query_ex(2, sa.ScoringSystem(-3, -1, 1, -1, False), 8192, 8192, 1)[0] == sa.SA_KERNEL_T16_ENDCELL
+    assert sa.plan_query_ex(2, sa.ScoringSystem(-9, -1, 1, -1, False), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32
+    assert sa.plan_query_ex(0, sa.ScoringSystem(-2, 1, -1, False), 1024, 1024, 10000)[0] == sa.SA_KERNEL_T16_ENDCELL
+    assert sa.plan_query_ex(1, sa.ScoringSystem(-1, 2), 1024, 1024, 10000)[0] == sa.SA_KERNEL_T16
+    assert sa.plan_query_ex(0, sa.ScoringSystem(-20, 1, -1, False), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32
     assert sa.plan_query_ex(2, sa.ScoringSystem(-3, 0, 1, -1), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32
     assert sa.plan_query_ex(2, aff, 1024, 1024, 10000, nsym=5)[0] == sa.SA_KERNEL_INT32
 

@@ -12,7 +12,8 @@ from util import oracle_align_matrix
 pytestmark = pytest.mark.gpu
 
 SCORINGS = {0: [(-1, 2, -1), (-2, 1, -1, False)], 1: [(-1, 2, -1), (-1, 2)],
-            2: [(-3, -1, 2, -1), (-3, -1, 1, -1, False)], 3: [(-3, -1, 2, -1)]}
+            2: [(-3, -1, 2, -1), (-3, -1, 1, -1, False)], 3: [(-3, -1, 2, -1)],
+            4: [(-1, 2, -1), (-2, 1, -1, False)], 5: [(-3, -1, 2, -1), (-3, -1, 1, -1, False)]}
 PREDICATES = {"equal": None, "near": lambda x, y: abs(x - y) <= 2, "mod7": lambda x, y: x % 7 == y % 7}
 
 
@@ -63,10 +64,12 @@ def check(engine, algo, args, pairs, match):
         assert r.flags & ~sa.SA_FLAG_SIZE_HACK == 0
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+@pytest.mark.parametrize("algo", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("pred", list(PREDICATES))
 def test_generic_ints_vs_oracle(engine, algo, pred):
-    """Lists of ints, ~5000 distinct values per batch, few pairs (one wave per pair traceback)."""
+    """Lists of ints, ~5000 distinct values per batch, few pairs (one wave per pair traceback);
+    HirschbergSA / MyersMillerSA (4, 5) run their whole-wave and packed sweeps and their leaves on
+    pair-local indices and the pairs' bitmaps (SAHirschberg.h:74, :90; SAMyersMiller.h:24-37)."""
     pairs = int_pairs(10 + algo, 24, 50, 700)
     pairs += [([], [1, 2, 3]), ([4], []), (list(range(1000, 1314)), list(range(1100, 1388)))]   # empty, size hack
     distinct = {x for a, b in pairs for x in a + b}
@@ -100,9 +103,19 @@ def test_generic_objects_unhashable(engine):
 def test_bits_path_equals_symbol_path(engine):
     """DNA through the bitmap path gives exactly what the byte-symbol path gives."""
     pairs = [(sa.synth_dna(300 + k, 200 + 37 * k), sa.synth_dna(400 + k, 180 + 29 * k)) for k in range(40)]
-    for algo, args in ((0, (-1, 1, -1)), (1, (-1, 2, -1)), (2, (-3, -1, 1, -1)), (3, (-3, -1, 1, -1))):
+    for algo, args in ((0, (-1, 1, -1)), (1, (-1, 2, -1)), (2, (-3, -1, 1, -1)), (3, (-3, -1, 1, -1)),
+                       (4, (-1, 2, -1)), (5, (-3, -1, 1, -1))):
         ref = engine.align(algo, sa.ScoringSystem(*args), pairs)
         got = engine.align_generic(algo, sa.ScoringSystem(*args), [(list(a), list(b)) for a, b in pairs])
         for r, g in zip(ref, got):
             assert (r.score, r.end_i, r.end_j, r.start_i, r.start_j, r.ops) == \
                    (g.score, g.end_i, g.end_j, g.start_i, g.start_j, g.ops)
+
+
+@pytest.mark.parametrize("algo", [4, 5])
+def test_generic_linear_space_batch(engine, algo):
+    """HirschbergSA / MyersMillerSA over a batch of 300 wide-alphabet pairs up to 1,500 long
+    (several device levels with R = 16 whole-wave sweeps, then packed sweeps and leaves), against
+    the matrix-driven oracle."""
+    pairs = int_pairs(60 + algo, 300, 10, 400, vocab=4000) + int_pairs(70 + algo, 4, 1200, 1500, vocab=4000)
+    check(engine, algo, SCORINGS[algo][0], pairs, PREDICATES["near"])

@@ -307,8 +307,14 @@ def test_t16_eligibility(engine, algo):
     if algo == 1:
         compare_with_oracle(engine, algo, (-1, 5, -1), big)
         assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
-    # !allowMismatch -> int32 kernel
+    # !allowMismatch runs T16 with a mismatch score below 2 * gap, which never wins a max (as the
+    # reference's INT_MIN diagonal): t16_mode, sa_api.hip
     compare_with_oracle(engine, algo, (-2, 1, -1, False), dna)
+    assert engine.last_plan()[0] in T16_KERNELS
+    compare_with_oracle(engine, algo, (-1, 2), dna)   # the 2-argument ScoringSystem: !allow too
+    assert engine.last_plan()[0] in T16_KERNELS
+    # ... unless that score does not fit the int8 profile (gap -20: mismatch' = -41)
+    compare_with_oracle(engine, algo, (-20, 1, -1, False), dna)
     assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
     if algo == 0:
         # SW with gap 0: the T16 cell folds the zero clamp into a saturating up term, which needs
@@ -347,7 +353,8 @@ def test_t16_affine_eligibility_and_retry(engine):
     """T16 affine kernel choice and headroom: LocalGotoh runs T16 at any size and re-runs on int32
     exactly the pairs whose maximum passes 4095 - match (8*M in int16), on the batch plan and the
     few-pairs plan; GlobalGotoh runs T16 while its affine path bounds fit (2048^2) and int32
-    beyond (the reference's 4096^2 GlobalGotoh probe); !allowMismatch and five symbols -> int32."""
+    beyond (the reference's 4096^2 GlobalGotoh probe); !allowMismatch on T16 too (config 4's
+    scoring, the reference's 8192^2 probe); five symbols -> int32."""
     lg = (-3, -1, 1, -1, True)
     rng = np.random.default_rng(29)
     pairs = [(sa.synth_dna(90_000 + k, int(rng.integers(50, 300))), sa.synth_dna(91_000 + k, int(rng.integers(50, 300))))
@@ -372,6 +379,14 @@ def test_t16_affine_eligibility_and_retry(engine):
         assert engine.last_plan()[0] == sa.SA_KERNEL_T16_ENDCELL, pid
     dna = dna_pairs(31, 6, 400)
     compare_with_oracle(engine, 2, (-3, -1, 1, -1, False), dna)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16_ENDCELL
+    compare_with_oracle(engine, 3, (-3, -1, 1, -1, False), dna)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    compare_with_oracle(engine, 2, (-3, -1, 1, -1, False), pairs)   # batch plan, retried pairs
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16_ENDCELL
+    assert check_golden(engine, [big["probe8192/lg/-3_-1_1_-1_0/equal"]]) == 1   # config 4
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16_ENDCELL
+    compare_with_oracle(engine, 2, (-9, -1, 1, -1, False), dna)   # 2 * GOE - 1 = -21: no int8 room
     assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
     five = dna[:-1] + [(dna[-1][0] + b"N", dna[-1][1])]
     compare_with_oracle(engine, 3, gg, five)

@@ -113,7 +113,8 @@ def test_oracle_batch_matches_single():
 
 def test_oracle_matrix_form_matches_symbol_form():
     """oracle_align_matrix (generic Ty: an m x n match matrix) equals oracle_align on byte symbols
-    whose match matrix it is, for every algorithm with a bitmap path, equality and a LUT."""
+    whose match matrix it is, for every algorithm (HirschbergSA and MyersMillerSA included: their
+    match is taken by position there), equality and a LUT."""
     import numpy as np
     from util import oracle_align_matrix
     import seqalib_amd as sa
@@ -121,7 +122,8 @@ def test_oracle_matrix_form_matches_symbol_form():
     pairs = [(sa.synth_dna(70 + k, 30 + 17 * k), sa.synth_mutate(sa.synth_dna(70 + k, 30 + 17 * k), k)) for k in range(10)]
     pairs += [(b"", b"ACG"), (b"A", b""), (b"A" * 314, b"C" * 288)]   # empty sides, LocalGotoh size hack
     for algo, args in ((0, (-1, 1, -1)), (0, (-2, 1, -1, False)), (1, (-1, 2, -1)), (1, (-1, 2)),
-                       (2, (-3, -1, 1, -1)), (2, (-3, -1, 1, -1, False)), (3, (-3, -1, 1, -1))):
+                       (2, (-3, -1, 1, -1)), (2, (-3, -1, 1, -1, False)), (3, (-3, -1, 1, -1)),
+                       (4, (-1, 2, -1)), (4, (-2, 1, -1, False)), (5, (-3, -1, 2, -1)), (5, (-3, -1, 1, -1, False))):
         for table in (None, lut):
             for a, b in pairs:
                 av = np.frombuffer(a, np.uint8) if a else np.zeros(0, np.uint8)
@@ -152,3 +154,19 @@ def test_match_bitmaps_layout():
                 for j in range(n):
                     exp = (a[i] == b[j]) if match is None else near(a[i], b[j])
                     assert bool((int(w[i, j // 32]) >> (j % 32)) & 1) == bool(exp)
+
+
+def test_match_bitmaps_type_sensitive_predicate():
+    """Symbols that hash and compare equal but differ in type (1, 1.0, True) are not merged: a
+    MatchFnTy that tells them apart gets the per-cell answers the reference's cacheAllMatches
+    would record."""
+    import numpy as np
+    import seqalib_amd as sa
+    a = [1, 1.0, True, 2]
+    b = [True, 1, 1.0, 2.0]
+    same = lambda x, y: x == y and type(x) is type(y)
+    off1, off2, bits, bits_off = sa.match_bitmaps([(a, b)], same)
+    w = int(bits[0]), int(bits[1]), int(bits[2]), int(bits[3])
+    for i in range(4):
+        for j in range(4):
+            assert bool((w[i] >> j) & 1) == same(a[i], b[j]), (i, j)
