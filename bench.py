@@ -57,9 +57,13 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pairs", type=int, default=10000, help="pairs per GPU")
     ap.add_argument("--len", type=int, default=4096, help="length of both sequences")
-    ap.add_argument("--cpu-pairs", type=int, default=256, help="CPU baseline sample, all-core leg (pairs)")
+    ap.add_argument("--cpu-pairs", type=int, default=0,
+                    help="CPU baseline sample, all-core leg (pairs; 0 = 64 per thread, ~10 s)")
     ap.add_argument("--cpu-pairs-1t", type=int, default=12, help="CPU baseline sample, 1-thread leg (pairs)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
+    ap.add_argument("--dropin-pairs", type=int, default=10000,
+                    help="C++ drop-in end-to-end leg (tests/cpp/dropin_bench): pairs (0 = skip)")
+    ap.add_argument("--dropin-reps", type=int, default=3)
     ap.add_argument("--e2e-steps", type=int, default=2,
                     help="host-API steps (H2D + fill + traceback + D2H of results and ops) timed after the run")
     ap.add_argument("--no-cpu", action="store_true")
@@ -112,11 +116,32 @@ def shard_seed_base(rank: int, world: int, pairs_per_gpu: int) -> int:
     return SEED_BASE + 2 * start
 
 
+def host_cores():
+    """Cores this process may use: its CPU affinity, capped by the cgroup CPU quota (a GPU box
+    shows the whole machine in os.cpu_count() but grants a share of it)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except Exception:
+        pass
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota_cores": quota,
+            "usable": min(aff, quota) if quota else aff}
+
+
 def cpu_baseline(args, s1, o1, s2, o2, threads=None, pairs=None):
     """The reference (oracle/_ref, compiled from /root/reference) — or the oracle port if that is
-    not built — on a bounded sample of the same pairs, on the host cores."""
-    k = min(pairs or args.cpu_pairs, len(o1) - 1)
-    threads = max(1, min(threads or args.cpu_threads, os.cpu_count() or 1))
+    not built — on a bounded sample of the same pairs, on the host cores (all usable cores by
+    default)."""
+    hc = host_cores()
+    threads = max(1, threads or args.cpu_threads or hc["usable"])
+    k = min(pairs or args.cpu_pairs or 64 * threads, len(o1) - 1)
     sub1, sub2 = s1[: int(o1[k])].copy(), s2[: int(o2[k])].copy()
     so1, so2 = o1[: k + 1].copy(), o2[: k + 1].copy()
     cells = float(np.sum((so1[1:] - so1[:-1]).astype(np.float64) * (so2[1:] - so2[:-1])))
@@ -143,8 +168,26 @@ def cpu_baseline(args, s1, o1, s2, o2, threads=None, pairs=None):
         kind = "port"
         what = "oracle/sa_oracle.c SW (full-matrix restatement)"
     return {"value": round(cells / dt / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": kind,
+            "nproc": hc["nproc"], "affinity": hc["affinity"], "cgroup_quota_cores": hc["cgroup_quota_cores"],
             "sample": f"first {k} pairs of this rank's batch ({args.len}x{args.len}), {what}, "
                       f"{threads} threads, {dt:.2f} s wall"}
+
+
+def dropin_e2e(args):
+    """The C++ drop-in exactly as a SeqALib user calls it (tests/cpp/dropin_bench.cpp:
+    SmithWatermanSA<std::string, char, '-'>::getAlignments over host std::strings, symbol coding,
+    host API (pinned chunked upload, fill, traceback, download) and every AlignedSequence's
+    std::list), run as a child process after the timed region."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "cpp", "dropin_bench")
+    if args.dropin_pairs <= 0 or not os.path.exists(exe):
+        return None
+    try:
+        out = subprocess.run([exe, str(args.dropin_pairs), str(args.len), str(args.dropin_reps)],
+                             capture_output=True, text=True, timeout=300, check=True).stdout
+        return json.loads(out.strip().splitlines()[-1])
+    except Exception as e:   # reported, never fatal for the bench line
+        return {"error": str(e)[:200]}
 
 
 def load_pmc_traffic(workload: str):
@@ -303,11 +346,15 @@ def main():
         "fill_ms": round(fill_ms, 2), "endcell_traceback_ms": round(tb_ms, 2),
         "e2e_ms_per_step": round(e2e_ms, 2) if e2e_ms else None,
         "e2e_gcups": round(world * cells_rank / (e2e_ms / 1e3) / 1e9, 1) if e2e_ms else None,
-        "e2e_basis": "host API sa_align_batch: pageable H2D of sequences + offsets, fill, end cell, traceback, "
-                     "D2H of results and op streams, one call at a time",
+        "e2e_basis": "host API sa_align_batch from pageable host buffers: pinned, chunked and pipelined "
+                     "upload of sequences + offsets, fill, end cell, traceback, download of results and op "
+                     "streams; one call at a time",
         "pipelined": pipelined, "serial_ms_per_step": round(serial_ms, 2) if serial_ms else None,
         "parity": f"{checked - bad}/{checked} sampled pairs bit-exact vs oracle, {int(np.count_nonzero(res['flags']))} flagged",
     }
+    if world == 1:
+        eng.L.sa_trim(eng.h)   # free this process's workspace for the child's
+        line["dropin_e2e"] = dropin_e2e(args)
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args, s1, o1, s2, o2)
         line["cpu_baseline_1thread"] = cpu_baseline(args, s1, o1, s2, o2, threads=1, pairs=args.cpu_pairs_1t)

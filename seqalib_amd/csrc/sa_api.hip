@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sa_dc.h"
@@ -50,7 +51,10 @@ struct sa_ctx {
     uint64_t split_bytes = 0;
     // HirschbergSA / MyersMillerSA level-loop buffers and the host API's pinned upload staging
     sa::DcWork dc;
-    sa::HostBuf<uint8_t> stage;
+    sa::HostBuf<uint8_t> stage, ostage;
+    // host API: download stream and per-chunk events (align_host)
+    hipStream_t s_out = nullptr;
+    std::vector<hipEvent_t> host_ev;
     // Calls on one context are ordered: every call's stream waits for ev_last, the end of the
     // last un-pipelined call (whatever stream it ran on), since they share the workspace, the
     // I/O cache and the DC buffers.
@@ -94,6 +98,7 @@ int drain(sa_ctx* c) {
     SA_HIP(c, hipStreamSynchronize(c->stream));
     if (c->s_fill) SA_HIP(c, hipStreamSynchronize(c->s_fill));
     if (c->s_tb) SA_HIP(c, hipStreamSynchronize(c->s_tb));
+    if (c->s_out) SA_HIP(c, hipStreamSynchronize(c->s_out));
     if (c->ev_last_set) SA_HIP(c, hipEventSynchronize(c->ev_last));
     return SA_OK;
 }
@@ -159,7 +164,8 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t
     // tuning override: SEQALIB_PLAN="R,W" (W = 0: SPLIT plan with R in {1, 2, 4, 8})
     if (const char* ov = getenv("SEQALIB_PLAN")) {
         int r = 0, w = 0;
-        if (sscanf(ov, "%d,%d", &r, &w) == 2 && w == 0 && (r == 1 || r == 2 || r == 4 || r == 8)) {
+        // (never for a plan that must not be SPLIT: the SPLIT fallback of build_variants)
+        if (sscanf(ov, "%d,%d", &r, &w) == 2 && w == 0 && allow_split && (r == 1 || r == 2 || r == 4 || r == 8)) {
             p.R = r;
             p.W = 1;
             p.split = true;
@@ -753,6 +759,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             if (e != hipSuccess) return hip_fail(c, e, "traceback kernel launch");
         }
         if (has_fb) {
+            if (vars[nv].pl.split) return fail(c, SA_ERR_UNSUPPORTED, "internal: SPLIT fallback plan");
             // SPLIT fallback, after every traceback of this launch (it rewrites the records of the
             // pairs it re-runs): fill + traceback of exactly the pairs flagged SA_FLAG_TIMEOUT,
             // launches that return at once when there is none
@@ -825,24 +832,76 @@ int lg_hack_split(sa_ctx* c, const uint64_t* off1, const uint64_t* off2, uint32_
     return SA_OK;
 }
 
+// Host copy of a large buffer on several threads (the caller's pageable memory <-> pinned
+// staging; one thread copies ~5-10 GB/s).
+void par_copy(void* dst, const void* src, uint64_t n) {
+    constexpr uint64_t kPiece = 4ull << 20;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const uint64_t T = std::min<uint64_t>(std::min(8u, hw), n / kPiece);
+    if (T < 2) {
+        if (n) memcpy(dst, src, n);
+        return;
+    }
+    const uint64_t part = (n / T + 4095) & ~(uint64_t)4095;
+    std::vector<std::thread> th;
+    for (uint64_t t = 1; t < T; ++t) {
+        const uint64_t a = t * part;
+        if (a >= n) break;
+        th.emplace_back([=] { memcpy((uint8_t*)dst + a, (const uint8_t*)src + a, std::min(part, n - a)); });
+    }
+    memcpy(dst, src, std::min(part, n));
+    for (auto& x : th) x.join();
+}
+
+// Host API batches are cut into contiguous pair ranges ("chunks") of near-equal cells and run
+// through the cross-call pipeline, so chunk g+1's upload and chunk g-1's download overlap chunk
+// g's fill and traceback.  A chunk must still fill the chip (every fill launch has a tail), so
+// batches below 2 x kHostChunkPairs stay one chunk.  SEQALIB_HOST_CHUNKS overrides (tuning).
+constexpr uint32_t kHostChunkPairs = 4096;
+uint32_t host_chunks(int algo, uint32_t npairs) {
+    if (algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER) return 1;   // one DC work set per context
+    uint32_t G = npairs >= 2 * kHostChunkPairs ? std::min<uint32_t>(4, npairs / kHostChunkPairs) : 1;
+    if (G == 3) G = 2;
+    if (const char* e = getenv("SEQALIB_HOST_CHUNKS")) G = (uint32_t)std::max(1, atoi(e));
+    return std::max<uint32_t>(1, std::min(G, npairs));
+}
+
+// contiguous [cut[g], cut[g+1]) ranges with near-equal sum of m*n
+std::vector<uint32_t> cut_by_cells(const uint64_t* off1, const uint64_t* off2, uint32_t npairs, uint32_t parts) {
+    std::vector<double> csum(npairs + 1, 0.0);
+    for (uint32_t p = 0; p < npairs; ++p)
+        csum[p + 1] = csum[p] + (double)(off1[p + 1] - off1[p]) * (double)(off2[p + 1] - off2[p]) + 1.0;
+    std::vector<uint32_t> cut(parts + 1, npairs);
+    cut[0] = 0;
+    uint32_t p = 0;
+    for (uint32_t g = 1; g < parts; ++g) {
+        const double target = csum[npairs] * (double)g / (double)parts;
+        while (p < npairs && csum[p] < target) ++p;
+        cut[g] = std::max(p, cut[g - 1]);
+    }
+    return cut;
+}
+
 int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, const uint64_t* off1,
                const uint8_t* seq2, const uint64_t* off2, uint32_t npairs, const uint8_t* lut,
                sa_result* results, uint8_t* ops, uint64_t ops_cap) {
     const uint64_t t1 = off1[npairs], t2 = off2[npairs];
-    uint32_t max_m = 0, max_n = 0;
-    for (uint32_t p = 0; p < npairs; ++p) {
+    for (uint32_t p = 0; p < npairs; ++p)
         if (off1[p + 1] < off1[p] || off2[p + 1] < off2[p]) return fail(c, SA_ERR_ARG, "offsets must be non-decreasing");
-        max_m = (uint32_t)std::max<uint64_t>(max_m, off1[p + 1] - off1[p]);
-        max_n = (uint32_t)std::max<uint64_t>(max_n, off2[p + 1] - off2[p]);
-    }
     const uint64_t ops_total = t1 + t2 + npairs;
     if (ops_cap < ops_total) return fail(c, SA_ERR_CAPACITY, "ops buffer needs " + std::to_string(ops_total) + " bytes");
+    if (!npairs) return SA_OK;
     const bool use_lut = lut && !lut_is_identity(lut);
+    const bool dc = algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER;
+    const uint32_t G = host_chunks(algo, npairs);
+    const std::vector<uint32_t> cut = cut_by_cells(off1, off2, npairs, G);
 
-    // device I/O layout (16-byte aligned pieces)
+    // device I/O layout (256-byte aligned pieces); chunk g's offsets (rebased to its first pair)
+    // live at do1 / do2 + cut[g] + g
     auto al = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
-    const uint64_t b_s1 = al(t1 + 1), b_s2 = al(t2 + 1), b_o = al(8ull * (npairs + 1));
-    const uint64_t b_res = al(sizeof(sa_result) * (uint64_t)std::max<uint32_t>(npairs, 1));
+    const uint64_t n_off = (uint64_t)npairs + G;
+    const uint64_t b_s1 = al(t1 + 1), b_s2 = al(t2 + 1), b_o = al(8 * n_off);
+    const uint64_t b_res = al(sizeof(sa_result) * (uint64_t)npairs);
     const uint64_t b_ops = al(ops_total + 1), b_lut = al(65536), b_bits = al(8192);
     const uint64_t io_need = b_s1 + b_s2 + 2 * b_o + b_res + b_ops + b_lut + b_bits;
     if (int rc = ensure_io(c, io_need)) return rc;
@@ -855,56 +914,90 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     uint8_t* dops = p; p += b_ops;
     uint8_t* dlut = p; p += b_lut;
     uint32_t* dbits = reinterpret_cast<uint32_t*>(p);
-    hipStream_t st = c->stream;
-    const bool dc = algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER;
-    if (dc) {
-        // upload from pinned staging (a pageable copy inside a process that also runs PyTorch was
-        // measured to stall 10-25 ms per call)
-        const uint64_t bo = 8ull * (npairs + 1);
-        SA_HIP(c, c->stage.alloc(t1 + t2 + 2 * bo));
-        uint8_t* q = c->stage.data();
-        memcpy(q, seq1, t1);
-        memcpy(q + t1, seq2, t2);
-        memcpy(q + t1 + t2, off1, bo);
-        memcpy(q + t1 + t2 + bo, off2, bo);
-        if (t1) SA_HIP(c, hipMemcpyAsync(d1, q, t1, hipMemcpyHostToDevice, st));
-        if (t2) SA_HIP(c, hipMemcpyAsync(d2, q + t1, t2, hipMemcpyHostToDevice, st));
-        SA_HIP(c, hipMemcpyAsync(do1, q + t1 + t2, bo, hipMemcpyHostToDevice, st));
-        SA_HIP(c, hipMemcpyAsync(do2, q + t1 + t2 + bo, bo, hipMemcpyHostToDevice, st));
-    } else {
-        if (t1) SA_HIP(c, hipMemcpyAsync(d1, seq1, t1, hipMemcpyHostToDevice, st));
-        if (t2) SA_HIP(c, hipMemcpyAsync(d2, seq2, t2, hipMemcpyHostToDevice, st));
-        SA_HIP(c, hipMemcpyAsync(do1, off1, 8ull * (npairs + 1), hipMemcpyHostToDevice, st));
-        SA_HIP(c, hipMemcpyAsync(do2, off2, 8ull * (npairs + 1), hipMemcpyHostToDevice, st));
+    // pinned staging (pageable copies were measured to stall 10-25 ms per call next to PyTorch):
+    // in = [seq1][seq2][off1'][off2'], out = [results][ops]
+    SA_HIP(c, c->stage.alloc(t1 + t2 + 16 * n_off));
+    SA_HIP(c, c->ostage.alloc(sizeof(sa_result) * (uint64_t)npairs + ops_total));
+    uint8_t* const si = c->stage.data();
+    uint64_t* const so1 = reinterpret_cast<uint64_t*>(si + t1 + t2);
+    uint64_t* const so2 = so1 + n_off;
+    sa_result* const sres = reinterpret_cast<sa_result*>(c->ostage.data());
+    uint8_t* const sops = c->ostage.data() + sizeof(sa_result) * (uint64_t)npairs;
+    const bool pipe = G > 1;
+    if (!c->s_out) SA_HIP(c, hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking));
+    if (pipe && !c->s_fill) {
+        SA_HIP(c, hipStreamCreateWithFlags(&c->s_fill, hipStreamNonBlocking));
+        SA_HIP(c, hipStreamCreateWithFlags(&c->s_tb, hipStreamNonBlocking));
+        SA_HIP(c, hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     }
+    while (c->host_ev.size() < 2 * (size_t)G) {
+        hipEvent_t ev;
+        SA_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        c->host_ev.push_back(ev);
+    }
+    hipStream_t st = c->stream;   // uploads (and, un-pipelined, the kernels)
     if (use_lut) {
         SA_HIP(c, hipMemcpyAsync(dlut, lut, 65536, hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(lut_to_bits, dim3(8), dim3(256), 0, st, dlut, dbits);
         SA_HIP(c, hipGetLastError());
     }
-    if (npairs && dc) {
-        std::string e;
-        c->launches = 0;
-        const auto run = algo == SA_HIRSCHBERG ? hirschberg_run : myersmiller_run;
-        DcBounds b;
-        b.t1 = t1;
-        b.t2 = t2;
-        b.max_m = max_m;
-        b.max_n = max_n;
-        const DcInputs in{d1, do1, d2, do2, npairs, use_lut ? dbits : nullptr, DcBits{}};
-        if (run(c->dc, c->ev_last_set ? c->ev_last : nullptr, sc, in, b, st, dres, dops, &e))
-            return fail(c, SA_ERR_HIP, (algo == SA_HIRSCHBERG ? "hirschberg: " : "myers-miller: ") + e);
-        SA_HIP(c, hipMemcpyAsync(results, dres, sizeof(sa_result) * npairs, hipMemcpyDeviceToHost, st));
-        SA_HIP(c, hipMemcpyAsync(ops, dops, ops_total, hipMemcpyDeviceToHost, st));
-        SA_HIP(c, hipStreamSynchronize(st));
-        return SA_OK;
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t p0 = cut[g], p1 = cut[g + 1], cnt = p1 - p0;
+        if (!cnt) continue;
+        const uint64_t a1 = off1[p0], a2 = off2[p0], n1 = off1[p1] - a1, n2 = off2[p1] - a2;
+        const uint64_t ob = a1 + a2 + p0, on = off1[p1] + off2[p1] + p1 - ob;   // the chunk's op bytes
+        uint32_t mm = 0, mn = 0;
+        for (uint32_t q = 0; q <= cnt; ++q) {
+            so1[p0 + g + q] = off1[p0 + q] - a1;
+            so2[p0 + g + q] = off2[p0 + q] - a2;
+            if (q) {
+                mm = (uint32_t)std::max<uint64_t>(mm, off1[p0 + q] - off1[p0 + q - 1]);
+                mn = (uint32_t)std::max<uint64_t>(mn, off2[p0 + q] - off2[p0 + q - 1]);
+            }
+        }
+        par_copy(si + a1, seq1 + a1, n1);
+        par_copy(si + t1 + a2, seq2 + a2, n2);
+        if (n1) SA_HIP(c, hipMemcpyAsync(d1 + a1, si + a1, n1, hipMemcpyHostToDevice, st));
+        if (n2) SA_HIP(c, hipMemcpyAsync(d2 + a2, si + t1 + a2, n2, hipMemcpyHostToDevice, st));
+        SA_HIP(c, hipMemcpyAsync(do1 + p0 + g, so1 + p0 + g, 8ull * (cnt + 1), hipMemcpyHostToDevice, st));
+        SA_HIP(c, hipMemcpyAsync(do2 + p0 + g, so2 + p0 + g, 8ull * (cnt + 1), hipMemcpyHostToDevice, st));
+        hipStream_t done = st;
+        if (dc) {
+            std::string e;
+            c->launches = 0;
+            const auto run = algo == SA_HIRSCHBERG ? hirschberg_run : myersmiller_run;
+            DcBounds b;
+            b.t1 = n1;
+            b.t2 = n2;
+            b.max_m = mm;
+            b.max_n = mn;
+            const DcInputs in{d1 + a1, do1 + p0 + g, d2 + a2, do2 + p0 + g, cnt, use_lut ? dbits : nullptr, DcBits{}};
+            if (run(c->dc, c->ev_last_set ? c->ev_last : nullptr, sc, in, b, st, dres + p0, dops + ob, &e))
+                return fail(c, SA_ERR_HIP, (algo == SA_HIRSCHBERG ? "hirschberg: " : "myers-miller: ") + e);
+        } else {
+            int rc = run_device(c, algo, sc, d1 + a1, do1 + p0 + g, d2 + a2, do2 + p0 + g, cnt, mm, mn,
+                                use_lut ? dbits : nullptr, dres + p0, dops + ob, st, pipe);
+            if (rc) return rc;
+            if (pipe) done = c->s_tb;   // the chunk's last kernel (its traceback) ran there
+        }
+        SA_HIP(c, hipEventRecord(c->host_ev[2 * g], done));
+        SA_HIP(c, hipStreamWaitEvent(c->s_out, c->host_ev[2 * g], 0));
+        SA_HIP(c, hipMemcpyAsync(sres + p0, dres + p0, sizeof(sa_result) * cnt, hipMemcpyDeviceToHost, c->s_out));
+        SA_HIP(c, hipMemcpyAsync(sops + ob, dops + ob, on, hipMemcpyDeviceToHost, c->s_out));
+        SA_HIP(c, hipEventRecord(c->host_ev[2 * g + 1], c->s_out));
     }
-    if (npairs) {
-        int rc = run_device(c, algo, sc, d1, do1, d2, do2, npairs, max_m, max_n,
-                            use_lut ? dbits : nullptr, dres, dops, st);
-        if (rc) return rc;
-        SA_HIP(c, hipMemcpyAsync(results, dres, sizeof(sa_result) * npairs, hipMemcpyDeviceToHost, st));
-        SA_HIP(c, hipMemcpyAsync(ops, dops, ops_total, hipMemcpyDeviceToHost, st));
+    // each chunk's results reach the caller's buffers while later chunks still run
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t p0 = cut[g], p1 = cut[g + 1];
+        if (p1 == p0) continue;
+        SA_HIP(c, hipEventSynchronize(c->host_ev[2 * g + 1]));
+        const uint64_t ob = off1[p0] + off2[p0] + p0, on = off1[p1] + off2[p1] + p1 - ob;
+        memcpy(results + p0, sres + p0, sizeof(sa_result) * (p1 - p0));
+        par_copy(ops + ob, sops + ob, on);
+    }
+    if (pipe) {
+        SA_HIP(c, hipStreamSynchronize(c->s_fill));
+        SA_HIP(c, hipStreamSynchronize(c->s_tb));
     }
     SA_HIP(c, hipStreamSynchronize(st));
     return SA_OK;
@@ -1019,7 +1112,10 @@ void sa_destroy(sa_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)drain(c);
+    if (c->s_out) (void)hipStreamSynchronize(c->s_out);
     for (auto ev : c->events) (void)hipEventDestroy(ev);
+    for (auto ev : c->host_ev) (void)hipEventDestroy(ev);
+    if (c->s_out) (void)hipStreamDestroy(c->s_out);
     for (auto ev : {c->ev_in, c->ev_slot[0], c->ev_slot[1], c->ev_sel, c->ev_last})
         if (ev) (void)hipEventDestroy(ev);
     if (c->s_fill) (void)hipStreamDestroy(c->s_fill);

@@ -109,6 +109,14 @@ constexpr int fill_max_threads() { return (R >= 32 || (WIDE && R >= 16)) ? 256 :
 // waiting altogether: the pair is flagged SA_FLAG_TIMEOUT and re-run by the call's
 // single-workgroup fallback launch (run_device, sa_api.hip).
 
+// SPLIT hand-off granule: a band publishes its last row every kHandGran steps (lanes 0..7 store
+// the values lane 63 parked in LDS), and its consumer polls kHandGran columns at a time, each
+// group prefetched one group ahead.  With the 32-column chunks of round 2 a band ran ~161 steps
+// behind its producer (63 inherent, ~64 chunk quantisation, the rest latency); the inherent
+// lag plus one granule at each end plus the poll latency is ~90 (tools/split_stats.py).
+constexpr int kHandGran = 8;
+static_assert(kChunk % kHandGran == 0, "granules tile a chunk");
+
 #ifdef SA_TB_STATS
 // Debug build only (-DSA_TB_STATS, tools/split_stats.py): per SPLIT ticket {slot * bands + band,
 // start, end, ticks spent polling for the producer} in s_memrealtime ticks (100 MHz, chip-wide).
@@ -536,16 +544,58 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
             if constexpr (AFF) y = __hip_atomic_load(gh + P.hand_x_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     };
+    // SPLIT consumer, before step q (q % kHandGran == 0) of the chunk at kC: the granules of
+    // columns kC + [q, q + kHandGran) (lanes q.. of pre_h, loaded one granule group earlier) must
+    // carry their tag; while one does not, the wave re-polls.  They become the steps' lane-0
+    // inputs (s_step), then the next group is prefetched (columns of the chunk it falls in).
+    auto split_sub = [&](int band, int kC, int q) {
+        if constexpr (SPLIT) {
+            const bool mine = lane >= q && lane < q + kHandGran;
+            const bool need = mine && kC + lane < n;
+            uint64_t t0 = 0;
+            for (;;) {
+                const bool pend = need && ((pre_h >> 32) == 0 || (AFF && (pre_x >> 32) == 0));
+                if (__builtin_amdgcn_ballot_w64(pend) == 0 || tmo) {
+#ifdef SA_TB_STATS
+                    if (t0) st_wait += __builtin_amdgcn_s_memrealtime() - t0;
+#endif
+                    break;
+                }
+                const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                if (t0 == 0) t0 = now;
+                else if (now - t0 > P.wait_ticks) { tmo = 1; break; }
+                __builtin_amdgcn_s_sleep(1);
+                split_load(band, kC, pre_h, pre_x);
+            }
+            if (mine) {
+                s_step[lane] = need ? (int)(uint32_t)pre_h : 0;
+                if constexpr (AFF) s_step[32 + lane] = need ? (int)(uint32_t)pre_x : XB;
+            }
+            split_load(band, q + kHandGran < kChunk ? kC : kC + kChunk, pre_h, pre_x);
+        }
+    };
+    // SPLIT producer, after step q + kHandGran - 1: lanes 0..7 publish the band's last row at the
+    // columns lane 63 reached in steps [q, q + kHandGran) (kC + q - 63 + lane), write-through
+    // {tag = 1, value} granules polled by the next band.
+    auto split_put = [&](int band, int kC, int q) {
+        if constexpr (SPLIT) {
+            const int cc = kC + q + lane - (kWave - 1);
+            if (band + 1 < B && lane < kHandGran && cc >= 0 && cc < n) {
+                gu64* const gh = hand_pair + (uint64_t)band * P.max_n;
+                __hip_atomic_store(gh + cc, (1ull << 32) | (uint32_t)s_step[96 + q + lane], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                if constexpr (AFF)
+                    __hip_atomic_store(gh + P.hand_x_off + cc, (1ull << 32) | (uint32_t)s_step[128 + q + lane],
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    };
     // One chunk of kChunk steps of one band.
     auto run_chunk = [&](auto steady, int band, int kC, int bch, int bcx, int symc, int& acc_h,
                          int& acc_x) {
         uint8_t* const dband = dslot + (uint64_t)band * P.band_stride;
 #pragma unroll 1
         for (int q0 = 0; q0 < kChunk; q0 += SPP) {
-            // SPLIT: the next chunk's hand-off granules are fetched mid-chunk rather than at the
-            // chunk start: the producer is then 16 steps further along, so the load finds them
-            // ready at a smaller band lag (each failed poll costs a memory round trip)
-            if (SPLIT && q0 == kChunk / 2 && band > 0) split_load(band, kC + kChunk, pre_h, pre_x);
             uint32_t pk[4 * PPS];
 #pragma unroll
             for (int e = 0; e < 4 * PPS; ++e) pk[e] = 0;
@@ -553,6 +603,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
 #pragma unroll
             for (int g = 0; g < SPP; ++g) {
                 const int q = q0 + g;
+                if (SPLIT && band > 0 && q % kHandGran == 0) split_sub(band, kC, q);
                 uint32_t rec[RW];
                 if (g & 1) step(steady, q, kC + q, bch, bcx, symc, rec, std::true_type{});
                 else step(steady, q, kC + q, bch, bcx, symc, rec, std::false_type{});
@@ -565,6 +616,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                 // lane 63 holds the band's last row at column kC + q - 63: park it in LDS
                 s_park[q] = hl;
                 if constexpr (AFF) s_park[32 + q] = xl;
+                if (SPLIT && (q + 1) % kHandGran == 0) split_put(band, kC, q + 1 - kHandGran);
             }
             const uint64_t pkt0 = (uint64_t)((kC + q0) / SPP) * PPS;
 #pragma unroll
@@ -600,7 +652,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                 if constexpr (ALG == SA_NW) vh = SC * (J * G - P.t16_delta);
                 else if constexpr (ALG == SA_GLOBAL_GOTOH) vh = SC * (GO + J * GE - P.t16_delta);
             } else if constexpr (SPLIT) {
-                // polled below, after the branch (the wave must poll together)
+                // polled per granule group inside the chunk (split_sub)
             } else if (band % W != 0) {
                 vh = ring(band % W, 0)[c % kRing];
                 if constexpr (AFF) vx = ring(band % W, 1)[c % kRing];
@@ -609,32 +661,8 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                 if constexpr (AFF) vx = rb_x[(uint64_t)(band - 1) * rbs + c];
             }
         }
-        if constexpr (SPLIT) {
-            if (band > 0) {
-                // The granules of this chunk were loaded one chunk ahead, so the memory latency
-                // overlaps the previous chunk; while any lane's tag is still 0 the wave re-polls.
-                const bool need = lane < kChunk && c < n;
-                uint64_t t0 = 0;
-                for (;;) {
-                    const bool pend = need && ((pre_h >> 32) == 0 || (AFF && (pre_x >> 32) == 0));
-                    if (__builtin_amdgcn_ballot_w64(pend) == 0 || tmo) {
-#ifdef SA_TB_STATS
-                        if (t0) st_wait += __builtin_amdgcn_s_memrealtime() - t0;
-#endif
-                        break;
-                    }
-                    const uint64_t now = __builtin_amdgcn_s_memrealtime();
-                    if (t0 == 0) t0 = now;
-                    else if (now - t0 > P.wait_ticks) { tmo = 1; break; }
-                    __builtin_amdgcn_s_sleep(2);
-                    split_load(band, c0, pre_h, pre_x);
-                }
-                if (need) {
-                    vh = (int)(uint32_t)pre_h;
-                    if constexpr (AFF) vx = (int)(uint32_t)pre_x;
-                }
-            }
-        }
+        // SPLIT, band > 0: the lane-0 inputs are polled per granule group inside the chunk
+        // (split_sub); the values written to s_step here are placeholders
     };
 
     for (uint32_t ph = 0; ph < total; ++ph) {
@@ -710,12 +738,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     if (lane < kChunk && cc >= 0 && cc < n) {
                         const int nw = (band + 1) % W;
                         if constexpr (SPLIT) {
-                            gu64* const gh = hand_pair + (uint64_t)band * P.max_n;
-                            __hip_atomic_store(gh + cc, (1ull << 32) | (uint32_t)acc_h, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                            if constexpr (AFF)
-                                __hip_atomic_store(gh + P.hand_x_off + cc, (1ull << 32) | (uint32_t)acc_x,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            // published per granule group inside the chunk (split_put)
                         } else if (nw != 0) {
                             ring(nw, 0)[cc % kRing] = acc_h;
                             if constexpr (AFF) ring(nw, 1)[cc % kRing] = acc_x;

@@ -155,3 +155,35 @@ def test_multi_handle_linear_space(engine):
                 assert gops.tobytes() == rops.tobytes()
     finally:
         me.close()
+
+
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
+def test_host_api_chunked_pipeline(engine, algo, monkeypatch):
+    """The host API cuts big batches into pair ranges and pipelines them (upload of range g+1 and
+    download of g-1 under the kernels of g, sa_api.hip align_host).  Forced to 1, 3 and 5 ranges
+    on a ragged batch (LUT and equality): identical results and op streams."""
+    rng = np.random.default_rng(70 + algo)
+    pairs = []
+    for k in range(157):
+        m = int(rng.integers(0, 500))
+        a = sa.synth_dna(50_000 + 2 * k, m)
+        b = sa.synth_mutate(a, k)[: int(rng.integers(0, 520))] if k % 3 else sa.synth_dna(50_001 + 2 * k, int(rng.integers(0, 500)))
+        pairs.append((a, b))
+    s1, o1, s2, o2 = sa.pack_pairs(pairs)
+    args = SCORINGS[algo][0]
+    out = {}
+    for g in ("1", "3", "5"):
+        monkeypatch.setenv("SEQALIB_HOST_CHUNKS", g)
+        for lut in (None, "purine"):
+            from util import named_lut
+            out[(g, lut)] = engine.align_packed(algo, sc_obj(args), s1, o1, s2, o2, named_lut(lut))
+    for lut in (None, "purine"):
+        r1, p1 = out[("1", lut)]
+        for g in ("3", "5"):
+            r, q = out[(g, lut)]
+            assert r.tobytes() == r1.tobytes(), (g, lut)
+            for p in range(len(pairs)):   # (bytes past a pair's nops are unspecified)
+                off = int(o1[p] + o2[p]) + p
+                assert q[off:off + int(r["nops"][p])].tobytes() == p1[off:off + int(r1["nops"][p])].tobytes(), (g, lut, p)
+    monkeypatch.setenv("SEQALIB_HOST_CHUNKS", "3")
+    compare_with_oracle(engine, algo, args, pairs)
