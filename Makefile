@@ -38,7 +38,7 @@ STATS_LIB = build/libstats.so
 stats: $(STATS_LIB)
 $(STATS_LIB): $(HIP_SRCS) $(CPP_SRCS) $(HDRS)
 	@mkdir -p build/stats
-	for f in $(HIP_SRCS) $(CPP_SRCS); do $(HIPCC) $(HIPFLAGS) -DSA_TB_STATS -c $$f -o build/stats/$$(basename $$f).o || exit 1; done
+	printf '%s\n' $(HIP_SRCS) $(CPP_SRCS) | xargs -P 8 -I{} sh -c '$(HIPCC) $(HIPFLAGS) -DSA_TB_STATS -c {} -o build/stats/$$(basename {}).o'
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ build/stats/*.o -lpthread
 
 oracle:

@@ -68,6 +68,8 @@ def parse():
                     help="host-API steps (H2D + fill + traceback + D2H of results and ops) timed after the run")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
+    ap.add_argument("--rank-out", default="",
+                    help="directory: every rank writes rank<r>.json (its own time, shard and parity; tests)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run steps back to back without overlapping step k's traceback with step k+1's fill")
     ap.add_argument("--serial-steps", type=int, default=3,
@@ -87,9 +89,15 @@ def dist_setup(args):
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if torch.cuda.is_available():
-            torch.cuda.set_device(local)
+            torch.cuda.set_device(gpu_index(local))
         dist.init_process_group(backend="gloo")
     return world, rank, local
+
+
+def gpu_index(local: int) -> int:
+    """GPU of this rank: LOCAL_RANK, unless SEQALIB_BENCH_DEVICE pins every rank to one device
+    (the multi-process test rehearses N ranks on a one-GPU box)."""
+    return int(os.environ.get("SEQALIB_BENCH_DEVICE", local))
 
 
 def barrier(world):
@@ -217,8 +225,9 @@ def main():
 
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (no CPU fallback)")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = gpu_index(local)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     P, Lq = args.pairs, args.len
     workload = f"sw_batch_{P}x{Lq}x{Lq}"
 
@@ -229,7 +238,7 @@ def main():
     # while step k+1 fills, so consecutive steps must not share result buffers
     d_res = [torch.zeros(P * 32, dtype=torch.uint8, device=dev) for _ in range(2)]
     d_ops = [torch.zeros(len(s1) + len(s2) + P, dtype=torch.uint8, device=dev) for _ in range(2)]
-    eng = sa.Engine(local)
+    eng = sa.Engine(gpu)
     scoring = sa.ScoringSystem(*SCORING)
     stream = torch.cuda.current_stream(dev)
     pipelined = not args.no_pipeline
@@ -252,7 +261,8 @@ def main():
     torch.cuda.synchronize()
     barrier(world)
     t1 = time.perf_counter()
-    elapsed = max_over_ranks(t1 - t0, world)
+    own = t1 - t0
+    elapsed = max_over_ranks(own, world)
     fill_ms, tb_ms, launches = eng.last_timings()   # HIP events of the last step (fill stream / traceback stream)
     last = (args.steps - 1) % 2
     serial_ms = None
@@ -299,6 +309,11 @@ def main():
             bad += 1
         checked += 1
 
+    if args.rank_out:
+        os.makedirs(args.rank_out, exist_ok=True)
+        with open(os.path.join(args.rank_out, f"rank{rank}.json"), "w") as f:
+            json.dump({"rank": rank, "world": world, "own_s": own, "max_s": elapsed, "seed_base": shard_seed_base(rank, world, P),
+                       "checked": checked, "bad": bad, "flags": int(np.count_nonzero(res["flags"]))}, f)
     if rank != 0:
         return
     per_launch_cells = cells_rank  # one fill launch covers the whole batch when it fits HBM

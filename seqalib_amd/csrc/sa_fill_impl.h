@@ -109,11 +109,16 @@ constexpr int fill_max_threads() { return (R >= 32 || (WIDE && R >= 16)) ? 256 :
 // waiting altogether: the pair is flagged SA_FLAG_TIMEOUT and re-run by the call's
 // single-workgroup fallback launch (run_device, sa_api.hip).
 
-// SPLIT hand-off granule: a band publishes its last row every kHandGran steps (lanes 0..7 store
-// the values lane 63 parked in LDS), and its consumer polls kHandGran columns at a time, each
-// group prefetched one group ahead.  With the 32-column chunks of round 2 a band ran ~161 steps
-// behind its producer (63 inherent, ~64 chunk quantisation, the rest latency); the inherent
-// lag plus one granule at each end plus the poll latency is ~90 (tools/split_stats.py).
+// SPLIT hand-off.  A SPLIT workgroup is three waves: the COMPUTE wave runs the band; the POLLER
+// loads the producer band's last row -- write-through {tag, value} granules -- and copies it into
+// an LDS ring (kRing columns), publishing how many columns are ready; the PUBLISHER reads this
+// band's last row, which the compute wave parks per step in a second LDS ring, and stores it as
+// granules for the next band.  The compute wave only touches LDS: every kHandGran steps it
+// compares the poller's count (re-read only when short) and posts its own step count.  Polls or
+// publishes in the compute wave cost +26..33 % per step (round 3, tools/split_stats.py): a vector
+// load's s_waitcnt vmcnt also waits for every record store in flight (gfx9's vmcnt counts stores),
+// and a publish is an LDS read + wait + store.  With the 32-column chunks of round 2 a band ran
+// ~161 steps behind its producer (63 inherent, ~64 chunk quantisation, the rest latency).
 constexpr int kHandGran = 8;
 static_assert(kChunk % kHandGran == 0, "granules tile a chunk");
 
@@ -170,6 +175,13 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     __shared__ int s_red[16 * 3];
     __shared__ int s_score;   // H[m][n] for the global modes, stored by the owning lane
+    // SPLIT: [0] columns the poller has copied into the ring, [1] columns the compute wave has
+    // consumed, [2] the poller's bounded wait expired; s_ticket: the band's ticket
+    //   [3] steps the compute wave has run (its parked last-row values), [4] steps the publisher
+    //   has stored
+    __shared__ int s_sync[8];
+    __shared__ uint32_t s_ticket;
+    __shared__ int s_pring[SPLIT ? 2 * kRing : 1];   // SPLIT: the parked last row (H, then Ix), by step
 
     // the batch selected the other kernel variant: leave -- except an int32 launch re-running the
     // pairs a T16 fill flagged kFlagRetry (checked below, once the pair is known)
@@ -187,9 +199,12 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     // is always already running or done: no wait can deadlock whatever the residency.
     uint32_t slot, band0 = 0;
     if constexpr (SPLIT) {
-        uint32_t t = 0;
-        if (threadIdx.x == 0) t = atomicAdd(P.ticket, 1u);
-        t = __builtin_amdgcn_readfirstlane(t);
+        if (threadIdx.x == 0) {
+            s_ticket = atomicAdd(P.ticket, 1u);
+            s_sync[0] = 0; s_sync[1] = 0; s_sync[2] = 0; s_sync[3] = 0; s_sync[4] = 0;
+        }
+        __syncthreads();   // (the compute wave and the poller)
+        const uint32_t t = __builtin_amdgcn_readfirstlane(s_ticket);
         slot = t / P.split_bands;
         band0 = t - slot * P.split_bands;
     } else {
@@ -263,6 +278,85 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     typedef unsigned long long __attribute__((address_space(1))) gu64;
     gu64* const hand_pair = SPLIT ? (gu64*)(P.hand + (uint64_t)slot * P.split_bands * P.max_n) : nullptr;
     uint32_t tmo = 0;   // SPLIT: a bounded wait expired
+    // SPLIT poller (wave 1, see kHandGran): copies the producer band's granules into the LDS ring
+    // s_ring (the hand-off ring of the multi-wave plans, unused here) and publishes the count of
+    // ready columns, never more than kRing columns beyond what the compute wave has consumed.
+    // Its loads wait only for themselves; on a bounded-wait expiry it flags the band and releases
+    // the compute wave (the pair is flagged SA_FLAG_TIMEOUT and re-run by the call's fallback).
+    if constexpr (SPLIT) {
+        if (w == 1) {
+            if (band0 == 0) return;   // band 0 has no producer
+            gu64* const src = hand_pair + (uint64_t)(band0 - 1) * P.max_n;
+            int pub = 0;
+            uint64_t t0 = 0;
+            while (pub < n) {
+                const int cons = __hip_atomic_load(&s_sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int lim = min(n, cons + kRing);
+                if (lim <= pub) {   // ring full: the compute wave is behind (not a wait for the producer)
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                const int c = pub + lane;
+                const int cl = min(c, n - 1);
+                const unsigned long long x = __hip_atomic_load(src + cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                unsigned long long y = 1ull << 32;
+                if constexpr (AFF) y = __hip_atomic_load(src + P.hand_x_off + cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const bool ok = c < lim && (x >> 32) != 0 && (y >> 32) != 0;
+                const uint64_t notok = __builtin_amdgcn_ballot_w64(!ok);
+                const int adv = notok ? (int)__builtin_ctzll(notok) : kWave;   // the ready prefix
+                if (adv > 0) {
+                    if (lane < adv) {
+                        s_ring[c & (kRing - 1)] = (int)(uint32_t)x;
+                        if constexpr (AFF) s_ring[kRing + (c & (kRing - 1))] = (int)(uint32_t)y;
+                    }
+                    pub += adv;
+                    __hip_atomic_store(&s_sync[0], pub, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    t0 = 0;
+                } else {
+                    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                    if (t0 == 0) {
+                        t0 = now;
+                    } else if (now - t0 > P.wait_ticks) {
+                        __hip_atomic_store(&s_sync[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_store(&s_sync[0], n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        return;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            return;
+        }
+        if (w == 2) {
+            // PUBLISHER: step s of the band parked lane 63's value, the last row at column s - 63,
+            // in ring slot s % kRing; store the columns of every step the compute wave has posted
+            if ((int)band0 + 1 >= B) return;   // the last band has no consumer
+            gu64* const dst = hand_pair + (uint64_t)band0 * P.max_n;
+            const int total_steps = n + kWave - 1;
+            int done = 0;
+            while (done < total_steps) {
+                const int avail = min(total_steps, __hip_atomic_load(&s_sync[3], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if (avail <= done) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                for (int s0 = done; s0 < avail; s0 += kWave) {
+                    const int st = s0 + lane;
+                    const int col = st - (kWave - 1);
+                    if (st < avail && col >= 0) {
+                        __hip_atomic_store(dst + col, (1ull << 32) | (uint32_t)s_pring[st & (kRing - 1)],
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if constexpr (AFF)
+                            __hip_atomic_store(dst + P.hand_x_off + col,
+                                               (1ull << 32) | (uint32_t)s_pring[kRing + (st & (kRing - 1))],
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+                done = avail;
+                __hip_atomic_store(&s_sync[4], done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            return;
+        }
+    }
 
     uint8_t* const dslot = P.dirs + (uint64_t)slot * P.dir_slot;
     int32_t* const rb_h = P.rowbuf + (uint64_t)slot * P.rowbuf_slot;
@@ -293,14 +387,21 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     // One step: lane computes column j = s - lane for its R rows.  STEADY: every lane is in
     // range, no exec-mask branch.  Returns the packed record words in rec.
     uint32_t kprev[R];   // T16 steady chunks: the previous step's keys, merged pairwise by v_max3
-    auto step = [&](auto steady, int q, int s, int bch, int bcx, int symc, uint32_t (&rec)[RW],
-                    auto odd) {
+    // where step q of the current chunk reads lane 0's row-above inputs: the step buffer, or for a
+    // SPLIT band > 0 the poller's ring at the chunk's first column
+    const int32_t* in_h = s_step;
+    const int32_t* in_x = s_step + 32;
+    // where step q parks lane 63's last-row values (the other lanes write a discard slot)
+    int32_t* park_h = s_park;
+    int32_t* park_x = s_park + 32;
+    // vh / vx / vs: lane 0's row-above inputs (H, Ix) and the column symbol of this step
+    auto step = [&](auto steady, int q, int s, int vh, int vx, int vs, uint32_t (&rec)[RW], auto odd) {
         constexpr bool STEADY = decltype(steady)::value;
         constexpr bool ODD = decltype(odd)::value;
-        const int up_h = shr1(s_step[q], hl);
+        const int up_h = shr1(vh, hl);
         int up_x = 0;
-        if constexpr (AFF) up_x = shr1(s_step[32 + q], xl);
-        sym = shr1(s_step[64 + q], sym);
+        if constexpr (AFF) up_x = shr1(vx, xl);
+        sym = shr1(vs, sym);
         const int j = s - lane;
         // T16 with whole record words: the v_alignbit pushes shift every bit a word held out of
         // it, and a lane-step outside the matrix only fills its own (never read) record bytes
@@ -532,61 +633,36 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
         }
     };
 
-    // SPLIT: granules of the producer band for the chunk at column c0 (lane q: column c0 + q,
-    // clamped to the row, so every lane loads and no value is conditionally defined -- that keeps
-    // the prefetched registers in place instead of a copy that would wait for the load).
-    unsigned long long pre_h = 0, pre_x = 0;
-    auto split_load = [&](int band, int c0, unsigned long long& x, unsigned long long& y) {
+    // SPLIT compute wave, band > 0, before step q (q % kHandGran == 0) of the chunk at kC: the
+    // ring must hold columns up to kC + q + kHandGran (have: the last published count seen).
+    int have = 0, pubd = 0;
+    auto split_wait = [&](int band, int kC, int q) {
         if constexpr (SPLIT) {
-            const int cl = min(c0 + lane, n - 1);
-            gu64* const gh = hand_pair + (uint64_t)(band > 0 ? band - 1 : 0) * P.max_n + cl;
-            x = __hip_atomic_load(gh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if constexpr (AFF) y = __hip_atomic_load(gh + P.hand_x_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    };
-    // SPLIT consumer, before step q (q % kHandGran == 0) of the chunk at kC: the granules of
-    // columns kC + [q, q + kHandGran) (lanes q.. of pre_h, loaded one granule group earlier) must
-    // carry their tag; while one does not, the wave re-polls.  They become the steps' lane-0
-    // inputs (s_step), then the next group is prefetched (columns of the chunk it falls in).
-    auto split_sub = [&](int band, int kC, int q) {
-        if constexpr (SPLIT) {
-            const bool mine = lane >= q && lane < q + kHandGran;
-            const bool need = mine && kC + lane < n;
-            uint64_t t0 = 0;
-            for (;;) {
-                const bool pend = need && ((pre_h >> 32) == 0 || (AFF && (pre_x >> 32) == 0));
-                if (__builtin_amdgcn_ballot_w64(pend) == 0 || tmo) {
+            // the park ring slots of steps kC + q .. + kHandGran - 1 held steps kRing earlier: the
+            // publisher must have stored those
+            if (band + 1 < B && pubd < kC + q + kHandGran - kRing) {
+                do {
+                    pubd = __hip_atomic_load(&s_sync[4], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (pubd >= kC + q + kHandGran - kRing) break;
+                    __builtin_amdgcn_s_sleep(1);
+                } while (true);
+            }
+            if (band == 0) return;
+            const int need = min(n, kC + q + kHandGran);
+            if (have < need) {
+                have = __hip_atomic_load(&s_sync[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (have < need) {
 #ifdef SA_TB_STATS
-                    if (t0) st_wait += __builtin_amdgcn_s_memrealtime() - t0;
+                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-                    break;
+                    do {
+                        __builtin_amdgcn_s_sleep(1);
+                        have = __hip_atomic_load(&s_sync[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } while (have < need);
+#ifdef SA_TB_STATS
+                    st_wait += __builtin_amdgcn_s_memrealtime() - t0;
+#endif
                 }
-                const uint64_t now = __builtin_amdgcn_s_memrealtime();
-                if (t0 == 0) t0 = now;
-                else if (now - t0 > P.wait_ticks) { tmo = 1; break; }
-                __builtin_amdgcn_s_sleep(1);
-                split_load(band, kC, pre_h, pre_x);
-            }
-            if (mine) {
-                s_step[lane] = need ? (int)(uint32_t)pre_h : 0;
-                if constexpr (AFF) s_step[32 + lane] = need ? (int)(uint32_t)pre_x : XB;
-            }
-            split_load(band, q + kHandGran < kChunk ? kC : kC + kChunk, pre_h, pre_x);
-        }
-    };
-    // SPLIT producer, after step q + kHandGran - 1: lanes 0..7 publish the band's last row at the
-    // columns lane 63 reached in steps [q, q + kHandGran) (kC + q - 63 + lane), write-through
-    // {tag = 1, value} granules polled by the next band.
-    auto split_put = [&](int band, int kC, int q) {
-        if constexpr (SPLIT) {
-            const int cc = kC + q + lane - (kWave - 1);
-            if (band + 1 < B && lane < kHandGran && cc >= 0 && cc < n) {
-                gu64* const gh = hand_pair + (uint64_t)band * P.max_n;
-                __hip_atomic_store(gh + cc, (1ull << 32) | (uint32_t)s_step[96 + q + lane], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                if constexpr (AFF)
-                    __hip_atomic_store(gh + P.hand_x_off + cc, (1ull << 32) | (uint32_t)s_step[128 + q + lane],
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     };
@@ -600,23 +676,49 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
 #pragma unroll
             for (int e = 0; e < 4 * PPS; ++e) pk[e] = 0;
             static_assert(SPP % 2 == 0 || !T16 || R >= 32 || AFF, "steps pair up for the key max3");
+            // SPLIT (a lone wave, whose LDS read latency no other wave hides): a group of SG steps'
+            // inputs is read into registers at once (broadcast reads), not one read per step
+            constexpr int SG = SPP >= kHandGran ? kHandGran : SPP;
+            int gh[SPLIT ? SG : 1], gx[SPLIT ? SG : 1], gs[SPLIT ? SG : 1];
 #pragma unroll
             for (int g = 0; g < SPP; ++g) {
                 const int q = q0 + g;
-                if (SPLIT && band > 0 && q % kHandGran == 0) split_sub(band, kC, q);
+                int vh, vx = 0, vs;
+                if constexpr (SPLIT) {
+                    if (q % kHandGran == 0) split_wait(band, kC, q);
+                    if (g % SG == 0) {
+#pragma unroll
+                        for (int k = 0; k < SG; ++k) {
+                            gh[k] = in_h[q + k];
+                            gs[k] = s_step[64 + q + k];
+                            if constexpr (AFF) gx[k] = in_x[q + k];
+                        }
+                    }
+                    vh = gh[g % SG];
+                    vs = gs[g % SG];
+                    if constexpr (AFF) vx = gx[g % SG];
+                } else {
+                    vh = in_h[q];
+                    vs = s_step[64 + q];
+                    if constexpr (AFF) vx = in_x[q];
+                }
                 uint32_t rec[RW];
-                if (g & 1) step(steady, q, kC + q, bch, bcx, symc, rec, std::true_type{});
-                else step(steady, q, kC + q, bch, bcx, symc, rec, std::false_type{});
+                if (g & 1) step(steady, q, kC + q, vh, vx, vs, rec, std::true_type{});
+                else step(steady, q, kC + q, vh, vx, vs, rec, std::false_type{});
                 if constexpr (BPS >= 4) {
 #pragma unroll
                     for (int e = 0; e < RW; ++e) pk[g * RW + e] = rec[e];
                 } else {
                     pk[(g * BPS) / 4] |= rec[0] << (((g * BPS) % 4) * 8);
                 }
-                // lane 63 holds the band's last row at column kC + q - 63: park it in LDS
-                s_park[q] = hl;
-                if constexpr (AFF) s_park[32 + q] = xl;
-                if (SPLIT && (q + 1) % kHandGran == 0) split_put(band, kC, q + 1 - kHandGran);
+                // lane 63 holds the band's last row at column kC + q - 63: park it in LDS (SPLIT: in
+                // the park ring, posting the step count every kHandGran steps for the publisher)
+                park_h[q] = hl;
+                if constexpr (AFF) park_x[q] = xl;
+                if constexpr (SPLIT) {
+                    if ((q + 1) % kHandGran == 0 && band + 1 < B && lane == 0)
+                        __hip_atomic_store(&s_sync[3], kC + q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
             }
             const uint64_t pkt0 = (uint64_t)((kC + q0) / SPP) * PPS;
 #pragma unroll
@@ -692,7 +794,12 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     }
                     lkey = 0;
                     cml = 0;
-                    split_load(band, 0, pre_h, pre_x);
+                    have = 0;
+                    // retire the row loads above here, once per band: left pending, they make the
+                    // compiler wait vmcnt(0) at every chunk's loop entry, which also drains the
+                    // record stores in flight (gfx9's vmcnt counts stores) -- a stall per chunk
+                    // that a lone wave (SPLIT) cannot hide
+                    __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
                     if constexpr (ALG == SA_NW) prev_up = SC * (row0 * G - P.t16_delta);
                     else if constexpr (ALG == SA_GLOBAL_GOTOH) prev_up = SC * ((row0 == 0 ? 0 : GO + row0 * GE) - P.t16_delta);
                     else prev_up = 0;
@@ -701,6 +808,16 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                 const int kC = (int)chunk * kChunk;
                 int bch, bcx, symc;
                 load_chunk(band, kC, bch, bcx, symc);
+                if (SPLIT && band > 0) {
+                    // the poller may now refill the ring slots of the columns before kC
+                    __hip_atomic_store(&s_sync[1], kC, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    in_h = s_ring + (kC & (kRing - 1));
+                    in_x = s_ring + kRing + (kC & (kRing - 1));
+                }
+                if constexpr (SPLIT) {
+                    park_h = lane == 63 ? s_pring + (kC & (kRing - 1)) : s_step + 160;
+                    park_x = lane == 63 ? s_pring + kRing + (kC & (kRing - 1)) : s_step + 192;
+                }
                 if (lane < kChunk) {   // the chunk's per-step broadcast inputs (LDS-fed steps)
                     s_step[lane] = bch;
                     if constexpr (AFF) s_step[32 + lane] = bcx;
@@ -738,7 +855,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     if (lane < kChunk && cc >= 0 && cc < n) {
                         const int nw = (band + 1) % W;
                         if constexpr (SPLIT) {
-                            // published per granule group inside the chunk (split_put)
+                            // stored by the publisher wave from the park ring
                         } else if (nw != 0) {
                             ring(nw, 0)[cc % kRing] = acc_h;
                             if constexpr (AFF) ring(nw, 1)[cc % kRing] = acc_x;
@@ -808,7 +925,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                 }
             }
         }
-        __syncthreads();
+        if constexpr (!SPLIT) __syncthreads();   // (SPLIT: one compute wave; the poller takes no barriers)
     }
 
     // ------------------------------------------------------------------------ results
@@ -826,6 +943,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
         } else {
             best_h = ((m - 1) / BAND == (int)band0) ? s_score : 0;   // ordered by the loop's barrier
         }
+        tmo = (uint32_t)__hip_atomic_load(&s_sync[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (threadIdx.x == 0) {
             int32_t* q = P.part + ((uint64_t)slot * P.split_bands + band0) * 4;
             q[0] = best_h; q[1] = best_i; q[2] = best_j; q[3] = (int32_t)tmo;
@@ -898,7 +1016,9 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
     const int R = v.R;
     const bool lut = (v.t16 || v.bits) ? false : v.lut, allow = v.allow;
     const bool keyed = LOCAL && v.keyed;
-    const dim3 block(kWave * p.waves);
+    // SPLIT: the compute wave + its poller and publisher waves (see kHandGran); LDS for one
+    // compute wave
+    const dim3 block(kWave * (v.split ? 3 : p.waves));
     const size_t lds = lds_layout(lut, is_affine(ALG), p.waves, p.stage_seq2 ? p.max_n : 0).total;
     if (lds > kMaxLds) return hipErrorInvalidConfiguration;
     const bool split = v.split;
