@@ -33,13 +33,15 @@ $(LIB): $(OBJS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -lpthread
 
-# debug build with traceback counters (tools/tb_stats.py): build/libstats.so
+# debug build with traceback / SPLIT counters (tools/tb_stats.py, tools/split_stats.py):
+# build/libstats.so, copied to tools/bin/ (build/ does not travel to the GPU box)
 STATS_LIB = build/libstats.so
 stats: $(STATS_LIB)
 $(STATS_LIB): $(HIP_SRCS) $(CPP_SRCS) $(HDRS)
 	@mkdir -p build/stats
 	printf '%s\n' $(HIP_SRCS) $(CPP_SRCS) | xargs -P 8 -I{} sh -c '$(HIPCC) $(HIPFLAGS) -DSA_TB_STATS -c {} -o build/stats/$$(basename {}).o'
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ build/stats/*.o -lpthread
+	@mkdir -p tools/bin && cp $@ tools/bin/libstats.so
 
 oracle:
 	$(MAKE) -C oracle
@@ -53,4 +55,10 @@ clean:
 	rm -rf build $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: lib stats oracle ref all-checkers clean
+# A/B variant of the engine: make variant V=name DEFS="-DSOMETHING" -> seqalib_amd/lib/ab/lib<name>.so
+variant:
+	@mkdir -p build/ab_$(V) seqalib_amd/lib/ab
+	printf '%s\n' $(HIP_SRCS) $(CPP_SRCS) | xargs -P 8 -I{} sh -c '$(HIPCC) $(HIPFLAGS) $(DEFS) -c {} -o build/ab_$(V)/$$(basename {}).o'
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o seqalib_amd/lib/ab/lib$(V).so build/ab_$(V)/*.o -lpthread
+
+.PHONY: lib stats variant oracle ref all-checkers clean

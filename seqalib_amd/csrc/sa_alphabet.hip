@@ -58,7 +58,8 @@ __global__ __launch_bounds__(256) void alphabet_scan(const uint8_t* d1, const ui
 
 // The T16 decision, on the device (so the host never waits for the scan): with <= 4 distinct
 // symbols, sym_pack = the symbols padded with absent byte values (codes stay distinct),
-// prof[c] byte c' = (int8)(4 * s(sym c, sym c') + 3) -- (8 * s + 6) for the affine kernel --,
+// prof[c] byte c' = (int8)(4 * s(sym c, sym c') + 3) -- (8 * s + 6) for the affine kernel
+// (affine = 1), s itself for the 16-bit linear-space sweeps (affine = 2, sa_dc.h) --,
 // s = match ? match : mismatch; sel = 1.
 // More symbols: sel = 0 (the int32 kernel's launches run, the T16 ones return at once).
 __global__ void decide_t16(const uint32_t* lutbits, int match, int mismatch, int affine, uint32_t* aux) {
@@ -85,7 +86,7 @@ __global__ void decide_t16(const uint32_t* lutbits, int match, int mismatch, int
             const uint32_t a = syms[c], b = syms[c2];
             const bool v = lutbits ? ((lutbits[(a << 3) | (b >> 5)] >> (b & 31u)) & 1u) : (a == b);
             const int s = v ? match : mismatch;
-            const int t = affine ? 8 * s + 6 : 4 * s + 3;
+            const int t = affine == 2 ? s : affine ? 8 * s + 6 : 4 * s + 3;
             w |= ((uint32_t)t & 255u) << (8 * c2);
         }
         aux[kAuxProf + c] = w;

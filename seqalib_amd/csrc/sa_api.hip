@@ -930,11 +930,24 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         SA_HIP(c, hipStreamCreateWithFlags(&c->s_tb, hipStreamNonBlocking));
         SA_HIP(c, hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     }
-    while (c->host_ev.size() < 2 * (size_t)G) {
+    // downloads go in pieces of kHostPiece bytes, each with its own event, so the host copy of
+    // piece k (pinned -> caller) overlaps the D2H of piece k+1; uploads likewise (host copy of
+    // piece k+1 while piece k is in flight)
+    constexpr uint64_t kHostPiece = 16ull << 20;
+    struct OutPiece { uint32_t g; uint64_t ob, on; };
+    std::vector<OutPiece> outp;
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t p0 = cut[g], p1 = cut[g + 1];
+        if (p1 == p0) continue;
+        const uint64_t ob = off1[p0] + off2[p0] + p0, on = off1[p1] + off2[p1] + p1 - ob;
+        for (uint64_t x = 0; x < on || x == 0; x += kHostPiece) outp.push_back({g, ob + x, std::min(kHostPiece, on - x)});
+    }
+    while (c->host_ev.size() < (size_t)G + outp.size()) {
         hipEvent_t ev;
         SA_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         c->host_ev.push_back(ev);
     }
+    size_t next_out = 0;
     hipStream_t st = c->stream;   // uploads (and, un-pipelined, the kernels)
     if (use_lut) {
         SA_HIP(c, hipMemcpyAsync(dlut, lut, 65536, hipMemcpyHostToDevice, st));
@@ -955,10 +968,16 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
                 mn = (uint32_t)std::max<uint64_t>(mn, off2[p0 + q] - off2[p0 + q - 1]);
             }
         }
-        par_copy(si + a1, seq1 + a1, n1);
-        par_copy(si + t1 + a2, seq2 + a2, n2);
-        if (n1) SA_HIP(c, hipMemcpyAsync(d1 + a1, si + a1, n1, hipMemcpyHostToDevice, st));
-        if (n2) SA_HIP(c, hipMemcpyAsync(d2 + a2, si + t1 + a2, n2, hipMemcpyHostToDevice, st));
+        for (uint64_t x = 0; x < n1; x += kHostPiece) {
+            const uint64_t k = std::min(kHostPiece, n1 - x);
+            par_copy(si + a1 + x, seq1 + a1 + x, k);
+            SA_HIP(c, hipMemcpyAsync(d1 + a1 + x, si + a1 + x, k, hipMemcpyHostToDevice, st));
+        }
+        for (uint64_t x = 0; x < n2; x += kHostPiece) {
+            const uint64_t k = std::min(kHostPiece, n2 - x);
+            par_copy(si + t1 + a2 + x, seq2 + a2 + x, k);
+            SA_HIP(c, hipMemcpyAsync(d2 + a2 + x, si + t1 + a2 + x, k, hipMemcpyHostToDevice, st));
+        }
         SA_HIP(c, hipMemcpyAsync(do1 + p0 + g, so1 + p0 + g, 8ull * (cnt + 1), hipMemcpyHostToDevice, st));
         SA_HIP(c, hipMemcpyAsync(do2 + p0 + g, so2 + p0 + g, 8ull * (cnt + 1), hipMemcpyHostToDevice, st));
         hipStream_t done = st;
@@ -980,20 +999,23 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
             if (rc) return rc;
             if (pipe) done = c->s_tb;   // the chunk's last kernel (its traceback) ran there
         }
-        SA_HIP(c, hipEventRecord(c->host_ev[2 * g], done));
-        SA_HIP(c, hipStreamWaitEvent(c->s_out, c->host_ev[2 * g], 0));
+        (void)on;
+        SA_HIP(c, hipEventRecord(c->host_ev[g], done));
+        SA_HIP(c, hipStreamWaitEvent(c->s_out, c->host_ev[g], 0));
         SA_HIP(c, hipMemcpyAsync(sres + p0, dres + p0, sizeof(sa_result) * cnt, hipMemcpyDeviceToHost, c->s_out));
-        SA_HIP(c, hipMemcpyAsync(sops + ob, dops + ob, on, hipMemcpyDeviceToHost, c->s_out));
-        SA_HIP(c, hipEventRecord(c->host_ev[2 * g + 1], c->s_out));
+        for (; next_out < outp.size() && outp[next_out].g == g; ++next_out) {
+            const OutPiece& o = outp[next_out];
+            SA_HIP(c, hipMemcpyAsync(sops + o.ob, dops + o.ob, o.on, hipMemcpyDeviceToHost, c->s_out));
+            SA_HIP(c, hipEventRecord(c->host_ev[G + next_out], c->s_out));
+        }
     }
-    // each chunk's results reach the caller's buffers while later chunks still run
-    for (uint32_t g = 0; g < G; ++g) {
-        const uint32_t p0 = cut[g], p1 = cut[g + 1];
-        if (p1 == p0) continue;
-        SA_HIP(c, hipEventSynchronize(c->host_ev[2 * g + 1]));
-        const uint64_t ob = off1[p0] + off2[p0] + p0, on = off1[p1] + off2[p1] + p1 - ob;
-        memcpy(results + p0, sres + p0, sizeof(sa_result) * (p1 - p0));
-        par_copy(ops + ob, sops + ob, on);
+    // each piece reaches the caller's buffers while later pieces and chunks still run
+    for (size_t k = 0; k < outp.size(); ++k) {
+        const OutPiece& o = outp[k];
+        SA_HIP(c, hipEventSynchronize(c->host_ev[G + k]));
+        if (k == 0 || outp[k - 1].g != o.g)
+            memcpy(results + cut[o.g], sres + cut[o.g], sizeof(sa_result) * (cut[o.g + 1] - cut[o.g]));
+        par_copy(ops + o.ob, sops + o.ob, o.on);
     }
     if (pipe) {
         SA_HIP(c, hipStreamSynchronize(c->s_fill));

@@ -72,6 +72,14 @@ struct HostBuf {
     ~HostBuf() { if (p) (void)hipHostFree(p); }
 };
 
+// 8 x the code of byte b in a 16-bit sweep's alphabet (sym_pack sp: byte c = the symbol of code c,
+// distinct; decide_t16, sa_alphabet.hip)
+__device__ __forceinline__ uint32_t dc_code8(uint32_t sp, uint32_t b) {
+    return (b == ((sp >> 8) & 255u) ? 8u : 0u) | (b == ((sp >> 16) & 255u) ? 16u : 0u) | (b == (sp >> 24) ? 24u : 0u);
+}
+// the low 16 bits of a 16-bit sweep register, sign-extended, plus the offset
+__device__ __forceinline__ int32_t dc_unpack16(int32_t v, int32_t delta) { return (int32_t)(int16_t)(v & 0xffff) + delta; }
+
 // ---- match sources
 // match(a, b): the 256x256 LUT as bits (lut_to_bits), or byte equality
 __device__ __forceinline__ bool dc_match(const uint32_t* lut, uint32_t a, uint32_t b) {
@@ -220,6 +228,7 @@ struct DcBounds {
 // a level splits at most t1 / (leaf_rows + 1) + 1 of them; leaves have >= 1 row (or are a whole
 // empty pair), so there are at most t1 + npairs of them.
 struct DcWork {
+    DevBuf<uint32_t> aux;   // 16-bit sweeps: alphabet bitmap, profile and decision (sa_internal.h kAux*)
     DevBuf<DcSub> cur, next, split, leaves;
     DevBuf<DcLevel> lvl;
     DevBuf<int32_t> rows, scratch, mark;
@@ -228,7 +237,7 @@ struct DcWork {
     int levels = 0;
     uint32_t* nleaf() { return &lvl.p[levels + 1].nsplit; }   // lvl[0..levels]: the levels
     void release() {
-        cur.reset(); next.reset(); split.reset(); leaves.reset(); lvl.reset();
+        aux.reset(); cur.reset(); next.reset(); split.reset(); leaves.reset(); lvl.reset();
         rows.reset(); scratch.reset(); mark.reset(); stage.reset();
     }
     // prev: the context's last call (its kernels may still read these buffers on another
@@ -259,6 +268,48 @@ struct DcWork {
         return hipMemsetAsync(mark.p, 0, sizeof(int32_t) * keys, st);
     }
 };
+
+// 16-bit whole-wave sweeps (sa_hirschberg.hip, sa_myersmiller.hip).  When the batch has at most four
+// distinct symbols (decided on the device: alphabet_scan + decide_t16 with a plain profile) and the
+// host proves every value a sweep can produce lies within 2^15 of an offset `delta`, the sweeps keep
+// their rows as 16-bit values v - delta and run 16-bit VOP2 adds / maxes (twice the issue rate of
+// the 32-bit integer max / compare ops on gfx950) with the substitution score from a per-row byte
+// profile: one v_bfe_i32 per cell.  !AllowMismatch runs with mismatch' = 2 * Gap - 1
+// (2 * (GapOpen + GapExtend) - 1 for Myers-Miller), which never wins a max -- the same argument as
+// the fill's T16 kernels -- so the rows are the reference's exactly.
+struct Dc16 {
+    const uint32_t* aux = nullptr;   // NULL: int32 sweeps only
+    int32_t delta = 0;
+    int32_t mismatch = 0;            // the profile's mismatch score
+};
+// Host: is the 16-bit sweep exact for the batch's shapes and scoring?  lo / hi: bounds of every
+// row value and candidate of any sweep of at most max_m x max_n.
+inline Dc16 dc16_plan(bool affine, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
+    Dc16 d;
+    if (const char* e = getenv("SEQALIB_DC16")) if (e[0] == '0') return d;
+    const int64_t m = max_m, n = max_n, k = std::min(m, n);
+    const int64_t MA = sc->match;
+    const int64_t G = affine ? (int64_t)sc->gap_open : (int64_t)sc->gap;
+    const int64_t H = affine ? (int64_t)sc->gap_extend : 0;
+    int64_t MI = sc->mismatch;
+    if (!sc->allow_mismatch) MI = affine ? 2 * (G + H) - 1 : 2 * G - 1;
+    if (MA < -127 || MA > 127 || MI < -128 || MI > 127 || G > 0 || H > 0 || MI > MA) return d;
+    if (MA < 0) return d;
+    int64_t lo, hi;
+    if (affine) {   // C, D, e >= the all-gap path (>= 3g + (m + n)h), each candidate one step below
+        lo = 3 * G + (m + n) * H + std::min<int64_t>(std::min(G + H, MI), 0) + H;
+        hi = k * MA + MA;
+    } else {        // H >= the all-gap path (m + n) G; candidates one step below
+        lo = (m + n) * G + std::min<int64_t>(std::min(G, MI), 0);
+        hi = k * MA + MA;
+    }
+    const int64_t delta = (hi + lo) / 2;
+    if (hi - delta > 32000 || lo - delta < -32000) return d;
+    d.aux = reinterpret_cast<const uint32_t*>(1);   // placeholder: set to the device aux by the driver
+    d.delta = (int32_t)delta;
+    d.mismatch = (int32_t)MI;
+    return d;
+}
 
 // Inputs of a batch: byte symbols (d1 / d2 with the LUT bits, or NULL for equality) or, when
 // bits.mbits != NULL, per-pair match bitmaps (the generic-Ty path; d1 / d2 are then not read).

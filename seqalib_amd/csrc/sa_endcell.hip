@@ -69,8 +69,15 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
     const int32_t* top = b > 0 ? P.rowbuf + (uint64_t)slot * P.rowbuf_slot + (uint64_t)(b - 1) * P.max_n * rs : nullptr;
     const int32_t* lmax = P.snap_m + (uint64_t)slot * P.snap_p_slot + (uint64_t)b * P.snap_nch * kWave + tstar;
     int rbest = -1, jbest = -1;
-    for (int cc = 0; cc <= c; ++cc) {
-        if (lmax[(uint64_t)cc * kWave] != 4 * S) continue;   // uniform: lane tstar never reached S here
+    __shared__ uint8_t s_sym[kWave + kChunk];   // the chunk's column codes, columns cc*32 - 63 ..
+    __shared__ int s_top[kChunk];               // the band's top row at the chunk's columns
+    // the chunks to replay, found 64 at a time (one load per lane, not a dependent load per chunk)
+    for (int base = 0; base <= c; base += kWave) {
+        const int ccl = base + lane;
+        uint64_t hits = __builtin_amdgcn_ballot_w64(ccl <= c && lmax[(uint64_t)ccl * kWave] == 4 * S);
+        while (hits) {
+        const int cc = base + (int)__builtin_ctzll(hits);
+        hits &= hits - 1;
         int Hp[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) Hp[r] = 0;
@@ -84,16 +91,26 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
                 Hp[2 * q] = (int)(w & 0xffffu) >> 2;        // stored as 4H (non-negative)
                 Hp[2 * q + 1] = (int)(w >> 16) >> 2;
             }
-            prev_up = P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] >> 2;
+            prev_up = (int)(P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] & 0xffff) >> 2;
         }
+        __syncthreads();   // (a previous candidate's reads of the staging arrays)
+        for (int k = lane; k < kWave + kChunk; k += kWave) {
+            const int j = cc * kChunk - (kWave - 1) + k;
+            s_sym[k] = (uint8_t)(j >= 0 && j < n ? ec_code8(symp, s2[j]) : 0u);
+        }
+        if (lane < kChunk) {
+            const int j = cc * kChunk + lane;
+            s_top[lane] = (top && j < n) ? (top[(uint64_t)j * rs] >> 2) : 0;
+        }
+        __syncthreads();
         int hl = Hp[R - 1];
         for (int q = 0; q < kChunk; ++q) {
             const int s = cc * kChunk + q;
             const int j0 = s - lane;
             int up_h = __shfl_up(hl, 1);
-            if (lane == 0) up_h = (top && s < n) ? (top[(uint64_t)s * rs] >> 2) : 0;
+            if (lane == 0) up_h = s_top[q];
             if (j0 >= 0 && j0 < n) {
-                const uint32_t sym = ec_code8(symp, s2[j0]);
+                const uint32_t sym = s_sym[q - lane + (kWave - 1)];
                 int hd = prev_up, hu = up_h;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
@@ -115,6 +132,7 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
                 prev_up = up_h;
                 hl = Hp[R - 1];
             }
+        }
         }
     }
     if (lane == tstar) {
@@ -176,8 +194,14 @@ __global__ __launch_bounds__(64) void endcell_lg_kernel(EndcellParams P) {
     const int32_t* topx = top ? top + P.rowbuf_x_off : nullptr;
     const int32_t* lmax = P.snap_m + (uint64_t)slot * P.snap_p_slot + (uint64_t)b * P.snap_nch * kWave + tstar;
     int rbest = -1, jbest = -1;
-    for (int cc = 0; cc <= c; ++cc) {
-        if (lmax[(uint64_t)cc * kWave] != 8 * S) continue;   // uniform: lane tstar never reached S here
+    __shared__ uint8_t s_sym[kWave + kChunk];
+    __shared__ int s_top[2 * kChunk];   // M, then Ix, of the band's top row at the chunk's columns
+    for (int base = 0; base <= c; base += kWave) {   // candidate chunks, as endcell_kernel
+        const int ccl = base + lane;
+        uint64_t hits = __builtin_amdgcn_ballot_w64(ccl <= c && lmax[(uint64_t)ccl * kWave] == 8 * S);
+        while (hits) {
+        const int cc = base + (int)__builtin_ctzll(hits);
+        hits &= hits - 1;
         int Mp[R], Yp[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) { Mp[r] = 0; Yp[r] = kNeg; }
@@ -194,8 +218,20 @@ __global__ __launch_bounds__(64) void endcell_lg_kernel(EndcellParams P) {
                 Yp[2 * q + 1] = (int)(int16_t)(y >> 16) >> 3;
             }
             xl = (int)(int16_t)(sh[R * kWave] & 0xffffu) >> 3;
-            prev_up = P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] >> 3;
+            prev_up = (int)(P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] & 0xffff) >> 3;
         }
+        __syncthreads();
+        for (int k = lane; k < kWave + kChunk; k += kWave) {
+            const int j = cc * kChunk - (kWave - 1) + k;
+            s_sym[k] = (uint8_t)(j >= 0 && j < n ? ec_code8(symp, s2[j]) : 0u);
+        }
+        if (lane < kChunk) {
+            const int j = cc * kChunk + lane;
+            const bool t = top && j < n;
+            s_top[lane] = t ? (top[(uint64_t)j * rs] >> 3) : 0;
+            s_top[kChunk + lane] = t ? ((int)(int16_t)(topx[(uint64_t)j * rs] & 0xffff) >> 3) : kNeg;
+        }
+        __syncthreads();
         int hl = Mp[R - 1];
         for (int q = 0; q < kChunk; ++q) {
             const int s = cc * kChunk + q;
@@ -203,12 +239,11 @@ __global__ __launch_bounds__(64) void endcell_lg_kernel(EndcellParams P) {
             int up_h = __shfl_up(hl, 1);
             int up_x = __shfl_up(xl, 1);
             if (lane == 0) {
-                const bool t = top && s < n;
-                up_h = t ? (top[(uint64_t)s * rs] >> 3) : 0;
-                up_x = t ? ((int)(int16_t)(topx[(uint64_t)s * rs] & 0xffff) >> 3) : kNeg;
+                up_h = s_top[q];
+                up_x = s_top[kChunk + q];
             }
             if (j0 >= 0 && j0 < n) {
-                const uint32_t sym = ec_code8(symp, s2[j0]);
+                const uint32_t sym = s_sym[q - lane + (kWave - 1)];
                 int hd = prev_up, hu = up_h, xu = up_x;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
@@ -232,6 +267,7 @@ __global__ __launch_bounds__(64) void endcell_lg_kernel(EndcellParams P) {
                 hl = Mp[R - 1];
                 xl = xu;
             }
+        }
         }
     }
     if (lane == tstar) {

@@ -128,18 +128,33 @@ static_assert(kChunk % kHandGran == 0, "granules tile a chunk");
 // One copy per fill translation unit (no relocatable device code), read with
 // sa_debug_split_stats_<algo> (SA_SPLIT_STATS_ACCESSOR in sa_fill_{sw,nw,lg,gg}.hip).
 static __device__ unsigned long long g_split_stats[4096][4];
+// hand-off events of the granule at columns kEvCol..kEvCol+7 (mid-band, steady state), same
+// index: [0] the compute wave posts step kEvCol+71 (the granule parked), [1] the publisher sees
+// that post, [2] the publisher has issued the granule's stores, [3] the poller publishes the
+// granule to its compute wave, [6] the compute wave asks for the group at kEvCol, [4] it has its
+// inputs.  Kept in registers, written when the wave leaves.
+static __device__ unsigned long long g_split_ev[4096][8];
+constexpr int kEvCol = 2048;
 #define SA_SPLIT_STATS_ACCESSOR(NAME)                                                               \
     extern "C" int NAME(unsigned long long* out, int reset) {                                       \
         if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_split_stats), sizeof(g_split_stats)) != hipSuccess) \
             return 1;                                                                               \
+        if (hipMemcpyFromSymbol(out + 4096 * 4, HIP_SYMBOL(g_split_ev), sizeof(g_split_ev)) != hipSuccess) \
+            return 1;                                                                               \
         if (reset) {                                                                                \
-            static unsigned long long z[4096][4];                                                   \
-            if (hipMemcpyToSymbol(HIP_SYMBOL(g_split_stats), z, sizeof(z)) != hipSuccess) return 1; \
+            static unsigned long long z[4096][8];                                                   \
+            if (hipMemcpyToSymbol(HIP_SYMBOL(g_split_stats), z, sizeof(g_split_stats)) != hipSuccess) return 1; \
+            if (hipMemcpyToSymbol(HIP_SYMBOL(g_split_ev), z, sizeof(g_split_ev)) != hipSuccess) return 1; \
         }                                                                                           \
         return 0;                                                                                   \
     }
+#define SA_EV(k, cond) do { if (ev[k] == 0 && (cond)) ev[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define SA_EV_FLUSH() do { const uint64_t id_ = (uint64_t)slot * P.split_bands + band0;            \
+    if (id_ < 4096 && lane == 0) for (int k_ = 0; k_ < 8; ++k_) if (ev[k_]) g_split_ev[id_][k_] = ev[k_]; } while (0)
 #else
 #define SA_SPLIT_STATS_ACCESSOR(NAME)
+#define SA_EV(k, cond) do {} while (0)
+#define SA_EV_FLUSH() do {} while (0)
 #endif
 
 // MM: how a cell learns whether its two symbols match -- kMatchEq (byte equality), kMatchLut (the
@@ -249,6 +264,9 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
         for (int k = threadIdx.x; k < n; k += blockDim.x)
             s_seq2[k] = T16 ? (uint8_t)t16_code8(symp, s2[k]) : s2[k];
     }
+    if constexpr (SPLIT) {   // tag 0 = no column yet (LDS holds a previous workgroup's data)
+        for (int k = threadIdx.x; k < (AFF ? 2 : 1) * kRing; k += blockDim.x) s_ring[k] = 0;
+    }
     __syncthreads();
     const int G = P.gap, MA = P.match, MI = P.mismatch;
     const int GO = P.gap_open, GE = P.gap_extend;
@@ -278,6 +296,9 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     typedef unsigned long long __attribute__((address_space(1))) gu64;
     gu64* const hand_pair = SPLIT ? (gu64*)(P.hand + (uint64_t)slot * P.split_bands * P.max_n) : nullptr;
     uint32_t tmo = 0;   // SPLIT: a bounded wait expired
+#ifdef SA_TB_STATS
+    unsigned long long ev[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     // SPLIT poller (wave 1, see kHandGran): copies the producer band's granules into the LDS ring
     // s_ring (the hand-off ring of the multi-wave plans, unused here) and publishes the count of
     // ready columns, never more than kRing columns beyond what the compute wave has consumed.
@@ -289,29 +310,58 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
             gu64* const src = hand_pair + (uint64_t)(band0 - 1) * P.max_n;
             int pub = 0;
             uint64_t t0 = 0;
-            while (pub < n) {
+            // two window loads in flight (A and B alternate): a granule is seen about half a load
+            // round trip after it lands.  The loads are write-through-coherent (sc1) vector loads
+            // in inline asm with explicit vmcnt waits tied to their results: compiled from C++, the
+            // loop-header wait the compiler inserts drains both (vmcnt(0)).
+            auto issue = [&](int b, unsigned long long& x, unsigned long long& y) {
+                const int cl = min(b + lane, n - 1);
+                gu64* const pa = src + cl;
+#ifdef SA_POLL_CXX
+                x = __hip_atomic_load(pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                y = 1ull << 32;
+                if constexpr (AFF) y = __hip_atomic_load(pa + P.hand_x_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+                asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=&v"(x) : "v"(pa) : "memory");
+                y = 1ull << 32;
+                if constexpr (AFF) {
+                    gu64* const px = pa + P.hand_x_off;
+                    asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=&v"(y) : "v"(px) : "memory");
+                }
+#endif
+            };
+            // the older window's loads are done once only the newer window's remain in flight
+            auto settle = [&](unsigned long long& x, unsigned long long& y) {
+#ifdef SA_POLL_CXX
+                return;
+#endif
+                if constexpr (AFF) asm volatile("s_waitcnt vmcnt(2)" : "+v"(x), "+v"(y) :: "memory");
+                else asm volatile("s_waitcnt vmcnt(1)" : "+v"(x) :: "memory");
+            };
+            // columns b + lane of one window: extend the ready run from pub; false once the
+            // bounded wait expired (the band is flagged and the compute wave released)
+            auto take = [&](int b, unsigned long long x, unsigned long long y) -> bool {
                 const int cons = __hip_atomic_load(&s_sync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const int lim = min(n, cons + kRing);
-                if (lim <= pub) {   // ring full: the compute wave is behind (not a wait for the producer)
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                const int c = pub + lane;
-                const int cl = min(c, n - 1);
-                const unsigned long long x = __hip_atomic_load(src + cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                unsigned long long y = 1ull << 32;
-                if constexpr (AFF) y = __hip_atomic_load(src + P.hand_x_off + cl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int c = b + lane;
                 const bool ok = c < lim && (x >> 32) != 0 && (y >> 32) != 0;
-                const uint64_t notok = __builtin_amdgcn_ballot_w64(!ok);
-                const int adv = notok ? (int)__builtin_ctzll(notok) : kWave;   // the ready prefix
-                if (adv > 0) {
-                    if (lane < adv) {
-                        s_ring[c & (kRing - 1)] = (int)(uint32_t)x;
-                        if constexpr (AFF) s_ring[kRing + (c & (kRing - 1))] = (int)(uint32_t)y;
+                const uint64_t bad = __builtin_amdgcn_ballot_w64(c >= pub && !ok);
+                const int npub = max(pub, b + (bad ? (int)__builtin_ctzll(bad) : kWave));
+                if (npub > pub) {
+                    if (c >= pub && c < npub) {
+                        // T16: the 16-bit value tagged with its granule number + 1 in the upper
+                        // half, so the compute wave's read of a granule is its own readiness check
+                        const uint32_t tg = T16 ? ((uint32_t)c / kHandGran + 1u) << 16 : 0u;
+                        const uint32_t vm = T16 ? 0xffffu : 0xffffffffu;
+                        s_ring[c & (kRing - 1)] = (int)(((uint32_t)x & vm) | tg);
+                        if constexpr (AFF) s_ring[kRing + (c & (kRing - 1))] = (int)(((uint32_t)y & vm) | tg);
                     }
-                    pub += adv;
+                    pub = npub;
                     __hip_atomic_store(&s_sync[0], pub, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    SA_EV(3, pub >= kEvCol + 8);
                     t0 = 0;
+                } else if (lim <= pub) {
+                    __builtin_amdgcn_s_sleep(1);   // ring full: the compute wave is behind
                 } else {
                     const uint64_t now = __builtin_amdgcn_s_memrealtime();
                     if (t0 == 0) {
@@ -319,11 +369,29 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     } else if (now - t0 > P.wait_ticks) {
                         __hip_atomic_store(&s_sync[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         __hip_atomic_store(&s_sync[0], n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        return;
+                        return false;
                     }
-                    __builtin_amdgcn_s_sleep(1);
                 }
+                return true;
+            };
+            unsigned long long xa, ya, xb, yb;
+            int ba = pub, bb;
+            issue(ba, xa, ya);
+            while (true) {
+                bb = pub;
+                issue(bb, xb, yb);
+                settle(xa, ya);
+                if (!take(ba, xa, ya) || pub >= n) break;
+                ba = pub;
+                issue(ba, xa, ya);
+                settle(xb, yb);
+                if (!take(bb, xb, yb) || pub >= n) break;
             }
+            // the window load still in flight: its registers stay live up to here, so no exit
+            // code (the compiler sinks the timeout stores to the exit) can take them before the
+            // load lands
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(xa), "+v"(ya), "+v"(xb), "+v"(yb) :: "memory");
+            SA_EV_FLUSH();
             return;
         }
         if (w == 2) {
@@ -339,6 +407,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     __builtin_amdgcn_s_sleep(1);
                     continue;
                 }
+                SA_EV(1, avail >= kEvCol + 72);
                 for (int s0 = done; s0 < avail; s0 += kWave) {
                     const int st = s0 + lane;
                     const int col = st - (kWave - 1);
@@ -352,8 +421,10 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     }
                 }
                 done = avail;
+                SA_EV(2, avail >= kEvCol + 72);
                 __hip_atomic_store(&s_sync[4], done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
+            SA_EV_FLUSH();
             return;
         }
     }
@@ -633,35 +704,78 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
         }
     };
 
-    // SPLIT compute wave, band > 0, before step q (q % kHandGran == 0) of the chunk at kC: the
-    // ring must hold columns up to kC + q + kHandGran (have: the last published count seen).
+    // SPLIT compute wave, before the group of SG steps at step q of the chunk at kC: back-pressure
+    // from the publisher (the park ring slots of the next kHandGran steps held steps kRing earlier),
+    // then, band > 0, the group's lane-0 inputs.  T16 ring entries carry their granule number, so
+    // a whole group inside the matrix is read and checked in one LDS round trip (re-read while
+    // stale); otherwise the poller's column count is awaited first.
     int have = 0, pubd = 0;
-    auto split_wait = [&](int band, int kC, int q) {
+    auto split_inputs = [&](int band, int kC, int q, auto sg, int* gh, int* gx, int* gs) {
+        constexpr int G_ = decltype(sg)::value;
         if constexpr (SPLIT) {
-            // the park ring slots of steps kC + q .. + kHandGran - 1 held steps kRing earlier: the
-            // publisher must have stored those
-            if (band + 1 < B && pubd < kC + q + kHandGran - kRing) {
+            if (q % kHandGran == 0 && band + 1 < B && pubd < kC + q + kHandGran - kRing) {
                 do {
                     pubd = __hip_atomic_load(&s_sync[4], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                     if (pubd >= kC + q + kHandGran - kRing) break;
                     __builtin_amdgcn_s_sleep(1);
                 } while (true);
             }
-            if (band == 0) return;
-            const int need = min(n, kC + q + kHandGran);
-            if (have < need) {
-                have = __hip_atomic_load(&s_sync[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const bool tagged = T16 && band > 0 && kC + q + G_ <= n;
+            if (band > 0 && !tagged) {
+                const int need = min(n, kC + q + G_);
                 if (have < need) {
+                    have = __hip_atomic_load(&s_sync[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (have < need) {
 #ifdef SA_TB_STATS
-                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-                    do {
-                        __builtin_amdgcn_s_sleep(1);
-                        have = __hip_atomic_load(&s_sync[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    } while (have < need);
+                        do {
+                            __builtin_amdgcn_s_sleep(1);
+                            have = __hip_atomic_load(&s_sync[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        } while (have < need);
 #ifdef SA_TB_STATS
-                    st_wait += __builtin_amdgcn_s_memrealtime() - t0;
+                        st_wait += __builtin_amdgcn_s_memrealtime() - t0;
 #endif
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < G_; ++k) {
+                gh[k] = in_h[q + k];
+                gs[k] = s_step[64 + q + k];
+                if constexpr (AFF) gx[k] = in_x[q + k];
+            }
+            if constexpr (T16) {
+                if (tagged) {
+                    const uint32_t want = ((uint32_t)(kC + q) / kHandGran + 1u) << 16;
+                    auto fresh = [&]() {
+                        uint32_t mn = (uint32_t)gh[0];
+#pragma unroll
+                        for (int k = 1; k < G_; ++k) mn = min(mn, (uint32_t)gh[k]);
+                        if constexpr (AFF) {
+#pragma unroll
+                            for (int k = 0; k < G_; ++k) mn = min(mn, (uint32_t)gx[k]);
+                        }
+                        return mn >= want;
+                    };
+                    if (!fresh()) {
+#ifdef SA_TB_STATS
+                        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+                        do {
+                            // the poller's bounded wait expired: go on (the pair is re-run)
+                            if (__hip_atomic_load(&s_sync[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                            for (int k = 0; k < G_; ++k) {
+                                gh[k] = __hip_atomic_load(&in_h[q + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                if constexpr (AFF) gx[k] = __hip_atomic_load(&in_x[q + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            }
+                        } while (!fresh());
+#ifdef SA_TB_STATS
+                        st_wait += __builtin_amdgcn_s_memrealtime() - t0;
+#endif
+                    }
                 }
             }
         }
@@ -685,14 +799,10 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                 const int q = q0 + g;
                 int vh, vx = 0, vs;
                 if constexpr (SPLIT) {
-                    if (q % kHandGran == 0) split_wait(band, kC, q);
                     if (g % SG == 0) {
-#pragma unroll
-                        for (int k = 0; k < SG; ++k) {
-                            gh[k] = in_h[q + k];
-                            gs[k] = s_step[64 + q + k];
-                            if constexpr (AFF) gx[k] = in_x[q + k];
-                        }
+                        SA_EV(6, kC + q >= kEvCol);
+                        split_inputs(band, kC, q, std::integral_constant<int, SG>{}, gh, gx, gs);
+                        SA_EV(4, kC + q >= kEvCol);
                     }
                     vh = gh[g % SG];
                     vs = gs[g % SG];
@@ -716,8 +826,11 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                 park_h[q] = hl;
                 if constexpr (AFF) park_x[q] = xl;
                 if constexpr (SPLIT) {
-                    if ((q + 1) % kHandGran == 0 && band + 1 < B && lane == 0)
+                    // (every lane stores the same count: no exec-mask switch)
+                    if ((q + 1) % kHandGran == 0 && band + 1 < B) {
                         __hip_atomic_store(&s_sync[3], kC + q + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        SA_EV(0, kC + q + 1 >= kEvCol + 72);
+                    }
                 }
             }
             const uint64_t pkt0 = (uint64_t)((kC + q0) / SPP) * PPS;
@@ -955,6 +1068,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                 g_split_stats[id][2] = __builtin_amdgcn_s_memrealtime();
                 g_split_stats[id][3] = st_wait;
             }
+            SA_EV_FLUSH();
 #endif
         }
     } else if constexpr (LOCAL) {

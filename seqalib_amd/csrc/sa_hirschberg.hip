@@ -77,12 +77,90 @@ __device__ __forceinline__ int32_t hb_cell_v(int32_t hd, int32_t hu, int32_t hl,
 }
 
 // ------------------------------------------------------------------ batched NWScore sweeps
+// 16-bit band of a whole-wave NWScore sweep (Dc16, sa_dc.h): registers hold H - delta in their low
+// 16 bits; per cell max(Hd + s, max(Hu, Hl) + Gap) = v_max_i16, v_add_u16, v_bfe_i32 (the row's
+// byte profile at 8 x the column's symbol code), v_add_u16, v_max_i16 -- one 32-bit op, four
+// 16-bit ops, against seven 32-bit ops of the int32 cell.  Same wavefront and hand-off as below.
+template <int R>
+__device__ __forceinline__ void hb_band16(const HbSweep& d, const uint8_t* s1, const uint8_t* s2, const uint32_t* aux,
+                                          int32_t delta, int32_t G, int band, int lastb, int tl, int rl, int32_t* out,
+                                          int32_t& hl) {
+    const int lane = threadIdx.x;
+    const int m = d.alen, n = d.blen;
+    constexpr int BAND = 64 * R;
+    const uint32_t symp = aux[kAuxProf + 4];
+    const uint32_t g16 = (uint32_t)G & 0xffffu;
+    const int row0 = band * BAND + lane * R;
+    uint32_t a[R];
+    int32_t Hp[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int row = row0 + r;
+        a[r] = row < m ? aux[kAuxProf + (dc_code8(symp, d.rev ? s1[d.a - row] : s1[d.a + row]) >> 3)] : 0u;
+        Hp[r] = (row + 1) * G - delta;                      // H[i][0] = i * Gap (:37)
+    }
+    int32_t prev_up = row0 * G - delta;                      // H[row0][0]
+    auto load_chunk = [&](int c0, int32_t& vu, uint32_t& vs) {
+        const int j = c0 + lane;
+        vu = 0;
+        vs = 0;
+        if (j < n) {
+            vu = (band == 0 ? (j + 1) * G : out[j + 1]) - delta;
+            vs = dc_code8(symp, d.rev ? s2[d.b - j] : s2[d.b + j]);
+        }
+    };
+    int32_t vup, nvup;
+    uint32_t vsym, nvsym, sym = 0;
+    load_chunk(0, vup, vsym);
+    for (int c0 = 0; c0 < n + 63; c0 += 64) {
+        load_chunk(c0 + 64, nvup, nvsym);
+        const int steps = min(64, n + 63 - c0);
+        for (int q = 0; q < steps; ++q) {
+            const int s = c0 + q;
+            const int32_t up_h = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vup, q), hl, 0x138, 0xf, 0xf, false);
+            sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vsym, q), sym, 0x138, 0xf, 0xf, false);
+            const int j0 = s - lane;
+            if (j0 >= 0 && j0 < n) {
+                int32_t hd = prev_up, hu = up_h;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    int32_t h, t;
+                    asm("v_max_i16 %0, %2, %3\n\t"
+                        "v_add_u16 %0, %4, %0\n\t"
+                        "v_bfe_i32 %1, %5, %6, 8\n\t"
+                        "v_add_u16 %1, %7, %1\n\t"
+                        "v_max_i16 %0, %1, %0"
+                        : "=&v"(h), "=&v"(t)
+                        : "v"(hu), "v"(Hp[r]), "s"(g16), "v"(a[r]), "v"(sym), "v"(hd));
+                    hd = Hp[r];
+                    Hp[r] = h;
+                    hu = h;
+                }
+                prev_up = up_h;
+                hl = Hp[R - 1];
+                if (band < lastb) {
+                    if (lane == 63) out[j0 + 1] = dc_unpack16(hl, delta);   // this band's last row, in place
+                } else if (lane == tl) {
+                    int32_t v = Hp[0];
+#pragma unroll
+                    for (int r = 1; r < R; ++r)
+                        if (r == rl) v = Hp[r];
+                    out[j0 + 1] = dc_unpack16(v, delta);                   // row m of the sweep
+                }
+            }
+        }
+        vup = nvup;
+        vsym = nvsym;
+    }
+}
+
 // MM: kMatchEq / kMatchLut (byte symbols) or kMatchBits (pair-local indices + the pair's match
-// bitmap, the generic-Ty path; DcSrc in sa_dc.h).
+// bitmap, the generic-Ty path; DcSrc in sa_dc.h).  d16.aux: the 16-bit path may run (the device's
+// alphabet decision picks it, uniformly for the grid).
 template <int R, int MM, bool ALLOW>
 __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* split,
                                                       const DcLevel* lvl, int32_t* rows, const uint32_t* lutbits,
-                                                      DcBits bits, HbScore sc) {
+                                                      DcBits bits, HbScore sc, Dc16 d16) {
     constexpr bool LUT = MM == kMatchLut;
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];
     const int lane = threadIdx.x;
@@ -96,6 +174,21 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
     const DcSrc<MM> src = bits.src<MM>(s1, s2, s_lut, sub.pair, true);
     int32_t* out = rows + d.out;
     const int m = d.alen, n = d.blen, G = sc.gap;
+    if constexpr (MM != kMatchBits) {
+        if (d16.aux && d16.aux[kAuxSel] == 1) {
+            constexpr int BAND = 64 * R;
+            const int bands = (m + BAND - 1) / BAND;
+            const int tl = ((m - 1) % BAND) / R, rl = (m - 1) % R;
+            int32_t hl = 0;
+            for (int band = 0; band < bands; ++band) {
+                hb_band16<R>(d, s1, s2, d16.aux, d16.delta, G, band, bands - 1, tl, rl, out, hl);
+                __threadfence_block();
+                __syncthreads();
+            }
+            if (lane == 0) out[0] = m * G;
+            return;
+        }
+    }
     auto symA = [&](int k) -> uint32_t { return src.a(d.rev ? d.a - k : d.a + k); };
     auto symB = [&](int k) -> uint32_t { return src.b(d.rev ? d.b - k : d.b + k); };
     constexpr int BAND = 64 * R;
@@ -429,6 +522,7 @@ struct HbLaunch {
     const uint32_t* lut;
     DcBits bits;
     HbScore sc;
+    Dc16 d16;
 };
 
 template <int MM, bool ALLOW>
@@ -438,7 +532,7 @@ void launch_sweeps_t(int R, int G, uint32_t count, const HbLaunch& a, hipStream_
     hipLaunchKernelGGL((hb_sweep_seg_kernel<GG, MM, ALLOW>), dim3((count + 64 / GG - 1) / (64 / GG)), block, 0, st, \
                        a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc)
 #define SA_HB_SW(RR) \
-    hipLaunchKernelGGL((hb_sweep_kernel<RR, MM, ALLOW>), dim3(count), block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc)
+    hipLaunchKernelGGL((hb_sweep_kernel<RR, MM, ALLOW>), dim3(count), block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc, a.d16)
     if (G == 8) SA_HB_SEG(8);
     else if (G == 16) SA_HB_SEG(16);
     else if (G == 32) SA_HB_SEG(32);
@@ -484,6 +578,15 @@ int hirschberg_run(DcWork& w, hipEvent_t prev, const sa_scoring* scoring, const 
     sc.mismatch = sc.allow ? scoring->mismatch : INT_MIN;
     const bool bits = in.bits.mbits != nullptr;
     SA_DC_HIP(w.prepare(b, npairs, leaf_rows, 2, 2, 6, st, prev));
+    // 16-bit whole-wave sweeps when the shapes and scoring admit them (sa_dc.h Dc16); the device
+    // takes them when the batch alphabet has <= 4 symbols
+    Dc16 d16 = bits ? Dc16{} : dc16_plan(false, scoring, b.max_m, b.max_n);
+    if (d16.aux) {
+        SA_DC_HIP(w.aux.alloc(kAuxWords));
+        SA_DC_HIP(launch_alphabet_scan(in.d1, in.o1, in.d2, in.o2, npairs, w.aux.p, st));
+        SA_DC_HIP(launch_decide_t16(in.lutbits, sc.match, d16.mismatch, 2, w.aux.p, st));
+        d16.aux = w.aux.p;
+    }
     SA_DC_HIP(hipMemsetAsync(d_res, 0, sizeof(sa_result) * npairs, st));
     SA_DC_HIP(dc_launch_init(in.o1, in.o2, npairs, 0, b, w.cur.p, d_res, st));
     uint32_t cap = npairs;     // upper bound on this level's subproblems
@@ -497,7 +600,7 @@ int hirschberg_run(DcWork& w, hipEvent_t prev, const sa_scoring* scoring, const 
         int R = 1;
         while (R < rmax && 64 * R < maxa) R *= 2;   // bands of 64 R rows
         const int G = !seg_sweeps ? 0 : maxa <= 8 ? 8 : maxa <= 16 ? 16 : maxa <= 32 ? 32 : 0;
-        const HbLaunch a{in.d1, in.d2, w.split.p, w.lvl.p + l, w.rows.p, in.lutbits, in.bits, sc};
+        const HbLaunch a{in.d1, in.d2, w.split.p, w.lvl.p + l, w.rows.p, in.lutbits, in.bits, sc, d16};
         SA_DC_HIP(launch_sweeps(R, G, 2 * splits, a, st));
         hipLaunchKernelGGL(hb_split_kernel, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p, w.next.p,
                            d_res);

@@ -166,10 +166,115 @@ __device__ __forceinline__ void mm_band(const MmSweep& d, const DcSrc<MM>& src, 
     }
 }
 
+// 16-bit band of a whole-wave affine sweep (Dc16, sa_dc.h): C, e and D kept as value - delta in the
+// low 16 bits.  Per cell (per row): e = max(Ep, Cp + g) + h and D = max(Du, Cu + g) + h (three
+// 16-bit ops each), the diagonal Cd + s (v_bfe_i32 of the row's byte profile + v_add_u16), and
+// C = max(max(D, e), diag) (two v_max_i16): ten instructions, one of them 32-bit.
+template <int R, bool LAST>
+__device__ __forceinline__ void mm_band16(const MmSweep& d, const uint8_t* s1, const uint8_t* s2, const uint32_t* aux,
+                                          int32_t delta, const MmScore& sc, int band, int32_t* outC, int32_t* outD,
+                                          int tl, int rl, int32_t& cl, int32_t& dl) {
+    const int lane = threadIdx.x;
+    const int m = d.alen, n = d.blen, g = sc.g, h = sc.h;
+    constexpr int BAND = 64 * R;
+    const uint32_t symp = aux[kAuxProf + 4];
+    const uint32_t g16 = (uint32_t)g & 0xffffu, h16 = (uint32_t)h & 0xffffu;
+    const int row0 = band * BAND + lane * R;
+    uint32_t a[R];
+    int32_t Cp[R], Ep[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int row = row0 + r;
+        a[r] = row < m ? aux[kAuxProf + (dc_code8(symp, d.rev ? s1[d.a - row] : s1[d.a + row]) >> 3)] : 0u;
+        Cp[r] = d.t0 + h * (row + 1) - delta;                // C[i][0] = t0 + i h (:192-197)
+        Ep[r] = Cp[r] + g;                                   // e = t + g (:198)
+    }
+    int32_t prev_up = (row0 == 0 ? 0 : d.t0 + h * row0) - delta;   // C[row0][0]; C[0][0] = 0 (:172)
+    auto load_chunk = [&](int c0, int32_t& vc, int32_t& vd, uint32_t& vs) {
+        const int j = c0 + lane;
+        vc = 0;
+        vd = 0;
+        vs = 0;
+        if (j < n) {
+            if (band == 0) {
+                vc = g + h * (j + 1);                        // CC[j] = g + j h, DD[j] = CC[j] + g (:183-188)
+                vd = vc + g;
+            } else {
+                vc = outC[j + 1];
+                vd = outD[j + 1];
+            }
+            vc -= delta;
+            vd -= delta;
+            vs = dc_code8(symp, d.rev ? s2[d.b - j] : s2[d.b + j]);
+        }
+    };
+    int32_t vc, vd, nvc, nvd;
+    uint32_t vs, nvs, sym = 0;
+    load_chunk(0, vc, vd, vs);
+    for (int c0 = 0; c0 < n + 63; c0 += 64) {
+        load_chunk(c0 + 64, nvc, nvd, nvs);
+        const int steps = min(64, n + 63 - c0);
+        for (int q = 0; q < steps; ++q) {
+            const int s = c0 + q;
+            const int32_t up_c = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vc, q), cl, 0x138, 0xf, 0xf, false);
+            const int32_t up_d = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vd, q), dl, 0x138, 0xf, 0xf, false);
+            sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vs, q), sym, 0x138, 0xf, 0xf, false);
+            const int j0 = s - lane;
+            if (j0 >= 0 && j0 < n) {
+                int32_t cd = prev_up, cu = up_c, du = up_d, dsel = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    int32_t e, dd, c, t;
+                    asm("v_add_u16 %0, %7, %8\n\t"        // e = max(Ep, Cp + g) + h      (:202)
+                        "v_max_i16 %0, %9, %0\n\t"
+                        "v_add_u16 %0, %10, %0\n\t"
+                        "v_add_u16 %1, %7, %11\n\t"       // D = max(Du, Cu + g) + h      (:203)
+                        "v_max_i16 %1, %12, %1\n\t"
+                        "v_add_u16 %1, %10, %1\n\t"
+                        "v_bfe_i32 %3, %13, %14, 8\n\t"   // diag = Cd + s(a, b)
+                        "v_add_u16 %3, %15, %3\n\t"
+                        "v_max_i16 %2, %1, %0\n\t"        // C = max(max(D, e), diag)
+                        "v_max_i16 %2, %3, %2"
+                        : "=&v"(e), "=&v"(dd), "=&v"(c), "=&v"(t)
+                        : "0"(0), "1"(0), "2"(0), "s"(g16), "v"(Cp[r]), "v"(Ep[r]), "s"(h16), "v"(cu), "v"(du),
+                          "v"(a[r]), "v"(sym), "v"(cd));
+                    cd = Cp[r];
+                    Cp[r] = c;
+                    Ep[r] = e;
+                    cu = c;
+                    du = dd;
+                    if constexpr (LAST) {
+                        if (r == rl) dsel = dd;
+                    }
+                }
+                prev_up = up_c;
+                cl = Cp[R - 1];
+                dl = du;
+                if constexpr (!LAST) {
+                    if (lane == 63) {                         // this band's last row, in place
+                        outC[j0 + 1] = dc_unpack16(cl, delta);
+                        outD[j0 + 1] = dc_unpack16(dl, delta);
+                    }
+                } else if (lane == tl) {
+                    int32_t csel = Cp[0];
+#pragma unroll
+                    for (int r = 1; r < R; ++r)
+                        if (r == rl) csel = Cp[r];
+                    outC[j0 + 1] = dc_unpack16(csel, delta);  // row m of the sweep
+                    outD[j0 + 1] = dc_unpack16(dsel, delta);
+                }
+            }
+        }
+        vc = nvc;
+        vd = nvd;
+        vs = nvs;
+    }
+}
+
 template <int R, int MM, bool ALLOW>
 __global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* split,
                                                       const DcLevel* lvl, int32_t* rows, const uint32_t* lutbits,
-                                                      DcBits bits, MmScore sc) {
+                                                      DcBits bits, MmScore sc, Dc16 d16) {
     constexpr bool LUT = MM == kMatchLut;
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];
     const int lane = threadIdx.x;
@@ -188,7 +293,20 @@ __global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const u
     const int bands = (m + BAND - 1) / BAND;
     const int tl = ((m - 1) % BAND) / R, rl = (m - 1) % R;   // owner of row m-1 in the last band
     int32_t cl = 0, dl = 0;                                   // this lane's last row: C, D
+    bool b16 = false;
+    if constexpr (MM != kMatchBits) b16 = d16.aux && d16.aux[kAuxSel] == 1;   // uniform over the grid
     for (int band = 0; band < bands; ++band) {
+        if constexpr (MM != kMatchBits) {
+            if (b16) {
+                if (band < bands - 1)
+                    mm_band16<R, false>(d, s1, s2, d16.aux, d16.delta, sc, band, outC, outD, tl, rl, cl, dl);
+                else
+                    mm_band16<R, true>(d, s1, s2, d16.aux, d16.delta, sc, band, outC, outD, tl, rl, cl, dl);
+                __threadfence_block();
+                __syncthreads();
+                continue;
+            }
+        }
         if (band < bands - 1)
             mm_band<R, MM, ALLOW, false>(d, src, sc, band, outC, outD, tl, rl, cl, dl);
         else
@@ -509,6 +627,7 @@ struct MmLaunch {
     const uint32_t* lut;
     DcBits bits;
     MmScore sc;
+    Dc16 d16;
 };
 
 template <int MM, bool ALLOW>
@@ -518,7 +637,7 @@ void launch_mm_sweeps_t(int R, int G, uint32_t count, const MmLaunch& a, hipStre
     hipLaunchKernelGGL((mm_sweep_seg_kernel<GG, MM, ALLOW>), dim3((count + 64 / GG - 1) / (64 / GG)), block, 0, st, \
                        a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc)
 #define SA_MM_SW(RR) \
-    hipLaunchKernelGGL((mm_sweep_kernel<RR, MM, ALLOW>), dim3(count), block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc)
+    hipLaunchKernelGGL((mm_sweep_kernel<RR, MM, ALLOW>), dim3(count), block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc, a.d16)
     if (G == 8) SA_MM_SEG(8);
     else if (G == 16) SA_MM_SEG(16);
     else if (G == 32) SA_MM_SEG(32);
@@ -564,6 +683,14 @@ int myersmiller_run(DcWork& w, hipEvent_t prev, const sa_scoring* scoring, const
     sc.mismatch = sc.allow ? scoring->mismatch : INT_MIN;
     const bool bits = in.bits.mbits != nullptr;
     SA_DC_HIP(w.prepare(b, npairs, leaf_rows, 3, 4, 6, st, prev));
+    // 16-bit whole-wave sweeps (sa_dc.h Dc16), as hirschberg_run
+    Dc16 d16 = bits ? Dc16{} : dc16_plan(true, scoring, b.max_m, b.max_n);
+    if (d16.aux) {
+        SA_DC_HIP(w.aux.alloc(kAuxWords));
+        SA_DC_HIP(launch_alphabet_scan(in.d1, in.o1, in.d2, in.o2, npairs, w.aux.p, st));
+        SA_DC_HIP(launch_decide_t16(in.lutbits, sc.match, d16.mismatch, 2, w.aux.p, st));
+        d16.aux = w.aux.p;
+    }
     SA_DC_HIP(hipMemsetAsync(d_res, 0, sizeof(sa_result) * npairs, st));
     // getAlignment: buildResultRec(.., GapOpen, GapOpen) (:417)
     SA_DC_HIP(dc_launch_init(in.o1, in.o2, npairs, sc.g, b, w.cur.p, d_res, st));
@@ -578,7 +705,7 @@ int myersmiller_run(DcWork& w, hipEvent_t prev, const sa_scoring* scoring, const
         int R = 1;
         while (R < rmax && 64 * R < maxa) R *= 2;   // bands of 64 R rows
         const int G = !seg_sweeps ? 0 : maxa <= 8 ? 8 : maxa <= 16 ? 16 : maxa <= 32 ? 32 : 0;
-        const MmLaunch a{in.d1, in.d2, w.split.p, w.lvl.p + l, w.rows.p, in.lutbits, in.bits, sc};
+        const MmLaunch a{in.d1, in.d2, w.split.p, w.lvl.p + l, w.rows.p, in.lutbits, in.bits, sc, d16};
         SA_DC_HIP(launch_mm_sweeps(R, G, 2 * splits, a, st));
         hipLaunchKernelGGL(mm_split_kernel, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p, w.next.p,
                            d_res, sc.g);

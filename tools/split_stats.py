@@ -22,7 +22,8 @@ if algo == "sw":
 else:
     A, args, n = sa.SA_LOCAL_GOTOH, (-3, -1, 1, -1, False), 8192
 pairs = [(sa.synth_dna(1, n), sa.synth_dna(2, n))]
-out = (C.c_ulonglong * (4096 * 4))()
+out = (C.c_ulonglong * (4096 * 12))()
+EV = ["post71", "pub_sees", "pub_stored", "poll_has8", "cmp_has", "cmp_start"]
 for R in Rs:
     os.environ["SEQALIB_PLAN"] = f"{R},0"
     for rep in range(2):
@@ -30,9 +31,13 @@ for R in Rs:
         eng.align(A, sa.ScoringSystem(*args), pairs)
         f, tb, _ = eng.last_timings()
         fn(out, 0)
-    st = np.frombuffer(out, dtype=np.uint64).reshape(4096, 4)
-    st = st[st[:, 0] > 0]
-    st = st[np.argsort(st[:, 0])]
+    allst = np.frombuffer(out, dtype=np.uint64)
+    st = allst[:4096 * 4].reshape(4096, 4)
+    ev = allst[4096 * 4:].reshape(4096, 8)
+    keep = st[:, 0] > 0
+    st, ev = st[keep], ev[keep]
+    order = np.argsort(st[:, 0])
+    st, ev = st[order], ev[order]
     t0 = st[:, 1].min()
     start = (st[:, 1] - t0) / 100.0
     end = (st[:, 2] - t0) / 100.0
@@ -46,3 +51,19 @@ for R in Rs:
           f"last band ends {end.max():.0f} us; step {busy.min() / steps * 1e3:.1f} ns in the fastest band")
     for b in list(range(0, min(4, len(st)))) + list(range(max(4, len(st) - 3), len(st))):
         print(f"   band {b:3d}: start {start[b]:8.1f}  end {end[b]:8.1f}  busy {busy[b]:7.1f}  polled {wait[b]:7.1f}")
+    # hand-off chain of the granule at column 2048 (kEvCol), band b-1 -> band b (us): producer
+    # compute posts it -> its publisher sees the post -> has issued the stores -> consumer poller
+    # has it -> consumer compute has it (after asking for it at [6])
+    rel = lambda x: (x.astype(np.int64) - int(t0)) / 100.0
+    hops = []
+    for b in range(1, len(st)):
+        p, c = ev[b - 1], ev[b]
+        if p[0] and p[1] and p[2] and c[3] and c[4] and c[6]:
+            hops.append([rel(p[1]) - rel(p[0]), rel(p[2]) - rel(p[1]), rel(c[3]) - rel(p[2]), rel(c[4]) - rel(c[3]),
+                         rel(c[4]) - rel(c[6]), rel(c[4]) - rel(p[0])])
+    if hops:
+        h = np.array(hops)
+        print(f"   hand-off of the granule at column 2048, median us: publisher wake {np.median(h[:, 0]):.2f}, "
+              f"store issue {np.median(h[:, 1]):.2f}, store -> poller {np.median(h[:, 2]):.2f}, poller -> compute "
+              f"{np.median(h[:, 3]):.2f}; compute waited {np.median(h[:, 4]):.2f} (mean {h[:, 4].mean():.2f}); "
+              f"post -> consumer has it {np.median(h[:, 5]):.2f} (min {h[:, 5].min():.2f}, max {h[:, 5].max():.2f})")
