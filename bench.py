@@ -299,6 +299,7 @@ def main():
     ops = d_ops[last].cpu().numpy()
     bad = int(np.count_nonzero(res["flags"]))
     checked = 0
+    diffs = []
     for p in (0, P - 1):
         a, b = s1[o1[p]:o1[p + 1]].tobytes(), s2[o2[p]:o2[p + 1]].tobytes()
         o = oracle_align(0, SCORING, a, b)
@@ -307,13 +308,16 @@ def main():
                ops[off:off + int(res["nops"][p])].tobytes())
         if got != (o["score"], o["end_i"], o["end_j"], o["ops"]):
             bad += 1
+            diffs.append({"pair": int(p), "got": list(got[:3]) + [len(got[3])], "want": [o["score"], o["end_i"], o["end_j"], len(o["ops"])],
+                          "first_op_diff": next((i for i, (x, y) in enumerate(zip(got[3], o["ops"])) if x != y), -1)})
         checked += 1
 
     if args.rank_out:
         os.makedirs(args.rank_out, exist_ok=True)
         with open(os.path.join(args.rank_out, f"rank{rank}.json"), "w") as f:
             json.dump({"rank": rank, "world": world, "own_s": own, "max_s": elapsed, "seed_base": shard_seed_base(rank, world, P),
-                       "checked": checked, "bad": bad, "flags": int(np.count_nonzero(res["flags"]))}, f)
+                       "checked": checked, "bad": bad, "flags": int(np.count_nonzero(res["flags"])), "diffs": diffs,
+                       "plan": list(eng.last_plan())}, f)
     if rank != 0:
         return
     per_launch_cells = cells_rank  # one fill launch covers the whole batch when it fits HBM

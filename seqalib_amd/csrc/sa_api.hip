@@ -659,6 +659,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fp.hand_x_off = pl.split ? hand_x_off : 0;
             fp.part = pl.split ? reinterpret_cast<int32_t*>(spbase + sp_part) : nullptr;
             fp.wait_ticks = wait_ticks;
+            fp.no_start = getenv("SEQALIB_NO_START") ? 1 : 0;
             return FillVariant{pl.R, lut, allow || v.t16, keyed, v.t16, v.cmax, pl.split, bits};
         };
         for (int k = 0; k < nv; ++k) {

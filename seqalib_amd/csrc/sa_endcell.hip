@@ -21,6 +21,13 @@
 namespace sa {
 
 
+// the band's top row: the fill's row buffer or, SPLIT, its write-through hand-off granules, read
+// write-through-coherent (sc1) like sa_traceback_seg.hip's seg_hand
+__device__ __forceinline__ int32_t ec_top(const int32_t* p) {
+    typedef const int32_t __attribute__((address_space(1))) cgi32;
+    return __hip_atomic_load((cgi32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ uint32_t ec_code8(uint32_t sp, uint32_t b) {
     return (b == ((sp >> 8) & 255u) ? 8u : 0u) | (b == ((sp >> 16) & 255u) ? 16u : 0u) |
            (b == (sp >> 24) ? 24u : 0u);
@@ -100,7 +107,7 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
         }
         if (lane < kChunk) {
             const int j = cc * kChunk + lane;
-            s_top[lane] = (top && j < n) ? (top[(uint64_t)j * rs] >> 2) : 0;
+            s_top[lane] = (top && j < n) ? (ec_top(top + (uint64_t)j * rs) >> 2) : 0;
         }
         __syncthreads();
         int hl = Hp[R - 1];
@@ -110,6 +117,11 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
             int up_h = __shfl_up(hl, 1);
             if (lane == 0) up_h = s_top[q];
             if (j0 >= 0 && j0 < n) {
+                if (j0 == 0) {   // the lane's first column: the matrix border (the fill's snapshot
+                    prev_up = 0; // of a lane that had not started holds its start-mode garbage)
+#pragma unroll
+                    for (int r = 0; r < R; ++r) Hp[r] = 0;
+                }
                 const uint32_t sym = s_sym[q - lane + (kWave - 1)];
                 int hd = prev_up, hu = up_h;
 #pragma unroll
@@ -228,8 +240,8 @@ __global__ __launch_bounds__(64) void endcell_lg_kernel(EndcellParams P) {
         if (lane < kChunk) {
             const int j = cc * kChunk + lane;
             const bool t = top && j < n;
-            s_top[lane] = t ? (top[(uint64_t)j * rs] >> 3) : 0;
-            s_top[kChunk + lane] = t ? ((int)(int16_t)(topx[(uint64_t)j * rs] & 0xffff) >> 3) : kNeg;
+            s_top[lane] = t ? (ec_top(top + (uint64_t)j * rs) >> 3) : 0;
+            s_top[kChunk + lane] = t ? ((int)(int16_t)(ec_top(topx + (uint64_t)j * rs) & 0xffff) >> 3) : kNeg;
         }
         __syncthreads();
         int hl = Mp[R - 1];
@@ -243,6 +255,11 @@ __global__ __launch_bounds__(64) void endcell_lg_kernel(EndcellParams P) {
                 up_x = s_top[kChunk + q];
             }
             if (j0 >= 0 && j0 < n) {
+                if (j0 == 0) {   // the lane's first column: the matrix border (as endcell_kernel)
+                    prev_up = 0;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) { Mp[r] = 0; Yp[r] = kNeg; }
+                }
                 const uint32_t sym = s_sym[q - lane + (kWave - 1)];
                 int hd = prev_up, hu = up_h, xu = up_x;
 #pragma unroll

@@ -120,6 +120,7 @@ constexpr int fill_max_threads() { return (R >= 32 || (WIDE && R >= 16)) ? 256 :
 // and a publish is an LDS read + wait + store.  With the 32-column chunks of round 2 a band ran
 // ~161 steps behind its producer (63 inherent, ~64 chunk quantisation, the rest latency).
 constexpr int kHandGran = 8;
+enum : int { kStepAny = 0, kStepSteady = 1, kStepStart = 2 };   // fill_kernel's step modes
 static_assert(kChunk % kHandGran == 0, "granules tile a chunk");
 
 #ifdef SA_TB_STATS
@@ -133,7 +134,7 @@ static __device__ unsigned long long g_split_stats[4096][4];
 // that post, [2] the publisher has issued the granule's stores, [3] the poller publishes the
 // granule to its compute wave, [6] the compute wave asks for the group at kEvCol, [4] it has its
 // inputs.  Kept in registers, written when the wave leaves.
-static __device__ unsigned long long g_split_ev[4096][8];
+static __device__ unsigned long long g_split_ev[4096][12];
 constexpr int kEvCol = 2048;
 #define SA_SPLIT_STATS_ACCESSOR(NAME)                                                               \
     extern "C" int NAME(unsigned long long* out, int reset) {                                       \
@@ -142,7 +143,7 @@ constexpr int kEvCol = 2048;
         if (hipMemcpyFromSymbol(out + 4096 * 4, HIP_SYMBOL(g_split_ev), sizeof(g_split_ev)) != hipSuccess) \
             return 1;                                                                               \
         if (reset) {                                                                                \
-            static unsigned long long z[4096][8];                                                   \
+            static unsigned long long z[4096][12];                                                   \
             if (hipMemcpyToSymbol(HIP_SYMBOL(g_split_stats), z, sizeof(g_split_stats)) != hipSuccess) return 1; \
             if (hipMemcpyToSymbol(HIP_SYMBOL(g_split_ev), z, sizeof(g_split_ev)) != hipSuccess) return 1; \
         }                                                                                           \
@@ -150,7 +151,7 @@ constexpr int kEvCol = 2048;
     }
 #define SA_EV(k, cond) do { if (ev[k] == 0 && (cond)) ev[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define SA_EV_FLUSH() do { const uint64_t id_ = (uint64_t)slot * P.split_bands + band0;            \
-    if (id_ < 4096 && lane == 0) for (int k_ = 0; k_ < 8; ++k_) if (ev[k_]) g_split_ev[id_][k_] = ev[k_]; } while (0)
+    if (id_ < 4096 && lane == 0) for (int k_ = 0; k_ < 12; ++k_) if (ev[k_]) g_split_ev[id_][k_] = ev[k_]; } while (0)
 #else
 #define SA_SPLIT_STATS_ACCESSOR(NAME)
 #define SA_EV(k, cond) do {} while (0)
@@ -297,7 +298,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     gu64* const hand_pair = SPLIT ? (gu64*)(P.hand + (uint64_t)slot * P.split_bands * P.max_n) : nullptr;
     uint32_t tmo = 0;   // SPLIT: a bounded wait expired
 #ifdef SA_TB_STATS
-    unsigned long long ev[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long ev[12] = {};
 #endif
     // SPLIT poller (wave 1, see kHandGran): copies the producer band's granules into the LDS ring
     // s_ring (the hand-off ring of the multi-wave plans, unused here) and publishes the count of
@@ -466,22 +467,43 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     int32_t* park_h = s_park;
     int32_t* park_x = s_park + 32;
     // vh / vx / vs: lane 0's row-above inputs (H, Ix) and the column symbol of this step
-    auto step = [&](auto steady, int q, int s, int vh, int vx, int vs, uint32_t (&rec)[RW], auto odd) {
-        constexpr bool STEADY = decltype(steady)::value;
+    // Step modes (kStepAny: any lane may be outside the matrix, per-lane branch; kStepSteady: every
+    // lane inside; kStepStart, T16 local CMAX only: the band's first chunks, where lanes left of
+    // their first column run the cell on garbage and are reset to the matrix border at it -- no
+    // per-lane branch, so a lone SPLIT wave's first granule is not slowed by the band's start)
+    auto step = [&](auto mode, int q, int s, int vh, int vx, int vs, uint32_t (&rec)[RW], auto odd) {
+        constexpr int MODE = (int)decltype(mode)::value;
+        constexpr bool STEADY = MODE == kStepSteady;
+        constexpr bool START = MODE == kStepStart;
+        // T16 records narrower than a word: pushed straight into the packet word (acc_rec)
+        constexpr bool ACC = T16 && RB < 32 && MODE != kStepAny;
         constexpr bool ODD = decltype(odd)::value;
         const int up_h = shr1(vh, hl);
         int up_x = 0;
         if constexpr (AFF) up_x = shr1(vx, xl);
         sym = shr1(vs, sym);
         const int j = s - lane;
-        // T16 with whole record words: the v_alignbit pushes shift every bit a word held out of
-        // it, and a lane-step outside the matrix only fills its own (never read) record bytes
-        if constexpr (!T16 || RB % 32 != 0) {
+        // T16: the v_alignbit pushes shift every bit a word held out of it, and a lane-step outside
+        // the matrix only fills its own (never read) record bytes -- except a narrow record of
+        // kStepAny, ORed into its packet word unshifted when the lane-step is outside: zeroed
+        if constexpr (!T16 || (RB < 32 && !ACC) || (RB > 32 && RB % 32 != 0)) {
 #pragma unroll
             for (int e = 0; e < RW; ++e) rec[e] = 0;
         }
-        if (STEADY || (unsigned)j < (unsigned)n) {
+        if (STEADY || START || (unsigned)j < (unsigned)n) {
             const int jkey = j + 1;      // 1-based column, < 2^16 when KEYED
+            if constexpr (START) {
+                // this lane's first column: the left border (H = 0, Iy = border) and the
+                // diagonal of its first row (H[i-1][0] = 0); the chunk maximum restarts
+                const bool f = j == 0;
+                prev_up = f ? 0 : prev_up;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    Hp[r] = f ? 0 : Hp[r];
+                    if constexpr (AFF) Yp[r] = f ? XB : Yp[r];
+                }
+                cml = f ? 0u : cml;
+            }
             int hd = prev_up;            // H[i-1][j-1] of my first row
             int hu = up_h;               // H[i-1][j]
             int xu = up_x;               // Ix[i-1][j]
@@ -700,7 +722,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
             prev_up = up_h;
             hl = Hp[R - 1];
             if constexpr (AFF) xl = xu;
-            if constexpr (T16 && RB < 32) rec[0] >>= (32 - RB);   // alignbit filled from the top
+            if constexpr (T16 && RB < 32 && !ACC) rec[0] >>= (32 - RB);   // alignbit filled from the top
         }
     };
 
@@ -812,14 +834,23 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     vs = s_step[64 + q];
                     if constexpr (AFF) vx = in_x[q];
                 }
-                uint32_t rec[RW];
-                if (g & 1) step(steady, q, kC + q, vh, vx, vs, rec, std::true_type{});
-                else step(steady, q, kC + q, vh, vx, vs, rec, std::false_type{});
-                if constexpr (BPS >= 4) {
-#pragma unroll
-                    for (int e = 0; e < RW; ++e) pk[g * RW + e] = rec[e];
+                constexpr bool ACC = T16 && RB < 32 && (int)decltype(steady)::value != kStepAny;
+                if constexpr (ACC) {
+                    // every lane pushes every step: the packet word fills from the top, step by
+                    // step, into the same byte layout as the shifted-and-ORed records below
+                    uint32_t(&acc_rec)[1] = *reinterpret_cast<uint32_t(*)[1]>(&pk[(g * BPS) / 4]);
+                    if (g & 1) step(steady, q, kC + q, vh, vx, vs, acc_rec, std::true_type{});
+                    else step(steady, q, kC + q, vh, vx, vs, acc_rec, std::false_type{});
                 } else {
-                    pk[(g * BPS) / 4] |= rec[0] << (((g * BPS) % 4) * 8);
+                    uint32_t rec[RW];
+                    if (g & 1) step(steady, q, kC + q, vh, vx, vs, rec, std::true_type{});
+                    else step(steady, q, kC + q, vh, vx, vs, rec, std::false_type{});
+                    if constexpr (BPS >= 4) {
+#pragma unroll
+                        for (int e = 0; e < RW; ++e) pk[g * RW + e] = rec[e];
+                    } else {
+                        pk[(g * BPS) / 4] |= rec[0] << (((g * BPS) % 4) * 8);
+                    }
                 }
                 // lane 63 holds the band's last row at column kC + q - 63: park it in LDS (SPLIT: in
                 // the park ring, posting the step count every kHandGran steps for the publisher)
@@ -960,8 +991,21 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                 }
                 int acc_h = 0, acc_x = 0;
                 const bool steady = kC >= kWave - 1 && kC + kChunk <= n;
-                if (steady) run_chunk(std::true_type{}, band, kC, bch, bcx, symc, acc_h, acc_x);
-                else run_chunk(std::false_type{}, band, kC, bch, bcx, symc, acc_h, acc_x);
+                if constexpr (SPLIT) {
+                    SA_EV(7, true);   // [7] chunk 0, [5] chunk 2 (the first steady one)
+                    SA_EV(5, kC >= 64);
+                    SA_EV(8, kC >= 64 + 32 * 8);   // chunk 10
+                }
+                if (steady) {
+                    run_chunk(std::integral_constant<int, kStepSteady>{}, band, kC, bch, bcx, symc, acc_h, acc_x);
+                } else if (T16 && LOCAL && CMAX && !P.no_start && n >= kWave && kC < kWave - 1) {
+                    // a band's first chunks (n >= 64: every lane reaches its first column inside
+                    // them, so none starts from start-mode garbage in a kStepAny chunk)
+                    if constexpr (T16 && LOCAL && CMAX)
+                        run_chunk(std::integral_constant<int, kStepStart>{}, band, kC, bch, bcx, symc, acc_h, acc_x);
+                } else {
+                    run_chunk(std::integral_constant<int, kStepAny>{}, band, kC, bch, bcx, symc, acc_h, acc_x);
+                }
                 // hand the band's last row (columns kC-63 .. kC-32) to the next band
                 if (band + 1 < B) {
                     const int cc = kC + lane - (kWave - 1);
@@ -980,6 +1024,8 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                 }
                 // ------------------------------------------------ CMAX: chunk maxima, snapshot
                 if constexpr (CMAX) {
+                    // (start mode: a lane that has not reached its first column holds garbage)
+                    if (kC + kChunk - 1 < lane) cml = 0;
                     const uint32_t ck = chunk + 1;
                     const uint64_t e = (uint64_t)band * P.snap_nch + chunk;
                     P.snap_m[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = (int32_t)cml;

@@ -79,6 +79,7 @@ struct FillParams {
     uint64_t wait_ticks;       // SPLIT: bounded wait for the producer band (s_memrealtime ticks)
     // the fallback launch: re-runs only the pairs a SPLIT fill flagged SA_FLAG_TIMEOUT
     int rerun;
+    int no_start;              // debugging aid (SEQALIB_NO_START): no start-mode steps
 };
 
 // SPLIT fills: per-pair fold of the per-band partials into sa_result (split_reduce_kernel).

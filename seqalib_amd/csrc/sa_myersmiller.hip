@@ -225,19 +225,19 @@ __device__ __forceinline__ void mm_band16(const MmSweep& d, const uint8_t* s1, c
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     int32_t e, dd, c, t;
-                    asm("v_add_u16 %0, %7, %8\n\t"        // e = max(Ep, Cp + g) + h      (:202)
-                        "v_max_i16 %0, %9, %0\n\t"
-                        "v_add_u16 %0, %10, %0\n\t"
-                        "v_add_u16 %1, %7, %11\n\t"       // D = max(Du, Cu + g) + h      (:203)
-                        "v_max_i16 %1, %12, %1\n\t"
-                        "v_add_u16 %1, %10, %1\n\t"
-                        "v_bfe_i32 %3, %13, %14, 8\n\t"   // diag = Cd + s(a, b)
-                        "v_add_u16 %3, %15, %3\n\t"
+                    asm("v_add_u16 %0, %4, %5\n\t"        // e = max(Ep, Cp + g) + h      (:202)
+                        "v_max_i16 %0, %6, %0\n\t"
+                        "v_add_u16 %0, %7, %0\n\t"
+                        "v_add_u16 %1, %4, %8\n\t"        // D = max(Du, Cu + g) + h      (:203)
+                        "v_max_i16 %1, %9, %1\n\t"
+                        "v_add_u16 %1, %7, %1\n\t"
+                        "v_bfe_i32 %3, %10, %11, 8\n\t"   // diag = Cd + s(a, b)
+                        "v_add_u16 %3, %12, %3\n\t"
                         "v_max_i16 %2, %1, %0\n\t"        // C = max(max(D, e), diag)
                         "v_max_i16 %2, %3, %2"
                         : "=&v"(e), "=&v"(dd), "=&v"(c), "=&v"(t)
-                        : "0"(0), "1"(0), "2"(0), "s"(g16), "v"(Cp[r]), "v"(Ep[r]), "s"(h16), "v"(cu), "v"(du),
-                          "v"(a[r]), "v"(sym), "v"(cd));
+                        : "s"(g16), "v"(Cp[r]), "v"(Ep[r]), "s"(h16), "v"(cu), "v"(du), "v"(a[r]), "v"(sym),
+                          "v"(cd));
                     cd = Cp[r];
                     Cp[r] = c;
                     Ep[r] = e;

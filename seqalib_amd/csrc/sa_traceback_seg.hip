@@ -242,11 +242,19 @@ __device__ bool seg_walk(const TbParams& P, const Geom& g, const SegBand& S, int
     return stop;
 }
 
-// hand-off granule of band b (its last row), column j (1-based) -> the walk's score there
-__device__ __forceinline__ int seg_hand(const TbParams& P, uint32_t slot, int b, int j, bool ix) {
+// hand-off granule of band b (its last row), column j (1-based) -> the walk's score there.  The
+// granules were stored write-through (sc1) by the fill; read them the same way (sc1), as its
+// poller does: a plain load here was seen to return the zeros of the pre-launch memset from a
+// stale L2 line (~1 in 10 two-process runs, tests/test_gpu_multiproc.py).  The fill wrote every
+// granule of columns 1..n with tag 1; a zero tag still read is kSegErr (the pair is then walked
+// serially and flagged SA_FLAG_RECOVERED).
+__device__ __forceinline__ int seg_hand(const TbParams& P, uint32_t slot, int b, int j, bool ix, uint32_t& fl) {
     if (j < 1) return 0;
     const uint64_t g = ((uint64_t)slot * P.split_bands + b) * P.max_n + (uint64_t)(j - 1) + (ix ? P.hand_x_off : 0);
-    const int32_t v = (int32_t)(uint32_t)P.hand[g];
+    typedef const unsigned long long __attribute__((address_space(1))) cgu64;
+    const unsigned long long x = __hip_atomic_load((cgu64*)(P.hand + g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((x >> 32) == 0) fl |= kSegErr;
+    const int32_t v = (int32_t)(uint32_t)x;
     return P.hand_shift ? ((int)(int16_t)(v & 0xffff) >> P.hand_shift) : v;
 }
 
@@ -284,6 +292,7 @@ __global__ __launch_bounds__(512) void seg_exit_kernel(TbParams P) {
     const uint64_t rs = (uint64_t)NST * ((uint64_t)P.max_n + 1) + 1;   // records per band
     int4* const band_rec = P.seg_rec + ((uint64_t)slot * P.split_bands + (uint64_t)b) * rs;
     int i = 0, j = 0, st = 0, V = 0;
+    uint32_t fl = 0;
     int4* out = nullptr;
     if (endw) {
         if (t == 0) {
@@ -298,14 +307,14 @@ __global__ __launch_bounds__(512) void seg_exit_kernel(TbParams P) {
             st = s0;
             i = (b + 1) * BR;   // the band's last row (< m: b < b_e)
             j = c;
-            if (SCORED) V = seg_hand(P, slot, b, c, st == 1);
+            if (SCORED) V = seg_hand(P, slot, b, c, st == 1, fl);
             out = band_rec + ((uint64_t)s0 * ((uint64_t)P.max_n + 1) + (uint64_t)c);
         }
     }
     const SegBand S = seg_stage<ALG, R, LUT>(P, g, dir, s1, s2, m, n, b, jmax, s_lds);
     __syncthreads();
     if (out == nullptr) return;
-    uint32_t k = 0, fl = 0;
+    uint32_t k = 0;
     const bool stop = seg_walk<ALG, R, LUT, TAG, false>(P, g, S, b * BR, i, j, st, V, k, fl, nullptr);
     int4 r;
     r.x = i; r.y = j; r.z = (int)k;
@@ -340,7 +349,7 @@ __global__ __launch_bounds__(256) void seg_emit_kernel(TbParams P) {
         bool on = true;
         while (cb > b) {
             const int4 r = rec[(uint64_t)cb * rs + idx];
-            if (r.w & kSegStop) { on = false; break; }
+            if (r.w & (kSegStop | kSegErr)) { on = false; break; }   // (kSegErr: no band records the end)
             off += (uint32_t)r.z;
             cj = r.y;
             cst = (r.w >> 2) & 3;
@@ -359,6 +368,7 @@ __global__ __launch_bounds__(256) void seg_emit_kernel(TbParams P) {
     const uint8_t* s1 = P.seq1 + o1;
     const uint8_t* s2 = P.seq2 + o2;
     int i, j, st = s_entry[1], V = 0;
+    uint32_t fl = 0;
     if (b == b_e) {
         st = 0;
         if (SCORED) { i = res.end_i; j = res.end_j; V = res.score; }
@@ -366,14 +376,14 @@ __global__ __launch_bounds__(256) void seg_emit_kernel(TbParams P) {
     } else {
         i = (b + 1) * BR;
         j = s_entry[0];
-        if (SCORED) V = seg_hand(P, slot, b, j, st == 1);
+        if (SCORED) V = seg_hand(P, slot, b, j, st == 1, fl);
     }
     const SegBand S = seg_stage<ALG, R, LUT>(P, g, dir, s1, s2, m, n, b, max(j, 1), s_lds);
     __syncthreads();
     if (threadIdx.x != 0) return;
     const uint32_t off = (uint32_t)s_entry[2];
     uint8_t* ops = P.ops + o1 + o2 + pidx + off;
-    uint32_t k = 0, fl = 0;
+    uint32_t k = 0;
     SegBand Sc = S;
     Sc.cap = (uint32_t)(m + n + 1) - min(off, (uint32_t)(m + n + 1));
     const bool stop = seg_walk<ALG, R, LUT, TAG, true>(P, g, Sc, b * BR, i, j, st, V, k, fl, ops);

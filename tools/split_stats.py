@@ -22,7 +22,7 @@ if algo == "sw":
 else:
     A, args, n = sa.SA_LOCAL_GOTOH, (-3, -1, 1, -1, False), 8192
 pairs = [(sa.synth_dna(1, n), sa.synth_dna(2, n))]
-out = (C.c_ulonglong * (4096 * 12))()
+out = (C.c_ulonglong * (4096 * 16))()
 EV = ["post71", "pub_sees", "pub_stored", "poll_has8", "cmp_has", "cmp_start"]
 for R in Rs:
     os.environ["SEQALIB_PLAN"] = f"{R},0"
@@ -33,7 +33,7 @@ for R in Rs:
         fn(out, 0)
     allst = np.frombuffer(out, dtype=np.uint64)
     st = allst[:4096 * 4].reshape(4096, 4)
-    ev = allst[4096 * 4:].reshape(4096, 8)
+    ev = allst[4096 * 4:].reshape(4096, 12)
     keep = st[:, 0] > 0
     st, ev = st[keep], ev[keep]
     order = np.argsort(st[:, 0])
@@ -61,6 +61,11 @@ for R in Rs:
         if p[0] and p[1] and p[2] and c[3] and c[4] and c[6]:
             hops.append([rel(p[1]) - rel(p[0]), rel(p[2]) - rel(p[1]), rel(c[3]) - rel(p[2]), rel(c[4]) - rel(c[3]),
                          rel(c[4]) - rel(c[6]), rel(c[4]) - rel(p[0])])
+    e0 = ev[0]
+    if e0[7] and e0[5] and e0[8]:
+        ns = (int(e0[5]) - int(e0[7])) / 100.0 / 64 * 1e3
+        sd = (int(e0[8]) - int(e0[5])) / 100.0 / 256 * 1e3
+        print(f"   band 0: chunks 0-1 (non-steady) {ns:.1f} ns per step, chunks 2-9 (steady) {sd:.1f} ns per step")
     if hops:
         h = np.array(hops)
         print(f"   hand-off of the granule at column 2048, median us: publisher wake {np.median(h[:, 0]):.2f}, "
