@@ -570,7 +570,10 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     const bool seg_on = seg_mode != 0 && per_launch * sp_bands <= (seg_mode == 2 ? 16384 : kSegMaxBands);
     const uint64_t seg_rs = (uint64_t)aff2 * ((uint64_t)max_n + 1) + 1;
     const uint64_t sp_seg = (sp_part + per_launch * sp_bands * 16 + 255) & ~(uint64_t)255;
-    const uint64_t sp_slot = sp_seg + (seg_on ? (per_launch * sp_bands * seg_rs + per_launch) * 16 : 0);
+    // (a whole number of 256-byte blocks: slot 1 begins at (split_bytes / 2) rounded down to 256,
+    // so an unaligned slot size let slot 0's last exit records and slot 1's ticket share bytes --
+    // the pipelined calls then corrupted each other's scratch now and then)
+    const uint64_t sp_slot = (sp_seg + (seg_on ? (per_launch * sp_bands * seg_rs + per_launch) * 16 : 0) + 255) & ~(uint64_t)255;
     const uint64_t sp_need = any_split ? sp_slot * (pipe ? 2 : 1) : 0;
     if (any_split && c->split_bytes < sp_need) {
         if (c->split) {
@@ -590,6 +593,9 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     uint8_t* const wbase = c->ws + (pipe ? slot * ((c->ws_bytes / 2) & ~(uint64_t)255) : 0);
     // (fixed halves of the scratch, as the workspace: a slot's block never moves with the shape)
     uint8_t* const spbase = any_split ? c->split + (pipe ? slot * ((c->split_bytes / 2) & ~(uint64_t)255) : 0) : nullptr;
+    // the two pipeline slots must not share a byte (each holds what its calls write)
+    if (pipe && (((c->ws_bytes / 2) & ~(uint64_t)255) < need || (any_split && ((c->split_bytes / 2) & ~(uint64_t)255) < sp_slot)))
+        return fail(c, SA_ERR_HIP, "internal: pipeline slots overlap");
 
     // reset timing
     c->launches = 0;

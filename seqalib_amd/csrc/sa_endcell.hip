@@ -22,7 +22,7 @@ namespace sa {
 
 
 // the band's top row: the fill's row buffer or, SPLIT, its write-through hand-off granules, read
-// write-through-coherent (sc1) like sa_traceback_seg.hip's seg_hand
+// as the fill's poller reads them (sc1), like sa_traceback_seg.hip's seg_hand
 __device__ __forceinline__ int32_t ec_top(const int32_t* p) {
     typedef const int32_t __attribute__((address_space(1))) cgi32;
     return __hip_atomic_load((cgi32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -242,12 +242,11 @@ __device__ bool seg_walk(const TbParams& P, const Geom& g, const SegBand& S, int
     return stop;
 }
 
-// hand-off granule of band b (its last row), column j (1-based) -> the walk's score there.  The
-// granules were stored write-through (sc1) by the fill; read them the same way (sc1), as its
-// poller does: a plain load here was seen to return the zeros of the pre-launch memset from a
-// stale L2 line (~1 in 10 two-process runs, tests/test_gpu_multiproc.py).  The fill wrote every
-// granule of columns 1..n with tag 1; a zero tag still read is kSegErr (the pair is then walked
-// serially and flagged SA_FLAG_RECOVERED).
+// hand-off granule of band b (its last row), column j (1-based) -> the walk's score there, read
+// as the fill's poller reads it (sc1).  The fill wrote every granule of columns 1..n with tag 1,
+// so a zero tag means the scratch was overwritten: kSegErr (the pair is then walked serially and
+// flagged SA_FLAG_RECOVERED).  (This guard found the pipeline slots' scratch overlap fixed in
+// run_device, sa_api.hip: ~1 in 10 two-process runs of tests/test_gpu_multiproc.py.)
 __device__ __forceinline__ int seg_hand(const TbParams& P, uint32_t slot, int b, int j, bool ix, uint32_t& fl) {
     if (j < 1) return 0;
     const uint64_t g = ((uint64_t)slot * P.split_bands + b) * P.max_n + (uint64_t)(j - 1) + (ix ? P.hand_x_off : 0);
