@@ -173,7 +173,7 @@ std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std
     auto fn = self.getMatchOperation();
     const bool has_fn = !(fn == nullptr);
     const sa_scoring sc = self.getScoring().toC();
-    std::vector<uint8_t> ops;
+    raw_vector<uint8_t> ops;
     std::vector<uint64_t> off;
     align<Ty>(ALGO, sc, fn, has_fn, pairs, res, ops, off);
     std::vector<AlignedSequence<Ty, Blank>> out(pairs.size());
@@ -194,25 +194,7 @@ std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std
         PhaseTimer& t;
         ~Lap() { t.lap("AlignedSequence lists"); }
     } lap{tm};
-    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t nth = std::min<size_t>(std::min<size_t>(hw, 16), P / 32);
-    if (nth <= 1) {
-        build(0, P);
-        return out;
-    }
-    std::vector<std::exception_ptr> errs(nth);
-    std::vector<std::thread> pool;
-    for (size_t t = 0; t < nth; ++t)
-        pool.emplace_back([&, t] {
-            try {
-                build(P * t / nth, P * (t + 1) / nth);
-            } catch (...) {
-                errs[t] = std::current_exception();
-            }
-        });
-    for (auto& th : pool) th.join();
-    for (auto& e : errs)
-        if (e) std::rethrow_exception(e);
+    parallel_pairs(P, host_threads(P), [&](size_t, size_t p0, size_t p1) { build(p0, p1); });
     return out;
 }
 

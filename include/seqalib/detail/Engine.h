@@ -3,14 +3,19 @@
 // table built from the user's MatchFnTy, and op-stream -> AlignedSequence assembly.
 #pragma once
 
+#include <algorithm>
+#include <array>
 #include <chrono>
 #include <climits>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
+#include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -76,6 +81,64 @@ inline sa_multi* multi_context() {
         }
     }
     return m.h;
+}
+
+// Host staging buffers that are written in full before they are read: a vector whose resize()
+// leaves elements default-initialised (no zero fill of ~80 MB per headline batch).
+template <typename T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <typename U>
+    struct rebind {
+        using other = DefaultInitAlloc<U>;
+    };
+    DefaultInitAlloc() = default;
+    template <typename U>
+    DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+    template <typename U>
+    void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <typename U, typename... A>
+    void construct(U* p, A&&... a) {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
+template <typename T>
+using raw_vector = std::vector<T, DefaultInitAlloc<T>>;
+
+// Host threads for per-pair work of a batch of P pairs (symbol coding, list construction): at most
+// 16 (the GPU box's CPU share), at least 32 pairs each.
+inline size_t host_threads(size_t P) {
+    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+    return std::max<size_t>(1, std::min<size_t>(std::min<size_t>(hw, 16), P / 32));
+}
+
+// Runs body(t, p0, p1) over nth contiguous pair ranges [P*t/nth, P*(t+1)/nth), one host thread
+// each (the caller's thread takes the first); rethrows the first exception.
+template <typename Body>
+void parallel_pairs(size_t P, size_t nth, Body&& body) {
+    if (nth <= 1) {
+        body((size_t)0, (size_t)0, P);
+        return;
+    }
+    std::vector<std::exception_ptr> errs(nth);
+    std::vector<std::thread> pool;
+    for (size_t t = 1; t < nth; ++t)
+        pool.emplace_back([&, t] {
+            try {
+                body(t, P * t / nth, P * (t + 1) / nth);
+            } catch (...) {
+                errs[t] = std::current_exception();
+            }
+        });
+    try {
+        body((size_t)0, (size_t)0, P / nth);
+    } catch (...) {
+        errs[0] = std::current_exception();
+    }
+    for (auto& th : pool) th.join();
+    for (auto& e : errs)
+        if (e) std::rethrow_exception(e);
 }
 
 // $SEQALIB_HOST_TIMING: print the host-side phases of each batch to stderr.
@@ -157,7 +220,7 @@ std::vector<uint8_t> build_lut(SymbolCoder<Ty, Direct>& coder, MatchFnTy& fn) {
 template <typename Ty, typename ContainerType, typename MatchFnTy>
 void align_bits(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
                 const std::vector<std::pair<ContainerType*, ContainerType*>>& pairs, std::vector<sa_result>& res,
-                std::vector<uint8_t>& ops, std::vector<uint64_t>& ops_off) {
+                raw_vector<uint8_t>& ops, std::vector<uint64_t>& ops_off) {
     PhaseTimer tm;
     const uint32_t np = (uint32_t)pairs.size();
     std::vector<uint64_t> o1(1, 0), o2(1, 0), bo(1, 0);
@@ -201,7 +264,7 @@ void align_bits(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
 template <typename Ty, typename ContainerType, typename MatchFnTy>
 void align(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
            const std::vector<std::pair<ContainerType*, ContainerType*>>& pairs,
-           std::vector<sa_result>& res, std::vector<uint8_t>& ops, std::vector<uint64_t>& ops_off) {
+           std::vector<sa_result>& res, raw_vector<uint8_t>& ops, std::vector<uint64_t>& ops_off) {
     PhaseTimer tm;
     SymbolCoder<Ty> coder;
     std::vector<uint64_t> o1(1, 0), o2(1, 0);
@@ -211,15 +274,38 @@ void align(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
         o1.push_back(o1.back() + (uint64_t)p.first->size());
         o2.push_back(o2.back() + (uint64_t)p.second->size());
     }
-    std::vector<uint8_t> s1(o1.back() + 1), s2(o2.back() + 1);   // +1: never a NULL pointer
-    for (size_t q = 0; q < pairs.size(); ++q) {
-        ContainerType& a = *pairs[q].first;
-        ContainerType& b = *pairs[q].second;
-        uint8_t* d1 = s1.data() + o1[q];
-        uint8_t* d2 = s2.data() + o2[q];
-        for (size_t k = 0; k < (size_t)a.size(); ++k) d1[k] = coder.code(a[k]);
-        for (size_t k = 0; k < (size_t)b.size(); ++k) d2[k] = coder.code(b[k]);
-        if (coder.overflow) break;
+    raw_vector<uint8_t> s1(o1.back() + 1), s2(o2.back() + 1);   // +1: never a NULL pointer
+    constexpr bool kDirect = std::is_integral<Ty>::value && sizeof(Ty) == 1;
+    if constexpr (kDirect) {
+        // byte symbols are their own codes: copy them on the host threads, each marking the
+        // symbols it saw (for the match table) in a table of its own
+        const size_t nth = host_threads(pairs.size());
+        std::vector<std::array<uint8_t, 256>> seen(nth);
+        parallel_pairs(pairs.size(), nth, [&](size_t t, size_t p0, size_t p1) {
+            std::array<uint8_t, 256>& sn = seen[t];
+            sn.fill(0);
+            for (size_t q = p0; q < p1; ++q) {
+                ContainerType& a = *pairs[q].first;
+                ContainerType& b = *pairs[q].second;
+                uint8_t* d1 = s1.data() + o1[q];
+                uint8_t* d2 = s2.data() + o2[q];
+                for (size_t k = 0; k < (size_t)a.size(); ++k) sn[d1[k] = (uint8_t)a[k]] = 1;
+                for (size_t k = 0; k < (size_t)b.size(); ++k) sn[d2[k] = (uint8_t)b[k]] = 1;
+            }
+        });
+        for (auto& sn : seen)
+            for (int c = 0; c < 256; ++c)
+                if (sn[c]) coder.code((Ty)(uint8_t)c);
+    } else {
+        for (size_t q = 0; q < pairs.size(); ++q) {
+            ContainerType& a = *pairs[q].first;
+            ContainerType& b = *pairs[q].second;
+            uint8_t* d1 = s1.data() + o1[q];
+            uint8_t* d2 = s2.data() + o2[q];
+            for (size_t k = 0; k < (size_t)a.size(); ++k) d1[k] = coder.code(a[k]);
+            for (size_t k = 0; k < (size_t)b.size(); ++k) d2[k] = coder.code(b[k]);
+            if (coder.overflow) break;
+        }
     }
     tm.lap("symbol coding");
     if (coder.overflow) {   // more than 256 distinct symbols: the generic-Ty (bitmap) path

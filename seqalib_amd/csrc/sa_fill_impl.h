@@ -998,10 +998,13 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                 }
                 if (steady) {
                     run_chunk(std::integral_constant<int, kStepSteady>{}, band, kC, bch, bcx, symc, acc_h, acc_x);
-                } else if (T16 && LOCAL && CMAX && !P.no_start && n >= kWave && kC < kWave - 1) {
+                } else if (T16 && LOCAL && CMAX && SPLIT && !P.no_start && n >= kWave && kC < kWave - 1) {
                     // a band's first chunks (n >= 64: every lane reaches its first column inside
-                    // them, so none starts from start-mode garbage in a kStepAny chunk)
-                    if constexpr (T16 && LOCAL && CMAX)
+                    // them, so none starts from start-mode garbage in a kStepAny chunk).  SPLIT
+                    // only: a third chunk body costs the many-pairs R = 32 kernel 31 VGPRs (138 ->
+                    // 169, i.e. 3 -> 2 waves per SIMD and a 6 % slower headline fill), and its
+                    // ramp chunks are hidden by the other waves anyway
+                    if constexpr (T16 && LOCAL && CMAX && SPLIT)
                         run_chunk(std::integral_constant<int, kStepStart>{}, band, kC, bch, bcx, symc, acc_h, acc_x);
                 } else {
                     run_chunk(std::integral_constant<int, kStepAny>{}, band, kC, bch, bcx, symc, acc_h, acc_x);
