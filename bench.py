@@ -322,10 +322,9 @@ def main():
         return
     per_launch_cells = cells_rank  # one fill launch covers the whole batch when it fits HBM
     fill_s = fill_ms / 1e3 / max(launches, 1)
-    x2 = kernel == sa.SA_KERNEL_T16_X2   # two pairs per wave (sa_fill_x2.hip)
-    t16 = kernel in (sa.SA_KERNEL_T16, sa.SA_KERNEL_T16_ENDCELL) or x2
-    endcell = kernel == sa.SA_KERNEL_T16_ENDCELL or x2
-    label = f"sw_{'x2' if x2 else 't16c' if endcell else 't16' if t16 else 'int32'}_r{plan_R}"
+    t16 = kernel in (sa.SA_KERNEL_T16, sa.SA_KERNEL_T16_ENDCELL)
+    endcell = kernel == sa.SA_KERNEL_T16_ENDCELL
+    label = f"sw_{'t16c' if endcell else 't16' if t16 else 'int32'}_r{plan_R}"
     model = issue_model(label)
     fill_gcups = per_launch_cells / fill_s / 1e9
     # algorithmic HBM bytes per cell: 2 traceback bits, plus the end-cell snapshots (64 lanes x
@@ -333,8 +332,7 @@ def main():
     bytes_per_cell = SW_FLAG_BYTES_PER_CELL + ((plan_R // 2 + 1) * 4 / (32 * plan_R) if endcell else 0.0)
     hbm_gbps = per_launch_cells * bytes_per_cell / fill_s / 1e9
     traffic = load_pmc_traffic(workload)
-    kname = (f"fill_x2_kernel<SW,R={plan_R},two pairs per wave (packed int16 halves),chunk-max end cell>" if x2 else
-             f"fill_kernel<SW,R={plan_R},W={plan_W}," + ("T16 tagged int16 profile" if t16 else "int32 flags")
+    kname = (f"fill_kernel<SW,R={plan_R},W={plan_W}," + ("T16 tagged int16 profile" if t16 else "int32 flags")
              + (",chunk-max end cell>" if endcell else ",KEYED>"))
     # achieved = fill cells/s x ISA-counted VALU instructions per cell (each lane computes its own
     # cells, so lane-instructions); peak = the guide's VALU issue peak (VALU_PEAK_TLANE)

@@ -192,7 +192,6 @@ int sa_last_timings(sa_ctx* ctx, float* fill_ms, float* traceback_ms, int* fill_
 #define SA_KERNEL_INT32 0
 #define SA_KERNEL_T16 1
 #define SA_KERNEL_T16_ENDCELL 2   /* T16 SW / LocalGotoh with per-chunk maxima + end-cell replay */
-#define SA_KERNEL_T16_X2 3        /* the same for SW, two pairs per wave on packed 16-bit halves */
 int sa_last_plan(sa_ctx* ctx, int* kernel, int* rows_per_lane, int* waves);
 
 /* Plan of the int32 kernel for a batch (host-only query, no device needed): rows per lane R,

@@ -37,7 +37,7 @@ SA_SW, SA_NW, SA_LOCAL_GOTOH, SA_GLOBAL_GOTOH, SA_HIRSCHBERG, SA_MYERS_MILLER = 
 ALGO_NAMES = {SA_SW: "sw", SA_NW: "nw", SA_LOCAL_GOTOH: "local_gotoh", SA_GLOBAL_GOTOH: "global_gotoh",
               SA_HIRSCHBERG: "hirschberg", SA_MYERS_MILLER: "myers_miller"}
 SA_FLAG_DIVERGED, SA_FLAG_BAD_SHAPE, SA_FLAG_SIZE_HACK, SA_FLAG_TIMEOUT = 1, 2, 4, 8
-SA_KERNEL_INT32, SA_KERNEL_T16, SA_KERNEL_T16_ENDCELL, SA_KERNEL_T16_X2 = 0, 1, 2, 3
+SA_KERNEL_INT32, SA_KERNEL_T16, SA_KERNEL_T16_ENDCELL = 0, 1, 2
 INT32_MIN = -(2 ** 31)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -480,7 +480,7 @@ class Engine:
 
     def last_plan(self) -> Tuple[int, int, int]:
         """(kernel, R, W) of the last call: kernel is SA_KERNEL_INT32, SA_KERNEL_T16,
-        SA_KERNEL_T16_ENDCELL or SA_KERNEL_T16_X2 (two pairs per wave); W = 0 for the multi-workgroup plan (one single-wave workgroup per
+        or SA_KERNEL_T16_ENDCELL; W = 0 for the multi-workgroup plan (one single-wave workgroup per
         band of 64*R rows)."""
         k, R, W = C.c_int(), C.c_int(), C.c_int()
         self._check(self.L.sa_last_plan(self.h, C.byref(k), C.byref(R), C.byref(W)), "sa_last_plan")

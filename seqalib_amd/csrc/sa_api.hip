@@ -190,7 +190,6 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t
 struct Variant {
     Plan pl;
     bool t16 = false, cmax = false;
-    bool x2 = false;   // two pairs per wave (sa_fill_x2.hip)
     uint32_t snap_nch = 0;
     uint64_t snap_h_slot = 0, snap_p_slot = 0;   // 32-bit words per pair
     uint64_t slot_bytes = 0;
@@ -206,17 +205,6 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
     v.cmax = t16 && v.pl.W == 1 && v.pl.R >= 2 &&
              ((algo == SA_SW && v.pl.R <= 32) || (algo == SA_LOCAL_GOTOH && v.pl.R <= 16));
     if (const char* ec = getenv("SEQALIB_CMAX")) if (ec[0] == '0') v.cmax = false;
-    // Two pairs per wave on packed 16-bit halves (sa_fill_x2.hip, bands of 1024 rows, 5 waves per
-    // SIMD) for many long SW pairs: opt-in (SEQALIB_X2=1).  It takes the same shader cycles as
-    // the one-pair kernel on the headline batch (rocprofv3 GRBM_GUI_ACTIVE 5.34e8 vs 5.20e8,
-    // profiles/pmc_clock_r02.txt), so the default stays one pair per wave.
-    v.x2 = false;
-    if (const char* e2 = getenv("SEQALIB_X2"))
-        v.x2 = e2[0] == '1' && v.cmax && algo == SA_SW && !v.pl.split && v.pl.W == 1 && v.pl.R >= 16 && npairs >= 1024;
-    if (v.x2) {
-        v.pl.R = 16;
-        v.pl.g = make_geom(algo, 16, max_m, max_n, 2);
-    }
     if (v.cmax) {
         v.snap_nch = chunks_per_band(max_n);
         v.snap_p_slot = (uint64_t)v.pl.g.bands * v.snap_nch * kWave;
@@ -225,7 +213,7 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
         v.pl.rowbuf_elems = (uint64_t)(is_affine(algo) ? 2 : 1) * v.pl.g.bands * std::max<uint32_t>(max_n, 1);
     }
     if (v.pl.split) v.pl.rowbuf_elems = 0;   // hand-off granules live in c->split
-    v.kernel = v.x2 ? SA_KERNEL_T16_X2 : v.cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
+    v.kernel = v.cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
     v.slot_bytes = v.pl.g.dir_slot + v.pl.rowbuf_elems * 4 + (v.snap_h_slot + 2 * v.snap_p_slot) * 4;
     return v;
 }
@@ -381,8 +369,21 @@ T16Mode t16_mode_affine(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t
         lo = std::min(lo, lo_at(q[0], q[1]));
     }
     const int64_t cand_lo = lo + std::min<int64_t>(std::min(MI, GOE + GE), 0);
-    const int64_t delta = (hi + cand_lo) >> 1;
-    if (8 * (hi - delta) + 7 > 32767 || 8 * (cand_lo - delta) <= floor_ext) return t;
+    int64_t delta = (hi + cand_lo) >> 1;
+    if (8 * (hi - delta) + 7 > 32767 || 8 * (cand_lo - delta) <= floor_ext) {
+        // The a-priori width does not fit (e.g. 4096^2 at (-3, -1, 1, -1): [-4104, 4096]).  The low
+        // end is reached by the borders of every pair, the high end only by near-identical pairs:
+        // every value and candidate is the score of an alignment of prefixes, at most
+        // MA * (its matches) <= MA * L with L = sum over symbols of min(count in Seq1, count in
+        // Seq2).  Place the window at the low end and let the T16 fill screen each pair
+        // (retry_above = the largest MA * min(L, m, n) that fits); the int32 variant re-runs
+        // the screened-out pairs exactly (kFlagRetry), as for SW.
+        delta = cand_lo + 4100;
+        while (8 * (cand_lo - delta) <= floor_ext) --delta;   // the largest delta that fits the low end
+        const int64_t cap = delta + (32767 - 7) / 8;
+        if (cap < std::max<int64_t>(MA, 0) * k / 2) return t;   // not even typical pairs would fit
+        t.retry_above = (int32_t)cap;
+    }
     t.ok = true;
     t.delta = (int32_t)delta;
     t.sent = (int32_t)sent;
@@ -450,9 +451,14 @@ int validate_scoring(sa_ctx* c, int algo, const sa_scoring* s) {
 }
 
 // T16 by scoring and shape (the batch alphabet is checked on the device, decide_t16).
-T16Mode t16_candidate(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {
+T16Mode t16_candidate(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n, uint32_t npairs) {
     T16Mode t = t16_mode(algo, sc, max_m, max_n);
     if ((algo == SA_SW || algo == SA_LOCAL_GOTOH) && !keyed_ok(algo, sc, max_m, max_n)) t.ok = false;
+    // the screened GlobalGotoh T16 fill (retry_above set) runs on the many-pairs plans only: a
+    // SPLIT band cannot leave its pair alone
+    if (t.ok && algo == SA_GLOBAL_GOTOH && t.retry_above != INT_MAX &&
+        make_variant(algo, max_m, max_n, npairs, true, true).pl.split)
+        t.ok = false;
     if (const char* e16 = getenv("SEQALIB_T16")) if (e16[0] == '0') t.ok = false;
     return t;
 }
@@ -500,7 +506,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     const bool allow = sc->allow_mismatch != 0;
     const bool bits = d_mbits != nullptr;   // generic-Ty path: per-pair match bitmaps
     const bool lut = !bits && d_lutbits != nullptr;
-    const T16Mode tm = bits ? T16Mode{} : t16_candidate(algo, sc, max_m, max_n);
+    const T16Mode tm = bits ? T16Mode{} : t16_candidate(algo, sc, max_m, max_n, npairs);
     const bool t16 = tm.ok;
     if (!c->aux) SA_HIP(c, hipMalloc(&c->aux, 2 * kAuxWords * 4));
     if (!c->h_sel) {
@@ -674,8 +680,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             const FillVariant fv = make_fp(k);
             const FillParams& fp = fps[k];
             if (pl.split) SA_HIP(c, hipMemsetAsync(fp.ticket, 0, 256 + hand_x_off * 8 * aff2, sf));
-            hipError_t e = v.x2 ? launch_fill_sw_x2(pl.R, fp, cnt, sf)
-                                : launch_fill(algo, fv, fp, pl.split ? (uint32_t)(cnt * sp_bands) : cnt, sf);
+            hipError_t e = launch_fill(algo, fv, fp, pl.split ? (uint32_t)(cnt * sp_bands) : cnt, sf);
             if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
             if (pl.split) {
                 SplitReduceParams rp;
@@ -728,7 +733,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             tp.gap = fps[k].gap; tp.match = fps[k].match; tp.mismatch = fps[k].mismatch;
             tp.gap_open = fps[k].gap_open; tp.gap_extend = fps[k].gap_extend;
             tp.allow = (allow || v.t16) ? 1 : 0;
-            tp.tagged = v.x2 ? 2 : (v.t16 ? 1 : 0);
+            tp.tagged = v.t16 ? 1 : 0;
             tp.sel = fps[k].sel; tp.sel_want = fps[k].sel_want;
             tp.rerun = fps[k].rerun;
             return tp;
@@ -1356,7 +1361,7 @@ int sa_plan_query_ex(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t ma
                      int nsym, int* kernel, int* R, int* W, uint64_t* ws_bytes_per_pair) {
     if (algo < SA_SW || algo > SA_GLOBAL_GOTOH) return fail(nullptr, SA_ERR_ARG, "unknown algorithm");
     if (!sc) return fail(nullptr, SA_ERR_ARG, "scoring is NULL");
-    const bool cand = t16_candidate(algo, sc, max_m, max_n).ok;
+    const bool cand = t16_candidate(algo, sc, max_m, max_n, npairs).ok;
     // exactly the variants a call enqueues (build_variants: common record stride, SPLIT fallback)
     Variant vars[3];
     bool has_fb = false;

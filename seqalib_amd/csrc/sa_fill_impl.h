@@ -198,6 +198,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     __shared__ int s_sync[8];
     __shared__ uint32_t s_ticket;
     __shared__ int s_pring[SPLIT ? 2 * kRing : 1];   // SPLIT: the parked last row (H, then Ix), by step
+    __shared__ uint32_t s_comp[(T16 && ALG == SA_GLOBAL_GOTOH) ? 8 : 1];   // symbol counts (GG screen)
 
     // the batch selected the other kernel variant: leave -- except an int32 launch re-running the
     // pairs a T16 fill flagged kFlagRetry (checked below, once the pair is known)
@@ -245,6 +246,48 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
             P.res[pidx] = r;
         }
         return;
+    }
+    // Screened T16 GlobalGotoh (t16_mode_affine, retry_above != INT_MAX): the 16-bit window holds
+    // every value of a pair whose alignments of prefixes score at most retry_above.  Each such
+    // score is <= MA * (its matches) <= MA * min(L, m, n), L = sum over the (<= 4) symbols of
+    // min(count in Seq1, count in Seq2).  A pair above the cap leaves its fill to the int32
+    // variant (kFlagRetry, re-run exactly by the redo launch).
+    if constexpr (T16 && ALG == SA_GLOBAL_GOTOH && !SPLIT) {
+        if (P.retry_above != INT_MAX) {
+            if (threadIdx.x < 8) s_comp[threadIdx.x] = 0;
+            __syncthreads();
+            uint32_t ca[4] = {0, 0, 0, 0}, cb[4] = {0, 0, 0, 0};
+            const uint8_t* q1 = P.seq1 + o1;
+            const uint8_t* q2 = P.seq2 + o2;
+            for (int k = threadIdx.x; k < m; k += blockDim.x) {
+                const uint32_t c = t16_code8(symp, q1[k]) >> 3;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) ca[e] += c == (uint32_t)e ? 1u : 0u;
+            }
+            for (int k = threadIdx.x; k < n; k += blockDim.x) {
+                const uint32_t c = t16_code8(symp, q2[k]) >> 3;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) cb[e] += c == (uint32_t)e ? 1u : 0u;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (ca[e]) atomicAdd(&s_comp[e], ca[e]);
+                if (cb[e]) atomicAdd(&s_comp[4 + e], cb[e]);
+            }
+            __syncthreads();
+            int64_t L = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) L += (int64_t)min(s_comp[e], s_comp[4 + e]);
+            const int64_t hi = (int64_t)max(P.match, 0) * min<int64_t>(L, min(m, n));
+            if (hi > (int64_t)P.retry_above) {   // uniform over the workgroup
+                if (threadIdx.x == 0) {
+                    sa_result r = {};
+                    r.flags = kFlagRetry;
+                    P.res[pidx] = r;
+                }
+                return;
+            }
+        }
     }
     const LdsLayout lay = lds_layout(LUT, AFF, W, P.stage_seq2 ? P.max_n : 0);
     uint32_t* const s_lut = smem;

@@ -55,7 +55,8 @@ struct FillParams {
     uint32_t sel_want;
     int redo;
     // T16 only: NW keeps 4 * (H - t16_delta) (a constant offset that centres the score range in
-    // int16); SW flags pairs whose maximum exceeds retry_above (INT_MAX when proven to fit)
+    // int16); SW flags pairs whose maximum exceeds retry_above (INT_MAX when proven to fit);
+    // T16 GlobalGotoh: the per-pair composition cap of a screened window (fill_kernel)
     int32_t t16_delta;
     int32_t retry_above;
     // T16 affine only: the Ix / Iy border value (the reference's -10000), encoded below every
@@ -137,7 +138,7 @@ struct TbParams {
     uint32_t max_m, max_n;
     int32_t gap, match, mismatch, gap_open, gap_extend;
     int allow;
-    int tagged;                // record layout: 0 flags, 1 T16 max tags, 2 two-pair tags (sa_layout.h)
+    int tagged;                // record layout: 0 flags, 1 T16 max tags (sa_layout.h)
     int vrec;                  // kMatchBits fills: under fD the second flag bit is the match bit
     const uint32_t* sel;
     uint32_t sel_want;
@@ -165,16 +166,12 @@ struct FillVariant {
     int R;
     bool lut, allow, keyed, t16, cmax, split;
     bool bits = false;   // kMatchBits (then lut is ignored)
-    bool x2 = false;     // T16 SW chunk-max fill, two pairs per wave (sa_fill_x2.hip); keep it
-                         // last: launch sites brace-initialise the members above in order
 };
 hipError_t launch_fill(int algo, const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream);
 hipError_t launch_fill_sw(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_fill_nw(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_fill_lg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_fill_gg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
-// T16 SW chunk-max fill, two pairs per wave (sa_fill_x2.hip), R in {16, 32}
-hipError_t launch_fill_sw_x2(int R, const FillParams& p, uint32_t pairs, hipStream_t stream);
 // Batch alphabet scan (presence bitmap of every byte of both sequence sets, 8 words) and the
 // device-side T16 decision.  aux layout (kAux* below): [bitmap 8][profile 4][sym_pack][sel].
 constexpr int kAuxProf = 8, kAuxSel = 13, kAuxWords = 64;

@@ -99,8 +99,7 @@ struct Geom {
     uint32_t bands;     // bands for max_m
     uint64_t band_stride;  // bytes per band
     uint64_t dir_slot;     // bytes per pair
-    int tagged;            // 0 equality flags; 1 max tags (T16 kernels); 2 max tags in the
-                           // two-pair kernel's row order (sa_fill_x2.hip, cell_word_bit)
+    int tagged;            // 0 equality flags; 1 max tags (T16 kernels)
 };
 
 SA_HD uint32_t round_up(uint32_t x, uint32_t a) { return (x + a - 1) / a * a; }
@@ -123,15 +122,12 @@ SA_HD Geom make_geom(int algo, int R, uint32_t max_m, uint32_t max_n, int tagged
 // Bit index, inside its 32-bit record word, of the least significant bit of row r's group.
 // Flags: rows are pushed r = 0..R-1, BPC flags each, into words of min(32, R*BPC) bits, first row
 // most significant.  Tags: v_alignbit pushes each row in at the top, so row r ends at bits 2r.
-// Two-pair kernel (tagged == 2, BPC 2, R >= 16): each 16-bit half of a word holds 8 rows pushed
-// with rec = 4 rec + tag, so row r sits at bits 16 ((r % 16) / 8) + 2 (7 - r % 8).
 SA_HD void cell_word_bit(int R, int bpc, int r, int* word, int* lowbit, int tagged = 0) {
     const int rb = R * bpc;
     const int wb = rb < 32 ? rb : 32;
     const int rpw = wb / bpc;
     *word = r / rpw;
-    if (tagged == 2) *lowbit = 16 * ((r % 16) / 8) + 2 * (7 - r % 8);
-    else *lowbit = tagged ? bpc * (r % rpw) : wb - bpc * ((r % rpw) + 1);
+    *lowbit = tagged ? bpc * (r % rpw) : wb - bpc * ((r % rpw) + 1);
 }
 
 // Byte offset (inside a pair's slot) and bit shift of the flag group of cell (i, j), 1-based.

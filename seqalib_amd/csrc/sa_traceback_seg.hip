@@ -401,7 +401,6 @@ hipError_t launch_traceback_seg(int algo, int R, bool lut, const TbParams& p, hi
     const dim3 ge(1, p.split_bands, p.count), be(256);
     const uint64_t rs = (uint64_t)nst * ((uint64_t)p.max_n + 1) + 1;   // exit records per band
     const bool tag = p.tagged != 0;
-    if (p.tagged > 1) return hipErrorInvalidValue;   // two-pair records never come from SPLIT fills
 #define SA_SEG(AA, RR, LL, TT)                                                              \
     if (algo == AA && R == RR && lut == LL && tag == TT) {                                  \
         hipLaunchKernelGGL((seg_exit_kernel<AA, RR, LL, TT>), gx, bx, 0, stream, p);        \

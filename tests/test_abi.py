@@ -126,7 +126,11 @@ def test_plan_t16_eligibility_by_scoring():
     assert sa.plan_query_ex(2, aff, 1024, 1024, 10000)[:3] == (sa.SA_KERNEL_T16_ENDCELL, 16, 1)
     assert sa.plan_query_ex(2, aff, 8192, 8192, 10000)[0] == sa.SA_KERNEL_T16_ENDCELL
     assert sa.plan_query_ex(3, aff, 2048, 2048, 10000)[:3] == (sa.SA_KERNEL_T16, 16, 1)
-    assert sa.plan_query_ex(3, aff, 4096, 4096, 10000)[0] == sa.SA_KERNEL_INT32
+    # 4096^2 exceeds the a-priori width: the screened T16 kernel on batch plans (per-pair
+    # composition cap, int32 re-run above it), int32 for a single pair (SPLIT plan)
+    assert sa.plan_query_ex(3, aff, 4096, 4096, 10000)[0] == sa.SA_KERNEL_T16
+    assert sa.plan_query_ex(3, aff, 4096, 4096, 1)[0] == sa.SA_KERNEL_INT32
+    assert sa.plan_query_ex(3, aff, 16384, 16384, 10000)[0] == sa.SA_KERNEL_INT32   # cap below k / 2
     assert sa.plan_query_ex(2, sa.ScoringSystem(-3, -1, 1, -1, False), 1024, 1024, 10000)[0] == sa.SA_KERNEL_T16_ENDCELL
     assert sa.plan_query_ex(2, sa.ScoringSystem(-3, -1, 1, -1, False), 8192, 8192, 1)[0] == sa.SA_KERNEL_T16_ENDCELL
     assert sa.plan_query_ex(2, sa.ScoringSystem(-9, -1, 1, -1, False), 1024, 1024, 10000)[0] == sa.SA_KERNEL_INT32

@@ -85,15 +85,13 @@ def test_config5_shard_2048(engine):
     check_batch(engine, s1, o1, s2, o2, res, ops, score_sample=2048, ops_sample=64, seed=5)
 
 
-@pytest.mark.parametrize("x2", ["0", "1"])
-def test_north_star_shape_1024x4096(engine, x2, monkeypatch):
+def test_north_star_shape_1024x4096(engine):
     """North-star pair shape (4096 x 4096), 1,024 pairs in one launch: every end cell against the
-    linear-space oracle, 128 pairs' op streams against the full-matrix oracle -- on the shipped
-    one-pair kernel (R = 32) and on the opt-in two-pair kernel (SEQALIB_X2=1, R = 16)."""
-    monkeypatch.setenv("SEQALIB_X2", x2)
+    linear-space oracle, 128 pairs' op streams against the full-matrix oracle, on the shipped
+    one-pair kernel (R = 32)."""
     s1, o1, s2, o2 = sa.synth_dna_batch(9_000_000_000, 1024, 4096, 4096, threads=THREADS)
     res, ops = engine.align_packed(0, sa.ScoringSystem(*SW), s1, o1, s2, o2)
-    assert engine.last_plan() == ((sa.SA_KERNEL_T16_X2, 16, 1) if x2 == "1" else (sa.SA_KERNEL_T16_ENDCELL, 32, 1))
+    assert engine.last_plan() == (sa.SA_KERNEL_T16_ENDCELL, 32, 1)
     check_batch(engine, s1, o1, s2, o2, res, ops, score_sample=1024, ops_sample=128, seed=9)
 
 

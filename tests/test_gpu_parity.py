@@ -253,7 +253,7 @@ def test_split_plan_vs_oracle(engine, algo, monkeypatch):
     assert engine.last_plan()[1:] == (2, 0)
 
 
-T16_KERNELS = (sa.SA_KERNEL_T16, sa.SA_KERNEL_T16_ENDCELL, sa.SA_KERNEL_T16_X2)
+T16_KERNELS = (sa.SA_KERNEL_T16, sa.SA_KERNEL_T16_ENDCELL)
 
 
 def dna_pairs(seed, count, maxlen):
@@ -393,11 +393,39 @@ def test_t16_affine_eligibility_and_retry(engine):
     assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
 
 
+def test_t16_global_gotoh_screened_4096(engine, monkeypatch):
+    """GlobalGotoh past the a-priori 16-bit width (4096^2 at (-3, -1, 1, -1): values in
+    [-4104, 4096]) still runs the T16 affine kernel: the window sits at the low end (every pair's
+    borders reach it) and the fill screens each pair by its symbol composition (every prefix
+    alignment scores <= MA * sum_c min(count1(c), count2(c))).  Pairs above the cap -- identical or
+    near-identical sequences -- are re-run exactly on the int32 kernel; the rest stay T16.  Batch
+    plan (>= 1024 pairs) and the widened few-pairs plan (SEQALIB_SPLIT=0; SPLIT plans never take
+    the screened kernel)."""
+    gg = (-3, -1, 1, -1, True)
+    hot = sa.synth_dna(95_000, 4096)
+    big = [(sa.synth_dna(95_001, 4096), sa.synth_dna(95_002, 4096)),      # random: screened in
+           (hot, hot),                                                   # score 4096: int32
+           (hot, sa.synth_mutate(hot, 2)[:4096]),                         # near-identical: int32
+           (sa.synth_dna(95_003, 4000), sa.synth_dna(95_004, 4096))]
+    rng = np.random.default_rng(41)
+    pairs = [(sa.synth_dna(96_000 + k, int(rng.integers(20, 200))), sa.synth_dna(97_000 + k, int(rng.integers(20, 200))))
+             for k in range(1100)]
+    pairs[10], pairs[500], pairs[501], pairs[1099] = big
+    compare_with_oracle(engine, 3, gg, pairs)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    monkeypatch.setenv("SEQALIB_SPLIT", "0")
+    compare_with_oracle(engine, 3, gg, big)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    compare_with_oracle(engine, 3, (-3, -1, 1, -1, False), big)   # !allow: MI' = 2 GOE - 1
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    monkeypatch.delenv("SEQALIB_SPLIT")
+    compare_with_oracle(engine, 3, gg, big)   # few long pairs: SPLIT plan, int32
+    assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
+
+
 def test_endcell_replay_vs_oracle(engine, monkeypatch):
     """>= 1024 DNA SW pairs take the T16 plan with per-chunk maxima and the end-cell replay
-    (sa_endcell.hip): one pair per wave at R = 32 (max_m 4200 -> 3 bands), and with SEQALIB_X2=1
-    two pairs per wave at R = 16 (sa_fill_x2.hip; 5 bands, ragged shapes inside a wave, the odd
-    last pair alone).  Cases: all-zero matrices (end cell = last cell), periodic sequences (many
+    (sa_endcell.hip): one pair per wave at R = 32 (max_m 4200 -> 3 bands).  Cases: all-zero matrices (end cell = last cell), periodic sequences (many
     tied maxima across rows and chunks), identical sequences, multi-band pairs."""
     rng = np.random.default_rng(5)
     pairs = []
@@ -420,13 +448,6 @@ def test_endcell_replay_vs_oracle(engine, monkeypatch):
     for args in [(-1, 1, -1), (-3, 2, -2), (-1, 2, -1)]:
         compare_with_oracle(engine, 0, args, pairs)
         assert engine.last_plan()[:2] == (sa.SA_KERNEL_T16_ENDCELL, 32), args
-    monkeypatch.setenv("SEQALIB_X2", "1")
-    for args in [(-1, 1, -1), (-3, 2, -2)]:
-        compare_with_oracle(engine, 0, args, pairs)
-        assert engine.last_plan()[:2] == (sa.SA_KERNEL_T16_X2, 16), args
-    compare_with_oracle(engine, 0, (-1, 1, -1), pairs[:1029])   # odd count: the last wave has one pair
-    assert engine.last_plan()[:2] == (sa.SA_KERNEL_T16_X2, 16)
-    monkeypatch.delenv("SEQALIB_X2")
     # LocalGotoh: the affine end-cell replay (M, Iy and the last row's Ix per lane; the band's top
     # M and Ix rows), R = 16 (max_m 4200 -> 5 bands); the SPLIT plan's R = 2, 4, 8 replays below
     for args in [(-3, -1, 1, -1, True), (-2, -1, 2, -1, True), (-1, -1, 3, -2, True)]:
