@@ -416,8 +416,10 @@ def test_t16_global_gotoh_screened_4096(engine, monkeypatch):
     monkeypatch.setenv("SEQALIB_SPLIT", "0")
     compare_with_oracle(engine, 3, gg, big)
     assert engine.last_plan()[0] == sa.SA_KERNEL_T16
-    compare_with_oracle(engine, 3, (-3, -1, 1, -1, False), big)   # !allow: MI' = 2 GOE - 1
-    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    # !allowMismatch: no mismatched diagonal, so the a-priori low end is the all-gap path
+    # (2 GO + 8192 GE = -8198 at (4096, 4096)), wider than any 16-bit window: int32
+    compare_with_oracle(engine, 3, (-3, -1, 1, -1, False), big)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
     monkeypatch.delenv("SEQALIB_SPLIT")
     compare_with_oracle(engine, 3, gg, big)   # few long pairs: SPLIT plan, int32
     assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
