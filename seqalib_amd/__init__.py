@@ -391,16 +391,23 @@ class Engine:
         self._check(self.L.sa_set_workspace_limit(self.h, nbytes), "sa_set_workspace_limit")
 
     def align_packed(self, algo: int, scoring: ScoringSystem, s1: np.ndarray, off1: np.ndarray,
-                     s2: np.ndarray, off2: np.ndarray, lut: Optional[np.ndarray] = None):
-        """Host-buffer batch (sa_align_batch).  Returns (results structured array, ops uint8 array)."""
+                     s2: np.ndarray, off2: np.ndarray, lut: Optional[np.ndarray] = None, out=None):
+        """Host-buffer batch (sa_align_batch).  Returns (results structured array, ops uint8 array).
+        out: optional (results, ops) arrays of a previous call with the same shapes, reused as the
+        output buffers (a caller that keeps its buffers avoids re-faulting ~m+n bytes per pair)."""
         npairs = len(off1) - 1
         s1 = np.ascontiguousarray(s1, dtype=np.uint8)
         s2 = np.ascontiguousarray(s2, dtype=np.uint8)
         off1 = np.ascontiguousarray(off1, dtype=np.uint64)
         off2 = np.ascontiguousarray(off2, dtype=np.uint64)
-        res = np.zeros(max(npairs, 1), dtype=RESULT_DTYPE)
         ops_cap = int(off1[-1] + off2[-1]) + npairs + 1
-        ops = np.zeros(ops_cap, dtype=np.uint8)
+        if out is not None and out[0].base is not None and len(out[0].base) == max(npairs, 1) \
+                and out[0].base.dtype == RESULT_DTYPE and out[1].dtype == np.uint8 and len(out[1]) == ops_cap \
+                and out[1].flags.c_contiguous and out[1].flags.writeable:
+            res, ops = out[0].base, out[1]
+        else:
+            res = np.zeros(max(npairs, 1), dtype=RESULT_DTYPE)
+            ops = np.zeros(ops_cap, dtype=np.uint8)
         lut_p = 0
         if lut is not None:
             lut = np.ascontiguousarray(lut, dtype=np.uint8).reshape(65536)

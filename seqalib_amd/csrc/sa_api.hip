@@ -7,6 +7,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <chrono>
 #include <string>
 #include <thread>
@@ -845,24 +848,82 @@ int lg_hack_split(sa_ctx* c, const uint64_t* off1, const uint64_t* off2, uint32_
 }
 
 // Host copy of a large buffer on several threads (the caller's pageable memory <-> pinned
-// staging; one thread copies ~5-10 GB/s).
+// staging; one thread copies ~5-10 GB/s).  A process-wide pool of persistent workers (up to 15 +
+// the caller: the GPU box's 16-core share) takes 1 MiB slices of the copy: spawning threads per
+// 16 MiB piece cost ~1 ms per call and capped a copy at 4 threads.
+struct CopyPool {
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    std::vector<std::thread> workers;
+    uint8_t* dst = nullptr;
+    const uint8_t* src = nullptr;
+    uint64_t n = 0;
+    std::atomic<uint64_t> next{0};
+    size_t done = 0;         // workers finished with the current job (every worker takes part)
+    uint64_t gen = 0;        // job generation
+    bool quit = false;
+    static constexpr uint64_t kSlice = 1ull << 20;
+    explicit CopyPool(unsigned k) {
+        for (unsigned t = 0; t < k; ++t) workers.emplace_back([this] { run(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            quit = true;
+        }
+        cv.notify_all();
+        for (auto& w : workers) w.join();
+    }
+    void slices() {
+        for (;;) {
+            const uint64_t a = next.fetch_add(kSlice);
+            if (a >= n) return;
+            memcpy(dst + a, src + a, std::min(kSlice, n - a));
+        }
+    }
+    void run() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return quit || gen != seen; });
+            if (quit) return;
+            seen = gen;
+            lk.unlock();
+            slices();
+            lk.lock();
+            if (++done == workers.size()) done_cv.notify_all();
+        }
+    }
+    void copy(void* d, const void* s, uint64_t bytes) {   // one job at a time (callers serialise)
+        std::unique_lock<std::mutex> lk(mu);
+        dst = (uint8_t*)d;
+        src = (const uint8_t*)s;
+        n = bytes;
+        next.store(0);
+        done = 0;
+        ++gen;
+        cv.notify_all();
+        lk.unlock();
+        slices();
+        lk.lock();
+        // every worker reports the job (a late waker finds no slice left): the job's buffers
+        // are not touched after this returns
+        done_cv.wait(lk, [&] { return done == workers.size(); });
+    }
+};
+
 void par_copy(void* dst, const void* src, uint64_t n) {
-    constexpr uint64_t kPiece = 4ull << 20;
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const uint64_t T = std::min<uint64_t>(std::min(8u, hw), n / kPiece);
-    if (T < 2) {
+    if (n < (4ull << 20)) {
         if (n) memcpy(dst, src, n);
         return;
     }
-    const uint64_t part = (n / T + 4095) & ~(uint64_t)4095;
-    std::vector<std::thread> th;
-    for (uint64_t t = 1; t < T; ++t) {
-        const uint64_t a = t * part;
-        if (a >= n) break;
-        th.emplace_back([=] { memcpy((uint8_t*)dst + a, (const uint8_t*)src + a, std::min(part, n - a)); });
-    }
-    memcpy(dst, src, std::min(part, n));
-    for (auto& x : th) x.join();
+    static std::mutex pool_mu;   // one pooled copy at a time (contexts on several host threads)
+    static CopyPool* pool = [] {
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        return new CopyPool(std::min(15u, hw > 1 ? hw - 1 : 1u));   // never destroyed: exit-safe
+    }();
+    std::lock_guard<std::mutex> g(pool_mu);
+    pool->copy(dst, src, n);
 }
 
 // Host API batches are cut into contiguous pair ranges ("chunks") of near-equal cells and run
@@ -897,6 +958,13 @@ std::vector<uint32_t> cut_by_cells(const uint64_t* off1, const uint64_t* off2, u
 int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, const uint64_t* off1,
                const uint8_t* seq2, const uint64_t* off2, uint32_t npairs, const uint8_t* lut,
                sa_result* results, uint8_t* ops, uint64_t ops_cap) {
+    // $SEQALIB_HOST_TIMING: host-side phases of the call (stderr)
+    const bool timing = getenv("SEQALIB_HOST_TIMING") != nullptr;
+    const auto t_call = std::chrono::steady_clock::now();
+    double ms_in = 0, ms_wait = 0, ms_out = 0;
+    auto since = [](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    };
     const uint64_t t1 = off1[npairs], t2 = off2[npairs];
     for (uint32_t p = 0; p < npairs; ++p)
         if (off1[p + 1] < off1[p] || off2[p + 1] < off2[p]) return fail(c, SA_ERR_ARG, "offsets must be non-decreasing");
@@ -980,6 +1048,7 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
                 mn = (uint32_t)std::max<uint64_t>(mn, off2[p0 + q] - off2[p0 + q - 1]);
             }
         }
+        const auto t_in = std::chrono::steady_clock::now();
         for (uint64_t x = 0; x < n1; x += kHostPiece) {
             const uint64_t k = std::min(kHostPiece, n1 - x);
             par_copy(si + a1 + x, seq1 + a1 + x, k);
@@ -992,6 +1061,7 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         }
         SA_HIP(c, hipMemcpyAsync(do1 + p0 + g, so1 + p0 + g, 8ull * (cnt + 1), hipMemcpyHostToDevice, st));
         SA_HIP(c, hipMemcpyAsync(do2 + p0 + g, so2 + p0 + g, 8ull * (cnt + 1), hipMemcpyHostToDevice, st));
+        ms_in += since(t_in);
         hipStream_t done = st;
         if (dc) {
             std::string e;
@@ -1024,16 +1094,23 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     // each piece reaches the caller's buffers while later pieces and chunks still run
     for (size_t k = 0; k < outp.size(); ++k) {
         const OutPiece& o = outp[k];
+        const auto t_w = std::chrono::steady_clock::now();
         SA_HIP(c, hipEventSynchronize(c->host_ev[G + k]));
+        ms_wait += since(t_w);
+        const auto t_o = std::chrono::steady_clock::now();
         if (k == 0 || outp[k - 1].g != o.g)
             memcpy(results + cut[o.g], sres + cut[o.g], sizeof(sa_result) * (cut[o.g + 1] - cut[o.g]));
         par_copy(ops + o.ob, sops + o.ob, o.on);
+        ms_out += since(t_o);
     }
     if (pipe) {
         SA_HIP(c, hipStreamSynchronize(c->s_fill));
         SA_HIP(c, hipStreamSynchronize(c->s_tb));
     }
     SA_HIP(c, hipStreamSynchronize(st));
+    if (timing)
+        fprintf(stderr, "[seqalib host api] %u pairs, %u chunks: %.2f ms = staging in %.2f + waiting %.2f + copies out %.2f + other\n",
+                npairs, G, since(t_call), ms_in, ms_wait, ms_out);
     return SA_OK;
 }
 

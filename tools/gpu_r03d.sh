@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round-3 session: DC parity tests + DC batches (steady-chunk 16-bit sweeps), then the host-API
+# session (tools/gpu_host.sh).  Each GPU step has its own limit; the chain stops at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -k "hirschberg or myers or dc_ or generic or golden" --timeout 120 --timeout-method thread > gpurun_out/dc_tests.log 2>&1 || { echo dc tests failed; tail -30 gpurun_out/dc_tests.log; exit 1; }
+tail -2 gpurun_out/dc_tests.log
+: > gpurun_out/dc.jsonl
+for algo in hb mm; do for cfg in "10000 1024" "1000 4096"; do set -- $cfg
+  timeout -k 10 200 python tools/bench_dc.py --algo $algo --pairs $1 --len $2 --cpu-pairs 0 > gpurun_out/dc_run.log 2>&1 || { echo bench failed; tail -20 gpurun_out/dc_run.log; exit 1; }
+  grep '^{' gpurun_out/dc_run.log >> gpurun_out/dc.jsonl
+done; done
+cut -c1-220 gpurun_out/dc.jsonl
+bash tools/gpu_host.sh
