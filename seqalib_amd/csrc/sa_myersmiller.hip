@@ -173,7 +173,7 @@ __device__ __forceinline__ void mm_band(const MmSweep& d, const DcSrc<MM>& src, 
 template <int R, bool LAST>
 __device__ __forceinline__ void mm_band16(const MmSweep& d, const uint8_t* s1, const uint8_t* s2, const uint32_t* aux,
                                           int32_t delta, const MmScore& sc, int band, int32_t* outC, int32_t* outD,
-                                          int tl, int rl, int32_t& cl, int32_t& dl, int32_t* s_park) {
+                                          int tl, int rl, int32_t& cl, int32_t& dl) {
     const int lane = threadIdx.x;
     const int m = d.alen, n = d.blen, g = sc.g, h = sc.h;
     constexpr int BAND = 64 * R;
@@ -210,73 +210,9 @@ __device__ __forceinline__ void mm_band16(const MmSweep& d, const uint8_t* s1, c
     };
     int32_t vc, vd, nvc, nvd;
     uint32_t vs, nvs, sym = 0;
-    // Steady chunk (c0 >= 63, c0 + 64 <= n; as hb_band16): no per-lane branch; the handed-on row
-    // (C and D of lane 63's last row, or of row m at lane tl / register rl in the last band) is
-    // parked per step in LDS by every lane (others into a discard slot) and stored per chunk.
-    const int src_lane = LAST ? tl : 63;
-    auto steady = [&](int c0, auto SRC) {
-        constexpr int SR = decltype(SRC)::value;
-        int32_t* const park = s_park + (lane == src_lane ? 0 : 64);
-#pragma unroll 1
-        for (int q = 0; q < 64; ++q) {
-            const int32_t up_c = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vc, q), cl, 0x138, 0xf, 0xf, false);
-            const int32_t up_d = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vd, q), dl, 0x138, 0xf, 0xf, false);
-            sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vs, q), sym, 0x138, 0xf, 0xf, false);
-            int32_t cd = prev_up, cu = up_c, du = up_d, dsel = 0;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                int32_t e, dd, c, t;
-                asm("v_add_u16 %0, %4, %5\n\t"
-                    "v_max_i16 %0, %6, %0\n\t"
-                    "v_add_u16 %0, %7, %0\n\t"
-                    "v_add_u16 %1, %4, %8\n\t"
-                    "v_max_i16 %1, %9, %1\n\t"
-                    "v_add_u16 %1, %7, %1\n\t"
-                    "v_bfe_i32 %3, %10, %11, 8\n\t"
-                    "v_add_u16 %3, %12, %3\n\t"
-                    "v_max_i16 %2, %1, %0\n\t"
-                    "v_max_i16 %2, %3, %2"
-                    : "=&v"(e), "=&v"(dd), "=&v"(c), "=&v"(t)
-                    : "s"(g16), "v"(Cp[r]), "v"(Ep[r]), "s"(h16), "v"(cu), "v"(du), "v"(a[r]), "v"(sym),
-                      "v"(cd));
-                cd = Cp[r];
-                Cp[r] = c;
-                Ep[r] = e;
-                cu = c;
-                du = dd;
-                if (r == SR) dsel = dd;
-            }
-            prev_up = up_c;
-            cl = Cp[R - 1];
-            dl = du;
-            park[q] = Cp[SR];
-            park[128 + q] = dsel;
-        }
-        __syncthreads();   // (one wave: orders the parked writes before the reads)
-        outC[c0 - src_lane + 1 + lane] = dc_unpack16(s_park[lane], delta);
-        outD[c0 - src_lane + 1 + lane] = dc_unpack16(s_park[128 + lane], delta);
-        __syncthreads();
-    };
     load_chunk(0, vc, vd, vs);
     for (int c0 = 0; c0 < n + 63; c0 += 64) {
         load_chunk(c0 + 64, nvc, nvd, nvs);
-        if (c0 >= 63 && c0 + 64 <= n) {
-            const int src_r = LAST ? rl : R - 1;
-            switch (src_r) {   // uniform
-                case 0: steady(c0, std::integral_constant<int, 0>{}); break;
-                case 1: if constexpr (R > 1) steady(c0, std::integral_constant<int, (R > 1 ? 1 : 0)>{}); break;
-                case 2: if constexpr (R > 2) steady(c0, std::integral_constant<int, (R > 2 ? 2 : 0)>{}); break;
-                case 3: if constexpr (R > 3) steady(c0, std::integral_constant<int, (R > 3 ? 3 : 0)>{}); break;
-                case 4: if constexpr (R > 4) steady(c0, std::integral_constant<int, (R > 4 ? 4 : 0)>{}); break;
-                case 5: if constexpr (R > 5) steady(c0, std::integral_constant<int, (R > 5 ? 5 : 0)>{}); break;
-                case 6: if constexpr (R > 6) steady(c0, std::integral_constant<int, (R > 6 ? 6 : 0)>{}); break;
-                default: if constexpr (R > 7) steady(c0, std::integral_constant<int, (R > 7 ? 7 : 0)>{}); break;
-            }
-            vc = nvc;
-            vd = nvd;
-            vs = nvs;
-            continue;
-        }
         const int steps = min(64, n + 63 - c0);
         for (int q = 0; q < steps; ++q) {
             const int s = c0 + q;
@@ -341,7 +277,6 @@ __global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const u
                                                       DcBits bits, MmScore sc, Dc16 d16) {
     constexpr bool LUT = MM == kMatchLut;
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];
-    __shared__ int32_t s_park[256];   // Dc16 steady chunks: the handed-on C and D rows, per step
     const int lane = threadIdx.x;
     if (blockIdx.x / 2 >= lvl->nsplit) return;   // grid sized from an upper bound
     const DcSub sub = split[blockIdx.x / 2];
@@ -364,9 +299,9 @@ __global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const u
         if constexpr (MM != kMatchBits) {
             if (b16) {
                 if (band < bands - 1)
-                    mm_band16<R, false>(d, s1, s2, d16.aux, d16.delta, sc, band, outC, outD, tl, rl, cl, dl, s_park);
+                    mm_band16<R, false>(d, s1, s2, d16.aux, d16.delta, sc, band, outC, outD, tl, rl, cl, dl);
                 else
-                    mm_band16<R, true>(d, s1, s2, d16.aux, d16.delta, sc, band, outC, outD, tl, rl, cl, dl, s_park);
+                    mm_band16<R, true>(d, s1, s2, d16.aux, d16.delta, sc, band, outC, outD, tl, rl, cl, dl);
                 __threadfence_block();
                 __syncthreads();
                 continue;

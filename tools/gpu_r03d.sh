@@ -5,6 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+timeout -k 10 120 python tools/dbg_dc16.py 2>&1 | grep -v amdgpu.ids || exit 1
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -k "hirschberg or myers or dc_ or generic or golden" --timeout 120 --timeout-method thread > gpurun_out/dc_tests.log 2>&1 || { echo dc tests failed; tail -30 gpurun_out/dc_tests.log; exit 1; }
 tail -2 gpurun_out/dc_tests.log
 : > gpurun_out/dc.jsonl
