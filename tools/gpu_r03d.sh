@@ -15,3 +15,13 @@ for algo in hb mm; do for cfg in "10000 1024" "1000 4096"; do set -- $cfg
 done; done
 cut -c1-220 gpurun_out/dc.jsonl
 bash tools/gpu_host.sh
+echo "[d] headline-only rocprof $(date +%T)"
+rm -rf gpurun_out/prof_head
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_head -o run -- python3 bench.py --no-cpu --dropin-pairs 0 --steps 5 --warmup 1 --serial-steps 0 --e2e-steps 0 > gpurun_out/prof_head.log 2>&1 || { tail -20 gpurun_out/prof_head.log; exit 1; }
+tail -1 gpurun_out/prof_head.log | cut -c1-200
+echo "[d] full suite $(date +%T)"
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+echo "[d] bench $(date +%T)"
+timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log | cut -c1-400
