@@ -926,15 +926,16 @@ void par_copy(void* dst, const void* src, uint64_t n) {
     pool->copy(dst, src, n);
 }
 
-// Host API batches are cut into contiguous pair ranges ("chunks") of near-equal cells and run
+// Host API batches may be cut into contiguous pair ranges ("chunks") of near-equal cells run
 // through the cross-call pipeline, so chunk g+1's upload and chunk g-1's download overlap chunk
-// g's fill and traceback.  A chunk must still fill the chip (every fill launch has a tail), so
-// batches below 2 x kHostChunkPairs stay one chunk.  SEQALIB_HOST_CHUNKS overrides (tuning).
-constexpr uint32_t kHostChunkPairs = 4096;
+// g's fill and traceback.  Measured on 10,000 x 4096^2 (round 3, profiles/host_api_r03.txt): one
+// chunk 37.8-38.1 ms per call, two chunks 40.1-40.3 ms, four 51 ms -- each fill launch pays its own
+// tail and the next chunk's alphabet scan waits for CU slots behind the previous fill, which costs
+// more than the ~1 ms of upload the overlap hides.  So a batch is one chunk (its uploads and
+// downloads still overlap piece by piece); SEQALIB_HOST_CHUNKS=G splits it (tuning, tests).
 uint32_t host_chunks(int algo, uint32_t npairs) {
     if (algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER) return 1;   // one DC work set per context
-    uint32_t G = npairs >= 2 * kHostChunkPairs ? std::min<uint32_t>(4, npairs / kHostChunkPairs) : 1;
-    if (G == 3) G = 2;
+    uint32_t G = 1;
     if (const char* e = getenv("SEQALIB_HOST_CHUNKS")) G = (uint32_t)std::max(1, atoi(e));
     return std::max<uint32_t>(1, std::min(G, npairs));
 }
