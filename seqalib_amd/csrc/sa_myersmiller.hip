@@ -214,13 +214,16 @@ __device__ __forceinline__ void mm_band16(const MmSweep& d, const uint8_t* s1, c
     for (int c0 = 0; c0 < n + 63; c0 += 64) {
         load_chunk(c0 + 64, nvc, nvd, nvs);
         const int steps = min(64, n + 63 - c0);
+        // steady chunk (c0 >= 63, c0 + 64 <= n): every lane is inside the matrix for all 64 steps,
+        // so the per-lane range branch is skipped (the hand-off store keeps its lane test)
+        const bool steady = c0 >= 63 && c0 + 64 <= n;
         for (int q = 0; q < steps; ++q) {
             const int s = c0 + q;
             const int32_t up_c = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vc, q), cl, 0x138, 0xf, 0xf, false);
             const int32_t up_d = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vd, q), dl, 0x138, 0xf, 0xf, false);
             sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vs, q), sym, 0x138, 0xf, 0xf, false);
             const int j0 = s - lane;
-            if (j0 >= 0 && j0 < n) {
+            if (steady || (j0 >= 0 && j0 < n)) {
                 int32_t cd = prev_up, cu = up_c, du = up_d, dsel = 0;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
