@@ -226,13 +226,14 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
         for (int c0 = 0; c0 < n + 63; c0 += 64) {
             load_chunk(c0 + 64, nvup, nvsym);
             const int steps = min(64, n + 63 - c0);
+            const bool steady = c0 >= 63 && c0 + 64 <= n;   // every lane inside (as the 16-bit sweep)
             for (int q = 0; q < steps; ++q) {
                 const int s = c0 + q;
                 const int32_t up_h = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vup, q), hl, 0x138, 0xf,
                                                                  0xf, false);
                 sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vsym, q), sym, 0x138, 0xf, 0xf, false);
                 const int j0 = s - lane;
-                if (j0 >= 0 && j0 < n) {
+                if (steady || (j0 >= 0 && j0 < n)) {
                     int32_t hd = prev_up, hu = up_h;
 #pragma unroll
                     for (int r = 0; r < R; ++r) {

@@ -120,13 +120,14 @@ __device__ __forceinline__ void mm_band(const MmSweep& d, const DcSrc<MM>& src, 
     for (int c0 = 0; c0 < n + 63; c0 += 64) {
         load_chunk(c0 + 64, nvc, nvd, nvs);
         const int steps = min(64, n + 63 - c0);
+        const bool steady = c0 >= 63 && c0 + 64 <= n;   // every lane inside (as the 16-bit sweep)
         for (int q = 0; q < steps; ++q) {
             const int s = c0 + q;
             const int32_t up_c = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vc, q), cl, 0x138, 0xf, 0xf, false);
             const int32_t up_d = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vd, q), dl, 0x138, 0xf, 0xf, false);
             sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vs, q), sym, 0x138, 0xf, 0xf, false);
             const int j0 = s - lane;
-            if (j0 >= 0 && j0 < n) {
+            if (steady || (j0 >= 0 && j0 < n)) {
                 int32_t cd = prev_up, cu = up_c, du = up_d, dsel = 0;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
