@@ -193,6 +193,7 @@ Plan make_plan(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t
 struct Variant {
     Plan pl;
     bool t16 = false, cmax = false;
+    bool so = false;   // score-only fill + block-recompute traceback (sa_traceback_so.hip)
     uint32_t snap_nch = 0;
     uint64_t snap_h_slot = 0, snap_p_slot = 0;   // 32-bit words per pair
     uint64_t slot_bytes = 0;
@@ -215,6 +216,12 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
         v.snap_h_slot = v.snap_p_slot * (is_affine(algo) ? v.pl.R + 1 : v.pl.R / 2);
         v.pl.rowbuf_elems = (uint64_t)(is_affine(algo) ? 2 : 1) * v.pl.g.bands * std::max<uint32_t>(max_n, 1);
     }
+    // Score-only fill (T16 SW chunk-max, many-pairs plans): no per-cell records; the traceback
+    // recomputes the blocks along its path from the snapshots and the edge stream.
+    // SEQALIB_SO=0 keeps the tagged records (A/B, tests).
+    v.so = v.cmax && algo == SA_SW && !v.pl.split && v.pl.R >= 4 && v.pl.R <= 32;
+    if (const char* e = getenv("SEQALIB_SO")) if (e[0] == '0') v.so = false;
+    if (v.so) v.pl.g = make_geom(algo, v.pl.R, max_m, max_n, kGeomEdge);
     if (v.pl.split) v.pl.rowbuf_elems = 0;   // hand-off granules live in c->split
     v.kernel = v.cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
     v.slot_bytes = v.pl.g.dir_slot + v.pl.rowbuf_elems * 4 + (v.snap_h_slot + 2 * v.snap_p_slot) * 4;
@@ -675,7 +682,9 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fp.part = pl.split ? reinterpret_cast<int32_t*>(spbase + sp_part) : nullptr;
             fp.wait_ticks = wait_ticks;
             fp.no_start = getenv("SEQALIB_NO_START") ? 1 : 0;
-            return FillVariant{pl.R, lut, allow || v.t16, keyed, v.t16, v.cmax, pl.split, bits};
+            FillVariant fv{pl.R, lut, allow || v.t16, keyed, v.t16, v.cmax, pl.split, bits};
+            fv.so = v.so;
+            return fv;
         };
         for (int k = 0; k < nv; ++k) {
             const Variant& v = vars[k];
@@ -715,6 +724,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 ep.max_n = max_n;
                 ep.res = d_res; ep.pair_base = (uint32_t)base; ep.count = cnt;
                 ep.gap = sc->gap; ep.gap_open = sc->gap_open; ep.gap_extend = sc->gap_extend;
+                ep.hshift = v.so ? 0 : 2;
                 // on the fill stream, right after the fill: run beside the next call's fill (on the
                 // traceback stream) its 10,000 short waves slowed that fill by 4 % (measured)
                 e = launch_endcell(algo, pl.R, ep, sf);
@@ -739,6 +749,10 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             tp.tagged = v.t16 ? 1 : 0;
             tp.sel = fps[k].sel; tp.sel_want = fps[k].sel_want;
             tp.rerun = fps[k].rerun;
+            tp.band_stride = v.pl.g.band_stride;
+            tp.snap_h = fps[k].snap_h; tp.snap_p = fps[k].snap_p;
+            tp.snap_h_slot = v.snap_h_slot; tp.snap_p_slot = v.snap_p_slot; tp.snap_nch = v.snap_nch;
+            tp.prof = fps[k].prof;
             return tp;
         };
         for (int k = 0; k < nv; ++k) {
@@ -769,7 +783,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                     }
                 }
             }
-            hipError_t e = tb_wave(cnt) ? launch_traceback_wave(algo, v.pl.R, lut, tp, stb)
+            hipError_t e = v.so ? launch_traceback_so(v.pl.R, tp, stb)
+                         : tb_wave(cnt) ? launch_traceback_wave(algo, v.pl.R, lut, tp, stb)
                                         : launch_traceback(algo, v.pl.R, lut, tp, stb);
             if (e != hipSuccess) return hip_fail(c, e, "traceback kernel launch");
         }

@@ -56,6 +56,7 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
     const int tstar = ((iend - 1) % BAND) / R;
     const int row0 = b * BAND + lane * R;
     const int G = P.gap;
+    const int hs = P.hshift;   // values stored as H << hs: 4H (tagged fill) or H (score-only fill)
 
     if (S == 0) {   // every cell is 0: the last cell is the reference's maximum (MaxScore from INT_MIN)
         if (lane == 0) {
@@ -81,7 +82,7 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
     // the chunks to replay, found 64 at a time (one load per lane, not a dependent load per chunk)
     for (int base = 0; base <= c; base += kWave) {
         const int ccl = base + lane;
-        uint64_t hits = __builtin_amdgcn_ballot_w64(ccl <= c && lmax[(uint64_t)ccl * kWave] == 4 * S);
+        uint64_t hits = __builtin_amdgcn_ballot_w64(ccl <= c && lmax[(uint64_t)ccl * kWave] == (S << hs));
         while (hits) {
         const int cc = base + (int)__builtin_ctzll(hits);
         hits &= hits - 1;
@@ -95,10 +96,10 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
 #pragma unroll
             for (int q = 0; q < R / 2; ++q) {
                 const uint32_t w = sh[q * kWave];
-                Hp[2 * q] = (int)(w & 0xffffu) >> 2;        // stored as 4H (non-negative)
-                Hp[2 * q + 1] = (int)(w >> 16) >> 2;
+                Hp[2 * q] = (int)(w & 0xffffu) >> hs;        // stored as H << hs (non-negative)
+                Hp[2 * q + 1] = (int)(w >> 16) >> hs;
             }
-            prev_up = (int)(P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] & 0xffff) >> 2;
+            prev_up = (int)(P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] & 0xffff) >> hs;
         }
         __syncthreads();   // (a previous candidate's reads of the staging arrays)
         for (int k = lane; k < kWave + kChunk; k += kWave) {
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
         }
         if (lane < kChunk) {
             const int j = cc * kChunk + lane;
-            s_top[lane] = (top && j < n) ? (ec_top(top + (uint64_t)j * rs) >> 2) : 0;
+            s_top[lane] = (top && j < n) ? (ec_top(top + (uint64_t)j * rs) >> hs) : 0;
         }
         __syncthreads();
         int hl = Hp[R - 1];

@@ -90,6 +90,14 @@ __device__ __forceinline__ uint32_t t16_code8(uint32_t sp, uint32_t b) {
            (b == (sp >> 24) ? 24u : 0u);
 }
 
+// SO profile word: the tagged profile bytes 4s + 3 (decide_t16) back to s, byte by byte.
+__device__ __forceinline__ uint32_t so_profile(uint32_t w) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o |= ((uint32_t)(((int)(int8_t)(w >> (8 * k)) - 3) >> 2) & 255u) << (8 * k);
+    return o;
+}
+
 template <bool LUT>
 __device__ __forceinline__ bool match_bit(const uint32_t* s_lut, int a, int b) {
     if constexpr (LUT) {
@@ -161,7 +169,12 @@ constexpr int kEvCol = 2048;
 // MM: how a cell learns whether its two symbols match -- kMatchEq (byte equality), kMatchLut (the
 // 256 x 256 table of the user's match fn, LDS) or kMatchBits (a per-pair m x n match bitmap, the
 // generic-Ty path: any symbol type and count, the reference's cacheAllMatches packed to bits).
-template <int ALG, int R, int MM, bool ALLOW, bool KEYED, bool T16, bool CMAX, bool SPLIT>
+// SO (score-only, T16 SW CMAX many-pairs plans): the cell carries no move tags and the fill writes
+// no per-cell records -- only each lane's last row per step (the "edge" stream, 16 bits per
+// lane-step).  With the per-chunk snapshots every (lane, chunk) block of R x 32 cells can be
+// recomputed exactly from its left column (snapshot), its top row (edge stream of the lane above,
+// or the band's top row) and its corner, which sa_traceback_so.hip does along the path.
+template <int ALG, int R, int MM, bool ALLOW, bool KEYED, bool T16, bool CMAX, bool SPLIT, bool SO = false>
 // (Asking the headline kernel for 4 waves per SIMD -- 128 VGPRs, 8 spills outside the step loops
 // -- measured 29.6 ms per fill against 29.4 at its natural 3 waves: not taken.)
 __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)>())) void fill_kernel(FillParams P) {
@@ -171,7 +184,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
     constexpr int FBITS = AFF ? 4 : 2;            // flag bits per cell
     constexpr int BPC = record_bpc(ALG, R, T16);  // record bits per cell (padding above the flags)
-    constexpr int RB = R * BPC;                // bits per record
+    constexpr int RB = SO ? 16 : R * BPC;      // bits per record (SO: the lane's last row, 16 bits)
     constexpr int BPS = RB / 8;                // bytes per record
     constexpr int RW = (RB + 31) / 32;         // words per record
     constexpr int RPW = (RB < 32 ? RB : 32) / BPC;  // rows per record word
@@ -183,7 +196,9 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     static_assert(!T16 || (ALLOW && MM == kMatchEq && (RB <= 32 || RB % 32 == 0)),
                   "T16: allow-mismatch, profile");
     static_assert(!T16 || !LOCAL || KEYED, "T16 local mode tracks its maximum with keys");
-    constexpr int SC = T16 ? (AFF ? 8 : 4) : 1;   // score scale of the register values
+    constexpr int SC = SO ? 1 : T16 ? (AFF ? 8 : 4) : 1;   // score scale of the register values
+    static_assert(!SO || (T16 && CMAX && ALG == SA_SW && !SPLIT), "SO: T16 SW chunk-max, many pairs");
+    constexpr int CSH = SO ? 0 : (AFF ? 3 : 2);   // CMAX: chunk maxima are H << CSH
     static_assert(!CMAX || (T16 && LOCAL && R % 2 == 0), "CMAX: T16 Smith-Waterman / LocalGotoh");
 
     // Dynamic LDS (sizes from lds_layout(), host and device agree):
@@ -318,8 +333,9 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     // T16 tagged gaps.  Local modes take the up term as max(4U + 2, 0) = hu - CU with unsigned
     // saturation (v_sub_u16 clamp; hu >= 0, CU = -(4G + 2) > 0 since t16_ok demands G < 0),
     // which also applies the zero clamp of the cell: max(D, max(U, 0), L) == max(D, U, L, 0).
-    const uint32_t CU = LOCAL ? ((uint32_t)(-(4 * G + 2)) & 0xffffu) : (uint32_t)(4 * G + 2);
-    const uint32_t CL = (uint32_t)(4 * G + 1);
+    const uint32_t CU = SO ? ((uint32_t)(-G) & 0xffffu)
+                       : LOCAL ? ((uint32_t)(-(4 * G + 2)) & 0xffffu) : (uint32_t)(4 * G + 2);
+    const uint32_t CL = SO ? ((uint32_t)G & 0xffffu) : (uint32_t)(4 * G + 1);
     // T16 affine: class / extend tagged gap terms (u16 arithmetic, sa_fill_impl.h header).  The
     // LocalGotoh Ix open term is max(Mu + 8GOE + 4, 0) = Mu - CXO with unsigned saturation (Mu >= 0,
     // CXO = -(8GOE + 4) > 0 since t16_mode demands GOE < 0).
@@ -632,6 +648,36 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     }
                     xu = (int)xs;
                     Hc = Hp[r];
+                } else if constexpr (SO) {
+                    // Score-only cell (Hp = H, no tags): left = Hp + G, the next row's diagonal
+                    // Hp_old + s from the profile, up = max(Hu + G, 0) by unsigned saturation (so the
+                    // zero clamp is free, as in the tagged cell), two v_max_i16.  5 fast-class 16-bit
+                    // ops + v_bfe_i32 (tools/microbench_so.hip: 1.33x the tagged cell's rate).
+                    uint32_t t0, t1;
+                    if (r + 1 < R) {
+                        uint32_t dn;
+                        const uint32_t tabn = (uint32_t)a[r + 1 < R ? r + 1 : r];
+                        asm("v_add_u16 %[t0], %[cl], %[hp]\n\t"
+                            "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\t"
+                            "v_add_u16 %[dn], %[hp], %[dn]\n\t"
+                            "v_sub_u16_e64 %[t1], %[hu], %[cu] clamp\n\t"
+                            "v_max_i16 %[t0], %[dr], %[t0]\n\t"
+                            "v_max_i16 %[hp], %[t1], %[t0]"
+                            : [t0] "=&v"(t0), [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r])
+                            : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL), [tabn] "v"(tabn),
+                              [sym] "v"(sym));
+                        dcur = dn;
+                    } else {
+                        asm("v_add_u16 %[t0], %[cl], %[hp]\n\t"
+                            "v_sub_u16_e64 %[t1], %[hu], %[cu] clamp\n\t"
+                            "v_max_i16 %[t0], %[dr], %[t0]\n\t"
+                            "v_max_i16 %[hp], %[t1], %[t0]"
+                            : [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r])
+                            : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL));
+                    }
+                    if (r & 1)   // the lane's chunk maximum, one v_max3_u32 per two rows (H >= 0)
+                        asm("v_max3_u32 %0, %0, %1, %2" : "+v"(cml) : "v"(Hp[r >= 1 ? r - 1 : 0]), "v"(Hp[r]));
+                    Hc = Hp[r];
                 } else if constexpr (T16) {
                     // One asm block per cell (plain VALU->VALU dependences need no wait
                     // states; the compiler pads s_nop between separate asm statements).  The
@@ -765,7 +811,14 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
             prev_up = up_h;
             hl = Hp[R - 1];
             if constexpr (AFF) xl = xu;
-            if constexpr (T16 && RB < 32 && !ACC) rec[0] >>= (32 - RB);   // alignbit filled from the top
+            if constexpr (SO) {
+                // the step's record is the lane's last row: pushed into the packet word from the
+                // top (two steps per word), or, kStepAny, ORed in by the caller
+                if constexpr (ACC) rec[0] = __builtin_amdgcn_alignbit((uint32_t)hl, rec[0], 16u);
+                else rec[0] = (uint32_t)hl & 0xffffu;
+            } else if constexpr (T16 && RB < 32 && !ACC) {
+                rec[0] >>= (32 - RB);   // alignbit filled from the top
+            }
         }
     };
 
@@ -969,7 +1022,8 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                         const int row = row0 + r;
                         // CMAX: rows past m get substitution -128 (with gap < 0 their values stay
                         // below the matrix maximum, so they never win the lane's chunk maximum)
-                        if constexpr (T16) a[r] = row < m ? (int)P.prof[t16_code8(symp, s1[row]) >> 3] : (CMAX ? (int)0x80808080u : 0);
+                        if constexpr (SO) a[r] = row < m ? (int)so_profile(P.prof[t16_code8(symp, s1[row]) >> 3]) : (int)0x80808080u;
+                        else if constexpr (T16) a[r] = row < m ? (int)P.prof[t16_code8(symp, s1[row]) >> 3] : (CMAX ? (int)0x80808080u : 0);
                         else a[r] = row < m ? (int)s1[row] : 0;
                         const int i = row + 1;
                         if constexpr (ALG == SA_NW) Hp[r] = SC * (i * G - P.t16_delta);
@@ -1075,7 +1129,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     const uint32_t ck = chunk + 1;
                     const uint64_t e = (uint64_t)band * P.snap_nch + chunk;
                     P.snap_m[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = (int32_t)cml;
-                    lkey = max(lkey, (cml >> (AFF ? 3 : 2)) << 12 | ck);
+                    lkey = max(lkey, (cml >> CSH) << 12 | ck);
                     cml = 0;
                     if (chunk + 1 < nch) {   // state entering chunk + 1, for the end-cell replay
                         // R 16-bit values (affine: then the R Iy values and the last row's Ix)
@@ -1220,6 +1274,7 @@ template <int ALG>
 hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream) {
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
     const int R = v.R;
+    if (v.so && (ALG != SA_SW || !v.t16 || !v.cmax || v.split)) return hipErrorInvalidValue;
     const bool lut = (v.t16 || v.bits) ? false : v.lut, allow = v.allow;
     const bool keyed = LOCAL && v.keyed;
     // SPLIT: the compute wave + its poller and publisher waves (see kHandGran); LDS for one
@@ -1236,6 +1291,14 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
                 return hipErrorInvalidConfiguration;
 #define SA_LAUNCH16S(RR, SP)                                                                         \
     if (R == RR && split == SP) {                                                                    \
+        if constexpr (ALG == SA_SW && !SP) {                                                         \
+            if (v.cmax && v.so) {                                                                    \
+                hipLaunchKernelGGL((fill_kernel<ALG, RR, kMatchEq, true, LOCAL, true, true, SP, true>), dim3(grid), \
+                                   block, lds, stream, p);                                           \
+                return hipGetLastError();                                                            \
+            }                                                                                        \
+        }                                                                                            \
+        if (v.so) return hipErrorInvalidValue;                                                       \
         if constexpr (ALG == SA_SW) {                                                                \
             if (v.cmax) {                                                                            \
                 hipLaunchKernelGGL((fill_kernel<ALG, RR, kMatchEq, true, LOCAL, true, true, SP>), dim3(grid), \
@@ -1256,7 +1319,7 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
             SA_LAUNCH16S(4, true)
             SA_LAUNCH16S(8, true)
 #undef SA_LAUNCH16S
-            if (R == 1 && split && !v.cmax) {   // R = 1: the per-cell key (CMAX pairs rows)
+            if (R == 1 && split && !v.cmax && !v.so) {   // R = 1: the per-cell key (CMAX pairs rows)
                 hipLaunchKernelGGL((fill_kernel<ALG, 1, kMatchEq, true, LOCAL, true, false, true>), dim3(grid), block,
                                    lds, stream, p);
                 return hipGetLastError();
@@ -1294,7 +1357,7 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
             return hipErrorInvalidValue;
         }
     }
-    if (v.t16 || v.cmax) return hipErrorInvalidValue;
+    if (v.t16 || v.cmax || v.so) return hipErrorInvalidValue;
     const int mm = v.bits ? kMatchBits : lut ? kMatchLut : kMatchEq;
 #define SA_LAUNCH(RR, MMV, AA, KK)                                                             \
     if (R == RR && mm == MMV && allow == AA && keyed == KK) {                                  \

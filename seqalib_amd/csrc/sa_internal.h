@@ -122,6 +122,7 @@ struct EndcellParams {
     sa_result* res;
     uint32_t pair_base, count;
     int32_t gap, gap_open, gap_extend;
+    int hshift;                // SW: snapshots / chunk maxima / top rows hold H << hshift (2 tagged, 0 SO)
 };
 
 struct TbParams {
@@ -155,6 +156,14 @@ struct TbParams {
     int4* seg_rec;
     int4* seg_fin;
     int rerun;                 // the fallback launch: walks only the pairs flagged kFlagRerun
+    // score-only fills (sa_traceback_so.hip): the edge stream lives in dirs (band_stride bytes per
+    // band), the end-cell snapshots as FillParams, prof = the tagged T16 profile (prof[4] symbols)
+    uint64_t band_stride;
+    const uint32_t* snap_h;
+    const int32_t* snap_p;
+    uint64_t snap_h_slot, snap_p_slot;
+    uint32_t snap_nch;
+    const uint32_t* prof;
 };
 // SA_FLAG_TIMEOUT: a SPLIT band's bounded wait for its producer expired (results invalid)
 
@@ -166,6 +175,7 @@ struct FillVariant {
     int R;
     bool lut, allow, keyed, t16, cmax, split;
     bool bits = false;   // kMatchBits (then lut is ignored)
+    bool so = false;     // score-only T16 SW chunk-max fill (edge stream instead of records)
 };
 hipError_t launch_fill(int algo, const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream);
 hipError_t launch_fill_sw(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
@@ -226,4 +236,6 @@ hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStr
 // One wave per pair (sa_traceback_wave.hip): the few-pairs traceback.
 hipError_t launch_traceback_wave(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
 hipError_t launch_endcell(int algo, int R, const EndcellParams& p, hipStream_t stream);
+// Score-only SW fills: the block-recompute traceback (sa_traceback_so.hip), R in {4, 8, 16, 32}.
+hipError_t launch_traceback_so(int R, const TbParams& p, hipStream_t stream);
 }  // namespace sa

@@ -1,0 +1,304 @@
+// sa_traceback_so.hip — buildResult of SmithWatermanSA (SASmithWaterman.h:220-339) after a
+// SCORE-ONLY fill (sa_fill_impl.h, SO): the fill stored no per-cell records, so the walk recomputes
+// the move tags of the cells it visits, block by block, from what the fill did store:
+//   * the per-chunk snapshots (every lane's R row values entering chunk c, and its diagonal input),
+//   * the edge stream (every lane's last row at every step of its band, 16 bits per lane-step).
+// Block (band b, lane t, chunk c) = rows r0 .. r0+R-1 (r0 = b*64R + t*R) x columns j0 .. j0+31
+// (j0 = 32c - t, 0-based), the cells lane t computed during chunk c.  Its left column (j0 - 1) is
+// lane t's snapshot of chunk c-1, its corner the snapshot's diagonal input, its top row the edge
+// stream of the lane above (lane t-1 computed column j at step j + t - 1; for t = 0, lane 63 of
+// band b-1, at step j + 63).  The recompute runs the fill's tagged 16-bit cell (4H + tag, one
+// v_max_i16 chain gives value and move with the reference's tie order diag > up > left), so the
+// tags are exactly those the tagged fill would have stored (sa_traceback.hip reads those).
+//
+// The walk only moves up and left, so once it leaves a block it never returns, and inside a block
+// it needs only the rows above and the columns left of the cell it entered at: the recompute stops
+// at the entry column.  One lane per pair (64 pairs per wave); lanes whose next move leaves their
+// block park, and when every unfinished lane is parked they all recompute together (as
+// sa_traceback.hip batches its window refills).  The tags of a block live in LDS, item-major.
+#include <limits.h>
+
+#include "sa_internal.h"
+
+namespace sa {
+
+typedef const void __attribute__((address_space(1)))* so_gptr;
+typedef void __attribute__((address_space(3)))* so_lptr;
+
+// LDS per wave (bytes), words item-major ([item][lane], 256 B per item):
+//   tags      32 columns x RT words (RT = ceil(2R / 32)): column q, word w at item q * RT + w
+//   edge      5 packets of 16 B (the top row's 32 steps), lane t's packet k at k * 1024 + 16 * lane
+//   codes     R row codes then 32 column codes (8 * code, one byte each)
+//   ops       kSoOps op bytes per lane per round
+constexpr int kSoOps = 64;
+template <int R>
+struct SoLds {
+    static constexpr int RT = (2 * R + 31) / 32;
+    static constexpr int kTags = 0;
+    static constexpr int kEdge = kTags + 32 * RT * 256;
+    static constexpr int kRowCodes = kEdge + 5 * 1024;
+    static constexpr int kColCodes = kRowCodes + ((R + 3) / 4) * 256;
+    static constexpr int kOps = kColCodes + 8 * 256;
+    static constexpr int kBytes = kOps + kSoOps * 64;
+};
+
+__device__ __forceinline__ uint32_t so_code8(uint32_t sp, uint32_t b) {
+    return (b == ((sp >> 8) & 255u) ? 8u : 0u) | (b == ((sp >> 16) & 255u) ? 16u : 0u) |
+           (b == (sp >> 24) ? 24u : 0u);
+}
+
+template <int R>
+__global__ __launch_bounds__(64) void traceback_so_kernel(TbParams P) {
+    using L = SoLds<R>;
+    constexpr int RT = L::RT;
+    constexpr int BAND = kWave * R;
+    __shared__ __attribute__((aligned(16))) uint8_t s_so[L::kBytes];
+    typedef volatile uint8_t __attribute__((address_space(3))) lds_u8;
+    typedef volatile uint32_t __attribute__((address_space(3))) lds_u32;
+    typedef volatile uint16_t __attribute__((address_space(3))) lds_u16;
+    lds_u8* const vb = (lds_u8*)s_so;
+    lds_u32* const vw = (lds_u32*)s_so;
+    const int lane = threadIdx.x;
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= P.count) return;
+    const uint32_t pidx = P.pair_base + slot;
+    sa_result res = P.res[pidx];
+    if (res.flags & SA_FLAG_BAD_SHAPE) return;
+    if (!tb_mine(P, res.flags)) return;
+    res.flags &= ~(kFlagRetry | kFlagRedo | kFlagRerun);
+    const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
+    const int m = (int)(P.off1[pidx + 1] - o1);
+    const int n = (int)(P.off2[pidx + 1] - o2);
+    const uint8_t* s1 = P.seq1 + o1;
+    const uint8_t* s2 = P.seq2 + o2;
+    typedef uint8_t __attribute__((address_space(1))) glb_u8;
+    glb_u8* ops = (glb_u8*)(P.ops + o1 + o2 + pidx);
+    const uint8_t* const dir = P.dirs + (uint64_t)slot * P.dir_slot;
+    const uint64_t band_stride = P.band_stride;
+    const uint32_t npk = (uint32_t)(band_stride / (kWave * 16));   // edge packets per band
+    const uint32_t* const sh_base = P.snap_h + (uint64_t)slot * P.snap_h_slot;
+    const int32_t* const sp_base = P.snap_p + (uint64_t)slot * P.snap_p_slot;
+    const uint32_t snap_nch = P.snap_nch;
+    // the batch alphabet (T16: <= 4 symbols): tagged profile words 4s + 3 by row code, the symbols,
+    // and match(code a, code b) as a 16-bit table (the user's match function, or equality)
+    const uint32_t symp = P.prof[4];
+    const uint32_t pf0 = P.prof[0], pf1 = P.prof[1], pf2 = P.prof[2], pf3 = P.prof[3];
+    uint32_t mt = 0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t sa_ = (symp >> (8 * a)) & 255u, sb_ = (symp >> (8 * b)) & 255u;
+            const bool v = P.lutbits ? ((P.lutbits[(sa_ << 3) | (sb_ >> 5)] >> (sb_ & 31u)) & 1u) != 0 : sa_ == sb_;
+            mt |= (v ? 1u : 0u) << (a * 4 + b);
+        }
+    const bool allow = P.allow != 0;
+    const int G = P.gap, MA = P.match, MI = P.mismatch;
+    const uint32_t CU = (uint32_t)(-(4 * G + 2)) & 0xffffu;   // up: max(4U + 2, 0) by saturation
+    const uint32_t CL = (uint32_t)(4 * G + 1) & 0xffffu;      // left: 4L + 1
+
+    uint32_t k = 0, k0 = 0;   // ops emitted / already written to HBM
+    auto emit = [&](uint8_t op) __attribute__((always_inline)) {
+        const uint32_t q = k - k0;
+        vb[L::kOps + (q >> 2) * 256 + lane * 4 + (q & 3)] = op;
+        ++k;
+    };
+    auto flush = [&]() __attribute__((always_inline)) {
+        for (uint32_t q = 0; q < k - k0; ++q) ops[k0 + q] = vb[L::kOps + (q >> 2) * 256 + lane * 4 + (q & 3)];
+        k0 = k;
+    };
+
+    // ------------------------------------------------------------------ blocks
+    int wb = -1, wt = 0, wc = 0;     // current block (band, lane, chunk)
+    int cb = 0, ct = 0, cc = 0, cr = 0, cq = 0;   // cell located by locate(): block, row, column
+    auto locate = [&](int i, int j) __attribute__((always_inline)) {
+        const int ii = i - 1;
+        cb = ii / BAND;
+        const int rem = ii - cb * BAND;
+        ct = rem / R;
+        cr = rem - ct * R;
+        const int s = j - 1 + ct;
+        cc = s >> 5;
+        cq = s & 31;
+    };
+    auto ready = [&](int i, int j) __attribute__((always_inline)) -> bool {
+        if (k - k0 >= (uint32_t)kSoOps) return false;
+        if (!(i > 0 && j > 0)) return true;
+        locate(i, j);
+        return cb == wb && ct == wt && cc == wc;
+    };
+    // recompute the tags of the block holding (i, j), columns up to j
+    auto recompute = [&](int i, int j) __attribute__((always_inline)) {
+        if (!(i > 0 && j > 0)) return;
+        locate(i, j);
+        wb = cb; wt = ct; wc = cc;
+        const int r0 = cb * BAND + ct * R;
+        const int j0 = 32 * cc - ct;
+        // the top row: edge stream of lane tp of band bp, steps j + tp for j in [j0, j0 + 32)
+        const bool has_top = !(cb == 0 && ct == 0);
+        const int bp = ct > 0 ? cb : cb - 1, tp = ct > 0 ? ct - 1 : kWave - 1;
+        const int slo = j0 + tp;                 // 32c - 1 (t > 0) or 32c + 63 (t = 0): step of column j0
+        const int pk0 = slo >> 3;                // (arithmetic: -1 for slo = -1) first packet of the row
+        if (has_top) {
+            const uint8_t* base = dir + (uint64_t)bp * band_stride;
+#pragma unroll
+            for (int d = 0; d < 5; ++d) {        // steps slo .. slo + 31 lie in 5 packets of 8
+                const int pk = pk0 + d;
+                if (pk >= 0 && (uint32_t)pk < npk)
+                    __builtin_amdgcn_global_load_lds((so_gptr)(base + ((uint64_t)pk * kWave + tp) * 16),
+                                                     (so_lptr)(s_so + L::kEdge + d * 1024), 16, 0, 0);
+            }
+        }
+        // left column (lane t entering chunk c) and corner: the snapshot of chunk c - 1, or the
+        // matrix border (0) when the block starts at column 0 or before
+        int Hp[R];
+        int corner = 0;
+        const bool has_left = cc > 0 && j0 >= 1;
+        if (has_left) {
+            const uint64_t e = (uint64_t)cb * snap_nch + (cc - 1);
+            const uint32_t* sh = sh_base + e * (R / 2) * kWave + ct;
+#pragma unroll
+            for (int q = 0; q < R / 2; ++q) {
+                const uint32_t w = sh[q * kWave];
+                Hp[2 * q] = (int)(w & 0xffffu) << 2;
+                Hp[2 * q + 1] = (int)(w >> 16) << 2;
+            }
+            if (r0 > 0) corner = (sp_base[e * kWave + ct] & 0xffff) << 2;
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) Hp[r] = 0;
+        }
+        // row profiles and codes
+        uint32_t tab[R];
+#pragma unroll
+        for (int r = 0; r < R; r += 4) {
+            uint32_t cw = 0;
+#pragma unroll
+            for (int e = 0; e < 4 && r + e < R; ++e) {
+                const int row = r0 + r + e;
+                const uint32_t c8 = row < m ? so_code8(symp, s1[row]) : 0u;
+                tab[r + e] = c8 == 0 ? pf0 : c8 == 8 ? pf1 : c8 == 16 ? pf2 : pf3;
+                cw |= c8 << (8 * e);
+            }
+            vw[(L::kRowCodes >> 2) + (r >> 2) * 64 + lane] = cw;
+        }
+        const int qlo = j0 < 0 ? -j0 : 0;
+        const int qhi = j - 1 - j0;              // the entry column
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            uint32_t cw = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int q = 4 * w + e, jj = j0 + q;
+                cw |= (q >= qlo && q <= qhi && jj < n ? so_code8(symp, s2[jj]) : 0u) << (8 * e);
+            }
+            vw[(L::kColCodes >> 2) + w * 64 + lane] = cw;
+        }
+        // the edge DMA writes LDS behind the compiler's back: wait for it, keep reads after this
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int prev_top = corner;                   // 4 * H(r0 - 1, j0 + q - 1)
+        for (int q = qlo; q <= qhi; ++q) {
+            int top = 0;
+            if (has_top) {
+                const int s = slo + q;           // >= 0 here (q >= qlo)
+                const int d = (s >> 3) - pk0;
+                top = (int)((lds_u16*)(s_so + L::kEdge + d * 1024 + lane * 16 + (s & 7) * 2))[0] << 2;
+            }
+            const uint32_t sym = (vw[(L::kColCodes >> 2) + (q >> 2) * 64 + lane] >> (8 * (q & 3))) & 255u;
+            uint32_t dcur;
+            asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(dcur) : "v"(tab[0]), "v"(sym), "v"(prev_top));
+            uint32_t hu = (uint32_t)top;
+            uint32_t rec = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                uint32_t t0, t1;
+                if (r + 1 < R) {
+                    uint32_t dn;
+                    asm("v_add_u16 %[t0], %[cl], %[hp]\n\t"
+                        "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\t"
+                        "v_add_u16 %[dn], %[hp], %[dn]\n\t"
+                        "v_sub_u16_e64 %[t1], %[hu], %[cu] clamp\n\t"
+                        "v_max_i16 %[t0], %[dr], %[t0]\n\t"
+                        "v_max_i16 %[t0], %[t1], %[t0]\n\t"
+                        "v_and_b32 %[hp], -4, %[t0]\n\t"
+                        "v_alignbit_b32 %[rec], %[t0], %[rec], 2"
+                        : [t0] "=&v"(t0), [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r]), [rec] "+v"(rec)
+                        : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL),
+                          [tabn] "v"(tab[r + 1 < R ? r + 1 : r]), [sym] "v"(sym));
+                    dcur = dn;
+                } else {
+                    asm("v_add_u16 %[t0], %[cl], %[hp]\n\t"
+                        "v_sub_u16_e64 %[t1], %[hu], %[cu] clamp\n\t"
+                        "v_max_i16 %[t0], %[dr], %[t0]\n\t"
+                        "v_max_i16 %[t0], %[t1], %[t0]\n\t"
+                        "v_and_b32 %[hp], -4, %[t0]\n\t"
+                        "v_alignbit_b32 %[rec], %[t0], %[rec], 2"
+                        : [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r]), [rec] "+v"(rec)
+                        : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL));
+                }
+                hu = (uint32_t)Hp[r];
+                if ((r & 15) == 15 || r == R - 1) {
+                    // 16 rows per word, row r at bits 2 (r % 16) (alignbit fills from the top)
+                    const uint32_t wv = (r & 15) == 15 ? rec : rec >> (32 - 2 * ((r & 15) + 1));
+                    vw[(q * RT + (r >> 4)) * 64 + lane] = wv;
+                    rec = 0;
+                }
+            }
+            prev_top = top;
+        }
+    };
+    auto tag = [&]() __attribute__((always_inline)) -> uint32_t {
+        return (vw[(cq * RT + (cr >> 4)) * 64 + lane] >> (2 * (cr & 15))) & 3u;
+    };
+    auto cell_match = [&]() __attribute__((always_inline)) -> bool {
+        const uint32_t a = (vb[L::kRowCodes + (cr >> 2) * 256 + lane * 4 + (cr & 3)] >> 3) & 3u;
+        const uint32_t b = (vb[L::kColCodes + (cq >> 2) * 256 + lane * 4 + (cq & 3)] >> 3) & 3u;
+        return ((mt >> (a * 4 + b)) & 1u) != 0;
+    };
+
+    // ------------------------------------------------------------------ walk (as sa_traceback.hip)
+    int i = res.end_i, j = res.end_j, V = res.score;
+    if (m == 0 || n == 0) { i = 0; j = 0; }
+    bool fin = false, parked = true;
+    for (;;) {
+        if (__builtin_amdgcn_ballot_w64(!fin && !parked) == 0) {
+            if (__builtin_amdgcn_ballot_w64(!fin) == 0) break;
+            if (!fin) { flush(); recompute(i, j); parked = false; }
+        }
+        if (!fin && !parked) {
+            if (!(i > 0 && j > 0) || V == 0) {   // SASmithWaterman.h: stop on an edge or at H == 0
+                fin = true;
+            } else if (!ready(i, j)) {
+                parked = true;
+            } else {
+                const uint32_t f = tag();
+                const bool dg = f == 3u, up = f == 2u;
+                const bool v = dg && cell_match();
+                emit(dg ? (v ? 'M' : (allow ? 'S' : 'X')) : (up ? 'U' : 'L'));
+                V -= dg ? (v ? MA : MI) : G;
+                i -= (dg || up) ? 1 : 0;
+                j -= up ? 0 : 1;
+            }
+        }
+    }
+    flush();
+    res.start_i = i;
+    res.start_j = j;
+    res.nops = k;
+    P.res[pidx] = res;
+}
+
+hipError_t launch_traceback_so(int R, const TbParams& p, hipStream_t stream) {
+    const dim3 block(64);
+    const dim3 grid((p.count + 63) / 64);
+    switch (R) {
+        case 4: hipLaunchKernelGGL(traceback_so_kernel<4>, grid, block, 0, stream, p); break;
+        case 8: hipLaunchKernelGGL(traceback_so_kernel<8>, grid, block, 0, stream, p); break;
+        case 16: hipLaunchKernelGGL(traceback_so_kernel<16>, grid, block, 0, stream, p); break;
+        case 32: hipLaunchKernelGGL(traceback_so_kernel<32>, grid, block, 0, stream, p); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace sa

@@ -1,0 +1,162 @@
+"""Score-only Smith-Waterman fill + block-recompute traceback (sa_fill_impl.h SO,
+seqalib_amd/csrc/sa_traceback_so.hip) against the tagged-record path and the pinned oracle.
+
+The score-only fill stores no per-cell records; its traceback recomputes, block by block along the
+path, the move tags the tagged fill would have stored, from the per-chunk snapshots and the edge
+stream (each lane's last row per step).  Every test runs the same batch twice -- score-only (the
+default for T16 SW batches of >= 1,024 pairs) and SEQALIB_SO=0 (tagged records, the round-3 path)
+-- and requires every pair's result and op stream to be identical, then checks a sample against the
+oracle (itself pinned to the reference's golden vectors, tests/test_oracle_golden.py).
+Reference semantics: SASmithWaterman.h:89-117 (fill; last row-major maximum :110), :220-339
+(traceback).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import seqalib_amd as sa
+from util import linear_rescore, oracle_align, oracle_batch, oracle_sw_scores, subset
+
+pytestmark = pytest.mark.gpu
+
+SW = (-1, 1, -1)   # SmithWatermanSA::getDefaultScoring (SASmithWaterman.h:352)
+THREADS = 16
+FIELDS = ("score", "end_i", "end_j", "start_i", "start_j", "nops", "flags")
+
+
+def run(engine, so, *batch, scoring=SW, lut=None):
+    old = os.environ.get("SEQALIB_SO")
+    os.environ["SEQALIB_SO"] = "1" if so else "0"
+    try:
+        res, ops = engine.align_packed(0, sa.ScoringSystem(*scoring), *batch, lut=lut)
+        plan = engine.last_plan()
+    finally:
+        if old is None:
+            del os.environ["SEQALIB_SO"]
+        else:
+            os.environ["SEQALIB_SO"] = old
+    return res.copy(), ops.copy(), plan
+
+
+def assert_same(a, b, o1, o2):
+    ra, oa, _ = a
+    rb, ob, _ = b
+    for f in FIELDS:
+        bad = np.nonzero(ra[f] != rb[f])[0]
+        assert len(bad) == 0, (f, [(int(p), int(ra[f][p]), int(rb[f][p])) for p in bad[:5]])
+    n = len(ra)
+    starts = o1[:n].astype(np.int64) + o2[:n].astype(np.int64) + np.arange(n)
+    for p in range(n):
+        s, k = int(starts[p]), int(ra["nops"][p])
+        if oa[s:s + k].tobytes() != ob[s:s + k].tobytes():
+            raise AssertionError(f"op stream of pair {p} differs")
+
+
+def ragged_batch(seed, npairs, maxlen):
+    """Random DNA pairs of ragged lengths in [0, maxlen], with the edge shapes forced in, and one
+    pair in four a mutated copy of its partner (long local paths that cross many blocks)."""
+    rng = np.random.default_rng(seed)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    pairs = []
+    fixed = [(maxlen, maxlen), (1, maxlen), (maxlen, 1), (0, 5), (5, 0), (63, 64), (64, 63), (65, 65),
+             (maxlen, 33), (33, maxlen), (maxlen - 1, maxlen)]
+    for p in range(npairs):
+        if p < len(fixed):
+            m, n = fixed[p]
+        else:
+            m, n = int(rng.integers(0, maxlen + 1)), int(rng.integers(0, maxlen + 1))
+        a = acgt[rng.integers(0, 4, m)]
+        if p % 4 == 3 and m > 0 and n > 0:
+            b = a.copy()
+            mut = rng.random(len(b)) < 0.08
+            b[mut] = acgt[rng.integers(0, 4, int(mut.sum()))]
+            keep = rng.random(len(b)) > 0.03              # deletions
+            b = b[keep]
+            ins = np.nonzero(rng.random(len(b)) < 0.03)[0]   # insertions
+            b = np.insert(b, ins, acgt[rng.integers(0, 4, len(ins))])[:n]
+        else:
+            b = acgt[rng.integers(0, 4, n)]
+        pairs.append((a.tobytes(), b.tobytes()))
+    o1 = np.zeros(npairs + 1, np.uint64)
+    o2 = np.zeros(npairs + 1, np.uint64)
+    o1[1:] = np.cumsum([len(a) for a, _ in pairs])
+    o2[1:] = np.cumsum([len(b) for _, b in pairs])
+    s1 = np.frombuffer(b"".join(a for a, _ in pairs), np.uint8).copy()
+    s2 = np.frombuffer(b"".join(b for _, b in pairs), np.uint8).copy()
+    return s1, o1, s2, o2
+
+
+@pytest.mark.parametrize("maxlen,R", [(200, 4), (500, 8), (1000, 16), (2000, 32), (3000, 32)])
+def test_so_ragged_matches_tagged_and_oracle(engine, maxlen, R):
+    """Ragged batches on every score-only plan (R = 4 .. 32, one and two bands): identical to the
+    tagged path on every pair, and to the full-matrix oracle on a sample."""
+    batch = ragged_batch(40 + maxlen, 1100, maxlen)
+    so = run(engine, True, *batch)
+    tg = run(engine, False, *batch)
+    assert so[2] == (sa.SA_KERNEL_T16_ENDCELL, R, 1) and tg[2] == so[2]
+    s1, o1, s2, o2 = batch
+    assert (so[0]["flags"] == 0).all()
+    assert_same(so, tg, o1, o2)
+    assert (linear_rescore(SW, so[0], so[1], o1, o2) == so[0]["score"]).all()
+    idx = np.sort(np.random.default_rng(maxlen).choice(len(o1) - 1, 48, replace=False))
+    idx = np.unique(np.concatenate([np.arange(11), idx]))
+    sub = subset(s1, o1, s2, o2, idx)
+    ores, oops = oracle_batch(0, SW, *sub, threads=THREADS)
+    for q, p in enumerate(idx):
+        off = int(o1[p] + o2[p]) + int(p)
+        ooff = int(sub[1][q] + sub[3][q]) + q
+        got = tuple(int(so[0][f][p]) for f in ("score", "end_i", "end_j", "start_i", "start_j"))
+        exp = tuple(int(ores[f][q]) for f in ("score", "end_i", "end_j", "start_i", "start_j"))
+        assert got == exp, (int(p), got, exp)
+        assert so[1][off:off + int(so[0]["nops"][p])].tobytes() == oops[ooff:ooff + int(ores["nops"][q])].tobytes(), int(p)
+
+
+def test_so_scorings_and_lut(engine):
+    """Other scorings (match 2, mismatch -3, gap -2; !AllowMismatch) and a non-identity match table
+    on a 4-symbol alphabet (A~G, C~T): identical to the tagged path; a sample against the oracle."""
+    batch = ragged_batch(7, 1030, 700)
+    s1, o1, s2, o2 = batch
+    lut = np.zeros((256, 256), np.uint8)
+    for x in b"ACGT":
+        lut[x, x] = 1
+    for x, y in (b"AG", b"GA", b"CT", b"TC"):
+        lut[x, y] = 1
+    for scoring, lt in (((-2, 2, -3), None), ((-2, 1, -1, False), None), (SW, lut)):
+        so = run(engine, True, *batch, scoring=scoring, lut=lt)
+        tg = run(engine, False, *batch, scoring=scoring, lut=lt)
+        assert so[2][0] == sa.SA_KERNEL_T16_ENDCELL, scoring
+        assert_same(so, tg, o1, o2)
+        for p in (0, 1, 2, 3, 11, 12, 13, 14, 15, 1029):
+            a, b = s1[o1[p]:o1[p + 1]].tobytes(), s2[o2[p]:o2[p + 1]].tobytes()
+            o = oracle_align(0, scoring, a, b, lut=lt)
+            off = int(o1[p] + o2[p]) + p
+            got = (int(so[0]["score"][p]), int(so[0]["end_i"][p]), int(so[0]["end_j"][p]),
+                   so[1][off:off + int(so[0]["nops"][p])].tobytes())
+            assert got == (o["score"], o["end_i"], o["end_j"], o["ops"]), (scoring, p)
+
+
+def test_headline_batch_every_pair(engine):
+    """The bench workload itself (bench.py: seed base 1e10, 10,000 x 4096^2, (-1, 1, -1),
+    equal<char>): all 10,000 (MaxScore, MaxRow, MaxCol) against the linear-space oracle, 256 full op
+    streams against the full-matrix oracle, every op stream identical to the tagged path."""
+    s1, o1, s2, o2 = sa.synth_dna_batch(10 ** 10, 10000, 4096, 4096, threads=THREADS)
+    so = run(engine, True, s1, o1, s2, o2)
+    assert so[2] == (sa.SA_KERNEL_T16_ENDCELL, 32, 1)
+    res, ops = so[0], so[1]
+    assert (res["flags"] == 0).all()
+    assert (linear_rescore(SW, res, ops, o1, o2) == res["score"]).all()
+    exp = oracle_sw_scores(SW, s1, o1, s2, o2, threads=THREADS)
+    got = np.stack([res["score"], res["end_i"], res["end_j"]], axis=1)
+    bad = np.nonzero((got != exp).any(axis=1))[0]
+    assert len(bad) == 0, [(int(b), got[b].tolist(), exp[b].tolist()) for b in bad[:5]]
+    jdx = np.sort(np.random.default_rng(10).choice(10000, 256, replace=False))
+    sub = subset(s1, o1, s2, o2, jdx)
+    ores, oops = oracle_batch(0, SW, *sub, threads=THREADS)
+    for q, p in enumerate(jdx):
+        off = int(o1[p] + o2[p]) + int(p)
+        ooff = int(sub[1][q] + sub[3][q]) + q
+        assert (int(res["start_i"][p]), int(res["start_j"][p])) == (int(ores["start_i"][q]), int(ores["start_j"][q]))
+        assert ops[off:off + int(res["nops"][p])].tobytes() == oops[ooff:ooff + int(ores["nops"][q])].tobytes(), int(p)
+    tg = run(engine, False, s1, o1, s2, o2)
+    assert_same(so, tg, o1, o2)
