@@ -36,13 +36,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 METRIC = "GCUPS (DP cell updates/s) on batched 4k×4k SW; bit-exact score match"
 SEED_BASE = 10 ** 10          # workload "T" seed base (config id x 1e9 convention)
 SCORING = (-1, 1, -1)         # SmithWatermanSA::getDefaultScoring (SASmithWaterman.h:352)
-# The fill kernel is VALU-issue bound.  Its roofline peak is the issue ceiling of the steady
-# loop's own instruction mix, every opcode priced at its measured gfx950 issue rate
-# (tools/issue_model.py -> ISSUE_MODEL, rates from profiles/microbench_valu_issue_r01.txt).
+# The fill kernel is VALU-issue bound.  Its VALU instructions per cell come from an ISA count of
+# the steady chunk loop (tools/issue_model.py -> ISSUE_MODEL).
 ISSUE_MODEL = os.path.join(ROOT, "profiles", "issue_model_r04.json")
-# Register-only cell-level measurement of the same instruction mix (tools/microbench_cellmix.hip,
-# variant V8 = the shipped T16 end-cell cell): what the mix really issues at, no memory traffic.
-CELL_MIX_CEILING = {"sw_t16c_r32": (5677.8, "profiles/microbench_cellmix_r01.txt (V8, 3 waves/SIMD as the fill runs)")}
 HBM_PEAK_GBPS = 8000.0
 # VALU peak of the guide (/opt/skills/guides/MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 VALU
 # instruction issues over 2 cycles, 2400 MHz max clock): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz.
@@ -74,6 +70,12 @@ def parse():
                     help="run steps back to back without overlapping step k's traceback with step k+1's fill")
     ap.add_argument("--serial-steps", type=int, default=3,
                     help="after the timed run, also time this many non-pipelined steps (reported, not the value)")
+    ap.add_argument("--configs", default="2,3,4,5",
+                    help="BASELINE.json configs measured after the headline (tools/bench_configs.py); '' = none")
+    ap.add_argument("--parity-ops", type=int, default=16,
+                    help="headline parity: full op streams checked against the full-matrix oracle "
+                         "(every pair's end cell is always checked)")
+    ap.add_argument("--latency-reps", type=int, default=200, help="drop-in single-call latency leg (0 = skip)")
     return ap.parse_args()
 
 
@@ -198,14 +200,46 @@ def dropin_e2e(args):
         return {"error": str(e)[:200]}
 
 
-def load_pmc_traffic(workload: str):
-    """HBM bytes per fill launch measured by rocprofv3 --pmc (profiles/pmc_traffic.json, written
-    by tools/profile.sh from separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected)."""
+def dropin_latency(args):
+    """Single-call latency of the C++ drop-in (tests/cpp/dropin_latency: getAlignment per call on
+    test/Test.cpp's 11 x 8 NW pair and on one 1024^2 SW pair), beside the reference's own per-call
+    time (oracle/_ref ref_call_ns: construct the aligner + getAlignment, as include/Test.cpp:98-107
+    times it, 1 thread)."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "cpp", "dropin_latency")
+    if args.latency_reps <= 0 or not os.path.exists(exe):
+        return None
+    try:
+        out = subprocess.run([exe, str(args.latency_reps)], capture_output=True, text=True, timeout=300,
+                             check=True).stdout
+        d = json.loads(out.strip().splitlines()[-1])
+    except Exception as e:   # reported, never fatal for the bench line
+        return {"error": str(e)[:200]}
+    ref = os.path.join(ROOT, "oracle", "_ref", "libsaref.so")
+    if os.path.exists(ref):
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from bench_configs import ref_lib
+        import seqalib_amd as sa
+        L = ref_lib()
+        a, b = b"AAAGAATGCAT", b"AAACTCAT"
+        d["nw_11x8"]["reference_us"] = round(L.ref_call_ns(1, 2, -1, 2, 0, 0, a, len(a), b, len(b), 20000) / 1e3, 3)
+        x, y = sa.synth_dna(1_000_000_001, 1024), sa.synth_dna(1_000_000_002, 1024)
+        d["sw_1024x1024"]["reference_us"] = round(L.ref_call_ns(0, 3, -1, 1, -1, 1, x, 1024, y, 1024, 5) / 1e3, 1)
+        d["reference_basis"] = ("oracle/_ref ref_call_ns: SmithWatermanSA / NeedlemanWunschSA constructed + "
+                                "getAlignment per call, 1 thread, mean")
+    return d
+
+
+def load_pmc(workload: str, label: str):
+    """PMC figures of the shipped fill kernel (profiles/pmc_traffic.json, written by
+    tools/pmc_roofline.py from separate rocprofv3 --pmc passes): HBM bytes per fill launch
+    (FETCH_SIZE / WRITE_SIZE, gfx950-corrected) and the shader clock during the fill
+    (GRBM_GUI_ACTIVE / 8 XCDs / duration).  Entries are keyed by workload and kernel label, so a
+    record of another kernel is never reported for this one."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        d = json.load(open(path))
-        e = d.get(workload)
-        return None if e is None else float(e["hbm_bytes_per_launch"])
+        e = json.load(open(path)).get(workload)
+        return e if e is not None and e.get("label") == label else None
     except Exception:
         return None
 
@@ -292,64 +326,63 @@ def main():
     cells_rank = float(P) * Lq * Lq
     value = world * cells_rank * args.steps / elapsed / 1e9
     ms_per_step = elapsed / args.steps * 1e3
+    kernel, plan_R, plan_W, records = eng.last_plan_ex()
 
-    # parity spot check of this step's output (outside the timed region)
-    from util import oracle_align
+    # parity of this rank's batch, outside the timed region: every pair's (MaxScore, MaxRow, MaxCol)
+    # against the linear-space oracle, every alignment re-scored to the reported maximum, and
+    # --parity-ops full op streams against the full-matrix oracle (tools/bench_configs.py)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from bench_configs import parity_sw_batch
     res = np.frombuffer(d_res[last].cpu().numpy().tobytes(), dtype=sa.RESULT_DTYPE)
     ops = d_ops[last].cpu().numpy()
-    bad = int(np.count_nonzero(res["flags"]))
-    checked = 0
-    diffs = []
-    for p in (0, P - 1):
-        a, b = s1[o1[p]:o1[p + 1]].tobytes(), s2[o2[p]:o2[p + 1]].tobytes()
-        o = oracle_align(0, SCORING, a, b)
-        off = int(o1[p] + o2[p]) + p
-        got = (int(res["score"][p]), int(res["end_i"][p]), int(res["end_j"][p]),
-               ops[off:off + int(res["nops"][p])].tobytes())
-        if got != (o["score"], o["end_i"], o["end_j"], o["ops"]):
-            bad += 1
-            diffs.append({"pair": int(p), "got": list(got[:3]) + [len(got[3])], "want": [o["score"], o["end_i"], o["end_j"], len(o["ops"])],
-                          "first_op_diff": next((i for i, (x, y) in enumerate(zip(got[3], o["ops"])) if x != y), -1)})
-        checked += 1
+    cores = host_cores()["usable"]
+    par = parity_sw_batch(s1, o1, s2, o2, res, ops, args.parity_ops, cores, 10)
+    configs = None
+    if rank == 0 and world == 1 and args.configs:
+        from bench_configs import measure
+        eng.set_pipeline(False)
+        configs = measure(sa, torch, eng, dev, set(args.configs.split(",")), cores)
 
     if args.rank_out:
         os.makedirs(args.rank_out, exist_ok=True)
         with open(os.path.join(args.rank_out, f"rank{rank}.json"), "w") as f:
             json.dump({"rank": rank, "world": world, "own_s": own, "max_s": elapsed, "seed_base": shard_seed_base(rank, world, P),
-                       "checked": checked, "bad": bad, "flags": int(np.count_nonzero(res["flags"])), "diffs": diffs,
-                       "plan": list(eng.last_plan())}, f)
+                       "parity": par, "flags": int(np.count_nonzero(res["flags"])), "plan": list(eng.last_plan())}, f)
     if rank != 0:
         return
     per_launch_cells = cells_rank  # one fill launch covers the whole batch when it fits HBM
     fill_s = fill_ms / 1e3 / max(launches, 1)
     t16 = kernel in (sa.SA_KERNEL_T16, sa.SA_KERNEL_T16_ENDCELL)
     endcell = kernel == sa.SA_KERNEL_T16_ENDCELL
-    label = f"sw_{'t16c' if endcell else 't16' if t16 else 'int32'}_r{plan_R}"
+    so = records == sa.SA_RECORDS_SCORE_ONLY
+    label = f"sw_{'so' if so else 't16c' if endcell else 't16' if t16 else 'int32'}_r{plan_R}"
     model = issue_model(label)
     fill_gcups = per_launch_cells / fill_s / 1e9
-    # algorithmic HBM bytes per cell: 2 traceback bits, plus the end-cell snapshots (64 lanes x
-    # (R/2 + 1) words per 32-step chunk of a band = (R/2+1)*4 / (32*R) B per cell)
-    bytes_per_cell = SW_FLAG_BYTES_PER_CELL + ((plan_R // 2 + 1) * 4 / (32 * plan_R) if endcell else 0.0)
+    # algorithmic HBM bytes per cell: score-only fill -- the edge stream (16 bits per lane-step =
+    # 2/R B per cell), the end-cell snapshots ((R/2 + 1) words per lane per 32-step chunk) and the
+    # chunk maxima (1 word per lane-chunk); tagged fill -- 2 record bits per cell + the snapshots
+    snap = (plan_R // 2 + 1) * 4 / (32 * plan_R) if endcell else 0.0
+    bytes_per_cell = (2.0 / plan_R + snap + 4 / (32 * plan_R)) if so else (SW_FLAG_BYTES_PER_CELL + snap)
     hbm_gbps = per_launch_cells * bytes_per_cell / fill_s / 1e9
-    traffic = load_pmc_traffic(workload)
-    kname = (f"fill_kernel<SW,R={plan_R},W={plan_W}," + ("T16 tagged int16 profile" if t16 else "int32 flags")
+    pmc = load_pmc(workload, label)
+    kname = ("fill_so_kernel<R=%d> (score-only T16, chunk-max end cell, 4 waves/SIMD)" % plan_R if so else
+             f"fill_kernel<SW,R={plan_R},W={plan_W}," + ("T16 tagged int16 profile" if t16 else "int32 flags")
              + (",chunk-max end cell>" if endcell else ",KEYED>"))
-    # achieved = fill cells/s x ISA-counted VALU instructions per cell (each lane computes its own
-    # cells, so lane-instructions); peak = the guide's VALU issue peak (VALU_PEAK_TLANE)
+    # achieved = fill cells/s x ISA-counted VALU instructions per cell of the steady loop (each lane
+    # computes its own cells, so lane-instructions); peak = the guide's VALU issue peak at 2.4 GHz
     vpc = model["valu_per_cell"] if model else None
     achieved = fill_gcups * vpc / 1e3 if vpc else None
     roof = {"bound": "valu", "achieved": round(achieved, 2) if achieved else None, "peak": round(VALU_PEAK_TLANE, 2),
-            "unit": "T lane-instr/s", "frac": round(achieved / VALU_PEAK_TLANE, 4) if achieved else None}
-    roof.update({"traffic": traffic, "kernel": kname, "avg_launch_ms": round(fill_ms / max(launches, 1), 3),
+            "unit": "T lane-instr/s", "frac": round(achieved / VALU_PEAK_TLANE, 4) if achieved else None,
+            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None}
+    clk = pmc.get("clock_ghz") if pmc else None
+    roof.update({"kernel": kname, "avg_launch_ms": round(fill_ms / max(launches, 1), 3),
                  "fill_gcups": round(fill_gcups, 1), "valu_per_cell": vpc,
+                 "valu_per_cell_basis": f"ISA count of the steady chunk loop (tools/issue_model.py, {os.path.relpath(ISSUE_MODEL, ROOT)})",
                  "peak_basis": "MI355X_MICROARCH.md: 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz (wave64 VALU op = 2 cycles)",
-                 "issue_ceiling_gcups": model["peak_gcups"] if model else None,
-                 "issue_ceiling_frac": round(fill_gcups / model["peak_gcups"], 4) if model else None,
-                 "issue_ceiling_basis": "steady-loop VALU mix x measured per-opcode issue rates (tools/issue_model.py, "
-                                        "profiles/issue_model_r04.json)",
-                 "cell_mix_ceiling_gcups": CELL_MIX_CEILING.get(label, (None,))[0],
-                 "cell_mix_frac": (round(fill_gcups / CELL_MIX_CEILING[label][0], 4) if label in CELL_MIX_CEILING else None),
-                 "cell_mix_source": CELL_MIX_CEILING.get(label, (None, None))[1],
+                 "clock_ghz_measured": clk,
+                 "frac_at_measured_clock": round(achieved / (VALU_PEAK_TLANE * clk / 2.4), 4) if (achieved and clk) else None,
+                 "pmc_source": pmc.get("source") if pmc else None,
                  "bytes_per_cell": round(bytes_per_cell, 4), "hbm_achieved_GBps": round(hbm_gbps, 1),
                  "hbm_peak_GBps": HBM_PEAK_GBPS, "hbm_frac": round(hbm_gbps / HBM_PEAK_GBPS, 4)})
     line = {
@@ -361,17 +394,24 @@ def main():
                    "scoring": list(SCORING), "match": "equal<char>", "parallelism": f"pair-shard x{world}"},
         "roofline": roof,
         "fill_ms": round(fill_ms, 2), "endcell_traceback_ms": round(tb_ms, 2),
+        "records": "score-only fill + block-recompute traceback" if so else ("tagged" if t16 else "flags"),
         "e2e_ms_per_step": round(e2e_ms, 2) if e2e_ms else None,
         "e2e_gcups": round(world * cells_rank / (e2e_ms / 1e3) / 1e9, 1) if e2e_ms else None,
-        "e2e_basis": "host API sa_align_batch from pageable host buffers: pinned, chunked and pipelined "
-                     "upload of sequences + offsets, fill, end cell, traceback, download of results and op "
-                     "streams into the caller's (reused) pageable output buffers; one call at a time",
+        "e2e_basis": "host API sa_align_batch from pageable host buffers, one call at a time, one chunk: pinned "
+                     "upload of sequences + offsets in 16 MiB pieces (host copy of piece k+1 beside the H2D of "
+                     "piece k), fill, end cell, traceback, download of results and op streams into the caller's "
+                     "(reused) buffers piece by piece",
         "pipelined": pipelined, "serial_ms_per_step": round(serial_ms, 2) if serial_ms else None,
-        "parity": f"{checked - bad}/{checked} sampled pairs bit-exact vs oracle, {int(np.count_nonzero(res['flags']))} flagged",
+        "parity": (f"{par['end_cells']} pairs' (MaxScore, MaxRow, MaxCol) bit-exact vs oracle; {par['rescored']} "
+                   f"alignments re-score to MaxScore; {par['op_streams']} full op streams bit-exact; "
+                   f"{par['flagged']} flagged"),
+        "parity_exact": par["exact"],
+        "configs": configs,
     }
     if world == 1:
-        eng.L.sa_trim(eng.h)   # free this process's workspace for the child's
+        eng.L.sa_trim(eng.h)   # free this process's workspace for the children's
         line["dropin_e2e"] = dropin_e2e(args)
+        line["dropin_single_call"] = dropin_latency(args)
     if world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args, s1, o1, s2, o2)
         line["cpu_baseline_1thread"] = cpu_baseline(args, s1, o1, s2, o2, threads=1, pairs=args.cpu_pairs_1t)

@@ -179,6 +179,7 @@ struct SymbolCoder {
     }
     size_t size() const { return values.size(); }
     const Ty& value(size_t k) const { return values[k]; }
+    bool used(size_t) const { return true; }           // every code in [0, size()) is in use
     bool identity_on_equal() const { return true; }   // distinct values -> distinct codes
 };
 
@@ -201,17 +202,25 @@ std::vector<uint8_t> build_lut(SymbolCoder<Ty, Direct>& coder, MatchFnTy& fn) {
     std::vector<uint8_t> lut(65536, 0);
     const size_t k = Direct ? 256 : coder.size();
     for (size_t a = 0; a < k; ++a) {
-        if constexpr (Direct) {
-            if (!coder.used(a)) continue;
-        }
+        if (!coder.used(a)) continue;
         for (size_t b = 0; b < k; ++b) {
-            if constexpr (Direct) {
-                if (!coder.used(b)) continue;
-            }
+            if (!coder.used(b)) continue;
             lut[a * 256 + b] = fn(coder.value(a), coder.value(b)) ? 1 : 0;
         }
     }
     return lut;
+}
+
+// match(x, y) as the reference's cacheAllMatches evaluates it: the user's MatchFnTy, or == for a
+// nullptr one.  (Overloads rather than if constexpr: the headers build with the reference's own
+// -std=c++14, test/Makefile:2.)
+template <typename MatchFnTy, typename A>
+bool call_match(MatchFnTy& fn, bool has_fn, const A& x, const A& y) {
+    return has_fn ? (bool)fn(x, y) : (x == y);
+}
+template <typename A>
+bool call_match(std::nullptr_t&, bool, const A& x, const A& y) {
+    return x == y;
 }
 
 // Generic-Ty path: per-pair m x n match bitmaps, built exactly as the reference's
@@ -238,10 +247,7 @@ void align_bits(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
         uint32_t* w = bits.data() + bo[q];
         for (size_t i = 0; i < m; ++i)
             for (size_t j = 0; j < n; ++j) {
-                bool v;
-                if constexpr (std::is_same<MatchFnTy, std::nullptr_t>::value) v = a[i] == b[j];
-                else v = has_fn ? (bool)fn(a[i], b[j]) : (a[i] == b[j]);
-                if (v) w[i * wn + j / 32] |= 1u << (j % 32);
+                if (call_match(fn, has_fn, a[i], b[j])) w[i * wn + j / 32] |= 1u << (j % 32);
             }
     }
     tm.lap("match bitmaps");
@@ -257,6 +263,47 @@ void align_bits(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
     for (auto& r : res)
         if (r.flags & SA_FLAG_DIVERGED)
             throw std::runtime_error("seqalib: the reference traceback does not terminate for this scoring");
+}
+
+// Symbol coding of a batch into the packed byte buffers.  Byte symbols are their own codes: they
+// are copied on the host threads, each marking the symbols it saw (for the match table) in a table
+// of its own.  Other types get codes in order of first appearance (serial; stops on overflow).
+template <typename Coder, typename ContainerType>
+void code_symbols(std::true_type, Coder& coder, const std::vector<std::pair<ContainerType*, ContainerType*>>& pairs,
+                  const std::vector<uint64_t>& o1, const std::vector<uint64_t>& o2, raw_vector<uint8_t>& s1,
+                  raw_vector<uint8_t>& s2) {
+    const size_t nth = host_threads(pairs.size());
+    std::vector<std::array<uint8_t, 256>> seen(nth);
+    parallel_pairs(pairs.size(), nth, [&](size_t t, size_t p0, size_t p1) {
+        std::array<uint8_t, 256>& sn = seen[t];
+        sn.fill(0);
+        for (size_t q = p0; q < p1; ++q) {
+            ContainerType& a = *pairs[q].first;
+            ContainerType& b = *pairs[q].second;
+            uint8_t* d1 = s1.data() + o1[q];
+            uint8_t* d2 = s2.data() + o2[q];
+            for (size_t k = 0; k < (size_t)a.size(); ++k) sn[d1[k] = (uint8_t)a[k]] = 1;
+            for (size_t k = 0; k < (size_t)b.size(); ++k) sn[d2[k] = (uint8_t)b[k]] = 1;
+        }
+    });
+    using Ty = typename std::remove_reference<decltype((*pairs[0].first)[0])>::type;
+    for (auto& sn : seen)
+        for (int c = 0; c < 256; ++c)
+            if (sn[c]) coder.code((typename std::remove_cv<Ty>::type)(uint8_t)c);
+}
+template <typename Coder, typename ContainerType>
+void code_symbols(std::false_type, Coder& coder, const std::vector<std::pair<ContainerType*, ContainerType*>>& pairs,
+                  const std::vector<uint64_t>& o1, const std::vector<uint64_t>& o2, raw_vector<uint8_t>& s1,
+                  raw_vector<uint8_t>& s2) {
+    for (size_t q = 0; q < pairs.size(); ++q) {
+        ContainerType& a = *pairs[q].first;
+        ContainerType& b = *pairs[q].second;
+        uint8_t* d1 = s1.data() + o1[q];
+        uint8_t* d2 = s2.data() + o2[q];
+        for (size_t k = 0; k < (size_t)a.size(); ++k) d1[k] = coder.code(a[k]);
+        for (size_t k = 0; k < (size_t)b.size(); ++k) d2[k] = coder.code(b[k]);
+        if (coder.overflow) break;
+    }
 }
 
 // Aligns a batch of (Seq1, Seq2) pairs on the GPU.  Returns the per-pair results and the op
@@ -276,37 +323,7 @@ void align(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
     }
     raw_vector<uint8_t> s1(o1.back() + 1), s2(o2.back() + 1);   // +1: never a NULL pointer
     constexpr bool kDirect = std::is_integral<Ty>::value && sizeof(Ty) == 1;
-    if constexpr (kDirect) {
-        // byte symbols are their own codes: copy them on the host threads, each marking the
-        // symbols it saw (for the match table) in a table of its own
-        const size_t nth = host_threads(pairs.size());
-        std::vector<std::array<uint8_t, 256>> seen(nth);
-        parallel_pairs(pairs.size(), nth, [&](size_t t, size_t p0, size_t p1) {
-            std::array<uint8_t, 256>& sn = seen[t];
-            sn.fill(0);
-            for (size_t q = p0; q < p1; ++q) {
-                ContainerType& a = *pairs[q].first;
-                ContainerType& b = *pairs[q].second;
-                uint8_t* d1 = s1.data() + o1[q];
-                uint8_t* d2 = s2.data() + o2[q];
-                for (size_t k = 0; k < (size_t)a.size(); ++k) sn[d1[k] = (uint8_t)a[k]] = 1;
-                for (size_t k = 0; k < (size_t)b.size(); ++k) sn[d2[k] = (uint8_t)b[k]] = 1;
-            }
-        });
-        for (auto& sn : seen)
-            for (int c = 0; c < 256; ++c)
-                if (sn[c]) coder.code((Ty)(uint8_t)c);
-    } else {
-        for (size_t q = 0; q < pairs.size(); ++q) {
-            ContainerType& a = *pairs[q].first;
-            ContainerType& b = *pairs[q].second;
-            uint8_t* d1 = s1.data() + o1[q];
-            uint8_t* d2 = s2.data() + o2[q];
-            for (size_t k = 0; k < (size_t)a.size(); ++k) d1[k] = coder.code(a[k]);
-            for (size_t k = 0; k < (size_t)b.size(); ++k) d2[k] = coder.code(b[k]);
-            if (coder.overflow) break;
-        }
-    }
+    code_symbols(std::integral_constant<bool, kDirect>{}, coder, pairs, o1, o2, s1, s2);
     tm.lap("symbol coding");
     if (coder.overflow) {   // more than 256 distinct symbols: the generic-Ty (bitmap) path
         align_bits<Ty>(algo, sc, fn, has_fn, pairs, res, ops, ops_off);

@@ -193,6 +193,14 @@ int sa_last_timings(sa_ctx* ctx, float* fill_ms, float* traceback_ms, int* fill_
 #define SA_KERNEL_T16 1
 #define SA_KERNEL_T16_ENDCELL 2   /* T16 SW / LocalGotoh with per-chunk maxima + end-cell replay */
 int sa_last_plan(sa_ctx* ctx, int* kernel, int* rows_per_lane, int* waves);
+/* sa_last_plan plus what the fill stored for the traceback: SA_RECORDS_FLAGS (int32 equality
+ * flags), SA_RECORDS_TAGS (T16 move tags per cell) or SA_RECORDS_SCORE_ONLY (score-only T16 SW fill:
+ * per-chunk snapshots + each lane's last row per step; the traceback recomputes the blocks along
+ * its path).  Environment: SEQALIB_SO=0 keeps the tagged records. */
+#define SA_RECORDS_FLAGS 0
+#define SA_RECORDS_TAGS 1
+#define SA_RECORDS_SCORE_ONLY 2
+int sa_last_plan_ex(sa_ctx* ctx, int* kernel, int* rows_per_lane, int* waves, int* records);
 
 /* Plan of the int32 kernel for a batch (host-only query, no device needed): rows per lane R,
  * waves per workgroup W, direction bytes per pair, row-buffer bytes per pair.  The plan the

@@ -202,6 +202,29 @@ int ref_sw_batch(int gap, int match, int mismatch, int allow, const char* s1cat,
     return 0;
 }
 
+// Per-call latency of the reference's public API, timed the way include/Test.cpp:98-107 times it:
+// construct the aligner, getAlignment(seq1, seq2), with equal<char>; algo 0 SmithWatermanSA,
+// 1 NeedlemanWunschSA.  Runs `reps` calls on the calling thread and returns the mean ns per call.
+double ref_call_ns(int algo, int nargs, int a0, int a1, int a2, int allow, const char* s1, int m,
+                   const char* s2, int n, int reps) {
+    std::string q(s1, s1 + m), t(s2, s2 + n);
+    const ScoringSystem sc = nargs == 2 ? ScoringSystem(a0, a1) : ScoringSystem(a0, a1, a2, allow != 0);
+    size_t sink = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0; k < reps; ++k) {
+        if (algo == 0) {
+            AlignedSequence<char, '-'> r = SmithWatermanSA<std::string, char, '-'>(sc, equal_char).getAlignment(q, t);
+            sink += r.Data.size();
+        } else {
+            AlignedSequence<char, '-'> r = NeedlemanWunschSA<std::string, char, '-'>(sc, equal_char).getAlignment(q, t);
+            sink += r.Data.size();
+        }
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    if (sink == (size_t)-1) std::abort();
+    return std::chrono::duration<double, std::nano>(t1 - t0).count() / (reps > 0 ? reps : 1);
+}
+
 // std::mt19937_64 DNA generator: symbol = "ACGT"[g() & 3].  Pins the
 // product library's own generator (sa_synth_dna) bit for bit.
 void ref_gen_dna(uint64_t seed, int len, char* out) {

@@ -95,6 +95,7 @@ static int expand(const uint8_t* s1, int m, const uint8_t* s2, int n, const uint
 /* ---------------------------------------------------------------- Smith-Waterman (linear) */
 static int align_sw(const oracle_scoring* sc, const uint8_t* s1, int m, const uint8_t* s2, int n,
                     const uint8_t* mt, oracle_result* res, opbuf* ob) {
+    (void)s1; (void)s2;
     int32_t* H = (int32_t*)malloc(sizeof(int32_t) * (size_t)(m + 1) * (size_t)(n + 1));
     if (!H) return -2;
     const int32_t G = sc->gap;
@@ -703,24 +704,95 @@ static void sw_score_one(const oracle_scoring* sc, const uint8_t* a, int m, cons
     out[0] = best; out[1] = bi; out[2] = bj;
 }
 
+/* sw_score_one on 8 pairs of equal shape at once, lane l = pair l: the same recurrence, row-major
+ * order and ">=" maximum per lane, written so the compiler vectorises the lane loop (the batch
+ * checker of the 10,000 x 4096^2 headline would otherwise take minutes).  Pinned against
+ * sw_score_one by tests/test_oracle_golden.py. */
+#define SW8 8
+typedef int32_t sw_v8 __attribute__((vector_size(32)));
+typedef uint8_t sw_v8b __attribute__((vector_size(8)));
+#define SW_AVX2 __attribute__((target("avx2")))
+SW_AVX2 static inline sw_v8 sw_sel(sw_v8 mask, sw_v8 a, sw_v8 b) { return (mask & a) | (~mask & b); }
+SW_AVX2 static void sw_score_x8(const oracle_scoring* sc, const uint8_t* const* a, const uint8_t* const* b, int m,
+                        int n, sw_v8* rows, uint8_t* bt, int32_t* out) {
+    const sw_v8 G = (sw_v8){0} + sc->gap, MA = (sw_v8){0} + sc->match, MI = (sw_v8){0} + sc->mismatch;
+    const sw_v8 zero = (sw_v8){0}, neg = zero + INT_MIN;
+    const int allow = sc->allow_mismatch;
+    sw_v8 best = neg, bi = zero, bj = zero;
+    for (int j = 0; j < n; ++j)
+        for (int l = 0; l < SW8; ++l) bt[(size_t)j * SW8 + l] = b[l][j];
+    for (int j = 0; j <= n; ++j) rows[j] = zero;
+    for (int i = 1; i <= m; ++i) {
+        sw_v8 diag = zero, left = zero, ai;
+        for (int l = 0; l < SW8; ++l) ai[l] = a[l][i - 1];
+        const sw_v8 iv = zero + i;
+        for (int j = 1; j <= n; ++j) {
+            sw_v8b bb;
+            memcpy(&bb, bt + (size_t)(j - 1) * SW8, SW8);
+            const sw_v8 bv = __builtin_convertvector(bb, sw_v8);
+            const sw_v8 up = rows[j];
+            const sw_v8 dx = allow ? diag + MI : neg;
+            sw_v8 h = sw_sel(ai == bv, diag + MA, dx);
+            const sw_v8 u = up + G, lf = left + G;
+            h = sw_sel(u > h, u, h);
+            h = sw_sel(lf > h, lf, h);
+            h = sw_sel(h < zero, zero, h);
+            diag = up;
+            rows[j] = h;
+            left = h;
+            const sw_v8 take = h >= best;
+            best = sw_sel(take, h, best);
+            bi = sw_sel(take, iv, bi);
+            bj = sw_sel(take, zero + j, bj);
+        }
+    }
+    for (int l = 0; l < SW8; ++l) {
+        const int e = m == 0 || n == 0;
+        out[3 * l] = e ? INT_MIN : best[l];
+        out[3 * l + 1] = e ? 0 : bi[l];
+        out[3 * l + 2] = e ? 0 : bj[l];
+    }
+}
+
 static void* score_worker(void* arg) {
     score_job* J = (score_job*)arg;
     int32_t* row = NULL;
+    uint8_t* bt = NULL;
     int cap = -1;
     for (;;) {
         pthread_mutex_lock(&J->mu);
-        int p = J->next++;
+        const int p0 = J->next;
+        J->next += SW8;
         pthread_mutex_unlock(&J->mu);
-        if (p >= J->npairs) break;
-        int m = (int)(J->o1[p + 1] - J->o1[p]), n = (int)(J->o2[p + 1] - J->o2[p]);
-        if (n > cap) {
-            free(row);
-            row = (int32_t*)malloc(sizeof(int32_t) * ((size_t)n + 1));
-            cap = n;
+        if (p0 >= J->npairs) break;
+        const int p1 = p0 + SW8 <= J->npairs ? p0 + SW8 : J->npairs;
+        const int m = (int)(J->o1[p0 + 1] - J->o1[p0]), n = (int)(J->o2[p0 + 1] - J->o2[p0]);
+        int same = p1 - p0 == SW8, nmax = 0;
+        for (int p = p0; p < p1; ++p) {
+            const int mp = (int)(J->o1[p + 1] - J->o1[p]), np = (int)(J->o2[p + 1] - J->o2[p]);
+            same = same && mp == m && np == n;
+            nmax = np > nmax ? np : nmax;
         }
-        sw_score_one(J->sc, J->s1 + J->o1[p], m, J->s2 + J->o2[p], n, row, J->out + 3 * (size_t)p);
+        if (nmax > cap) {
+            free(row);
+            free(bt);
+            row = (int32_t*)aligned_alloc(32, sizeof(int32_t) * ((size_t)nmax + 1) * SW8);
+            bt = (uint8_t*)malloc((size_t)nmax * SW8 + 1);
+            cap = nmax;
+        }
+        if (same && __builtin_cpu_supports("avx2")) {
+            const uint8_t* a[SW8];
+            const uint8_t* b[SW8];
+            for (int l = 0; l < SW8; ++l) { a[l] = J->s1 + J->o1[p0 + l]; b[l] = J->s2 + J->o2[p0 + l]; }
+            sw_score_x8(J->sc, a, b, m, n, (sw_v8*)row, bt, J->out + 3 * (size_t)p0);
+        } else {
+            for (int p = p0; p < p1; ++p)
+                sw_score_one(J->sc, J->s1 + J->o1[p], (int)(J->o1[p + 1] - J->o1[p]), J->s2 + J->o2[p],
+                             (int)(J->o2[p + 1] - J->o2[p]), row, J->out + 3 * (size_t)p);
+        }
     }
     free(row);
+    free(bt);
     return NULL;
 }
 

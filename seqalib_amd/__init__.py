@@ -38,6 +38,7 @@ ALGO_NAMES = {SA_SW: "sw", SA_NW: "nw", SA_LOCAL_GOTOH: "local_gotoh", SA_GLOBAL
               SA_HIRSCHBERG: "hirschberg", SA_MYERS_MILLER: "myers_miller"}
 SA_FLAG_DIVERGED, SA_FLAG_BAD_SHAPE, SA_FLAG_SIZE_HACK, SA_FLAG_TIMEOUT = 1, 2, 4, 8
 SA_KERNEL_INT32, SA_KERNEL_T16, SA_KERNEL_T16_ENDCELL = 0, 1, 2
+SA_RECORDS_FLAGS, SA_RECORDS_TAGS, SA_RECORDS_SCORE_ONLY = 0, 1, 2
 INT32_MIN = -(2 ** 31)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -128,6 +129,7 @@ def load_library():
     L.sa_plan_query_ex.argtypes = [C.c_int, C.POINTER(_Scoring), C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
                                    i32p, i32p, i32p, u64p]
     L.sa_last_plan.argtypes = [vp, i32p, i32p, i32p]
+    L.sa_last_plan_ex.argtypes = [vp, i32p, i32p, i32p, i32p]
     L.sa_set_pipeline.argtypes = [vp, C.c_int]
     L.sa_wait.argtypes = [vp]
     L.sa_synth_dna.argtypes = [C.c_uint64, C.c_uint32, vp]
@@ -135,7 +137,7 @@ def load_library():
     L.sa_synth_dna_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_int]
     for fn in ("sa_set_workspace_limit", "sa_trim", "sa_align_batch", "sa_align_batch_bits", "sa_align_batch_device",
                "sa_multi_create", "sa_multi_align_batch",
-               "sa_last_timings", "sa_last_plan", "sa_plan_query", "sa_plan_query_ex", "sa_synth_dna", "sa_synth_mutate", "sa_synth_dna_batch",
+               "sa_last_timings", "sa_last_plan", "sa_last_plan_ex", "sa_plan_query", "sa_plan_query_ex", "sa_synth_dna", "sa_synth_mutate", "sa_synth_dna_batch",
                "sa_create", "sa_device_count", "sa_set_pipeline", "sa_wait"):
         getattr(L, fn).restype = C.c_int
     if L.sa_version() != 1:
@@ -484,6 +486,12 @@ class Engine:
         self._check(self.L.sa_last_timings(self.h, C.byref(f), C.byref(t), C.byref(n)), "sa_last_timings")
         return f.value, t.value, n.value
 
+
+    def last_plan_ex(self) -> Tuple[int, int, int, int]:
+        """last_plan() plus the records the fill stored (SA_RECORDS_FLAGS / _TAGS / _SCORE_ONLY)."""
+        k, R, W, rec = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        self._check(self.L.sa_last_plan_ex(self.h, C.byref(k), C.byref(R), C.byref(W), C.byref(rec)), "sa_last_plan_ex")
+        return k.value, R.value, W.value, rec.value
 
     def last_plan(self) -> Tuple[int, int, int]:
         """(kernel, R, W) of the last call: kernel is SA_KERNEL_INT32, SA_KERNEL_T16,

@@ -40,7 +40,7 @@ struct sa_ctx {
     // plan of the last call: one entry per kernel variant it enqueued (T16 first when the batch
     // was T16-eligible by scoring and shape; the device picked one by the batch alphabet, and
     // h_sel receives that choice asynchronously, ev_sel marks its arrival)
-    int nvar = 0, var_kernel[2] = {0, 0}, var_R[2] = {0, 0}, var_W[2] = {0, 0};
+    int nvar = 0, var_kernel[2] = {0, 0}, var_R[2] = {0, 0}, var_W[2] = {0, 0}, var_records[2] = {0, 0};
     uint32_t* h_sel = nullptr;
     hipEvent_t ev_sel = nullptr;
     // cross-call pipeline of the device API (sa_set_pipeline): fills on s_fill, tracebacks on
@@ -480,11 +480,13 @@ T16Mode t16_candidate(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t m
 // share one record stride (the int32 variant re-runs single pairs of a T16 batch, kFlagRetry,
 // while the T16 traceback still reads their neighbours).  Returns the number of variants;
 // vars[nv] is the fallback when *has_fb.
+// only: 0 both variants (as above), 1 the T16 variant alone, 2 the int32 variant alone (the host
+// decided the batch alphabet itself and T16 provably needs no int32 re-run, run_device).
 int build_variants(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bool t16, Variant (&vars)[3],
-                   bool* has_fb) {
+                   bool* has_fb, int only = 0) {
     int nv = 0;
-    if (t16) vars[nv++] = make_variant(algo, max_m, max_n, npairs, true, true);
-    vars[nv++] = make_variant(algo, max_m, max_n, npairs, false, true);
+    if (t16 && only != 2) vars[nv++] = make_variant(algo, max_m, max_n, npairs, true, true);
+    if (!t16 || only != 1) vars[nv++] = make_variant(algo, max_m, max_n, npairs, false, true);
     *has_fb = false;
     for (int k = 0; k < nv; ++k) *has_fb = *has_fb || vars[k].pl.split;
     if (*has_fb) vars[nv] = make_variant(algo, max_m, max_n, npairs, false, false);
@@ -498,6 +500,53 @@ int build_variants(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, bo
     return nv;
 }
 
+// The batch alphabet decided on the host (host API calls whose sequences are small enough to scan
+// here, align_host): the same decision and profile as decide_t16 (sa_alphabet.hip) -- <= 4
+// distinct bytes, padded with absent byte values, prof[c] byte c' = 4s + 3 (8s + 6 affine) with
+// s = match(sym c, sym c') ? match : mismatch -- so the device runs no scan and no decide kernel
+// and the host knows which variant to enqueue.
+struct HostAlphabet {
+    int sel = -1;          // -1: decide on the device; 1: T16; 0: int32
+    uint32_t prof[5] = {0, 0, 0, 0, 0};
+};
+HostAlphabet host_alphabet(const uint8_t* s1, uint64_t t1, const uint8_t* s2, uint64_t t2, const uint8_t* lut,
+                           int match, int mismatch, bool affine) {
+    HostAlphabet h;
+    bool seen[256] = {};
+    for (uint64_t k = 0; k < t1; ++k) seen[s1[k]] = true;
+    for (uint64_t k = 0; k < t2; ++k) seen[s2[k]] = true;
+    uint32_t syms[4] = {0, 0, 0, 0};
+    int nsym = 0;
+    for (int b = 0; b < 256; ++b)
+        if (seen[b]) {
+            if (nsym == 4) { h.sel = 0; return h; }
+            syms[nsym++] = (uint32_t)b;
+        }
+    for (int b = 0; nsym < 4 && b < 256; ++b)
+        if (!seen[b]) syms[nsym++] = (uint32_t)b;
+    for (int c = 0; c < 4; ++c) {
+        uint32_t w = 0;
+        for (int c2 = 0; c2 < 4; ++c2) {
+            const bool v = lut ? lut[syms[c] * 256 + syms[c2]] != 0 : syms[c] == syms[c2];
+            const int sc = v ? match : mismatch;
+            w |= ((uint32_t)(affine ? 8 * sc + 6 : 4 * sc + 3) & 255u) << (8 * c2);
+        }
+        h.prof[c] = w;
+    }
+    h.prof[4] = syms[0] | syms[1] << 8 | syms[2] << 16 | syms[3] << 24;
+    h.sel = 1;
+    return h;
+}
+// host API batches up to this many sequence bytes are scanned on the host
+constexpr uint64_t kHostScanBytes = 1ull << 16;
+struct HostSeqs {   // a host API batch's sequences (and host match table) for host_alphabet
+    const uint8_t* s1;
+    uint64_t t1;
+    const uint8_t* s2;
+    uint64_t t2;
+    const uint8_t* lut;   // 256 x 256 bytes or NULL (equality)
+};
+
 // Enqueue fill + traceback for pairs [0, npairs) whose inputs are on the device.  Nothing here
 // waits on the host: when the scoring and shapes admit the T16 kernel, the batch alphabet is
 // scanned on the device and BOTH variants (T16 and int32) are enqueued, each launch guarded by
@@ -509,7 +558,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                const uint8_t* d2, const uint64_t* o2, uint32_t npairs, uint32_t max_m,
                uint32_t max_n, const uint32_t* d_lutbits, sa_result* d_res, uint8_t* d_ops,
                hipStream_t stream, bool pipe = false, const uint32_t* d_mbits = nullptr,
-               const uint64_t* d_mbits_off = nullptr) {
+               const uint64_t* d_mbits_off = nullptr, const HostSeqs* hs = nullptr) {
     if (max_m >= (1u << 24) || max_n >= (1u << 24))
         return fail(c, SA_ERR_UNSUPPORTED, "sequence lengths must be < 2^24");
     const bool keyed = keyed_ok(algo, sc, max_m, max_n);
@@ -531,7 +580,25 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     uint32_t* aux = c->aux + kAuxWords * slot;
     if (pipe && c->ev_slot[slot]) SA_HIP(c, hipStreamWaitEvent(stream, c->ev_slot[slot], 0));   // slot free
     const uint32_t* sel = nullptr;
-    if (t16) {
+    int only = 0;   // build_variants: both variants, or the one the host chose
+    HostAlphabet hal;
+    if (t16 && hs) hal = host_alphabet(hs->s1, hs->t1, hs->s2, hs->t2, hs->lut, sc->match, tm.mismatch, is_affine(algo));
+    const HostAlphabet* ha = &hal;
+    if (t16 && ha->sel >= 0) {
+        // the host decided the alphabet (align_host): upload the profile; enqueue the chosen variant
+        // alone -- plus the int32 re-run when T16 may overflow (SW / LocalGotoh retry_above, the
+        // screened GlobalGotoh), which then reads the selection word as usual
+        *c->h_sel = (uint32_t)ha->sel;
+        uint32_t* const hp = c->h_sel + 8;   // pinned staging (the host API call is synchronous)
+        for (int k = 0; k < 5; ++k) hp[k] = ha->prof[k];
+        hp[5] = (uint32_t)ha->sel;
+        SA_HIP(c, hipMemcpyAsync(aux + kAuxProf, hp, 20, hipMemcpyHostToDevice, stream));
+        SA_HIP(c, hipMemcpyAsync(aux + kAuxSel, hp + 5, 4, hipMemcpyHostToDevice, stream));
+        SA_HIP(c, hipEventRecord(c->ev_sel, stream));
+        if (ha->sel == 0) only = 2;
+        else if (tm.retry_above == INT_MAX) only = 1;
+        else sel = aux + kAuxSel;
+    } else if (t16) {
         SA_HIP(c, launch_alphabet_scan(d1, o1, d2, o2, npairs, aux, stream));
         SA_HIP(c, launch_decide_t16(d_lutbits, sc->match, tm.mismatch, is_affine(algo) ? 1 : 0, aux, stream));
         SA_HIP(c, hipMemcpyAsync(c->h_sel, aux + kAuxSel, 4, hipMemcpyDeviceToHost, stream));
@@ -540,7 +607,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     }
     Variant vars[3];
     bool has_fb = false;
-    const int nv = build_variants(algo, max_m, max_n, npairs, t16, vars, &has_fb);
+    const int nv = build_variants(algo, max_m, max_n, npairs, t16, vars, &has_fb, only);
     if (const char* e = getenv("SEQALIB_SPLIT_FALLBACK")) has_fb = has_fb && e[0] != '0';   // tests only
     c->nvar = nv;
     uint64_t slot_bytes = 0, sp_bands = 0;
@@ -550,6 +617,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             c->var_kernel[k] = vars[k].kernel;
             c->var_R[k] = vars[k].pl.R;
             c->var_W[k] = vars[k].pl.split ? 0 : vars[k].pl.W;   // 0: SPLIT plan (one single-wave workgroup per band)
+            c->var_records[k] = vars[k].so ? SA_RECORDS_SCORE_ONLY : vars[k].t16 ? SA_RECORDS_TAGS : SA_RECORDS_FLAGS;
         }
         slot_bytes = std::max(slot_bytes, vars[k].slot_bytes);
         if (vars[k].pl.split) {
@@ -1092,8 +1160,11 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
             if (run(c->dc, c->ev_last_set ? c->ev_last : nullptr, sc, in, b, st, dres + p0, dops + ob, &e))
                 return fail(c, SA_ERR_HIP, (algo == SA_HIRSCHBERG ? "hirschberg: " : "myers-miller: ") + e);
         } else {
+            // small batches: the alphabet is decided here, on the host (no scan / decide kernels)
+            const HostSeqs hs{seq1 + a1, n1, seq2 + a2, n2, use_lut ? lut : nullptr};
             int rc = run_device(c, algo, sc, d1 + a1, do1 + p0 + g, d2 + a2, do2 + p0 + g, cnt, mm, mn,
-                                use_lut ? dbits : nullptr, dres + p0, dops + ob, st, pipe);
+                                use_lut ? dbits : nullptr, dres + p0, dops + ob, st, pipe, nullptr, nullptr,
+                                n1 + n2 <= kHostScanBytes ? &hs : nullptr);
             if (rc) return rc;
             if (pipe) done = c->s_tb;   // the chunk's last kernel (its traceback) ran there
         }
@@ -1426,7 +1497,7 @@ int sa_last_timings(sa_ctx* c, float* fill_ms, float* tb_ms, int* launches) {
     return SA_OK;
 }
 
-int sa_last_plan(sa_ctx* c, int* kernel, int* R, int* W) {
+int sa_last_plan_ex(sa_ctx* c, int* kernel, int* R, int* W, int* records) {
     if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
     int k = 0;
     if (c->nvar == 2) {   // T16 and int32 were both enqueued: the device's choice decides
@@ -1436,8 +1507,11 @@ int sa_last_plan(sa_ctx* c, int* kernel, int* R, int* W) {
     if (kernel) *kernel = c->var_kernel[k];
     if (R) *R = c->var_R[k];
     if (W) *W = c->var_W[k];
+    if (records) *records = c->var_records[k];
     return SA_OK;
 }
+
+int sa_last_plan(sa_ctx* c, int* kernel, int* R, int* W) { return sa_last_plan_ex(c, kernel, R, W, nullptr); }
 
 int sa_plan_query(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, int* R, int* W,
                   uint64_t* dir_bytes, uint64_t* rowbuf_bytes) {

@@ -177,7 +177,7 @@ constexpr int kEvCol = 2048;
 template <int ALG, int R, int MM, bool ALLOW, bool KEYED, bool T16, bool CMAX, bool SPLIT, bool SO = false>
 // (Asking the headline kernel for 4 waves per SIMD -- 128 VGPRs, 8 spills outside the step loops
 // -- measured 29.6 ms per fill against 29.4 at its natural 3 waves: not taken.)
-__global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)>())) void fill_kernel(FillParams P) {
+__device__ __forceinline__ void fill_body(const FillParams& P) {
     constexpr bool LUT = MM == kMatchLut;
     constexpr bool BITS = MM == kMatchBits;
     constexpr bool AFF = ALG >= SA_LOCAL_GOTOH;
@@ -264,8 +264,9 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     }
     // Screened T16 GlobalGotoh (t16_mode_affine, retry_above != INT_MAX): the 16-bit window holds
     // every value of a pair whose alignments of prefixes score at most retry_above.  Each such
-    // score is <= MA * (its matches) <= MA * min(L, m, n), L = sum over the (<= 4) symbols of
-    // min(count in Seq1, count in Seq2).  A pair above the cap leaves its fill to the int32
+    // score is <= MA * (its matches) <= MA * min(L, m, n), L a bound on the matches from the
+    // symbol counts (below; sum over the <= 4 symbols of min(count in Seq1, count in Seq2) for
+    // equality).  A pair above the cap leaves its fill to the int32
     // variant (kFlagRetry, re-run exactly by the redo launch).
     if constexpr (T16 && ALG == SA_GLOBAL_GOTOH && !SPLIT) {
         if (P.retry_above != INT_MAX) {
@@ -290,9 +291,32 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                 if (cb[e]) atomicAdd(&s_comp[4 + e], cb[e]);
             }
             __syncthreads();
-            int64_t L = 0;
+            // L bounds the matches of any alignment of prefixes: a Seq1 symbol a is matched at most
+            // min(count of a, count of the Seq2 symbols that match a) times -- and symmetrically.
+            // With equality this is sum_a min(ca[a], cb[a]); with the caller's match table
+            // (lutbits: the T16 profile follows it, decide_t16) different symbols may match.
+            uint32_t mt = 0;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) L += (int64_t)min(s_comp[e], s_comp[4 + e]);
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t xa = (symp >> (8 * a)) & 255u, xb = (symp >> (8 * b)) & 255u;
+                    const bool v = P.lutbits ? ((P.lutbits[(xa << 3) | (xb >> 5)] >> (xb & 31u)) & 1u) != 0 : xa == xb;
+                    mt |= (v ? 1u : 0u) << (4 * a + b);
+                }
+            int64_t L1 = 0, L2 = 0;
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                int64_t r1 = 0, r2 = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    if ((mt >> (4 * a + b)) & 1u) r1 += s_comp[4 + b];   // Seq2 symbols matching a
+                    if ((mt >> (4 * b + a)) & 1u) r2 += s_comp[b];       // Seq1 symbols matching a
+                }
+                L1 += min<int64_t>(s_comp[a], r1);
+                L2 += min<int64_t>(s_comp[4 + a], r2);
+            }
+            const int64_t L = min(L1, L2);
             const int64_t hi = (int64_t)max(P.match, 0) * min<int64_t>(L, min(m, n));
             if (hi > (int64_t)P.retry_above) {   // uniform over the workgroup
                 if (threadIdx.x == 0) {
@@ -534,8 +558,10 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
         constexpr int MODE = (int)decltype(mode)::value;
         constexpr bool STEADY = MODE == kStepSteady;
         constexpr bool START = MODE == kStepStart;
-        // T16 records narrower than a word: pushed straight into the packet word (acc_rec)
-        constexpr bool ACC = T16 && RB < 32 && MODE != kStepAny;
+        // T16 records narrower than a word: pushed straight into the packet word (acc_rec); SO
+        // pushes every step of every mode (a lane-step outside the matrix leaves a stale value in
+        // the edge stream, which the traceback never reads)
+        constexpr bool ACC = T16 && RB < 32 && (MODE != kStepAny || SO);
         constexpr bool ODD = decltype(odd)::value;
         const int up_h = shr1(vh, hl);
         int up_x = 0;
@@ -811,15 +837,11 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
             prev_up = up_h;
             hl = Hp[R - 1];
             if constexpr (AFF) xl = xu;
-            if constexpr (SO) {
-                // the step's record is the lane's last row: pushed into the packet word from the
-                // top (two steps per word), or, kStepAny, ORed in by the caller
-                if constexpr (ACC) rec[0] = __builtin_amdgcn_alignbit((uint32_t)hl, rec[0], 16u);
-                else rec[0] = (uint32_t)hl & 0xffffu;
-            } else if constexpr (T16 && RB < 32 && !ACC) {
-                rec[0] >>= (32 - RB);   // alignbit filled from the top
-            }
+            if constexpr (T16 && RB < 32 && !ACC) rec[0] >>= (32 - RB);   // alignbit filled from the top
         }
+        // SO: the step's record is the lane's last row, pushed into the packet word from the top
+        // (two steps per word)
+        if constexpr (SO) rec[0] = __builtin_amdgcn_alignbit((uint32_t)hl, rec[0], 16u);
     };
 
     // SPLIT compute wave, before the group of SG steps at step q of the chunk at kC: back-pressure
@@ -930,7 +952,7 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
                     vs = s_step[64 + q];
                     if constexpr (AFF) vx = in_x[q];
                 }
-                constexpr bool ACC = T16 && RB < 32 && (int)decltype(steady)::value != kStepAny;
+                constexpr bool ACC = T16 && RB < 32 && ((int)decltype(steady)::value != kStepAny || SO);
                 if constexpr (ACC) {
                     // every lane pushes every step: the packet word fills from the top, step by
                     // step, into the same byte layout as the shifted-and-ORed records below
@@ -1270,6 +1292,18 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
     }
 }
 
+template <int ALG, int R, int MM, bool ALLOW, bool KEYED, bool T16, bool CMAX, bool SPLIT, bool SO = false>
+__global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)>())) void fill_kernel(FillParams P) {
+    fill_body<ALG, R, MM, ALLOW, KEYED, T16, CMAX, SPLIT, SO>(P);
+}
+// The score-only kernel (one wave per workgroup): 4 waves per SIMD.  Its cell needs no record
+// registers, and the fourth wave hides the cell's dependent 16-bit chain (tools/microbench_so.hip:
+// 8,054 vs 7,520 GCUPS-equivalent at 4 vs 3 waves per SIMD).
+template <int R>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void fill_so_kernel(FillParams P) {
+    fill_body<SA_SW, R, kMatchEq, true, true, true, true, false, true>(P);
+}
+
 template <int ALG>
 hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream) {
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
@@ -1291,10 +1325,9 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
                 return hipErrorInvalidConfiguration;
 #define SA_LAUNCH16S(RR, SP)                                                                         \
     if (R == RR && split == SP) {                                                                    \
-        if constexpr (ALG == SA_SW && !SP) {                                                         \
+        if constexpr (ALG == SA_SW && !SP && RR <= 32) {                                              \
             if (v.cmax && v.so) {                                                                    \
-                hipLaunchKernelGGL((fill_kernel<ALG, RR, kMatchEq, true, LOCAL, true, true, SP, true>), dim3(grid), \
-                                   block, lds, stream, p);                                           \
+                hipLaunchKernelGGL((fill_so_kernel<RR>), dim3(grid), block, lds, stream, p);            \
                 return hipGetLastError();                                                            \
             }                                                                                        \
         }                                                                                            \

@@ -196,56 +196,123 @@ __global__ __launch_bounds__(64) void traceback_so_kernel(TbParams P) {
         }
         // the edge DMA writes LDS behind the compiler's back: wait for it, keep reads after this
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        int prev_top = corner;                   // 4 * H(r0 - 1, j0 + q - 1)
-        for (int q = qlo; q <= qhi; ++q) {
-            int top = 0;
-            if (has_top) {
-                const int s = slo + q;           // >= 0 here (q >= qlo)
-                const int d = (s >> 3) - pk0;
-                top = (int)((lds_u16*)(s_so + L::kEdge + d * 1024 + lane * 16 + (s & 7) * 2))[0] << 2;
+        auto top_of = [&](int q) -> int {       // 4 * H(r0 - 1, j0 + q)
+            if (!has_top) return 0;
+            const int s = slo + q;               // >= 0 here (q >= qlo)
+            const int d = (s >> 3) - pk0;
+            return (int)((lds_u16*)(s_so + L::kEdge + d * 1024 + lane * 16 + (s & 7) * 2))[0] << 2;
+        };
+        auto sym_of = [&](int q) -> uint32_t {
+            return (vw[(L::kColCodes >> 2) + (q >> 2) * 64 + lane] >> (8 * (q & 3))) & 255u;
+        };
+        // tags of rows r (16 per word, row r at bits 2 (r % 16): alignbit fills from the top)
+        auto put = [&](int q, int r, uint32_t& rec) __attribute__((always_inline)) {
+            if ((r & 15) == 15 || r == R - 1) {
+                const uint32_t wv = (r & 15) == 15 ? rec : rec >> (32 - 2 * ((r & 15) + 1));
+                vw[(q * RT + (r >> 4)) * 64 + lane] = wv;
+                rec = 0;
             }
-            const uint32_t sym = (vw[(L::kColCodes >> 2) + (q >> 2) * 64 + lane] >> (8 * (q & 3))) & 255u;
+        };
+#define SO_CELL(P, HP, HU, DR, REC, TAB, SYM)                                                      \
+    "v_add_u16 %[" #P "0], %[cl], %[" HP "]\n\t"                                                  \
+    "v_bfe_i32 %[" #P "dn], %[" TAB "], %[" SYM "], 8\n\t"                                         \
+    "v_add_u16 %[" #P "dn], %[" HP "], %[" #P "dn]\n\t"                                            \
+    "v_sub_u16_e64 %[" #P "1], %[" HU "], %[cu] clamp\n\t"                                         \
+    "v_max_i16 %[" #P "0], %[" DR "], %[" #P "0]\n\t"                                              \
+    "v_max_i16 %[" #P "0], %[" #P "1], %[" #P "0]\n\t"                                             \
+    "v_and_b32 %[" HP "], -4, %[" #P "0]\n\t"                                                      \
+    "v_alignbit_b32 %[" REC "], %[" #P "0], %[" REC "], 2\n\t"
+        // the two cells of a column pair's sub-step, instruction by instruction (A reads hb --
+        // Hp[r-1] -- as its up term before B's v_and_b32 overwrites it)
+#define SO_CELL2                                                                                   \
+    "v_add_u16 %[a0], %[cl], %[ha]\n\t"                                                            \
+    "v_add_u16 %[b0], %[cl], %[hb]\n\t"                                                            \
+    "v_bfe_i32 %[adn], %[taba], %[syma], 8\n\t"                                                    \
+    "v_bfe_i32 %[bdn], %[tabb], %[symb], 8\n\t"                                                    \
+    "v_add_u16 %[adn], %[ha], %[adn]\n\t"                                                          \
+    "v_add_u16 %[bdn], %[hb], %[bdn]\n\t"                                                          \
+    "v_sub_u16_e64 %[a1], %[hb], %[cu] clamp\n\t"                                                  \
+    "v_sub_u16_e64 %[b1], %[hub], %[cu] clamp\n\t"                                                 \
+    "v_max_i16 %[a0], %[da], %[a0]\n\t"                                                            \
+    "v_max_i16 %[b0], %[db], %[b0]\n\t"                                                            \
+    "v_max_i16 %[a0], %[a1], %[a0]\n\t"                                                            \
+    "v_max_i16 %[b0], %[b1], %[b0]\n\t"                                                            \
+    "v_and_b32 %[ha], -4, %[a0]\n\t"                                                               \
+    "v_and_b32 %[hb], -4, %[b0]\n\t"                                                               \
+    "v_alignbit_b32 %[reca], %[a0], %[reca], 2\n\t"                                                \
+    "v_alignbit_b32 %[recb], %[b0], %[recb], 2"
+        // one column: rows 0 .. R-1 in order (the up term of row r is row r-1 of this column)
+        auto column = [&](int q, int top, int ptop) __attribute__((always_inline)) {
+            const uint32_t sym = sym_of(q);
             uint32_t dcur;
-            asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(dcur) : "v"(tab[0]), "v"(sym), "v"(prev_top));
-            uint32_t hu = (uint32_t)top;
-            uint32_t rec = 0;
+            asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(dcur) : "v"(tab[0]), "v"(sym), "v"(ptop));
+            uint32_t hu = (uint32_t)top, rec = 0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                uint32_t t0, t1;
-                if (r + 1 < R) {
-                    uint32_t dn;
-                    asm("v_add_u16 %[t0], %[cl], %[hp]\n\t"
-                        "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\t"
-                        "v_add_u16 %[dn], %[hp], %[dn]\n\t"
-                        "v_sub_u16_e64 %[t1], %[hu], %[cu] clamp\n\t"
-                        "v_max_i16 %[t0], %[dr], %[t0]\n\t"
-                        "v_max_i16 %[t0], %[t1], %[t0]\n\t"
-                        "v_and_b32 %[hp], -4, %[t0]\n\t"
-                        "v_alignbit_b32 %[rec], %[t0], %[rec], 2"
-                        : [t0] "=&v"(t0), [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r]), [rec] "+v"(rec)
-                        : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL),
-                          [tabn] "v"(tab[r + 1 < R ? r + 1 : r]), [sym] "v"(sym));
-                    dcur = dn;
-                } else {
-                    asm("v_add_u16 %[t0], %[cl], %[hp]\n\t"
-                        "v_sub_u16_e64 %[t1], %[hu], %[cu] clamp\n\t"
-                        "v_max_i16 %[t0], %[dr], %[t0]\n\t"
-                        "v_max_i16 %[t0], %[t1], %[t0]\n\t"
-                        "v_and_b32 %[hp], -4, %[t0]\n\t"
-                        "v_alignbit_b32 %[rec], %[t0], %[rec], 2"
-                        : [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r]), [rec] "+v"(rec)
-                        : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL));
-                }
+                uint32_t a0, a1, adn;
+                asm(SO_CELL(a, "hp", "hu", "dr", "rec", "tabn", "sym")
+                    : [a0] "=&v"(a0), [a1] "=&v"(a1), [adn] "=&v"(adn), [hp] "+v"(Hp[r]), [rec] "+v"(rec)
+                    : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL),
+                      [tabn] "v"(tab[r + 1 < R ? r + 1 : r]), [sym] "v"(sym));
+                dcur = adn;
                 hu = (uint32_t)Hp[r];
-                if ((r & 15) == 15 || r == R - 1) {
-                    // 16 rows per word, row r at bits 2 (r % 16) (alignbit fills from the top)
-                    const uint32_t wv = (r & 15) == 15 ? rec : rec >> (32 - 2 * ((r & 15) + 1));
-                    vw[(q * RT + (r >> 4)) * 64 + lane] = wv;
-                    rec = 0;
-                }
+                put(q, r, rec);
             }
-            prev_top = top;
+        };
+        // two columns q (A) and q + 1 (B) as two interleaved dependence chains, B one row behind:
+        // at sub-step r, A computes row r and B row r - 1.  B's left and diagonal inputs are A's
+        // values of the previous sub-steps (Hp[r - 1] holds H(r - 1, q) until B overwrites it), so
+        // a lone wave issues the two chains back to back instead of stalling on each.
+        auto column_pair = [&](int q, int topA, int topB, int ptop) __attribute__((always_inline)) {
+            const uint32_t symA = sym_of(q), symB = sym_of(q + 1);
+            uint32_t da, db;
+            asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(da) : "v"(tab[0]), "v"(symA), "v"(ptop));
+            asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(db) : "v"(tab[0]), "v"(symB), "v"(topA));
+            uint32_t recA = 0, recB = 0;
+            {   // sub-step 0: A row 0
+                uint32_t a0, a1, adn;
+                asm(SO_CELL(a, "hp", "hu", "dr", "rec", "tabn", "sym")
+                    : [a0] "=&v"(a0), [a1] "=&v"(a1), [adn] "=&v"(adn), [hp] "+v"(Hp[0]), [rec] "+v"(recA)
+                    : [dr] "v"(da), [hu] "v"((uint32_t)topA), [cu] "s"(CU), [cl] "s"(CL),
+                      [tabn] "v"(tab[R > 1 ? 1 : 0]), [sym] "v"(symA));
+                da = adn;
+                put(q, 0, recA);
+            }
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                // A: row r (left Hp[r], up Hp[r-1] before B writes it); B: row r-1 (left Hp[r-1],
+                // up = B's row r-2, or its top)
+                const uint32_t hub = r >= 2 ? (uint32_t)Hp[r - 2] : (uint32_t)topB;
+                uint32_t a0, a1, adn, b0, b1, bdn;
+                asm(SO_CELL2
+                    : [a0] "=&v"(a0), [a1] "=&v"(a1), [adn] "=&v"(adn), [b0] "=&v"(b0), [b1] "=&v"(b1),
+                      [bdn] "=&v"(bdn), [ha] "+v"(Hp[r]), [hb] "+v"(Hp[r - 1]), [reca] "+v"(recA), [recb] "+v"(recB)
+                    : [da] "v"(da), [db] "v"(db), [hub] "v"(hub), [cu] "s"(CU), [cl] "s"(CL),
+                      [taba] "v"(tab[r + 1 < R ? r + 1 : r]), [syma] "v"(symA), [tabb] "v"(tab[r]), [symb] "v"(symB));
+                da = adn;
+                db = bdn;
+                put(q, r, recA);
+                put(q + 1, r - 1, recB);
+            }
+            {   // sub-step R: B row R-1
+                const uint32_t hub = R >= 2 ? (uint32_t)Hp[R - 2] : (uint32_t)topB;
+                uint32_t b0, b1, bdn;
+                asm(SO_CELL(b, "hp", "hu", "dr", "rec", "tabn", "sym")
+                    : [b0] "=&v"(b0), [b1] "=&v"(b1), [bdn] "=&v"(bdn), [hp] "+v"(Hp[R - 1]), [rec] "+v"(recB)
+                    : [dr] "v"(db), [hu] "v"(hub), [cu] "s"(CU), [cl] "s"(CL), [tabn] "v"(tab[R - 1]), [sym] "v"(symB));
+                put(q + 1, R - 1, recB);
+            }
+        };
+#undef SO_CELL
+#undef SO_CELL2
+        int ptop = corner;                       // 4 * H(r0 - 1, j0 + q - 1)
+        int q = qlo;
+        for (; q + 1 <= qhi; q += 2) {
+            const int ta = top_of(q), tb = top_of(q + 1);
+            column_pair(q, ta, tb, ptop);
+            ptop = tb;
         }
+        if (q == qhi) column(q, top_of(q), ptop);
     };
     auto tag = [&]() __attribute__((always_inline)) -> uint32_t {
         return (vw[(cq * RT + (cr >> 4)) * 64 + lane] >> (2 * (cr & 15))) & 3u;

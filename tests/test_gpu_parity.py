@@ -425,6 +425,30 @@ def test_t16_global_gotoh_screened_4096(engine, monkeypatch):
     assert engine.last_plan()[0] == sa.SA_KERNEL_INT32
 
 
+def test_t16_global_gotoh_screened_lut(engine):
+    """The screened T16 GlobalGotoh fill under a match table where DIFFERENT symbols match
+    (ADVICE r03): all-'A' against all-'a' with a case-insensitive table scores ~4096 although the
+    two sequences share no symbol, so the composition screen must count matches through the table
+    (sum over a of min(count of a, count of the Seq2 symbols matching a)) and send the pair to the
+    int32 re-run; purine/pyrimidine classes on DNA likewise.  Every pair against the oracle."""
+    gg = (-3, -1, 1, -1, True)
+    big = [(b"A" * 4096, b"a" * 4096),
+           (sa.synth_dna(95_101, 4096), sa.synth_dna(95_102, 4096).lower()),
+           (b"ACGT" * 1024, b"acgt" * 1024)]
+    rng = np.random.default_rng(43)
+    pairs = [(sa.synth_dna(96_500 + k, int(rng.integers(20, 120))), sa.synth_dna(97_500 + k, int(rng.integers(20, 120))).lower())
+             for k in range(1100)]
+    pairs[7], pairs[600], pairs[1099] = big
+    compare_with_oracle(engine, 3, gg, pairs, match="caseless")
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    pur = [(sa.synth_dna(95_200 + k, 4096), sa.synth_dna(95_300 + k, 4096)) for k in range(2)]
+    pur.append((b"AG" * 2048, b"GA" * 2048))
+    pairs = [(sa.synth_dna(98_000 + k, 60), sa.synth_dna(99_000 + k, 60)) for k in range(1100)]
+    pairs[3], pairs[700], pairs[1098] = pur
+    compare_with_oracle(engine, 3, gg, pairs, match="purine")
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+
+
 def test_endcell_replay_vs_oracle(engine, monkeypatch):
     """>= 1024 DNA SW pairs take the T16 plan with per-chunk maxima and the end-cell replay
     (sa_endcell.hip): one pair per wave at R = 32 (max_m 4200 -> 3 bands).  Cases: all-zero matrices (end cell = last cell), periodic sequences (many

@@ -93,6 +93,28 @@ def test_oracle_sw_score_batch_vs_golden():
     assert n > 200
 
 
+def test_oracle_sw_score_lanes_match_scalar():
+    """The 8-lane (AVX2) form of the linear-space SW score oracle, taken for runs of 8 pairs of equal
+    shape, returns exactly what the scalar form returns pair by pair (batches of one pair take the
+    scalar form): random and related DNA, every scoring kind, shapes 1 x n, m x 1 and square."""
+    import numpy as np
+    from util import oracle_sw_scores, pack_bytes
+    import seqalib_amd as sa
+    for (m, n) in ((1, 37), (37, 1), (64, 64), (150, 97), (301, 300)):
+        pairs = []
+        for k in range(16):
+            a = sa.synth_dna(7000 + 31 * k + m, m)
+            b = sa.synth_mutate(a, k)[:n] if k % 3 == 0 else sa.synth_dna(8000 + 17 * k + n, n)
+            b = (b + b"ACGT" * n)[:n]
+            pairs.append((a, b))
+        for args in ((-1, 1, -1), (-2, 2, -3), (-1, 2), (-2, 1, -1, False), (-1, 3, 1)):
+            s1, o1, s2, o2 = pack_bytes(pairs)
+            lanes = oracle_sw_scores(args, s1, o1, s2, o2, threads=2)
+            for p, (a, b) in enumerate(pairs):
+                one = oracle_sw_scores(args, *pack_bytes([(a, b)]), threads=1)
+                assert np.array_equal(lanes[p], one[0]), (m, n, args, p)
+
+
 def test_oracle_batch_matches_single():
     """oracle_batch (threaded, packed) returns exactly what oracle_align returns per pair."""
     import numpy as np
