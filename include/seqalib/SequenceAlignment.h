@@ -166,35 +166,68 @@ void build_from_ops(ContainerType& Seq1, ContainerType& Seq2, const sa_result& r
     }
 }
 
-// Shared getAlignment()/getAlignments() body of the four aligners.
+// Pairs per GPU call when a large batch is cut into chunks (run below): one chunk fills the chip's
+// 4 x 1,024 SIMD wave slots once (the score-only fill runs 4 single-wave workgroups per SIMD).
+constexpr size_t kChunkPairs = 4096;
+
+// Shared getAlignment()/getAlignments() body of the four aligners.  Building the std::list of
+// every pair (one allocation per Entry, as the reference's buildResult) dominates a large batch
+// end to end, so a batch of >= 2 chunks is aligned chunk by chunk and chunk g's lists are built on
+// the host threads while chunk g+1 runs on the GPU.
 template <int ALGO, typename Aligner, typename ContainerType, typename Ty, Ty Blank>
 std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std::pair<ContainerType*, ContainerType*>>& pairs,
                                             std::vector<sa_result>& res) {
     auto fn = self.getMatchOperation();
     const bool has_fn = !(fn == nullptr);
     const sa_scoring sc = self.getScoring().toC();
-    raw_vector<uint8_t> ops;
-    std::vector<uint64_t> off;
-    align<Ty>(ALGO, sc, fn, has_fn, pairs, res, ops, off);
-    std::vector<AlignedSequence<Ty, Blank>> out(pairs.size());
-    // Building the std::list of every pair dominates a large batch end to end (one allocation per
-    // Entry), and pairs are independent: split them over host threads.
-    auto build = [&](size_t p0, size_t p1) {
+    const size_t P = pairs.size();
+    std::vector<AlignedSequence<Ty, Blank>> out(P);
+    res.assign(P, sa_result{});
+    const size_t G = P >= 2 * kChunkPairs ? (P + kChunkPairs - 1) / kChunkPairs : 1;
+    // double-buffered chunk outputs: chunk g's lists are built from buffer g % 2
+    raw_vector<uint8_t> ops[2];
+    std::vector<uint64_t> off[2];
+    std::vector<sa_result> rc[2];
+    auto build = [&](size_t g, size_t p0, size_t p1) {
+        const size_t c0 = g * P / G;   // first pair of chunk g
         for (size_t p = p0; p < p1; ++p) {
-            build_from_ops<Ty, Blank>(*pairs[p].first, *pairs[p].second, res[p], ops.data() + off[p], out[p]);
-            const bool local = (ALGO == SA_SW || ALGO == SA_LOCAL_GOTOH) && !(res[p].flags & SA_FLAG_SIZE_HACK);
+            const sa_result& r = rc[g % 2][p - c0];
+            build_from_ops<Ty, Blank>(*pairs[p].first, *pairs[p].second, r, ops[g % 2].data() + off[g % 2][p - c0], out[p]);
+            const bool local = (ALGO == SA_SW || ALGO == SA_LOCAL_GOTOH) && !(r.flags & SA_FLAG_SIZE_HACK);
             if (local)
-                self.forceGlobal(*pairs[p].first, *pairs[p].second, out[p], res[p].start_i, res[p].start_j,
-                                 res[p].end_i, res[p].end_j);
+                self.forceGlobal(*pairs[p].first, *pairs[p].second, out[p], r.start_i, r.start_j, r.end_i, r.end_j);
         }
     };
-    const size_t P = pairs.size();
     PhaseTimer tm;
-    struct Lap {
-        PhaseTimer& t;
-        ~Lap() { t.lap("AlignedSequence lists"); }
-    } lap{tm};
-    parallel_pairs(P, host_threads(P), [&](size_t, size_t p0, size_t p1) { build(p0, p1); });
+    // the lists of chunk g, on a thread of their own (which fans out over the host threads)
+    struct Builder {
+        std::thread th;
+        std::exception_ptr err;
+        ~Builder() { join(); }
+        void join() {
+            if (th.joinable()) th.join();
+        }
+    } bld;
+    for (size_t g = 0; g < G; ++g) {
+        const size_t c0 = g * P / G, c1 = (g + 1) * P / G;
+        const std::vector<std::pair<ContainerType*, ContainerType*>> sub(pairs.begin() + c0, pairs.begin() + c1);
+        align<Ty>(ALGO, sc, fn, has_fn, G == 1 ? pairs : sub, rc[g % 2], ops[g % 2], off[g % 2]);
+        std::copy(rc[g % 2].begin(), rc[g % 2].end(), res.begin() + c0);
+        bld.join();   // chunk g-1's lists (they read buffer (g-1) % 2, which chunk g+1 reuses)
+        if (bld.err) std::rethrow_exception(bld.err);
+        tm.lap("GPU chunk (overlapped lists)");
+        bld.th = std::thread([&, g, c0, c1] {
+            try {
+                parallel_pairs(c1 - c0, host_threads(c1 - c0),
+                               [&](size_t, size_t q0, size_t q1) { build(g, c0 + q0, c0 + q1); });
+            } catch (...) {
+                bld.err = std::current_exception();
+            }
+        });
+    }
+    bld.join();
+    if (bld.err) std::rethrow_exception(bld.err);
+    tm.lap("AlignedSequence lists (last chunk)");
     return out;
 }
 

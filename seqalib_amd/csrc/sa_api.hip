@@ -2,6 +2,7 @@
 // workspace, batching and the host<->device plumbing around the fill and traceback kernels.
 #include <hip/hip_runtime.h>
 #include <limits.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -9,6 +10,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <chrono>
 #include <string>
@@ -795,7 +797,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 ep.hshift = v.so ? 0 : 2;
                 // on the fill stream, right after the fill: run beside the next call's fill (on the
                 // traceback stream) its 10,000 short waves slowed that fill by 4 % (measured)
-                e = launch_endcell(algo, pl.R, ep, sf);
+                e = v.so ? launch_endcell_so(pl.R, ep, sf) : launch_endcell(algo, pl.R, ep, sf);
                 if (e != hipSuccess) return hip_fail(c, e, "end-cell kernel launch");
             }
         }
@@ -931,21 +933,39 @@ int lg_hack_split(sa_ctx* c, const uint64_t* off1, const uint64_t* off2, uint32_
 }
 
 // Host copy of a large buffer on several threads (the caller's pageable memory <-> pinned
-// staging; one thread copies ~5-10 GB/s).  A process-wide pool of persistent workers (up to 15 +
-// the caller: the GPU box's 16-core share) takes 1 MiB slices of the copy: spawning threads per
-// 16 MiB piece cost ~1 ms per call and capped a copy at 4 threads.
+// staging; one thread copies ~5-10 GB/s).  A process-wide pool of persistent workers takes 1 MiB
+// slices of whatever copy jobs are posted; a caller copies slices of its own job too and returns as
+// soon as all of its bytes are done, so jobs of several contexts (sa_multi: one host thread per
+// device) run side by side instead of one after another, and no job waits for idle workers to
+// wake.  The pool is sized from the CPUs this process may use (affinity and cgroup quota -- a GPU
+// box shows all of its cores to hardware_concurrency() but grants a share).
+unsigned usable_cpus() {
+    unsigned n = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::min<unsigned>(n, (unsigned)std::max(1, CPU_COUNT(&set)));
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {   // cgroup v2: "<quota> <period>" or "max <period>"
+        char q[32] = {0};
+        unsigned long long per = 0;
+        if (fscanf(f, "%31s %llu", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0)
+            n = std::min<unsigned>(n, (unsigned)std::max<unsigned long long>(1, strtoull(q, nullptr, 10) / per));
+        fclose(f);
+    }
+    return n;
+}
+
 struct CopyPool {
+    struct Job {
+        uint8_t* dst;
+        const uint8_t* src;
+        uint64_t n;
+        std::atomic<uint64_t> next{0}, done{0};
+    };
+    static constexpr uint64_t kSlice = 1ull << 20;
     std::mutex mu;
     std::condition_variable cv, done_cv;
+    std::vector<std::shared_ptr<Job>> jobs;   // jobs with slices left
     std::vector<std::thread> workers;
-    uint8_t* dst = nullptr;
-    const uint8_t* src = nullptr;
-    uint64_t n = 0;
-    std::atomic<uint64_t> next{0};
-    size_t done = 0;         // workers finished with the current job (every worker takes part)
-    uint64_t gen = 0;        // job generation
     bool quit = false;
-    static constexpr uint64_t kSlice = 1ull << 20;
     explicit CopyPool(unsigned k) {
         for (unsigned t = 0; t < k; ++t) workers.emplace_back([this] { run(); });
     }
@@ -957,55 +977,64 @@ struct CopyPool {
         cv.notify_all();
         for (auto& w : workers) w.join();
     }
-    void slices() {
-        for (;;) {
-            const uint64_t a = next.fetch_add(kSlice);
-            if (a >= n) return;
-            memcpy(dst + a, src + a, std::min(kSlice, n - a));
+    // one slice of job j; false when it has none left
+    bool slice(Job& j) {
+        const uint64_t a = j.next.fetch_add(kSlice);
+        if (a >= j.n) return false;
+        const uint64_t k = std::min(kSlice, j.n - a);
+        memcpy(j.dst + a, j.src + a, k);
+        if (j.done.fetch_add(k) + k == j.n) {
+            std::lock_guard<std::mutex> g(mu);
+            done_cv.notify_all();
         }
+        return true;
     }
     void run() {
-        uint64_t seen = 0;
         std::unique_lock<std::mutex> lk(mu);
         for (;;) {
-            cv.wait(lk, [&] { return quit || gen != seen; });
+            cv.wait(lk, [&] { return quit || !jobs.empty(); });
             if (quit) return;
-            seen = gen;
+            std::shared_ptr<Job> j = jobs.front();
             lk.unlock();
-            slices();
+            if (!slice(*j)) {
+                lk.lock();
+                if (!jobs.empty() && jobs.front() == j) jobs.erase(jobs.begin());
+                continue;
+            }
             lk.lock();
-            if (++done == workers.size()) done_cv.notify_all();
         }
     }
-    void copy(void* d, const void* s, uint64_t bytes) {   // one job at a time (callers serialise)
-        std::unique_lock<std::mutex> lk(mu);
-        dst = (uint8_t*)d;
-        src = (const uint8_t*)s;
-        n = bytes;
-        next.store(0);
-        done = 0;
-        ++gen;
+    std::atomic<int> in_flight{0}, max_in_flight{0};   // copy jobs posted and not yet done
+    void copy(void* d, const void* s, uint64_t bytes) {
+        const int f = in_flight.fetch_add(1) + 1;
+        for (int m = max_in_flight.load(); f > m && !max_in_flight.compare_exchange_weak(m, f);) {}
+        auto j = std::make_shared<Job>();
+        j->dst = (uint8_t*)d;
+        j->src = (const uint8_t*)s;
+        j->n = bytes;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            jobs.push_back(j);
+        }
         cv.notify_all();
-        lk.unlock();
-        slices();
-        lk.lock();
-        // every worker reports the job (a late waker finds no slice left): the job's buffers
-        // are not touched after this returns
-        done_cv.wait(lk, [&] { return done == workers.size(); });
+        while (slice(*j)) {}
+        std::unique_lock<std::mutex> lk(mu);
+        done_cv.wait(lk, [&] { return j->done.load() == j->n; });
+        in_flight.fetch_sub(1);
+        // (a worker may still hold j to find it exhausted; it never touches dst / src again)
     }
 };
+CopyPool* g_copy_pool = nullptr;
 
 void par_copy(void* dst, const void* src, uint64_t n) {
     if (n < (4ull << 20)) {
         if (n) memcpy(dst, src, n);
         return;
     }
-    static std::mutex pool_mu;   // one pooled copy at a time (contexts on several host threads)
-    static CopyPool* pool = [] {
-        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        return new CopyPool(std::min(15u, hw > 1 ? hw - 1 : 1u));   // never destroyed: exit-safe
+    static CopyPool* pool = [] {   // never destroyed: exit-safe
+        const unsigned cpus = usable_cpus();
+        return g_copy_pool = new CopyPool(std::min(31u, cpus > 1 ? cpus - 1 : 1u));
     }();
-    std::lock_guard<std::mutex> g(pool_mu);
     pool->copy(dst, src, n);
 }
 
@@ -1196,8 +1225,10 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     }
     SA_HIP(c, hipStreamSynchronize(st));
     if (timing)
-        fprintf(stderr, "[seqalib host api] %u pairs, %u chunks: %.2f ms = staging in %.2f + waiting %.2f + copies out %.2f + other\n",
-                npairs, G, since(t_call), ms_in, ms_wait, ms_out);
+        fprintf(stderr, "[seqalib host api] %u pairs, %u chunks: %.2f ms = staging in %.2f + waiting %.2f + copies out %.2f + other"
+                "; copy pool %zu workers, max %d copy jobs in flight\n",
+                npairs, G, since(t_call), ms_in, ms_wait, ms_out, g_copy_pool ? g_copy_pool->workers.size() : (size_t)0,
+                g_copy_pool ? g_copy_pool->max_in_flight.load() : 0);
     return SA_OK;
 }
 
@@ -1346,6 +1377,8 @@ int sa_trim(sa_ctx* c) {
     c->io = nullptr; c->io_bytes = 0;
     c->split = nullptr; c->split_bytes = 0;
     c->dc.release();
+    c->stage.reset();    // the host API's pinned staging (~80 MB each way for the headline batch)
+    c->ostage.reset();
     return SA_OK;
 }
 

@@ -69,7 +69,12 @@ struct HostBuf {
     T& operator[](size_t k) { return p[k]; }
     const T& operator[](size_t k) const { return p[k]; }
     T* data() { return p; }
-    ~HostBuf() { if (p) (void)hipHostFree(p); }
+    void reset() {   // give the pinned pages back (sa_trim)
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    ~HostBuf() { reset(); }
 };
 
 // 8 x the code of byte b in a 16-bit sweep's alphabet (sym_pack sp: byte c = the symbol of code c,

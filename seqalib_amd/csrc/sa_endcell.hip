@@ -156,6 +156,131 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
     }
 }
 
+// Score-only SW fill (sa_fill_impl.h SO): the fill tracked the odd rows at the odd steps of its
+// steady chunks (every cell of ramp chunks) and stored, per (band, chunk), the wave's maximum of
+// the tracked cells; every cell is at most its tracked neighbour - 2G, so S lies in
+// [smax, smax - 2G] and only the chunks whose tracked maximum reaches smax + 2G can hold it.  This
+// kernel replays every such chunk of every band (all 64 lanes, from the fill's snapshots, as
+// endcell_kernel does), keeps per lane the lexicographically largest (H, i, j) -- the reference's
+// last row-major maximum, SASmithWaterman.h:110 -- and reduces over the wave.  An all-zero matrix
+// (smax = 0) replays every chunk and ends at (m, n), as the reference does.
+template <int R>
+__global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
+    if (sa_skip(P.sel, P.sel_want)) return;
+    const int lane = threadIdx.x;
+    const uint32_t slot = blockIdx.x;
+    if (slot >= P.count) return;
+    const uint32_t symp = P.prof[4];
+    const uint32_t pidx = P.pair_base + slot;
+    sa_result res = P.res[pidx];
+    if (res.reserved == 0 || (res.flags & (SA_FLAG_BAD_SHAPE | kFlagRetry))) return;   // uniform over the wave
+    const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
+    const int m = (int)(P.off1[pidx + 1] - o1);
+    const int n = (int)(P.off2[pidx + 1] - o2);
+    const uint8_t* s1 = P.seq1 + o1;
+    const uint8_t* s2 = P.seq2 + o2;
+    constexpr int BAND = kWave * R;
+    const int B = (m + BAND - 1) / BAND;
+    const int nch = (int)chunks_per_band((uint32_t)n);
+    const int G = P.gap;
+    const int thr = res.score + 2 * G;   // chunks whose tracked maximum reaches this may hold S
+    const int32_t* cm = P.snap_m + (uint64_t)slot * P.snap_p_slot;
+    int bv = -1, bi = -1, bj = -1;       // this lane's best (H, row, column), 0-based
+    __shared__ uint8_t s_sym[kWave + kChunk];
+    __shared__ int s_top[kChunk];
+    for (int b = 0; b < B; ++b) {
+        const int row0 = b * BAND + lane * R;
+        uint32_t tab[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int row = row0 + r;
+            tab[r] = row < m ? P.prof[ec_code8(symp, s1[row]) >> 3] : 0u;
+        }
+        const int32_t* top = b > 0 ? P.rowbuf + (uint64_t)slot * P.rowbuf_slot + (uint64_t)(b - 1) * P.max_n : nullptr;
+        for (int base = 0; base < nch; base += kWave) {
+            const int ccl = base + lane;
+            uint64_t hits = __builtin_amdgcn_ballot_w64(ccl < nch && cm[(uint64_t)b * P.snap_nch + ccl] >= thr);
+            while (hits) {
+                const int cc = base + (int)__builtin_ctzll(hits);
+                hits &= hits - 1;
+                int Hp[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) Hp[r] = 0;
+                int prev_up = 0;
+                if (cc > 0) {
+                    const uint64_t e = (uint64_t)b * P.snap_nch + (cc - 1);
+                    const uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + e * (R / 2) * kWave + lane;
+#pragma unroll
+                    for (int q = 0; q < R / 2; ++q) {
+                        const uint32_t w = sh[q * kWave];
+                        Hp[2 * q] = (int)(w & 0xffffu);
+                        Hp[2 * q + 1] = (int)(w >> 16);
+                    }
+                    prev_up = (int)(P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] & 0xffff);
+                }
+                __syncthreads();   // (a previous candidate's reads of the staging arrays)
+                for (int k = lane; k < kWave + kChunk; k += kWave) {
+                    const int j = cc * kChunk - (kWave - 1) + k;
+                    s_sym[k] = (uint8_t)(j >= 0 && j < n ? ec_code8(symp, s2[j]) : 0u);
+                }
+                if (lane < kChunk) {
+                    const int j = cc * kChunk + lane;
+                    s_top[lane] = (top && j < n) ? ec_top(top + j) : 0;
+                }
+                __syncthreads();
+                int hl = Hp[R - 1];
+                for (int q = 0; q < kChunk; ++q) {
+                    const int s = cc * kChunk + q;
+                    const int j0 = s - lane;
+                    int up_h = __shfl_up(hl, 1);
+                    if (lane == 0) up_h = s_top[q];
+                    if (j0 >= 0 && j0 < n) {
+                        if (j0 == 0) {   // the lane's first column: the matrix border
+                            prev_up = 0;
+#pragma unroll
+                            for (int r = 0; r < R; ++r) Hp[r] = 0;
+                        }
+                        const uint32_t sym = s_sym[q - lane + (kWave - 1)];
+                        int hd = prev_up, hu = up_h;
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            // profile byte = 4s+3 (signed); the builtin returns unsigned: shift as int
+                            const int sub = ((int)__builtin_amdgcn_sbfe(tab[r], sym, 8) - 3) >> 2;
+                            int H = hd + sub;
+                            H = max(H, hu + G);
+                            H = max(H, Hp[r] + G);
+                            H = max(H, 0);
+                            hd = Hp[r];
+                            Hp[r] = H;
+                            hu = H;
+                            const int row = row0 + r;
+                            if (row < m && (H > bv || (H == bv && (row > bi || (row == bi && j0 > bj))))) {
+                                bv = H;
+                                bi = row;
+                                bj = j0;
+                            }
+                        }
+                        prev_up = up_h;
+                        hl = Hp[R - 1];
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const int ov = __shfl_xor(bv, off), oi = __shfl_xor(bi, off), oj = __shfl_xor(bj, off);
+        if (ov > bv || (ov == bv && (oi > bi || (oi == bi && oj > bj)))) { bv = ov; bi = oi; bj = oj; }
+    }
+    if (lane == 0) {
+        res.score = bv;
+        res.end_i = bi + 1;
+        res.end_j = bj + 1;
+        res.reserved = 0;
+        P.res[pidx] = res;
+    }
+}
+
 // LocalGotoh (T16 affine CMAX fill): the same replay on the three-state recurrence
 // (SALocalGotoh.h:108-130).  The fill's snapshot of a lane holds its R values of M (8M), then its
 // R values of Iy (8Iy + 2) and the Ix of its last row (8Ix + 4, or 0 where the fill's clamped Ix
@@ -362,6 +487,18 @@ hipError_t launch_split_reduce(int algo, const SplitReduceParams& p, hipStream_t
         case SA_NW: hipLaunchKernelGGL(split_reduce_kernel<SA_NW>, grid, block, 0, stream, p); break;
         case SA_LOCAL_GOTOH: hipLaunchKernelGGL(split_reduce_kernel<SA_LOCAL_GOTOH>, grid, block, 0, stream, p); break;
         case SA_GLOBAL_GOTOH: hipLaunchKernelGGL(split_reduce_kernel<SA_GLOBAL_GOTOH>, grid, block, 0, stream, p); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_endcell_so(int R, const EndcellParams& p, hipStream_t stream) {
+    const dim3 grid(p.count), block(64);
+    switch (R) {
+        case 4: hipLaunchKernelGGL(endcell_so_kernel<4>, grid, block, 0, stream, p); break;
+        case 8: hipLaunchKernelGGL(endcell_so_kernel<8>, grid, block, 0, stream, p); break;
+        case 16: hipLaunchKernelGGL(endcell_so_kernel<16>, grid, block, 0, stream, p); break;
+        case 32: hipLaunchKernelGGL(endcell_so_kernel<32>, grid, block, 0, stream, p); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -532,6 +532,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     // CMAX: the lane's best chunk of the band so far as one key H << 12 | chunk + 1 (H < 2^13 by
     // t16_ok, chunks < 4096 since n < 65535): highest score, then last chunk
     uint32_t lkey = 0;
+    uint32_t smax = 0;   // SO: the largest tracked cell of the pair (wave-uniform), a lower bound of S
     int hl = 0, xl = 0, sym = 0, prev_up = 0;
     int row0 = 0;
     // Running best of this lane over its bands: (score, i, j), 1-based cell.
@@ -701,8 +702,19 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                             : [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r])
                             : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL));
                     }
-                    if (r & 1)   // the lane's chunk maximum, one v_max3_u32 per two rows (H >= 0)
+                    // The lane's chunk maximum (H >= 0, one v_max3_u32 per two tracked cells).  Steady
+                    // chunks track only the odd rows at the odd steps: every cell (i, j) of the chunk
+                    // has the tracked cell (i | 1, j | 1) of the same lane and chunk with
+                    // H(i, j) <= H(i, j + 1) - G <= H(i + 1, j + 1) - 2G (its left / up candidates),
+                    // so the lane's true maximum is <= cml - 2G and the end-cell replay
+                    // (endcell_so_kernel) re-runs every chunk that could hold it.  Ramp chunks
+                    // (columns past the matrix edge) track every cell.
+                    if constexpr (STEADY) {
+                        if (ODD && (r & 3) == 3)
+                            asm("v_max3_u32 %0, %0, %1, %2" : "+v"(cml) : "v"(Hp[r >= 2 ? r - 2 : 0]), "v"(Hp[r]));
+                    } else if (r & 1) {
                         asm("v_max3_u32 %0, %0, %1, %2" : "+v"(cml) : "v"(Hp[r >= 1 ? r - 1 : 0]), "v"(Hp[r]));
+                    }
                     Hc = Hp[r];
                 } else if constexpr (T16) {
                     // One asm block per cell (plain VALU->VALU dependences need no wait
@@ -1150,8 +1162,17 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                     if (kC + kChunk - 1 < lane) cml = 0;
                     const uint32_t ck = chunk + 1;
                     const uint64_t e = (uint64_t)band * P.snap_nch + chunk;
-                    P.snap_m[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = (int32_t)cml;
-                    lkey = max(lkey, (cml >> CSH) << 12 | ck);
+                    if constexpr (SO) {
+                        // one word per (band, chunk): the wave's maximum of the tracked cells
+                        uint32_t wm = cml;
+#pragma unroll
+                        for (int off = 32; off >= 1; off >>= 1) wm = max(wm, (uint32_t)__shfl_xor((int)wm, off));
+                        if (lane == 0) P.snap_m[(uint64_t)slot * P.snap_p_slot + e] = (int32_t)wm;
+                        smax = max(smax, wm);
+                    } else {
+                        P.snap_m[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = (int32_t)cml;
+                        lkey = max(lkey, (cml >> CSH) << 12 | ck);
+                    }
                     cml = 0;
                     if (chunk + 1 < nch) {   // state entering chunk + 1, for the end-cell replay
                         // R 16-bit values (affine: then the R Iy values and the last row's Ix)
@@ -1262,6 +1283,11 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                 // empty input: SW keeps MaxScore = INT_MIN, (MaxRow, MaxCol) = (0, 0);
                 // LocalGotoh reads M[0][0] = 0 there
                 r.score = (ALG == SA_SW) ? INT_MIN : 0;
+            } else if constexpr (SO) {
+                // S >= smax and S <= smax - 2G: endcell_so_kernel finds S and the last row-major cell
+                h = (int)smax - 2 * G;   // (the retry test below: the largest S this pair may have)
+                r.score = (int)smax; r.end_i = 0; r.end_j = 0;
+                r.reserved = 1;
             } else if constexpr (CMAX) {
                 r.score = h; r.end_i = bi; r.end_j = 0;
                 r.reserved = (uint32_t)bjj;   // chunk + 1: sa_endcell.hip resolves the column

@@ -238,4 +238,6 @@ hipError_t launch_traceback_wave(int algo, int R, bool lut, const TbParams& p, h
 hipError_t launch_endcell(int algo, int R, const EndcellParams& p, hipStream_t stream);
 // Score-only SW fills: the block-recompute traceback (sa_traceback_so.hip), R in {4, 8, 16, 32}.
 hipError_t launch_traceback_so(int R, const TbParams& p, hipStream_t stream);
+// Score-only SW fills: the end cell from the per-(band, chunk) maxima of the tracked cells.
+hipError_t launch_endcell_so(int R, const EndcellParams& p, hipStream_t stream);
 }  // namespace sa

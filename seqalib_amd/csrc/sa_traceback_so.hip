@@ -355,14 +355,288 @@ __global__ __launch_bounds__(64) void traceback_so_kernel(TbParams P) {
     P.res[pidx] = res;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Four lanes per pair (a quad, 16 pairs per wave).  The walk is the same, executed identically by
+// the quad's four lanes (sublane 0 writes the ops); a block's recompute is split by rows: sublane k
+// owns rows k*R/4 .. (k+1)*R/4 - 1 of the block and the quad sweeps the block's columns as a
+// four-lane anti-diagonal wavefront (sublane k at column q at sub-step q - qlo + k, its row above
+// from sublane k-1's previous sub-step by DPP quad_perm) -- the fill's own schedule on four lanes.
+// A lone wave's serial recompute per block drops from 32 columns x R rows of dependent cells to
+// (32 + 3) sub-steps x R/4 rows, and the wave's registers (R/4 rows of state) stay few, so the
+// traceback beside the next call's fill displaces fewer of its waves.
+constexpr int kSo4Pairs = 16;
+template <int R>
+struct So4Lds {
+    static constexpr int kTags = 0;                         // [column q][lane] words
+    static constexpr int kEdge = kTags + 32 * 64 * 4;       // [lane] 16 B: packet (lane & 3) of quad
+    static constexpr int kEdge2 = kEdge + 64 * 16;          // [lane] 16 B: packet 4 (sublane 0)
+    static constexpr int kRowC = kEdge2 + 64 * 16;          // [quad][32] row codes (8 x code)
+    static constexpr int kColC = kRowC + kSo4Pairs * 32;    // [quad][32] column codes
+    static constexpr int kOps = kColC + kSo4Pairs * 32;     // [quad][kSoOps] op bytes of a round
+    static constexpr int kBytes = kOps + kSo4Pairs * kSoOps;
+};
+
+template <int R>
+__global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
+    using L = So4Lds<R>;
+    constexpr int RS = R / 4;   // rows per sublane
+    constexpr int BAND = kWave * R;
+    static_assert(R >= 4 && R % 4 == 0 && RS <= 16, "four sublanes of <= 16 rows");
+    __shared__ __attribute__((aligned(16))) uint8_t s_so[L::kBytes];
+    typedef volatile uint8_t __attribute__((address_space(3))) lds_u8;
+    typedef volatile uint32_t __attribute__((address_space(3))) lds_u32;
+    typedef volatile uint16_t __attribute__((address_space(3))) lds_u16;
+    lds_u8* const vb = (lds_u8*)s_so;
+    lds_u32* const vw = (lds_u32*)s_so;
+    const int lane = threadIdx.x, quad = lane >> 2, sub = lane & 3;
+    const uint32_t slot = blockIdx.x * kSo4Pairs + quad;
+    // a quad whose pair is not walked here leaves as a whole (the four lanes agree)
+    bool live = slot < P.count;
+    const uint32_t pidx = P.pair_base + (live ? slot : 0);
+    sa_result res = P.res[pidx];
+    live = live && !(res.flags & SA_FLAG_BAD_SHAPE) && tb_mine(P, res.flags);
+    if (__builtin_amdgcn_ballot_w64(live) == 0) return;
+    res.flags &= ~(kFlagRetry | kFlagRedo | kFlagRerun);
+    const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
+    const int m = (int)(P.off1[pidx + 1] - o1);
+    const int n = (int)(P.off2[pidx + 1] - o2);
+    const uint8_t* s1 = P.seq1 + o1;
+    const uint8_t* s2 = P.seq2 + o2;
+    typedef uint8_t __attribute__((address_space(1))) glb_u8;
+    glb_u8* ops = (glb_u8*)(P.ops + o1 + o2 + pidx);
+    const uint8_t* const dir = P.dirs + (uint64_t)(live ? slot : 0) * P.dir_slot;
+    const uint64_t band_stride = P.band_stride;
+    const uint32_t npk = (uint32_t)(band_stride / (kWave * 16));
+    const uint32_t* const sh_base = P.snap_h + (uint64_t)(live ? slot : 0) * P.snap_h_slot;
+    const int32_t* const sp_base = P.snap_p + (uint64_t)(live ? slot : 0) * P.snap_p_slot;
+    const uint32_t snap_nch = P.snap_nch;
+    const uint32_t symp = P.prof[4];
+    const uint32_t pf0 = P.prof[0], pf1 = P.prof[1], pf2 = P.prof[2], pf3 = P.prof[3];
+    uint32_t mt = 0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t sa_ = (symp >> (8 * a)) & 255u, sb_ = (symp >> (8 * b)) & 255u;
+            const bool v = P.lutbits ? ((P.lutbits[(sa_ << 3) | (sb_ >> 5)] >> (sb_ & 31u)) & 1u) != 0 : sa_ == sb_;
+            mt |= (v ? 1u : 0u) << (a * 4 + b);
+        }
+    const bool allow = P.allow != 0;
+    const int G = P.gap, MA = P.match, MI = P.mismatch;
+    const uint32_t CU = (uint32_t)(-(4 * G + 2)) & 0xffffu;
+    const uint32_t CL = (uint32_t)(4 * G + 1) & 0xffffu;
+
+    uint32_t k = 0, k0 = 0;
+    const int opb = L::kOps + quad * kSoOps;
+    auto emit = [&](uint8_t op) __attribute__((always_inline)) {
+        vb[opb + (k - k0)] = op;   // (the quad's four lanes write the same byte)
+        ++k;
+    };
+    auto flush = [&]() __attribute__((always_inline)) {
+        if (sub == 0)
+            for (uint32_t q = 0; q < k - k0; ++q) ops[k0 + q] = vb[opb + q];
+        k0 = k;
+    };
+    int wb = -1, wt = 0, wc = 0;
+    int cb = 0, ct = 0, cc = 0, cr = 0, cq = 0;
+    auto locate = [&](int i, int j) __attribute__((always_inline)) {
+        const int ii = i - 1;
+        cb = ii / BAND;
+        const int rem = ii - cb * BAND;
+        ct = rem / R;
+        cr = rem - ct * R;
+        const int s = j - 1 + ct;
+        cc = s >> 5;
+        cq = s & 31;
+    };
+    auto ready = [&](int i, int j) __attribute__((always_inline)) -> bool {
+        if (k - k0 >= (uint32_t)kSoOps) return false;
+        locate(i, j);
+        return cb == wb && ct == wt && cc == wc;
+    };
+    // recompute the block holding (i, j), columns up to j; every lane of a live quad takes part
+    // (a finished or dead quad runs the same sub-step loop on a zero-width column range)
+    auto recompute = [&](bool act, int i, int j) __attribute__((always_inline)) {
+        int r0 = 0, j0 = 0, qlo = 0, qhi = -1, slo = 0, pk0 = 0, bp = 0, tp = 0;
+        bool has_top = false, has_left = false;
+        if (act) {
+            locate(i, j);
+            wb = cb; wt = ct; wc = cc;
+            r0 = cb * BAND + ct * R;
+            j0 = 32 * cc - ct;
+            qlo = j0 < 0 ? -j0 : 0;
+            qhi = j - 1 - j0;
+            has_top = !(cb == 0 && ct == 0);
+            bp = ct > 0 ? cb : cb - 1;
+            tp = ct > 0 ? ct - 1 : kWave - 1;
+            slo = j0 + tp;
+            pk0 = slo >> 3;
+            has_left = cc > 0 && j0 >= 1;
+            if (has_top) {   // the top row's five packets: sublane k loads packet k, sublane 0 also packet 4
+                const uint8_t* base = dir + (uint64_t)bp * band_stride;
+                const int pk = pk0 + sub;
+                if (pk >= 0 && (uint32_t)pk < npk)
+                    __builtin_amdgcn_global_load_lds((so_gptr)(base + ((uint64_t)pk * kWave + tp) * 16),
+                                                     (so_lptr)(s_so + L::kEdge), 16, 0, 0);
+                const int pk4 = pk0 + 4;
+                if (sub == 0 && pk4 >= 0 && (uint32_t)pk4 < npk)
+                    __builtin_amdgcn_global_load_lds((so_gptr)(base + ((uint64_t)pk4 * kWave + tp) * 16),
+                                                     (so_lptr)(s_so + L::kEdge2), 16, 0, 0);
+            }
+        }
+        // this sublane's rows: left column, corner (the row above its first row, column j0 - 1)
+        int Hp[RS];
+        int corner = 0;
+        uint32_t tab[RS];
+#pragma unroll
+        for (int r = 0; r < RS; ++r) { Hp[r] = 0; tab[r] = pf0; }
+        if (act) {
+            const int rs0 = sub * RS;   // block-relative first row
+            if (has_left) {
+                const uint64_t e = (uint64_t)cb * snap_nch + (cc - 1);
+                const uint32_t* sh = sh_base + e * (R / 2) * kWave + ct;
+#pragma unroll
+                for (int r = 0; r < RS; ++r) {
+                    const int rr = rs0 + r;
+                    const uint32_t w = sh[(rr >> 1) * kWave];
+                    Hp[r] = (int)((rr & 1) ? (w >> 16) : (w & 0xffffu)) << 2;
+                }
+                if (rs0 > 0) {
+                    const uint32_t w = sh[((rs0 - 1) >> 1) * kWave];
+                    corner = (int)(((rs0 - 1) & 1) ? (w >> 16) : (w & 0xffffu)) << 2;
+                } else if (r0 > 0) {
+                    corner = (sp_base[e * kWave + ct] & 0xffff) << 2;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < RS; ++r) {
+                const int row = r0 + rs0 + r;
+                const uint32_t c8 = row < m ? so_code8(symp, s1[row]) : 0u;
+                tab[r] = c8 == 0 ? pf0 : c8 == 8 ? pf1 : c8 == 16 ? pf2 : pf3;
+                vb[L::kRowC + quad * 32 + rs0 + r] = (uint8_t)c8;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int q = sub * 8 + e, jj = j0 + q;
+                vb[L::kColC + quad * 32 + q] = (uint8_t)(q >= qlo && q <= qhi && jj < n ? so_code8(symp, s2[jj]) : 0u);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the edge DMA and the code stores
+        // sub-steps: sublane k at column qlo + u - k; its row above from sublane k-1 (DPP)
+        int hl = Hp[RS - 1];
+        int prev_up = corner;
+        int nmax = qhi - qlo + 1 + 3;   // sub-steps of this quad; the wave runs the most of any
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
+        for (int u = 0; u < nmax; ++u) {
+            const int q = qlo + u - sub;
+            int up_h = __builtin_amdgcn_mov_dpp(hl, 0x90, 0xf, 0xf, false);   // quad_perm [0,0,1,2]
+            const bool on = act && q >= qlo && q <= qhi;
+            if (sub == 0) {
+                int top = 0;
+                if (on && has_top) {
+                    const int s = slo + q;
+                    const int d = (s >> 3) - pk0;
+                    const int off = d < 4 ? L::kEdge + (quad * 4 + d) * 16 : L::kEdge2 + quad * 64;
+                    top = (int)((lds_u16*)(s_so + off + (s & 7) * 2))[0] << 2;
+                }
+                up_h = top;
+            }
+            if (on) {
+                const uint32_t sym = vb[L::kColC + quad * 32 + q];
+                uint32_t dcur;
+                asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(dcur) : "v"(tab[0]), "v"(sym), "v"(prev_up));
+                uint32_t hu = (uint32_t)up_h, rec = 0;
+#pragma unroll
+                for (int r = 0; r < RS; ++r) {
+                    uint32_t a0, a1, adn;
+                    asm("v_add_u16 %[a0], %[cl], %[hp]\n\t"
+                        "v_bfe_i32 %[adn], %[tabn], %[sym], 8\n\t"
+                        "v_add_u16 %[adn], %[hp], %[adn]\n\t"
+                        "v_sub_u16_e64 %[a1], %[hu], %[cu] clamp\n\t"
+                        "v_max_i16 %[a0], %[dr], %[a0]\n\t"
+                        "v_max_i16 %[a0], %[a1], %[a0]\n\t"
+                        "v_and_b32 %[hp], -4, %[a0]\n\t"
+                        "v_alignbit_b32 %[rec], %[a0], %[rec], 2"
+                        : [a0] "=&v"(a0), [a1] "=&v"(a1), [adn] "=&v"(adn), [hp] "+v"(Hp[r]), [rec] "+v"(rec)
+                        : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL),
+                          [tabn] "v"(tab[r + 1 < RS ? r + 1 : r]), [sym] "v"(sym));
+                    dcur = adn;
+                    hu = (uint32_t)Hp[r];
+                }
+                vw[q * 64 + lane] = RS == 16 ? rec : rec >> (32 - 2 * RS);   // row r at bits 2r
+                prev_up = up_h;
+                hl = Hp[RS - 1];
+            }
+        }
+    };
+    auto tag = [&]() __attribute__((always_inline)) -> uint32_t {
+        return (vw[cq * 64 + quad * 4 + cr / RS] >> (2 * (cr % RS))) & 3u;
+    };
+    auto cell_match = [&]() __attribute__((always_inline)) -> bool {
+        const uint32_t a = (vb[L::kRowC + quad * 32 + cr] >> 3) & 3u;
+        const uint32_t b = (vb[L::kColC + quad * 32 + cq] >> 3) & 3u;
+        return ((mt >> (a * 4 + b)) & 1u) != 0;
+    };
+
+    int i = res.end_i, j = res.end_j, V = res.score;
+    if (m == 0 || n == 0) { i = 0; j = 0; }
+    bool fin = !live, parked = true;
+    for (;;) {
+        if (__builtin_amdgcn_ballot_w64(!fin && !parked) == 0) {
+            if (__builtin_amdgcn_ballot_w64(!fin) == 0) break;
+            if (!fin) flush();
+            recompute(!fin, i, j);   // every lane: the sub-step loop uses DPP across the quad
+            if (!fin) parked = false;
+        }
+        if (!fin && !parked) {
+            if (!(i > 0 && j > 0) || V == 0) {   // SASmithWaterman.h: stop on an edge or at H == 0
+                fin = true;
+            } else if (!ready(i, j)) {
+                parked = true;
+            } else {
+                const uint32_t f = tag();
+                const bool dg = f == 3u, up = f == 2u;
+                const bool v = dg && cell_match();
+                emit(dg ? (v ? 'M' : (allow ? 'S' : 'X')) : (up ? 'U' : 'L'));
+                V -= dg ? (v ? MA : MI) : G;
+                i -= (dg || up) ? 1 : 0;
+                j -= up ? 0 : 1;
+            }
+        }
+    }
+    if (live) {
+        flush();
+        if (sub == 0) {
+            res.start_i = i;
+            res.start_j = j;
+            res.nops = k;
+            P.res[pidx] = res;
+        }
+    }
+}
+
+// SEQALIB_TB_SO=1: one lane per pair (traceback_so_kernel); default four lanes per pair.
 hipError_t launch_traceback_so(int R, const TbParams& p, hipStream_t stream) {
     const dim3 block(64);
-    const dim3 grid((p.count + 63) / 64);
+    const char* e = getenv("SEQALIB_TB_SO");
+    if (e && e[0] == '1') {
+        const dim3 grid((p.count + 63) / 64);
+        switch (R) {
+            case 4: hipLaunchKernelGGL(traceback_so_kernel<4>, grid, block, 0, stream, p); break;
+            case 8: hipLaunchKernelGGL(traceback_so_kernel<8>, grid, block, 0, stream, p); break;
+            case 16: hipLaunchKernelGGL(traceback_so_kernel<16>, grid, block, 0, stream, p); break;
+            case 32: hipLaunchKernelGGL(traceback_so_kernel<32>, grid, block, 0, stream, p); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    const dim3 grid((p.count + kSo4Pairs - 1) / kSo4Pairs);
     switch (R) {
-        case 4: hipLaunchKernelGGL(traceback_so_kernel<4>, grid, block, 0, stream, p); break;
-        case 8: hipLaunchKernelGGL(traceback_so_kernel<8>, grid, block, 0, stream, p); break;
-        case 16: hipLaunchKernelGGL(traceback_so_kernel<16>, grid, block, 0, stream, p); break;
-        case 32: hipLaunchKernelGGL(traceback_so_kernel<32>, grid, block, 0, stream, p); break;
+        case 4: hipLaunchKernelGGL(traceback_so4_kernel<4>, grid, block, 0, stream, p); break;
+        case 8: hipLaunchKernelGGL(traceback_so4_kernel<8>, grid, block, 0, stream, p); break;
+        case 16: hipLaunchKernelGGL(traceback_so4_kernel<16>, grid, block, 0, stream, p); break;
+        case 32: hipLaunchKernelGGL(traceback_so4_kernel<32>, grid, block, 0, stream, p); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

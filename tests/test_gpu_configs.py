@@ -220,3 +220,30 @@ def test_multi_context_config5_shard_matches_single(engine):
     assert res.tobytes() == ref.tobytes()
     assert ops.tobytes() == ref_ops.tobytes()
     print(f"single context {1e3 * (t1 - t0):.1f} ms, two contexts on one GPU {1e3 * (t3 - t2):.1f} ms")
+
+
+def test_multi_engine_four_contexts_stage_concurrently(engine, capfd, monkeypatch):
+    """One process, four contexts (MultiEngine([0, 0, 0, 0]) -- four devices' host threads on the
+    one-GPU box): results identical to a single context, and the host API's staging copies of the
+    four contexts run side by side in the shared copy pool (SEQALIB_HOST_TIMING reports the most copy
+    jobs ever in flight; one process-wide lock would keep it at 1)."""
+    from seqalib_amd.multi import MultiEngine
+    s1, o1, s2, o2 = sa.synth_dna_batch(8_100_000_000, 4096, 4096, 4096, threads=THREADS)
+    sc = sa.ScoringSystem(*SW)
+    ref, ref_ops = engine.align_packed(0, sc, s1, o1, s2, o2)
+    me = MultiEngine([0, 0, 0, 0])
+    try:
+        me.align_packed(0, sc, s1, o1, s2, o2)   # warm the contexts' workspaces
+        capfd.readouterr()
+        monkeypatch.setenv("SEQALIB_HOST_TIMING", "1")
+        res, ops = me.align_packed(0, sc, s1, o1, s2, o2)
+        err = capfd.readouterr().err
+    finally:
+        me.close()
+    assert res.tobytes() == ref.tobytes()
+    assert ops.tobytes() == ref_ops.tobytes()
+    lines = [ln for ln in err.splitlines() if ln.startswith("[seqalib host api]")]
+    assert len(lines) == 4, err[-2000:]
+    inflight = max(int(ln.split("max ")[1].split(" copy jobs")[0]) for ln in lines)
+    print("\n".join(lines))
+    assert inflight >= 2, lines

@@ -2,7 +2,7 @@
 started by torch.distributed.run, gloo only for the barrier and the max-over-ranks timing, every
 rank aligning its own shard through the device API.  On a one-GPU box both ranks run on GPU 0
 (SEQALIB_BENCH_DEVICE=0); the ranks are spawned as child processes (never an exec of this
-process).  Checks: each rank's sampled pairs bit-exact vs the oracle, distinct shards, and the
+process).  Checks: each rank's pairs bit-exact vs the oracle (every end cell, sampled op streams), distinct shards, and the
 reported ms_per_step = the max over ranks."""
 import json
 import os
@@ -37,7 +37,8 @@ def test_two_hip_ranks_gloo(tmp_path, length):
     ranks = [json.load(open(tmp_path / f"rank{k}.json")) for k in (0, 1)]
     for rr in ranks:
         assert rr["world"] == 2
-        assert rr["checked"] == 2 and rr["bad"] == 0 and rr["flags"] == 0, rr
+        par = rr["parity"]
+        assert par["exact"] and par["end_cells"] == "40/40" and rr["flags"] == 0, rr
     assert ranks[0]["seed_base"] != ranks[1]["seed_base"]
     slowest = max(rr["own_s"] for rr in ranks)
     for rr in ranks:

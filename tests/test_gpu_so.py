@@ -25,17 +25,21 @@ THREADS = 16
 FIELDS = ("score", "end_i", "end_j", "start_i", "start_j", "nops", "flags")
 
 
-def run(engine, so, *batch, scoring=SW, lut=None):
-    old = os.environ.get("SEQALIB_SO")
+def run(engine, so, *batch, scoring=SW, lut=None, tb="4"):
+    """so: score-only fill (else SEQALIB_SO=0, tagged records); tb: SEQALIB_TB_SO, the score-only
+    traceback with four lanes per pair ("4", default) or one ("1")."""
+    old = {k: os.environ.get(k) for k in ("SEQALIB_SO", "SEQALIB_TB_SO")}
     os.environ["SEQALIB_SO"] = "1" if so else "0"
+    os.environ["SEQALIB_TB_SO"] = tb
     try:
         res, ops = engine.align_packed(0, sa.ScoringSystem(*scoring), *batch, lut=lut)
         plan = engine.last_plan()
     finally:
-        if old is None:
-            del os.environ["SEQALIB_SO"]
-        else:
-            os.environ["SEQALIB_SO"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     return res.copy(), ops.copy(), plan
 
 
@@ -87,12 +91,14 @@ def ragged_batch(seed, npairs, maxlen):
     return s1, o1, s2, o2
 
 
-@pytest.mark.parametrize("maxlen,R", [(200, 4), (500, 8), (1000, 16), (2000, 32), (3000, 32)])
-def test_so_ragged_matches_tagged_and_oracle(engine, maxlen, R):
-    """Ragged batches on every score-only plan (R = 4 .. 32, one and two bands): identical to the
-    tagged path on every pair, and to the full-matrix oracle on a sample."""
+@pytest.mark.parametrize("maxlen,R,tb", [(200, 4, "4"), (500, 8, "4"), (1000, 16, "4"), (2000, 32, "4"), (3000, 32, "4"),
+                                         (200, 4, "1"), (3000, 32, "1")])
+def test_so_ragged_matches_tagged_and_oracle(engine, maxlen, R, tb):
+    """Ragged batches on every score-only plan (R = 4 .. 32, one and two bands), both score-only
+    tracebacks: identical to the tagged path on every pair, and to the full-matrix oracle on a
+    sample."""
     batch = ragged_batch(40 + maxlen, 1100, maxlen)
-    so = run(engine, True, *batch)
+    so = run(engine, True, *batch, tb=tb)
     tg = run(engine, False, *batch)
     assert so[2] == (sa.SA_KERNEL_T16_ENDCELL, R, 1) and tg[2] == so[2]
     s1, o1, s2, o2 = batch
