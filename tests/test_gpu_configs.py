@@ -198,6 +198,18 @@ def test_device_selects_int32_for_wide_alphabet(engine):
     assert (res[5].score, res[5].end_i, res[5].end_j, res[5].ops) == (o["score"], o["end_i"], o["end_j"], o["ops"])
 
 
+def same_streams(res, ops, ref_ops, o1, o2):
+    """Every pair's op stream (the first nops bytes of its slot) equal; the bytes past nops in a
+    slot are unspecified (the device I/O buffers are reused between calls)."""
+    n = len(res)
+    starts = o1[:n].astype(np.int64) + o2[:n].astype(np.int64) + np.arange(n)
+    for p in range(n):
+        s, k = int(starts[p]), int(res["nops"][p])
+        if ops[s:s + k].tobytes() != ref_ops[s:s + k].tobytes():
+            return False
+    return True
+
+
 def test_multi_context_config5_shard_matches_single(engine):
     """sa_multi (two contexts on GPU 0 here; one per GPU on a node) over the config-5 shard
     returns byte for byte what one context returns; the ranges write in place, so there is no
@@ -218,7 +230,7 @@ def test_multi_context_config5_shard_matches_single(engine):
     finally:
         me.close()
     assert res.tobytes() == ref.tobytes()
-    assert ops.tobytes() == ref_ops.tobytes()
+    assert same_streams(res, ops, ref_ops, o1, o2)
     print(f"single context {1e3 * (t1 - t0):.1f} ms, two contexts on one GPU {1e3 * (t3 - t2):.1f} ms")
 
 
@@ -241,7 +253,7 @@ def test_multi_engine_four_contexts_stage_concurrently(engine, capfd, monkeypatc
     finally:
         me.close()
     assert res.tobytes() == ref.tobytes()
-    assert ops.tobytes() == ref_ops.tobytes()
+    assert same_streams(res, ops, ref_ops, o1, o2)
     lines = [ln for ln in err.splitlines() if ln.startswith("[seqalib host api]")]
     assert len(lines) == 4, err[-2000:]
     inflight = max(int(ln.split("max ")[1].split(" copy jobs")[0]) for ln in lines)

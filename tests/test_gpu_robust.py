@@ -152,7 +152,9 @@ def test_multi_handle_linear_space(engine):
                 ref, rops = engine.align_packed(algo, sc_obj(args), s1, o1, s2, o2)
                 for f in ("score", "nops", "flags"):
                     assert (got[f] == ref[f]).all()
-                assert gops.tobytes() == rops.tobytes()
+                for p in range(len(pairs)):   # (bytes past nops in a slot are unspecified)
+                    off, k = int(o1[p] + o2[p]) + p, int(ref["nops"][p])
+                    assert gops[off:off + k].tobytes() == rops[off:off + k].tobytes()
     finally:
         me.close()
 

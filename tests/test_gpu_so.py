@@ -104,7 +104,8 @@ def test_so_ragged_matches_tagged_and_oracle(engine, maxlen, R, tb):
     s1, o1, s2, o2 = batch
     assert (so[0]["flags"] == 0).all()
     assert_same(so, tg, o1, o2)
-    assert (linear_rescore(SW, so[0], so[1], o1, o2) == so[0]["score"]).all()
+    nonempty = (np.diff(o1) > 0) & (np.diff(o2) > 0)   # (an empty pair keeps MaxScore = INT_MIN)
+    assert (linear_rescore(SW, so[0], so[1], o1, o2) == so[0]["score"])[nonempty].all()
     idx = np.sort(np.random.default_rng(maxlen).choice(len(o1) - 1, 48, replace=False))
     idx = np.unique(np.concatenate([np.arange(11), idx]))
     sub = subset(s1, o1, s2, o2, idx)
