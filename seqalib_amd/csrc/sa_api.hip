@@ -795,6 +795,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 ep.res = d_res; ep.pair_base = (uint32_t)base; ep.count = cnt;
                 ep.gap = sc->gap; ep.gap_open = sc->gap_open; ep.gap_extend = sc->gap_extend;
                 ep.hshift = v.so ? 0 : 2;
+                ep.dirs = fp.dirs; ep.dir_slot = fp.dir_slot; ep.band_stride = fp.band_stride;
                 // on the fill stream, right after the fill: run beside the next call's fill (on the
                 // traceback stream) its 10,000 short waves slowed that fill by 4 % (measured)
                 e = v.so ? launch_endcell_so(pl.R, ep, sf) : launch_endcell(algo, pl.R, ep, sf);

@@ -85,6 +85,17 @@ __device__ __forceinline__ uint32_t dc_code8(uint32_t sp, uint32_t b) {
 // the low 16 bits of a 16-bit sweep register, sign-extended, plus the offset
 __device__ __forceinline__ int32_t dc_unpack16(int32_t v, int32_t delta) { return (int32_t)(int16_t)(v & 0xffff) + delta; }
 
+// f(std::integral_constant<int, K>{}) for the (wave-uniform) register index k in [0, N): a band's
+// handed-on row is a register picked at compile time.  Every index has its own case -- round 3's
+// hand-written switch sent every k >= 7 to register 7, so R = 16 sweeps parked the wrong row.
+template <int N, int K = 0, class F>
+__device__ __forceinline__ void dc_row_dispatch(int k, F&& f) {
+    if constexpr (K < N) {
+        if (k == K) f(std::integral_constant<int, K>{});
+        else dc_row_dispatch<N, K + 1>(k, f);
+    }
+}
+
 // ---- match sources
 // match(a, b): the 256x256 LUT as bits (lut_to_bits), or byte equality
 __device__ __forceinline__ bool dc_match(const uint32_t* lut, uint32_t a, uint32_t b) {
@@ -286,6 +297,8 @@ struct Dc16 {
     const uint32_t* aux = nullptr;   // NULL: int32 sweeps only
     int32_t delta = 0;
     int32_t mismatch = 0;            // the profile's mismatch score
+    int32_t park = 1;                // steady chunks park the handed-on row in LDS and store it per
+                                     // chunk (SEQALIB_DC16_PARK=0: a lane-masked store per step)
 };
 // Host: is the 16-bit sweep exact for the batch's shapes and scoring?  lo / hi: bounds of every
 // row value and candidate of any sweep of at most max_m x max_n.
@@ -313,6 +326,7 @@ inline Dc16 dc16_plan(bool affine, const sa_scoring* sc, uint32_t max_m, uint32_
     d.aux = reinterpret_cast<const uint32_t*>(1);   // placeholder: set to the device aux by the driver
     d.delta = (int32_t)delta;
     d.mismatch = (int32_t)MI;
+    if (const char* e = getenv("SEQALIB_DC16_PARK")) d.park = e[0] != '0';
     return d;
 }
 

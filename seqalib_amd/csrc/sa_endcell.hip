@@ -157,13 +157,19 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
 }
 
 // Score-only SW fill (sa_fill_impl.h SO): the fill tracked the odd rows at the odd steps of its
-// steady chunks (every cell of ramp chunks) and stored, per (band, chunk), the wave's maximum of
-// the tracked cells; every cell is at most its tracked neighbour - 2G, so S lies in
-// [smax, smax - 2G] and only the chunks whose tracked maximum reaches smax + 2G can hold it.  This
-// kernel replays every such chunk of every band (all 64 lanes, from the fill's snapshots, as
-// endcell_kernel does), keeps per lane the lexicographically largest (H, i, j) -- the reference's
-// last row-major maximum, SASmithWaterman.h:110 -- and reduces over the wave.  An all-zero matrix
-// (smax = 0) replays every chunk and ends at (m, n), as the reference does.
+// steady chunks (every cell of ramp chunks) and stored, per (band, chunk, lane), the lane's maximum
+// of its tracked cells; every cell is at most a tracked cell of the same lane and chunk - 2G, so S
+// lies in [smax, smax - 2G] and only the LANE BLOCKS (R rows x 32 columns) whose tracked maximum
+// reaches smax + 2G can hold it.  This kernel lists those blocks and recomputes each one alone,
+// as the score-only traceback recomputes a block on the path (sa_traceback_so.hip): its left
+// column from the snapshot of the chunk before, its top row from the edge stream (the last row of
+// the lane above, per step), one row per lane in a 32 + R - 1 step wavefront, 64 / R blocks per
+// round.  Every lane keeps the lexicographically largest (H, i, j) of its cells -- the reference's
+// last row-major maximum, SASmithWaterman.h:110 -- and the wave reduces them.  A pair with more
+// than kSoCand candidate blocks (an all-zero or low-scoring matrix: smax = 0 lists every block)
+// replays whole chunks instead (64 lanes, from the snapshots), as endcell_kernel does.
+constexpr int kSoCand = 1024;
+
 template <int R>
 __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
     if (sa_skip(P.sel, P.sel_want)) return;
@@ -182,41 +188,142 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
     constexpr int BAND = kWave * R;
     const int B = (m + BAND - 1) / BAND;
     const int nch = (int)chunks_per_band((uint32_t)n);
+    const uint32_t snch = P.snap_nch;
     const int G = P.gap;
-    const int thr = res.score + 2 * G;   // chunks whose tracked maximum reaches this may hold S
-    const int32_t* cm = P.snap_m + (uint64_t)slot * P.snap_p_slot;
+    const int thr = res.score + 2 * G;   // lane blocks whose tracked maximum reaches this may hold S
+    const int32_t* cm = P.snap_m + (uint64_t)slot * P.snap_p_slot;   // [band][chunk][lane]
+    const uint32_t* sh_base = P.snap_h + (uint64_t)slot * P.snap_h_slot;
+    const int32_t* sp_base = P.snap_p + (uint64_t)slot * P.snap_p_slot;
     int bv = -1, bi = -1, bj = -1;       // this lane's best (H, row, column), 0-based
-    __shared__ uint8_t s_sym[kWave + kChunk];
-    __shared__ int s_top[kChunk];
-    for (int b = 0; b < B; ++b) {
-        const int row0 = b * BAND + lane * R;
-        uint32_t tab[R];
+    auto take = [&](int H, int row, int col) __attribute__((always_inline)) {
+        if (H > bv || (H == bv && (row > bi || (row == bi && col > bj)))) { bv = H; bi = row; bj = col; }
+    };
+
+    // ---- the candidate lane blocks, in [band][chunk][lane] order: 4 entries per lane per load
+    __shared__ uint32_t s_cand[kSoCand];   // band << 22 | chunk << 6 | lane
+    // four (band, chunk) entries per iteration, one coalesced 256-B load each (issued together)
+    const uint32_t total = (uint32_t)B * snch;
+    int cnt = 0;
+    for (uint32_t e0 = 0; e0 < total; e0 += 4) {
+        int v[4];
+        uint32_t bb[4], cc[4];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int row = row0 + r;
-            tab[r] = row < m ? P.prof[ec_code8(symp, s1[row]) >> 3] : 0u;
+        for (int k = 0; k < 4; ++k) {   // (e0 + k is wave-uniform: scalar divide)
+            const uint32_t e = e0 + k;
+            bb[k] = e / snch;
+            cc[k] = e - bb[k] * snch;
+            v[k] = e < total && (int)cc[k] < nch ? cm[(uint64_t)e * kWave + lane] : INT_MIN;
         }
-        const int32_t* top = b > 0 ? P.rowbuf + (uint64_t)slot * P.rowbuf_slot + (uint64_t)(b - 1) * P.max_n : nullptr;
-        for (int base = 0; base < nch; base += kWave) {
-            const int ccl = base + lane;
-            uint64_t hits = __builtin_amdgcn_ballot_w64(ccl < nch && cm[(uint64_t)b * P.snap_nch + ccl] >= thr);
-            while (hits) {
-                const int cc = base + (int)__builtin_ctzll(hits);
-                hits &= hits - 1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool hit = v[k] >= thr;
+            const uint64_t hits = __builtin_amdgcn_ballot_w64(hit);
+            if (hit) {
+                const int pos = cnt + (int)__builtin_popcountll(hits & ((1ull << lane) - 1));
+                if (pos < kSoCand) s_cand[pos] = bb[k] << 22 | cc[k] << 6 | (uint32_t)lane;
+            }
+            cnt += (int)__builtin_popcountll(hits);
+        }
+    }
+    __syncthreads();
+
+    if (cnt <= kSoCand) {
+        // ---- lane blocks: 64 / R per round, lane = block g's row r
+        constexpr int NB = kWave / R;
+        const int g = lane / R, r = lane % R;
+        __shared__ uint32_t s_pk[NB][kChunk + 1];   // per block, q = -1 .. 31: top H | column code << 16
+        const uint8_t* const dir = P.dirs + (uint64_t)slot * P.dir_slot;
+        const uint64_t bst = P.band_stride;
+        for (int c0 = 0; c0 < cnt; c0 += NB) {
+            const int ci = c0 + g;
+            const bool act = ci < cnt;
+            const uint32_t cd = act ? s_cand[ci] : 0u;
+            const int b = (int)(cd >> 22), c = (int)((cd >> 6) & 0xffffu), t = (int)(cd & 63u);
+            const int i = b * BAND + t * R + r;   // this lane's row (0-based)
+            const int j0 = kChunk * c - t;        // the block's first column
+            int h = 0;                            // H at column j0 - 1 (left of the block)
+            if (act && j0 >= 1 && i < m) {
+                const uint32_t w = sh_base[(((uint64_t)b * snch + (c - 1)) * (R / 2) + (r >> 1)) * kWave + t];
+                h = (int)((r & 1) ? (w >> 16) : (w & 0xffffu));
+            }
+            // the top row (row i0 - 1, the last row of lane t - 1, or of lane 63 of band b - 1) and the
+            // column codes: lane tp computed column jj at step jj + tp of its band's edge stream
+            const bool has_top = !(b == 0 && t == 0);
+            const int bp = t > 0 ? b : b - 1, tp = t > 0 ? t - 1 : kWave - 1;
+            for (int q = r - 1; q < kChunk; q += R) {
+                const int jj = j0 + q;
+                uint32_t top = 0, code = 0;
+                if (act && jj >= 0 && jj < n) {
+                    if (has_top) {
+                        if (q < 0 && j0 >= 1) {
+                            top = (uint32_t)sp_base[((uint64_t)b * snch + (c - 1)) * kWave + t] & 0xffffu;
+                        } else {
+                            const int st = jj + tp;
+                            top = *reinterpret_cast<const uint16_t*>(dir + (uint64_t)bp * bst +
+                                                                     ((uint64_t)(st >> 3) * kWave + tp) * 16 + (st & 7) * 2);
+                        }
+                    }
+                    code = ec_code8(symp, s2[jj]);
+                }
+                s_pk[g][q + 1] = top | code << 16;
+            }
+            const uint32_t tab = act && i < m ? P.prof[ec_code8(symp, s1[i]) >> 3] : 0u;
+            __syncthreads();
+            uint32_t pk = 0;            // (top H | column code << 16) of this lane's current column
+            int up_prev = (int)(s_pk[g][0] & 0xffffu);   // row 0: the corner; other rows: set below
+            for (int u = 0; u < kChunk + R - 1; ++u) {
+                // row r at column q = u - r: up = row r - 1's H at q (its previous step), diagonal =
+                // row r - 1's H at q - 1 (the up of this lane's previous step)
+                int up = __builtin_amdgcn_update_dpp(0, h, 0x138, 0xf, 0xf, false);   // wave_shr:1
+                pk = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pk, 0x138, 0xf, 0xf, false);
+                if (r == 0) {
+                    pk = u < kChunk ? s_pk[g][u + 1] : 0u;
+                    up = (int)(pk & 0xffffu);
+                }
+                const int diag = up_prev;
+                up_prev = up;
+                const int q = u - r, j = j0 + q;
+                if (act && q >= 0 && q < kChunk && j >= 0 && j < n && i < m) {
+                    const int sub = ((int)__builtin_amdgcn_sbfe(tab, pk >> 16, 8) - 3) >> 2;
+                    int H = (j == 0 ? 0 : diag) + sub;
+                    H = max(H, up + G);
+                    H = max(H, (j == 0 ? 0 : h) + G);
+                    H = max(H, 0);
+                    h = H;
+                    take(H, i, j);
+                }
+            }
+            __syncthreads();   // (s_pk and s_cand reads of this round)
+        }
+    } else {
+        // ---- dense: whole chunks holding a candidate lane, all 64 lanes from the snapshots
+        __shared__ uint8_t s_sym[kWave + kChunk];
+        __shared__ int s_top[kChunk];
+        for (int b = 0; b < B; ++b) {
+            const int row0 = b * BAND + lane * R;
+            uint32_t tab[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int row = row0 + r;
+                tab[r] = row < m ? P.prof[ec_code8(symp, s1[row]) >> 3] : 0u;
+            }
+            const int32_t* top = b > 0 ? P.rowbuf + (uint64_t)slot * P.rowbuf_slot + (uint64_t)(b - 1) * P.max_n : nullptr;
+            for (int cc = 0; cc < nch; ++cc) {
+                if (__builtin_amdgcn_ballot_w64(cm[((uint64_t)b * snch + cc) * kWave + lane] >= thr) == 0) continue;
                 int Hp[R];
 #pragma unroll
                 for (int r = 0; r < R; ++r) Hp[r] = 0;
                 int prev_up = 0;
                 if (cc > 0) {
-                    const uint64_t e = (uint64_t)b * P.snap_nch + (cc - 1);
-                    const uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + e * (R / 2) * kWave + lane;
+                    const uint64_t e = (uint64_t)b * snch + (cc - 1);
+                    const uint32_t* sh = sh_base + e * (R / 2) * kWave + lane;
 #pragma unroll
                     for (int q = 0; q < R / 2; ++q) {
                         const uint32_t w = sh[q * kWave];
                         Hp[2 * q] = (int)(w & 0xffffu);
                         Hp[2 * q + 1] = (int)(w >> 16);
                     }
-                    prev_up = (int)(P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] & 0xffff);
+                    prev_up = (int)(sp_base[e * kWave + lane] & 0xffff);
                 }
                 __syncthreads();   // (a previous candidate's reads of the staging arrays)
                 for (int k = lane; k < kWave + kChunk; k += kWave) {
@@ -253,12 +360,7 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
                             hd = Hp[r];
                             Hp[r] = H;
                             hu = H;
-                            const int row = row0 + r;
-                            if (row < m && (H > bv || (H == bv && (row > bi || (row == bi && j0 > bj))))) {
-                                bv = H;
-                                bi = row;
-                                bj = j0;
-                            }
+                            if (row0 + r < m) take(H, row0 + r, j0);
                         }
                         prev_up = up_h;
                         hl = Hp[R - 1];
@@ -272,12 +374,12 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
         const int ov = __shfl_xor(bv, off), oi = __shfl_xor(bi, off), oj = __shfl_xor(bj, off);
         if (ov > bv || (ov == bv && (oi > bi || (oi == bi && oj > bj)))) { bv = ov; bi = oi; bj = oj; }
     }
-    if (lane == 0) {
-        res.score = bv;
-        res.end_i = bi + 1;
-        res.end_j = bj + 1;
-        res.reserved = 0;
-        P.res[pidx] = res;
+    if (lane == 0) {   // (the other fields stay as the fill wrote them)
+        sa_result* const o = P.res + pidx;
+        o->score = bv;
+        o->end_i = bi + 1;
+        o->end_j = bj + 1;
+        o->reserved = 0;
     }
 }
 

@@ -532,7 +532,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     // CMAX: the lane's best chunk of the band so far as one key H << 12 | chunk + 1 (H < 2^13 by
     // t16_ok, chunks < 4096 since n < 65535): highest score, then last chunk
     uint32_t lkey = 0;
-    uint32_t smax = 0;   // SO: the largest tracked cell of the pair (wave-uniform), a lower bound of S
+    uint32_t smax = 0;   // SO: the lane's largest tracked cell (the wave's: a lower bound of S)
     int hl = 0, xl = 0, sym = 0, prev_up = 0;
     int row0 = 0;
     // Running best of this lane over its bands: (score, i, j), 1-based cell.
@@ -1163,12 +1163,10 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                     const uint32_t ck = chunk + 1;
                     const uint64_t e = (uint64_t)band * P.snap_nch + chunk;
                     if constexpr (SO) {
-                        // one word per (band, chunk): the wave's maximum of the tracked cells
-                        uint32_t wm = cml;
-#pragma unroll
-                        for (int off = 32; off >= 1; off >>= 1) wm = max(wm, (uint32_t)__shfl_xor((int)wm, off));
-                        if (lane == 0) P.snap_m[(uint64_t)slot * P.snap_p_slot + e] = (int32_t)wm;
-                        smax = max(smax, wm);
+                        // per (band, chunk, lane): the lane's maximum of its tracked cells -- the
+                        // end-cell replay then recomputes only the lane blocks that may hold S
+                        P.snap_m[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = (int32_t)cml;
+                        smax = max(smax, cml);   // (per lane; reduced over the wave at the end)
                     } else {
                         P.snap_m[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = (int32_t)cml;
                         lkey = max(lkey, (cml >> CSH) << 12 | ck);
@@ -1261,6 +1259,10 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
 #endif
         }
     } else if constexpr (LOCAL) {
+        if constexpr (SO) {
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, off));
+        }
         // lexicographic max over (score, i, j): the reference's last row-major maximum
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {

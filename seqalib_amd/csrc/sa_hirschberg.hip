@@ -84,7 +84,7 @@ __device__ __forceinline__ int32_t hb_cell_v(int32_t hd, int32_t hu, int32_t hl,
 template <int R>
 __device__ __forceinline__ void hb_band16(const HbSweep& d, const uint8_t* s1, const uint8_t* s2, const uint32_t* aux,
                                           int32_t delta, int32_t G, int band, int lastb, int tl, int rl, int32_t* out,
-                                          int32_t& hl) {
+                                          int32_t& hl, int32_t* s_park) {
     const int lane = threadIdx.x;
     const int m = d.alen, n = d.blen;
     constexpr int BAND = 64 * R;
@@ -111,12 +111,56 @@ __device__ __forceinline__ void hb_band16(const HbSweep& d, const uint8_t* s1, c
     };
     int32_t vup, nvup;
     uint32_t vsym, nvsym, sym = 0;
+    // the lane and register holding the row this band hands on: its last row (lane 63, Hp[R-1]),
+    // or in the last band row m of the sweep (lane tl, Hp[rl])
+    const int src_lane = band < lastb ? 63 : tl;
+    const int src_r = band < lastb ? R - 1 : rl;
+    // Steady chunk (c0 >= 63, c0 + 64 <= n: every lane inside the matrix for all 64 steps): no
+    // per-lane branch, and the handed-on row is parked per step by an LDS write of every lane
+    // (src_lane into its slot, the others into a discard slot) and stored once per chunk,
+    // coalesced -- instead of an exec-masked global store per step.  SRC: src_r at compile time.
+    auto steady_park = [&](int c0, auto SRC) {
+        constexpr int SR = decltype(SRC)::value;
+        int32_t* const park = s_park + (lane == src_lane ? 0 : 64);
+#pragma unroll 1
+        for (int q = 0; q < 64; ++q) {
+            const int32_t up_h = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vup, q), hl, 0x138, 0xf, 0xf, false);
+            sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vsym, q), sym, 0x138, 0xf, 0xf, false);
+            int32_t hd = prev_up, hu = up_h;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                int32_t h, t;
+                asm("v_max_i16 %0, %2, %3\n\t"
+                    "v_add_u16 %0, %4, %0\n\t"
+                    "v_bfe_i32 %1, %5, %6, 8\n\t"
+                    "v_add_u16 %1, %7, %1\n\t"
+                    "v_max_i16 %0, %1, %0"
+                    : "=&v"(h), "=&v"(t)
+                    : "v"(hu), "v"(Hp[r]), "s"(g16), "v"(a[r]), "v"(sym), "v"(hd));
+                hd = Hp[r];
+                Hp[r] = h;
+                hu = h;
+            }
+            prev_up = up_h;
+            hl = Hp[R - 1];
+            park[q] = Hp[SR];
+        }
+        __syncthreads();   // (one wave: orders the parked writes before the reads)
+        out[c0 - src_lane + 1 + lane] = dc_unpack16(s_park[lane], delta);
+        __syncthreads();
+    };
     load_chunk(0, vup, vsym);
     for (int c0 = 0; c0 < n + 63; c0 += 64) {
         load_chunk(c0 + 64, nvup, nvsym);
+        if (s_park && c0 >= 63 && c0 + 64 <= n) {
+            dc_row_dispatch<R>(src_r, [&](auto SRC) { steady_park(c0, SRC); });   // (uniform)
+            vup = nvup;
+            vsym = nvsym;
+            continue;
+        }
         const int steps = min(64, n + 63 - c0);
-        // steady chunk (c0 >= 63, c0 + 64 <= n): every lane is inside the matrix for all 64 steps,
-        // so the per-lane range branch is skipped (the hand-off store keeps its lane test)
+        // steady chunk without parking (SEQALIB_DC16_PARK=0): every lane is inside the matrix for
+        // all 64 steps, so the per-lane range branch is skipped (the hand-off store keeps its lane test)
         const bool steady = c0 >= 63 && c0 + 64 <= n;
         for (int q = 0; q < steps; ++q) {
             const int s = c0 + q;
@@ -166,6 +210,7 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
                                                       DcBits bits, HbScore sc, Dc16 d16) {
     constexpr bool LUT = MM == kMatchLut;
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];
+    __shared__ int32_t s_park[128];   // Dc16 steady chunks: the handed-on row, parked per step
     const int lane = threadIdx.x;
     if (blockIdx.x / 2 >= lvl->nsplit) return;   // grid sized from an upper bound
     const DcSub sub = split[blockIdx.x / 2];
@@ -184,7 +229,7 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
             const int tl = ((m - 1) % BAND) / R, rl = (m - 1) % R;
             int32_t hl = 0;
             for (int band = 0; band < bands; ++band) {
-                hb_band16<R>(d, s1, s2, d16.aux, d16.delta, G, band, bands - 1, tl, rl, out, hl);
+                hb_band16<R>(d, s1, s2, d16.aux, d16.delta, G, band, bands - 1, tl, rl, out, hl, d16.park ? s_park : nullptr);
                 __threadfence_block();
                 __syncthreads();
             }

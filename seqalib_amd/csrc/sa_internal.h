@@ -123,6 +123,8 @@ struct EndcellParams {
     uint32_t pair_base, count;
     int32_t gap, gap_open, gap_extend;
     int hshift;                // SW: snapshots / chunk maxima / top rows hold H << hshift (2 tagged, 0 SO)
+    const uint8_t* dirs;       // score-only: the fill's edge stream (TbParams::dirs, band_stride)
+    uint64_t dir_slot, band_stride;
 };
 
 struct TbParams {

@@ -174,7 +174,7 @@ __device__ __forceinline__ void mm_band(const MmSweep& d, const DcSrc<MM>& src, 
 template <int R, bool LAST>
 __device__ __forceinline__ void mm_band16(const MmSweep& d, const uint8_t* s1, const uint8_t* s2, const uint32_t* aux,
                                           int32_t delta, const MmScore& sc, int band, int32_t* outC, int32_t* outD,
-                                          int tl, int rl, int32_t& cl, int32_t& dl) {
+                                          int tl, int rl, int32_t& cl, int32_t& dl, int32_t* s_park) {
     const int lane = threadIdx.x;
     const int m = d.alen, n = d.blen, g = sc.g, h = sc.h;
     constexpr int BAND = 64 * R;
@@ -211,12 +211,67 @@ __device__ __forceinline__ void mm_band16(const MmSweep& d, const uint8_t* s1, c
     };
     int32_t vc, vd, nvc, nvd;
     uint32_t vs, nvs, sym = 0;
+    // Steady chunk (c0 >= 63, c0 + 64 <= n; as hb_band16): no per-lane branch; the handed-on row
+    // (C and D of lane 63's last row, or of row m at lane tl / register rl in the last band) is
+    // parked per step in LDS by every lane (others into a discard slot) and stored per chunk.
+    const int src_lane = LAST ? tl : 63;
+    auto steady_park = [&](int c0, auto SRC) {
+        constexpr int SR = decltype(SRC)::value;
+        int32_t* const park = s_park + (lane == src_lane ? 0 : 64);
+#pragma unroll 1
+        for (int q = 0; q < 64; ++q) {
+            const int32_t up_c = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vc, q), cl, 0x138, 0xf, 0xf, false);
+            const int32_t up_d = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vd, q), dl, 0x138, 0xf, 0xf, false);
+            sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vs, q), sym, 0x138, 0xf, 0xf, false);
+            int32_t cd = prev_up, cu = up_c, du = up_d, dsel = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                int32_t e, dd, c, t;
+                asm("v_add_u16 %0, %4, %5\n\t"
+                    "v_max_i16 %0, %6, %0\n\t"
+                    "v_add_u16 %0, %7, %0\n\t"
+                    "v_add_u16 %1, %4, %8\n\t"
+                    "v_max_i16 %1, %9, %1\n\t"
+                    "v_add_u16 %1, %7, %1\n\t"
+                    "v_bfe_i32 %3, %10, %11, 8\n\t"
+                    "v_add_u16 %3, %12, %3\n\t"
+                    "v_max_i16 %2, %1, %0\n\t"
+                    "v_max_i16 %2, %3, %2"
+                    : "=&v"(e), "=&v"(dd), "=&v"(c), "=&v"(t)
+                    : "s"(g16), "v"(Cp[r]), "v"(Ep[r]), "s"(h16), "v"(cu), "v"(du), "v"(a[r]), "v"(sym),
+                      "v"(cd));
+                cd = Cp[r];
+                Cp[r] = c;
+                Ep[r] = e;
+                cu = c;
+                du = dd;
+                if (r == SR) dsel = dd;
+            }
+            prev_up = up_c;
+            cl = Cp[R - 1];
+            dl = du;
+            park[q] = Cp[SR];
+            park[128 + q] = dsel;
+        }
+        __syncthreads();   // (one wave: orders the parked writes before the reads)
+        outC[c0 - src_lane + 1 + lane] = dc_unpack16(s_park[lane], delta);
+        outD[c0 - src_lane + 1 + lane] = dc_unpack16(s_park[128 + lane], delta);
+        __syncthreads();
+    };
     load_chunk(0, vc, vd, vs);
     for (int c0 = 0; c0 < n + 63; c0 += 64) {
         load_chunk(c0 + 64, nvc, nvd, nvs);
+        if (s_park && c0 >= 63 && c0 + 64 <= n) {
+            const int src_r = LAST ? rl : R - 1;
+            dc_row_dispatch<R>(src_r, [&](auto SRC) { steady_park(c0, SRC); });   // (uniform)
+            vc = nvc;
+            vd = nvd;
+            vs = nvs;
+            continue;
+        }
         const int steps = min(64, n + 63 - c0);
-        // steady chunk (c0 >= 63, c0 + 64 <= n): every lane is inside the matrix for all 64 steps,
-        // so the per-lane range branch is skipped (the hand-off store keeps its lane test)
+        // steady chunk without parking (SEQALIB_DC16_PARK=0): every lane is inside the matrix for
+        // all 64 steps, so the per-lane range branch is skipped (the hand-off store keeps its lane test)
         const bool steady = c0 >= 63 && c0 + 64 <= n;
         for (int q = 0; q < steps; ++q) {
             const int s = c0 + q;
@@ -281,6 +336,7 @@ __global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const u
                                                       DcBits bits, MmScore sc, Dc16 d16) {
     constexpr bool LUT = MM == kMatchLut;
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];
+    __shared__ int32_t s_park[256];   // Dc16 steady chunks: the handed-on C and D rows, per step
     const int lane = threadIdx.x;
     if (blockIdx.x / 2 >= lvl->nsplit) return;   // grid sized from an upper bound
     const DcSub sub = split[blockIdx.x / 2];
@@ -303,9 +359,9 @@ __global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const u
         if constexpr (MM != kMatchBits) {
             if (b16) {
                 if (band < bands - 1)
-                    mm_band16<R, false>(d, s1, s2, d16.aux, d16.delta, sc, band, outC, outD, tl, rl, cl, dl);
+                    mm_band16<R, false>(d, s1, s2, d16.aux, d16.delta, sc, band, outC, outD, tl, rl, cl, dl, d16.park ? s_park : nullptr);
                 else
-                    mm_band16<R, true>(d, s1, s2, d16.aux, d16.delta, sc, band, outC, outD, tl, rl, cl, dl);
+                    mm_band16<R, true>(d, s1, s2, d16.aux, d16.delta, sc, band, outC, outD, tl, rl, cl, dl, d16.park ? s_park : nullptr);
                 __threadfence_block();
                 __syncthreads();
                 continue;

@@ -120,6 +120,25 @@ def test_myers_miller_batch_vs_oracle(engine, args, match):
     compare_with_oracle(engine, sa.SA_MYERS_MILLER, args, pairs, match)
 
 
+@pytest.mark.parametrize("algo,args", [(sa.SA_HIRSCHBERG, (-1, 2, -1)), (sa.SA_MYERS_MILLER, (-3, -1, 1, -1, True))])
+@pytest.mark.parametrize("park", ["1", "0"])
+def test_dc16_handoff_row_every_register(engine, monkeypatch, algo, args, park):
+    """16-bit whole-wave sweeps with R = 16 (a level whose longest sweep has 513..1024 rows): the
+    steady chunks hand on register (m - 1) % 16 of lane (m - 1) % 1024 / 16 in the last band (and
+    register 15 of lane 63 in the others), parked in LDS (SEQALIB_DC16_PARK=1, default) or stored
+    per step (0).  Top-level sweep heights 550 .. 1000 cover every register index; round 3's park
+    variant sent indices >= 7 to register 7.  (R = 32 and several bands: the
+    3000 x 2500 and 5000 x 7 pairs of the batch tests above.)"""
+    monkeypatch.setenv("SEQALIB_DC16_PARK", park)
+    pairs = []
+    for k in range(32):
+        m, n = 1100 + 29 * k, 1000 + 23 * k
+        a = sa.synth_dna(90_000 + 2 * k, m)
+        b = sa.synth_mutate(a, k)[:n] if k % 2 else sa.synth_dna(90_001 + 2 * k, n)
+        pairs.append((a, b))
+    compare_with_oracle(engine, algo, args, pairs, None)
+
+
 def test_golden_large(engine):
     assert check_golden(engine, load_golden("large.jsonl")) == 10
 
