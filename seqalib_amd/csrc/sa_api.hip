@@ -594,8 +594,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         uint32_t* const hp = c->h_sel + 8;   // pinned staging (the host API call is synchronous)
         for (int k = 0; k < 5; ++k) hp[k] = ha->prof[k];
         hp[5] = (uint32_t)ha->sel;
-        SA_HIP(c, hipMemcpyAsync(aux + kAuxProf, hp, 20, hipMemcpyHostToDevice, stream));
-        SA_HIP(c, hipMemcpyAsync(aux + kAuxSel, hp + 5, 4, hipMemcpyHostToDevice, stream));
+        static_assert(kAuxSel == kAuxProf + 5, "profile and selection word: one upload");
+        SA_HIP(c, hipMemcpyAsync(aux + kAuxProf, hp, 24, hipMemcpyHostToDevice, stream));
         SA_HIP(c, hipEventRecord(c->ev_sel, stream));
         if (ha->sel == 0) only = 2;
         else if (tm.retry_above == INT_MAX) only = 1;
@@ -1108,15 +1108,19 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     uint8_t* dops = p; p += b_ops;
     uint8_t* dlut = p; p += b_lut;
     uint32_t* dbits = reinterpret_cast<uint32_t*>(p);
-    // pinned staging (pageable copies were measured to stall 10-25 ms per call next to PyTorch):
-    // in = [seq1][seq2][off1'][off2'], out = [results][ops]
-    SA_HIP(c, c->stage.alloc(t1 + t2 + 16 * n_off));
-    SA_HIP(c, c->ostage.alloc(sizeof(sa_result) * (uint64_t)npairs + ops_total));
+    // pinned staging (pageable copies were measured to stall 10-25 ms per call next to PyTorch),
+    // laid out as the device I/O: in = [seq1][seq2][off1'][off2'], out = [results][ops], so that a
+    // small call moves its inputs in one copy and its outputs in one copy
+    SA_HIP(c, c->stage.alloc(b_s1 + b_s2 + 2 * b_o));
+    SA_HIP(c, c->ostage.alloc(b_res + ops_total));
     uint8_t* const si = c->stage.data();
-    uint64_t* const so1 = reinterpret_cast<uint64_t*>(si + t1 + t2);
-    uint64_t* const so2 = so1 + n_off;
+    uint64_t* const so1 = reinterpret_cast<uint64_t*>(si + b_s1 + b_s2);
+    uint64_t* const so2 = reinterpret_cast<uint64_t*>(si + b_s1 + b_s2 + b_o);
     sa_result* const sres = reinterpret_cast<sa_result*>(c->ostage.data());
-    uint8_t* const sops = c->ostage.data() + sizeof(sa_result) * (uint64_t)npairs;
+    uint8_t* const sops = c->ostage.data() + b_res;
+    // small call (one chunk, <= kSmallCall bytes each way): one upload, one download
+    constexpr uint64_t kSmallCall = 1ull << 20;
+    const bool small = G == 1 && b_s1 + b_s2 + 2 * b_o <= kSmallCall && b_res + ops_total <= kSmallCall;
     const bool pipe = G > 1;
     if (!c->s_out) SA_HIP(c, hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking));
     if (pipe && !c->s_fill) {
@@ -1163,18 +1167,25 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
             }
         }
         const auto t_in = std::chrono::steady_clock::now();
-        for (uint64_t x = 0; x < n1; x += kHostPiece) {
+        if (small) {
+            memcpy(si, seq1, n1);
+            memcpy(si + b_s1, seq2, n2);
+            SA_HIP(c, hipMemcpyAsync(d1, si, b_s1 + b_s2 + b_o + 8ull * (cnt + 1), hipMemcpyHostToDevice, st));
+        }
+        for (uint64_t x = 0; !small && x < n1; x += kHostPiece) {
             const uint64_t k = std::min(kHostPiece, n1 - x);
             par_copy(si + a1 + x, seq1 + a1 + x, k);
             SA_HIP(c, hipMemcpyAsync(d1 + a1 + x, si + a1 + x, k, hipMemcpyHostToDevice, st));
         }
-        for (uint64_t x = 0; x < n2; x += kHostPiece) {
+        for (uint64_t x = 0; !small && x < n2; x += kHostPiece) {
             const uint64_t k = std::min(kHostPiece, n2 - x);
-            par_copy(si + t1 + a2 + x, seq2 + a2 + x, k);
-            SA_HIP(c, hipMemcpyAsync(d2 + a2 + x, si + t1 + a2 + x, k, hipMemcpyHostToDevice, st));
+            par_copy(si + b_s1 + a2 + x, seq2 + a2 + x, k);
+            SA_HIP(c, hipMemcpyAsync(d2 + a2 + x, si + b_s1 + a2 + x, k, hipMemcpyHostToDevice, st));
         }
-        SA_HIP(c, hipMemcpyAsync(do1 + p0 + g, so1 + p0 + g, 8ull * (cnt + 1), hipMemcpyHostToDevice, st));
-        SA_HIP(c, hipMemcpyAsync(do2 + p0 + g, so2 + p0 + g, 8ull * (cnt + 1), hipMemcpyHostToDevice, st));
+        if (!small) {
+            SA_HIP(c, hipMemcpyAsync(do1 + p0 + g, so1 + p0 + g, 8ull * (cnt + 1), hipMemcpyHostToDevice, st));
+            SA_HIP(c, hipMemcpyAsync(do2 + p0 + g, so2 + p0 + g, 8ull * (cnt + 1), hipMemcpyHostToDevice, st));
+        }
         ms_in += since(t_in);
         hipStream_t done = st;
         if (dc) {
@@ -1201,6 +1212,12 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         (void)on;
         SA_HIP(c, hipEventRecord(c->host_ev[g], done));
         SA_HIP(c, hipStreamWaitEvent(c->s_out, c->host_ev[g], 0));
+        if (small) {   // results and op bytes are contiguous in both layouts
+            SA_HIP(c, hipMemcpyAsync(sres, dres, b_res + ops_total, hipMemcpyDeviceToHost, c->s_out));
+            SA_HIP(c, hipEventRecord(c->host_ev[G + next_out], c->s_out));
+            ++next_out;
+            continue;
+        }
         SA_HIP(c, hipMemcpyAsync(sres + p0, dres + p0, sizeof(sa_result) * cnt, hipMemcpyDeviceToHost, c->s_out));
         for (; next_out < outp.size() && outp[next_out].g == g; ++next_out) {
             const OutPiece& o = outp[next_out];
