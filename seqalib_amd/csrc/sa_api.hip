@@ -547,6 +547,14 @@ struct HostSeqs {   // a host API batch's sequences (and host match table) for h
     const uint8_t* s2;
     uint64_t t2;
     const uint8_t* lut;   // 256 x 256 bytes or NULL (equality)
+    // small calls (align_host): the inputs are not uploaded yet.  run_device writes the host-decided
+    // profile and selection word into the pinned header hhdr, then uploads [header][inputs] with ONE
+    // copy (up_bytes from up_src to up_dst; dhdr is where the header lands) before any kernel.
+    uint32_t* hhdr = nullptr;
+    const uint32_t* dhdr = nullptr;
+    void* up_dst = nullptr;
+    const void* up_src = nullptr;
+    uint64_t up_bytes = 0;
 };
 
 // Enqueue fill + traceback for pairs [0, npairs) whose inputs are on the device.  Nothing here
@@ -582,24 +590,32 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     uint32_t* aux = c->aux + kAuxWords * slot;
     if (pipe && c->ev_slot[slot]) SA_HIP(c, hipStreamWaitEvent(stream, c->ev_slot[slot], 0));   // slot free
     const uint32_t* sel = nullptr;
+    const uint32_t* prof = aux + kAuxProf;   // the T16 profile words (+5: the selection word)
+    static_assert(kAuxSel == kAuxProf + 5, "profile and selection word: one upload");
     int only = 0;   // build_variants: both variants, or the one the host chose
     HostAlphabet hal;
     if (t16 && hs) hal = host_alphabet(hs->s1, hs->t1, hs->s2, hs->t2, hs->lut, sc->match, tm.mismatch, is_affine(algo));
     const HostAlphabet* ha = &hal;
-    if (t16 && ha->sel >= 0) {
+    const bool host_sel = t16 && ha->sel >= 0;
+    if (host_sel) {
         // the host decided the alphabet (align_host): upload the profile; enqueue the chosen variant
         // alone -- plus the int32 re-run when T16 may overflow (SW / LocalGotoh retry_above, the
         // screened GlobalGotoh), which then reads the selection word as usual
         *c->h_sel = (uint32_t)ha->sel;
-        uint32_t* const hp = c->h_sel + 8;   // pinned staging (the host API call is synchronous)
+        const bool in_hdr = hs->hhdr != nullptr;   // (small call: travels with the inputs)
+        uint32_t* const hp = in_hdr ? hs->hhdr : c->h_sel + 8;   // pinned (the host API call is synchronous)
         for (int k = 0; k < 5; ++k) hp[k] = ha->prof[k];
         hp[5] = (uint32_t)ha->sel;
-        static_assert(kAuxSel == kAuxProf + 5, "profile and selection word: one upload");
-        SA_HIP(c, hipMemcpyAsync(aux + kAuxProf, hp, 24, hipMemcpyHostToDevice, stream));
-        SA_HIP(c, hipEventRecord(c->ev_sel, stream));
+        if (in_hdr) prof = hs->dhdr;
+        else SA_HIP(c, hipMemcpyAsync(aux + kAuxProf, hp, 24, hipMemcpyHostToDevice, stream));
         if (ha->sel == 0) only = 2;
         else if (tm.retry_above == INT_MAX) only = 1;
-        else sel = aux + kAuxSel;
+        else sel = prof + 5;
+    }
+    if (hs && hs->up_bytes)
+        SA_HIP(c, hipMemcpyAsync(hs->up_dst, hs->up_src, hs->up_bytes, hipMemcpyHostToDevice, stream));
+    if (host_sel) {
+        SA_HIP(c, hipEventRecord(c->ev_sel, stream));
     } else if (t16) {
         SA_HIP(c, launch_alphabet_scan(d1, o1, d2, o2, npairs, aux, stream));
         SA_HIP(c, launch_decide_t16(d_lutbits, sc->match, tm.mismatch, is_affine(algo) ? 1 : 0, aux, stream));
@@ -735,7 +751,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fp.waves = pl.W;
             fp.count = cnt;
             fp.stage_seq2 = max_n <= kMaxStagedSeq2 ? 1 : 0;
-            fp.prof = aux + kAuxProf;
+            fp.prof = prof;
             const bool fb = k == nv;
             fp.sel = fb ? nullptr : sel; fp.sel_want = v.t16 ? 1u : 0u;
             fp.redo = (!fb && nv == 2 && !v.t16) ? 1 : 0;
@@ -887,6 +903,19 @@ bool lut_is_identity(const uint8_t* lut) {
     for (int a = 0; a < 256; ++a)
         for (int b = 0; b < 256; ++b)
             if ((lut[a * 256 + b] != 0) != (a == b)) return false;
+    return true;
+}
+
+// the match table is equality on every symbol pair these sequences hold (seq1 symbol x seq2 symbol):
+// a caller's table for equal<char> then needs no upload (the kernels compare bytes)
+bool lut_identity_on(const uint8_t* lut, const uint8_t* s1, uint64_t t1, const uint8_t* s2, uint64_t t2) {
+    bool u1[256] = {}, u2[256] = {};
+    for (uint64_t k = 0; k < t1; ++k) u1[s1[k]] = true;
+    for (uint64_t k = 0; k < t2; ++k) u2[s2[k]] = true;
+    for (int a = 0; a < 256; ++a)
+        if (u1[a])
+            for (int b = 0; b < 256; ++b)
+                if (u2[b] && (lut[a * 256 + b] != 0) != (a == b)) return false;
     return true;
 }
 
@@ -1085,7 +1114,8 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     const uint64_t ops_total = t1 + t2 + npairs;
     if (ops_cap < ops_total) return fail(c, SA_ERR_CAPACITY, "ops buffer needs " + std::to_string(ops_total) + " bytes");
     if (!npairs) return SA_OK;
-    const bool use_lut = lut && !lut_is_identity(lut);
+    const bool use_lut = lut && !lut_is_identity(lut) &&
+                         !(t1 + t2 <= kHostScanBytes && lut_identity_on(lut, seq1, t1, seq2, t2));
     const bool dc = algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER;
     const uint32_t G = host_chunks(algo, npairs);
     const std::vector<uint32_t> cut = cut_by_cells(off1, off2, npairs, G);
@@ -1097,9 +1127,11 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     const uint64_t b_s1 = al(t1 + 1), b_s2 = al(t2 + 1), b_o = al(8 * n_off);
     const uint64_t b_res = al(sizeof(sa_result) * (uint64_t)npairs);
     const uint64_t b_ops = al(ops_total + 1), b_lut = al(65536), b_bits = al(8192);
-    const uint64_t io_need = b_s1 + b_s2 + 2 * b_o + b_res + b_ops + b_lut + b_bits;
+    constexpr uint64_t b_hdr = 256;   // small calls: the host-decided T16 profile (HostSeqs::hhdr)
+    const uint64_t io_need = b_hdr + b_s1 + b_s2 + 2 * b_o + b_res + b_ops + b_lut + b_bits;
     if (int rc = ensure_io(c, io_need)) return rc;
     uint8_t* p = c->io;
+    uint32_t* const dhdr = reinterpret_cast<uint32_t*>(p); p += b_hdr;
     uint8_t* d1 = p; p += b_s1;
     uint8_t* d2 = p; p += b_s2;
     uint64_t* do1 = reinterpret_cast<uint64_t*>(p); p += b_o;
@@ -1111,16 +1143,19 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     // pinned staging (pageable copies were measured to stall 10-25 ms per call next to PyTorch),
     // laid out as the device I/O: in = [seq1][seq2][off1'][off2'], out = [results][ops], so that a
     // small call moves its inputs in one copy and its outputs in one copy
-    SA_HIP(c, c->stage.alloc(b_s1 + b_s2 + 2 * b_o));
+    SA_HIP(c, c->stage.alloc(b_hdr + b_s1 + b_s2 + 2 * b_o));
     SA_HIP(c, c->ostage.alloc(b_res + ops_total));
-    uint8_t* const si = c->stage.data();
+    uint32_t* const shdr = reinterpret_cast<uint32_t*>(c->stage.data());
+    uint8_t* const si = c->stage.data() + b_hdr;
     uint64_t* const so1 = reinterpret_cast<uint64_t*>(si + b_s1 + b_s2);
     uint64_t* const so2 = reinterpret_cast<uint64_t*>(si + b_s1 + b_s2 + b_o);
     sa_result* const sres = reinterpret_cast<sa_result*>(c->ostage.data());
     uint8_t* const sops = c->ostage.data() + b_res;
-    // small call (one chunk, <= kSmallCall bytes each way): one upload, one download
+    // small call (one chunk, sequences the host scans, <= kSmallCall bytes each way): one upload
+    // (header + inputs, issued by run_device after it wrote the header) and one download
     constexpr uint64_t kSmallCall = 1ull << 20;
-    const bool small = G == 1 && b_s1 + b_s2 + 2 * b_o <= kSmallCall && b_res + ops_total <= kSmallCall;
+    const bool small = G == 1 && t1 + t2 <= kHostScanBytes && b_s1 + b_s2 + 2 * b_o <= kSmallCall &&
+                       b_res + ops_total <= kSmallCall;
     const bool pipe = G > 1;
     if (!c->s_out) SA_HIP(c, hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking));
     if (pipe && !c->s_fill) {
@@ -1167,10 +1202,11 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
             }
         }
         const auto t_in = std::chrono::steady_clock::now();
+        const uint64_t small_up = b_hdr + b_s1 + b_s2 + b_o + 8ull * (cnt + 1);   // [header][inputs]
         if (small) {
             memcpy(si, seq1, n1);
             memcpy(si + b_s1, seq2, n2);
-            SA_HIP(c, hipMemcpyAsync(d1, si, b_s1 + b_s2 + b_o + 8ull * (cnt + 1), hipMemcpyHostToDevice, st));
+            if (dc) SA_HIP(c, hipMemcpyAsync(dhdr, shdr, small_up, hipMemcpyHostToDevice, st));
         }
         for (uint64_t x = 0; !small && x < n1; x += kHostPiece) {
             const uint64_t k = std::min(kHostPiece, n1 - x);
@@ -1202,7 +1238,14 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
                 return fail(c, SA_ERR_HIP, (algo == SA_HIRSCHBERG ? "hirschberg: " : "myers-miller: ") + e);
         } else {
             // small batches: the alphabet is decided here, on the host (no scan / decide kernels)
-            const HostSeqs hs{seq1 + a1, n1, seq2 + a2, n2, use_lut ? lut : nullptr};
+            HostSeqs hs{seq1 + a1, n1, seq2 + a2, n2, use_lut ? lut : nullptr};
+            if (small) {
+                hs.hhdr = shdr;
+                hs.dhdr = dhdr;
+                hs.up_dst = dhdr;
+                hs.up_src = shdr;
+                hs.up_bytes = small_up;
+            }
             int rc = run_device(c, algo, sc, d1 + a1, do1 + p0 + g, d2 + a2, do2 + p0 + g, cnt, mm, mn,
                                 use_lut ? dbits : nullptr, dres + p0, dops + ob, st, pipe, nullptr, nullptr,
                                 n1 + n2 <= kHostScanBytes ? &hs : nullptr);

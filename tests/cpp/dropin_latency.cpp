@@ -5,7 +5,7 @@
 //     test/Test.cpp's pair "AAAGAATGCAT" / "AAACTCAT";
 //   * one 1024 x 1024 SmithWatermanSA (default scoring) DNA pair.
 // The first call (HIP context, workspace) is reported apart; then `reps` calls are timed one by one.
-// Prints one JSON line.   dropin_latency [reps=200]
+// Prints one JSON line.   dropin_latency [reps=200] [nw|sw: that call only]
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -39,16 +39,17 @@ void timed(const char* name, int reps, Call call, bool last) {
 
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 200;
+    const std::string only = argc > 2 ? argv[2] : "";
     std::string a = "AAAGAATGCAT", b = "AAACTCAT";   // test/Test.cpp:29-30
     std::string x(1024, 'A'), y(1024, 'A');
     sa_synth_dna(1000000001ull, 1024, reinterpret_cast<uint8_t*>(&x[0]));   // config 1 x 1e9 seeds
     sa_synth_dna(1000000002ull, 1024, reinterpret_cast<uint8_t*>(&y[0]));
     printf("{\"what\": \"C++ drop-in getAlignment per call (aligner constructed per call, as include/Test.cpp:98-107)\", ");
-    timed("nw_11x8", reps, [&] {
+    if (only != "sw") timed("nw_11x8", reps, [&] {
         AlignedSequence<char, '-'> r = NeedlemanWunschSA<std::string, char, '-'>(ScoringSystem(-1, 2), equal<char>).getAlignment(a, b);
         return r.Data.size();
-    }, false);
-    timed("sw_1024x1024", std::max(1, reps / 4), [&] {
+    }, only == "nw");
+    if (only != "nw") timed("sw_1024x1024", std::max(1, reps / 4), [&] {
         AlignedSequence<char, '-'> r = SmithWatermanSA<std::string, char, '-'>(ScoringSystem(-1, 1, -1), equal<char>).getAlignment(x, y);
         return r.Data.size();
     }, true);

@@ -21,6 +21,8 @@ for park in 1 0; do
   done
 done
 cut -c1-220 gpurun_out/dc_ab.jsonl
+echo "[e] launch count $(date +%T)"
+bash tools/launch_count.sh || exit 1
 echo "[e] full suite $(date +%T)"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 tail -8 gpurun_out/pytest_gpu.log
