@@ -16,10 +16,13 @@
 #include <algorithm>
 #include <cassert>
 #include <climits>
+#include <condition_variable>
+#include <deque>
 #include <exception>
 #include <functional>
 #include <limits>
 #include <list>
+#include <mutex>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -166,14 +169,15 @@ void build_from_ops(ContainerType& Seq1, ContainerType& Seq2, const sa_result& r
     }
 }
 
-// Pairs per GPU call when a large batch is cut into chunks (run below): one chunk fills the chip's
-// 4 x 1,024 SIMD wave slots once (the score-only fill runs 4 single-wave workgroups per SIMD).
-constexpr size_t kChunkPairs = 4096;
+// Pairs per chunk when a large batch is aligned in chunks (run below).  The GPU call is one
+// sa_align_batch_cb over the whole batch, pipelined chunk by chunk on the device; the lists of a
+// chunk are built while the GPU works on the chunks after it.
+constexpr size_t kChunkPairs = 2048;
 
 // Shared getAlignment()/getAlignments() body of the four aligners.  Building the std::list of
 // every pair (one allocation per Entry, as the reference's buildResult) dominates a large batch
-// end to end, so a batch of >= 2 chunks is aligned chunk by chunk and chunk g's lists are built on
-// the host threads while chunk g+1 runs on the GPU.
+// end to end, so a batch of >= 2 chunks is aligned in one chunked GPU call whose chunk
+// callbacks hand each landed range to a builder thread (which fans out over the host threads).
 template <int ALGO, typename Aligner, typename ContainerType, typename Ty, Ty Blank>
 std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std::pair<ContainerType*, ContainerType*>>& pairs,
                                             std::vector<sa_result>& res) {
@@ -182,52 +186,78 @@ std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std
     const sa_scoring sc = self.getScoring().toC();
     const size_t P = pairs.size();
     std::vector<AlignedSequence<Ty, Blank>> out(P);
-    res.assign(P, sa_result{});
-    const size_t G = P >= 2 * kChunkPairs ? (P + kChunkPairs - 1) / kChunkPairs : 1;
-    // double-buffered chunk outputs: chunk g's lists are built from buffer g % 2
-    raw_vector<uint8_t> ops[2];
-    std::vector<uint64_t> off[2];
-    std::vector<sa_result> rc[2];
-    auto build = [&](size_t g, size_t p0, size_t p1) {
-        const size_t c0 = g * P / G;   // first pair of chunk g
+    raw_vector<uint8_t> ops;
+    std::vector<uint64_t> off;
+    auto build = [&](size_t p0, size_t p1) {
         for (size_t p = p0; p < p1; ++p) {
-            const sa_result& r = rc[g % 2][p - c0];
-            build_from_ops<Ty, Blank>(*pairs[p].first, *pairs[p].second, r, ops[g % 2].data() + off[g % 2][p - c0], out[p]);
+            const sa_result& r = res[p];
+            build_from_ops<Ty, Blank>(*pairs[p].first, *pairs[p].second, r, ops.data() + off[p], out[p]);
             const bool local = (ALGO == SA_SW || ALGO == SA_LOCAL_GOTOH) && !(r.flags & SA_FLAG_SIZE_HACK);
             if (local)
                 self.forceGlobal(*pairs[p].first, *pairs[p].second, out[p], r.start_i, r.start_j, r.end_i, r.end_j);
         }
     };
+    auto build_range = [&](size_t p0, size_t p1) {
+        parallel_pairs(p1 - p0, host_threads(p1 - p0), [&](size_t, size_t q0, size_t q1) { build(p0 + q0, p0 + q1); });
+    };
     PhaseTimer tm;
-    // the lists of chunk g, on a thread of their own (which fans out over the host threads)
-    struct Builder {
-        std::thread th;
-        std::exception_ptr err;
-        ~Builder() { join(); }
-        void join() {
-            if (th.joinable()) th.join();
-        }
-    } bld;
-    for (size_t g = 0; g < G; ++g) {
-        const size_t c0 = g * P / G, c1 = (g + 1) * P / G;
-        const std::vector<std::pair<ContainerType*, ContainerType*>> sub(pairs.begin() + c0, pairs.begin() + c1);
-        align<Ty>(ALGO, sc, fn, has_fn, G == 1 ? pairs : sub, rc[g % 2], ops[g % 2], off[g % 2]);
-        std::copy(rc[g % 2].begin(), rc[g % 2].end(), res.begin() + c0);
-        bld.join();   // chunk g-1's lists (they read buffer (g-1) % 2, which chunk g+1 reuses)
-        if (bld.err) std::rethrow_exception(bld.err);
-        tm.lap("GPU chunk (overlapped lists)");
-        bld.th = std::thread([&, g, c0, c1] {
-            try {
-                parallel_pairs(c1 - c0, host_threads(c1 - c0),
-                               [&](size_t, size_t q0, size_t q1) { build(g, c0 + q0, c0 + q1); });
-            } catch (...) {
-                bld.err = std::current_exception();
-            }
-        });
+    const size_t G = P >= 2 * kChunkPairs ? (P + kChunkPairs - 1) / kChunkPairs : 1;
+    if (G == 1) {
+        align<Ty>(ALGO, sc, fn, has_fn, pairs, res, ops, off);
+        build_range(0, P);
+        tm.lap("AlignedSequence lists");
+        return out;
     }
-    bld.join();
-    if (bld.err) std::rethrow_exception(bld.err);
-    tm.lap("AlignedSequence lists (last chunk)");
+    // landed ranges, built in arrival order by one builder thread
+    struct Queue {
+        std::mutex mu;
+        std::condition_variable cv;
+        std::deque<std::pair<size_t, size_t>> q;
+        bool closed = false;
+        std::exception_ptr err;
+    } lq;
+    std::thread builder([&] {
+        for (;;) {
+            std::pair<size_t, size_t> r;
+            {
+                std::unique_lock<std::mutex> lk(lq.mu);
+                lq.cv.wait(lk, [&] { return lq.closed || !lq.q.empty(); });
+                if (lq.q.empty()) return;
+                r = lq.q.front();
+                lq.q.pop_front();
+            }
+            try {
+                build_range(r.first, r.second);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(lq.mu);
+                if (!lq.err) lq.err = std::current_exception();
+            }
+        }
+    });
+    auto close = [&] {
+        {
+            std::lock_guard<std::mutex> lk(lq.mu);
+            lq.closed = true;
+        }
+        lq.cv.notify_one();
+        builder.join();
+    };
+    try {
+        align<Ty>(ALGO, sc, fn, has_fn, pairs, res, ops, off, (uint32_t)G, [&](size_t p0, size_t p1) {
+            {
+                std::lock_guard<std::mutex> lk(lq.mu);
+                lq.q.emplace_back(p0, p1);
+            }
+            lq.cv.notify_one();
+        });
+    } catch (...) {
+        close();
+        throw;
+    }
+    tm.lap("GPU call (lists overlapped)");
+    close();
+    if (lq.err) std::rethrow_exception(lq.err);
+    tm.lap("AlignedSequence lists (tail)");
     return out;
 }
 

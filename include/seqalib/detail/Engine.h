@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -308,10 +309,17 @@ void code_symbols(std::false_type, Coder& coder, const std::vector<std::pair<Con
 
 // Aligns a batch of (Seq1, Seq2) pairs on the GPU.  Returns the per-pair results and the op
 // streams (traceback order).  has_fn = false means the reference's nullptr match fn (equality).
+// chunks > 1: the GPU call runs in that many pair ranges (sa_align_batch_cb) and on_chunk(p0, p1)
+// is called, on this thread, as soon as a range's results and op streams are in res / ops (the
+// other paths report the whole batch once at the end).
+using ChunkFn = std::function<void(size_t, size_t)>;
+inline void chunk_tramp(void* user, uint32_t p0, uint32_t p1) { (*static_cast<ChunkFn*>(user))(p0, p1); }
+
 template <typename Ty, typename ContainerType, typename MatchFnTy>
 void align(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
            const std::vector<std::pair<ContainerType*, ContainerType*>>& pairs,
-           std::vector<sa_result>& res, raw_vector<uint8_t>& ops, std::vector<uint64_t>& ops_off) {
+           std::vector<sa_result>& res, raw_vector<uint8_t>& ops, std::vector<uint64_t>& ops_off,
+           uint32_t chunks = 0, ChunkFn on_chunk = nullptr) {
     PhaseTimer tm;
     SymbolCoder<Ty> coder;
     std::vector<uint64_t> o1(1, 0), o2(1, 0);
@@ -327,6 +335,7 @@ void align(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
     tm.lap("symbol coding");
     if (coder.overflow) {   // more than 256 distinct symbols: the generic-Ty (bitmap) path
         align_bits<Ty>(algo, sc, fn, has_fn, pairs, res, ops, ops_off);
+        if (on_chunk && !pairs.empty()) on_chunk(0, pairs.size());
         return;
     }
     std::vector<uint8_t> lut;
@@ -344,9 +353,11 @@ void align(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
         if (rc != SA_OK)
             throw std::runtime_error(std::string("seqalib: sa_multi_align_batch: ") + sa_status_string(rc) + " (" +
                                      sa_multi_last_error(mg) + ")");
+        if (on_chunk && n) on_chunk(0, n);
     } else {
-        check(sa_align_batch(context(), algo, &sc, s1.data(), o1.data(), s2.data(), o2.data(), n,
-                             has_fn ? lut.data() : nullptr, res.data(), ops.data(), cap),
+        check(sa_align_batch_cb(context(), algo, &sc, s1.data(), o1.data(), s2.data(), o2.data(), n,
+                                has_fn ? lut.data() : nullptr, res.data(), ops.data(), cap, chunks,
+                                on_chunk ? chunk_tramp : nullptr, on_chunk ? &on_chunk : nullptr),
               "sa_align_batch");
     }
     tm.lap("sa_align_batch (GPU)");

@@ -140,6 +140,19 @@ int sa_align_batch(sa_ctx* ctx, int algo, const sa_scoring* scoring,
                    const uint8_t* seq2, const uint64_t* seq2_off, uint32_t npairs,
                    const uint8_t* match_lut, sa_result* results, uint8_t* ops, uint64_t ops_cap);
 
+/* sa_align_batch in `chunks` contiguous pair ranges of near-equal sum of m*n (0: one, or
+ * $SEQALIB_HOST_CHUNKS), pipelined on the device (chunk g's traceback beside chunk g+1's fill), and
+ * cb(user, pair_begin, pair_end) called on the calling thread as soon as a range's results and op
+ * streams are in the caller's buffers -- so a caller can post-process chunk g (the C++ drop-in
+ * builds its AlignedSequence lists) while later chunks are still on the GPU.  cb may be NULL.
+ * LocalGotoh reports the whole batch once at the end; Hirschberg / Myers-Miller run as one chunk. */
+typedef void (*sa_chunk_cb)(void* user, uint32_t pair_begin, uint32_t pair_end);
+int sa_align_batch_cb(sa_ctx* ctx, int algo, const sa_scoring* scoring,
+                      const uint8_t* seq1, const uint64_t* seq1_off,
+                      const uint8_t* seq2, const uint64_t* seq2_off, uint32_t npairs,
+                      const uint8_t* match_lut, sa_result* results, uint8_t* ops, uint64_t ops_cap,
+                      uint32_t chunks, sa_chunk_cb cb, void* user);
+
 /* Generic-Ty batch API (any symbol type, any number of distinct symbols: the path the C++
  * drop-in takes when a batch has more than 256 distinct symbols).  Instead of symbols the caller
  * passes each pair's match matrix -- the reference's cacheAllMatches (e.g. SASmithWaterman.h:
@@ -183,6 +196,10 @@ int sa_align_batch_device(sa_ctx* ctx, int algo, const sa_scoring* scoring,
  * recorded on the stream they ran on: total fill-kernel ms, total traceback-kernel ms, and the
  * number of fill launches.  Waits for those events. */
 int sa_last_timings(sa_ctx* ctx, float* fill_ms, float* traceback_ms, int* fill_launches);
+// With $SEQALIB_KERNEL_TIMING set during the last call: the fill kernels alone (HIP events around
+// each fill launch on its stream) and the whole fill-stream span (fill + end-cell replay, = the
+// fill_ms of sa_last_timings).  SA_ERR_ARG when the last call ran without the variable.
+int sa_last_kernel_timings(sa_ctx* ctx, float* fill_kernel_ms, float* fill_stream_ms);
 
 /* Fill kernel of the last sa_align_batch[_device] call: SA_KERNEL_INT32 (int32 scores, equality
  * flags; any alphabet, LUT, scoring) or SA_KERNEL_T16 (tagged 16-bit profile kernels: SW/NW and,

@@ -125,6 +125,7 @@ def load_library():
     L.sa_align_batch_device.argtypes = [vp, C.c_int, C.POINTER(_Scoring), vp, vp, vp, vp, C.c_uint32,
                                         C.c_uint32, C.c_uint32, vp, vp, vp, vp]
     L.sa_last_timings.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_float), i32p]
+    L.sa_last_kernel_timings.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_float)]
     L.sa_plan_query.argtypes = [C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, i32p, i32p, u64p, u64p]
     L.sa_plan_query_ex.argtypes = [C.c_int, C.POINTER(_Scoring), C.c_uint32, C.c_uint32, C.c_uint32, C.c_int,
                                    i32p, i32p, i32p, u64p]
@@ -137,7 +138,7 @@ def load_library():
     L.sa_synth_dna_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_int]
     for fn in ("sa_set_workspace_limit", "sa_trim", "sa_align_batch", "sa_align_batch_bits", "sa_align_batch_device",
                "sa_multi_create", "sa_multi_align_batch",
-               "sa_last_timings", "sa_last_plan", "sa_last_plan_ex", "sa_plan_query", "sa_plan_query_ex", "sa_synth_dna", "sa_synth_mutate", "sa_synth_dna_batch",
+               "sa_last_timings", "sa_last_kernel_timings", "sa_last_plan", "sa_last_plan_ex", "sa_plan_query", "sa_plan_query_ex", "sa_synth_dna", "sa_synth_mutate", "sa_synth_dna_batch",
                "sa_create", "sa_device_count", "sa_set_pipeline", "sa_wait"):
         getattr(L, fn).restype = C.c_int
     if L.sa_version() != 1:
@@ -485,6 +486,13 @@ class Engine:
         f, t, n = C.c_float(), C.c_float(), C.c_int()
         self._check(self.L.sa_last_timings(self.h, C.byref(f), C.byref(t), C.byref(n)), "sa_last_timings")
         return f.value, t.value, n.value
+
+    def last_kernel_timings(self) -> Tuple[float, float]:
+        """(fill kernels alone, fill stream = fill + end-cell replay) of the last call, ms; the call
+        must have run with $SEQALIB_KERNEL_TIMING set."""
+        f, s = C.c_float(), C.c_float()
+        self._check(self.L.sa_last_kernel_timings(self.h, C.byref(f), C.byref(s)), "sa_last_kernel_timings")
+        return f.value, s.value
 
 
     def last_plan_ex(self) -> Tuple[int, int, int, int]:

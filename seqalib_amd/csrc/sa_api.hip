@@ -22,6 +22,8 @@
 
 using namespace sa;
 
+constexpr int kKEv = 6;   // SEQALIB_KERNEL_TIMING events per fill launch (two per variant, <= 3)
+
 struct sa_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -36,6 +38,10 @@ struct sa_ctx {
     // timing of the last call
     std::vector<hipEvent_t> events;  // 3 per fill launch: start, fill end, traceback end
     int launches = 0;
+    // $SEQALIB_KERNEL_TIMING: per launch and variant, events around the fill kernel alone
+    // (kKEv per launch: [2k] before, [2k + 1] after variant k's fill; kvars[launch] variants)
+    std::vector<hipEvent_t> kevents;
+    std::vector<int> kvars;
     hipStream_t timed_stream = nullptr;
     // aux words of the T16 decision (sa_internal.h kAux*), one kAuxWords slot per pipeline slot
     uint32_t* aux = nullptr;
@@ -577,6 +583,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     const bool lut = !bits && d_lutbits != nullptr;
     const T16Mode tm = bits ? T16Mode{} : t16_candidate(algo, sc, max_m, max_n, npairs);
     const bool t16 = tm.ok;
+    const bool kernel_timing = getenv("SEQALIB_KERNEL_TIMING") != nullptr;
     if (!c->aux) SA_HIP(c, hipMalloc(&c->aux, 2 * kAuxWords * 4));
     if (!c->h_sel) {
         SA_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_sel), 64, hipHostMallocDefault));
@@ -718,6 +725,17 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             c->events.push_back(ev);
         }
         hipEvent_t* ev = &c->events[3 * c->launches];
+        hipEvent_t* kev = nullptr;   // SEQALIB_KERNEL_TIMING: fill-kernel-only events
+        if (kernel_timing) {
+            while ((int)c->kevents.size() < kKEv * (c->launches + 1)) {
+                hipEvent_t e;
+                SA_HIP(c, hipEventCreate(&e));
+                c->kevents.push_back(e);
+            }
+            c->kvars.resize(c->launches + 1);
+            c->kvars[c->launches] = nv;
+            kev = &c->kevents[kKEv * c->launches];
+        }
         // the launches of one call share the slot: launch k+1's fill overwrites the records
         // launch k's traceback reads (on the other stream when pipelined)
         if (pipe && c->launches > 0) SA_HIP(c, hipStreamWaitEvent(sf, c->events[3 * c->launches - 1], 0));
@@ -778,8 +796,10 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             const FillVariant fv = make_fp(k);
             const FillParams& fp = fps[k];
             if (pl.split) SA_HIP(c, hipMemsetAsync(fp.ticket, 0, 256 + hand_x_off * 8 * aff2, sf));
+            if (kev) SA_HIP(c, hipEventRecord(kev[2 * k], sf));
             hipError_t e = launch_fill(algo, fv, fp, pl.split ? (uint32_t)(cnt * sp_bands) : cnt, sf);
             if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
+            if (kev) SA_HIP(c, hipEventRecord(kev[2 * k + 1], sf));
             if (pl.split) {
                 SplitReduceParams rp;
                 rp.off1 = o1; rp.off2 = o2; rp.part = fp.part; rp.res = d_res;
@@ -1100,7 +1120,8 @@ std::vector<uint32_t> cut_by_cells(const uint64_t* off1, const uint64_t* off2, u
 
 int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, const uint64_t* off1,
                const uint8_t* seq2, const uint64_t* off2, uint32_t npairs, const uint8_t* lut,
-               sa_result* results, uint8_t* ops, uint64_t ops_cap) {
+               sa_result* results, uint8_t* ops, uint64_t ops_cap, uint32_t chunks = 0,
+               sa_chunk_cb cb = nullptr, void* cb_user = nullptr) {
     // $SEQALIB_HOST_TIMING: host-side phases of the call (stderr)
     const bool timing = getenv("SEQALIB_HOST_TIMING") != nullptr;
     const auto t_call = std::chrono::steady_clock::now();
@@ -1117,7 +1138,7 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     const bool use_lut = lut && !lut_is_identity(lut) &&
                          !(t1 + t2 <= kHostScanBytes && lut_identity_on(lut, seq1, t1, seq2, t2));
     const bool dc = algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER;
-    const uint32_t G = host_chunks(algo, npairs);
+    const uint32_t G = chunks && !dc ? std::min(chunks, npairs) : host_chunks(algo, npairs);
     const std::vector<uint32_t> cut = cut_by_cells(off1, off2, npairs, G);
 
     // device I/O layout (256-byte aligned pieces); chunk g's offsets (rebased to its first pair)
@@ -1279,6 +1300,7 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
             memcpy(results + cut[o.g], sres + cut[o.g], sizeof(sa_result) * (cut[o.g + 1] - cut[o.g]));
         par_copy(ops + o.ob, sops + o.ob, o.on);
         ms_out += since(t_o);
+        if (cb && (k + 1 == outp.size() || outp[k + 1].g != o.g)) cb(cb_user, cut[o.g], cut[o.g + 1]);   // chunk landed
     }
     if (pipe) {
         SA_HIP(c, hipStreamSynchronize(c->s_fill));
@@ -1404,6 +1426,7 @@ void sa_destroy(sa_ctx* c) {
     (void)drain(c);
     if (c->s_out) (void)hipStreamSynchronize(c->s_out);
     for (auto ev : c->events) (void)hipEventDestroy(ev);
+    for (auto ev : c->kevents) (void)hipEventDestroy(ev);
     for (auto ev : c->host_ev) (void)hipEventDestroy(ev);
     if (c->s_out) (void)hipStreamDestroy(c->s_out);
     for (auto ev : {c->ev_in, c->ev_slot[0], c->ev_slot[1], c->ev_sel, c->ev_last})
@@ -1446,6 +1469,14 @@ int sa_trim(sa_ctx* c) {
 int sa_align_batch(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1,
                    const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2, uint32_t npairs,
                    const uint8_t* lut, sa_result* results, uint8_t* ops, uint64_t ops_cap) {
+    return sa_align_batch_cb(c, algo, sc, seq1, off1, seq2, off2, npairs, lut, results, ops, ops_cap, 0, nullptr,
+                             nullptr);
+}
+
+int sa_align_batch_cb(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1,
+                      const uint64_t* off1, const uint8_t* seq2, const uint64_t* off2, uint32_t npairs,
+                      const uint8_t* lut, sa_result* results, uint8_t* ops, uint64_t ops_cap, uint32_t chunks,
+                      sa_chunk_cb cb, void* cb_user) {
     if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
     int rc = validate_scoring(c, algo, sc);
     if (rc) return rc;
@@ -1456,8 +1487,9 @@ int sa_align_batch(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq
     if ((rc = order_after_last(c, c->stream))) return rc;
 
     if (algo != SA_LOCAL_GOTOH)
-        return align_host(c, algo, sc, seq1, off1, seq2, off2, npairs, lut, results, ops, ops_cap);
-    return lg_hack_split(c, off1, off2, npairs, results, ops, ops_cap,
+        return align_host(c, algo, sc, seq1, off1, seq2, off2, npairs, lut, results, ops, ops_cap, chunks, cb, cb_user);
+    // LocalGotoh: the size-hack pairs run as their own NW batch, so the whole range lands at the end
+    rc = lg_hack_split(c, off1, off2, npairs, results, ops, ops_cap,
                          [&](int a, const std::vector<uint32_t>& sel, const std::vector<uint64_t>& o1,
                              const std::vector<uint64_t>& o2, sa_result* r, uint8_t* op, uint64_t cap) {
                              if (sel.size() == npairs)
@@ -1472,6 +1504,8 @@ int sa_align_batch(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq
                              return align_host(c, a, sc, s1.data(), o1.data(), s2.data(), o2.data(),
                                                (uint32_t)sel.size(), lut, r, op, cap);
                          });
+    if (rc == SA_OK && cb && npairs) cb(cb_user, 0, npairs);
+    return rc;
 }
 
 int sa_align_batch_bits(sa_ctx* c, int algo, const sa_scoring* sc, const uint64_t* off1, const uint64_t* off2,
@@ -1588,6 +1622,28 @@ int sa_last_timings(sa_ctx* c, float* fill_ms, float* tb_ms, int* launches) {
     if (fill_ms) *fill_ms = f;
     if (tb_ms) *tb_ms = t;
     if (launches) *launches = c->launches;
+    return SA_OK;
+}
+
+int sa_last_kernel_timings(sa_ctx* c, float* fill_kernel_ms, float* fill_stream_ms) {
+    if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
+    float f = 0.f, s = 0.f;
+    if ((int)c->kvars.size() < c->launches)
+        return fail(c, SA_ERR_ARG, "the last call ran without SEQALIB_KERNEL_TIMING");
+    for (int k = 0; k < c->launches; ++k) {
+        hipEvent_t* ev = &c->events[3 * k];
+        SA_HIP(c, hipEventSynchronize(ev[1]));
+        float a = 0.f;
+        SA_HIP(c, hipEventElapsedTime(&a, ev[0], ev[1]));
+        s += a;
+        for (int v = 0; v < c->kvars[k]; ++v) {
+            hipEvent_t* kev = &c->kevents[kKEv * k + 2 * v];
+            SA_HIP(c, hipEventElapsedTime(&a, kev[0], kev[1]));
+            f += a;
+        }
+    }
+    if (fill_kernel_ms) *fill_kernel_ms = f;
+    if (fill_stream_ms) *fill_stream_ms = s;
     return SA_OK;
 }
 

@@ -87,3 +87,46 @@ def test_types_over_two_contexts_matches_reference_build(binaries, engine):
     env = dict(os.environ, SEQALIB_DEVICES="0,0")
     out = subprocess.run([binaries[1]], capture_output=True, text=True, timeout=300, check=True, env=env).stdout
     assert out == ref
+
+
+def _fnv(s: str) -> int:
+    h = 1469598103934665603
+    for c in s.encode("latin-1"):
+        h = ((h ^ c) * 1099511628211) & (2 ** 64 - 1)
+    return h
+
+
+def test_chunked_batch_lists_match_oracle(binaries, engine):
+    """tests/cpp/dropin_chunks: 4,500 pairs through getAlignments(), aligned as three chunks of one
+    sa_align_batch_cb call whose lists are built while later chunks run (SequenceAlignment.h run):
+    every pair's printAlignment rows must equal the full-matrix oracle's (SASmithWaterman.h
+    getAlignment incl. forceGlobal)."""
+    import numpy as np
+    import seqalib_amd as sa
+    from util import oracle_batch, pack_bytes
+    P = 4500
+    out = subprocess.run([os.path.join(CPP, "dropin_chunks"), str(P)], capture_output=True, text=True, timeout=240,
+                         check=True).stdout.split()
+    assert len(out) == P
+    pairs = []
+    for p in range(P):
+        m, n = 40 + (37 * p) % 260, 30 + (53 * p) % 270
+        a = sa.synth_dna(7_000_000_000 + 2 * p + 1, m)
+        b = bytearray(sa.synth_dna(7_000_000_000 + 2 * p + 2, n))
+        if p % 3 == 0:
+            for k in range(min(m, n)):
+                if k % 11 != 5:
+                    b[k] = a[k]
+        pairs.append((a, bytes(b)))
+    sw = (-1, 1, -1)
+    s1, o1, s2, o2 = pack_bytes(pairs)
+    res, ops = oracle_batch(0, sw, s1, o1, s2, o2, threads=16)
+    bad = []
+    for p, (a, b) in enumerate(pairs):
+        off = int(o1[p] + o2[p]) + p
+        r = sa.PairResult(int(res["score"][p]), int(res["end_i"][p]), int(res["end_j"][p]), int(res["start_i"][p]),
+                          int(res["start_j"][p]), int(res["flags"][p]), ops[off:off + int(res["nops"][p])].tobytes())
+        rows = sa.expand_ops(sa.SA_SW, a.decode("latin-1"), b.decode("latin-1"), r).rows()
+        if int(out[p], 16) != _fnv("\n".join(rows)):
+            bad.append(p)
+    assert not bad, (len(bad), bad[:10])
