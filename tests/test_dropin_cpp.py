@@ -125,7 +125,7 @@ def test_chunked_batch_lists_match_oracle(binaries, engine):
     for p, (a, b) in enumerate(pairs):
         off = int(o1[p] + o2[p]) + p
         r = sa.PairResult(int(res["score"][p]), int(res["end_i"][p]), int(res["end_j"][p]), int(res["start_i"][p]),
-                          int(res["start_j"][p]), int(res["flags"][p]), ops[off:off + int(res["nops"][p])].tobytes())
+                          int(res["start_j"][p]), 0, ops[off:off + int(res["nops"][p])].tobytes())
         rows = sa.expand_ops(sa.SA_SW, a.decode("latin-1"), b.decode("latin-1"), r).rows()
         if int(out[p], 16) != _fnv("\n".join(rows)):
             bad.append(p)
