@@ -426,16 +426,10 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
     const uint32_t CU = (uint32_t)(-(4 * G + 2)) & 0xffffu;
     const uint32_t CL = (uint32_t)(4 * G + 1) & 0xffffu;
 
-    uint32_t k = 0, k0 = 0;
-    const int opb = L::kOps + quad * kSoOps;
+    uint32_t k = 0;
     auto emit = [&](uint8_t op) __attribute__((always_inline)) {
-        vb[opb + (k - k0)] = op;   // (the quad's four lanes write the same byte)
+        if (sub == 0) ops[k] = op;   // (a store in flight costs the walk nothing)
         ++k;
-    };
-    auto flush = [&]() __attribute__((always_inline)) {
-        if (sub == 0)
-            for (uint32_t q = 0; q < k - k0; ++q) ops[k0 + q] = vb[opb + q];
-        k0 = k;
     };
     int wb = -1, wt = 0, wc = 0;
     int cb = 0, ct = 0, cc = 0, cr = 0, cq = 0;
@@ -450,9 +444,33 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         cq = s & 31;
     };
     auto ready = [&](int i, int j) __attribute__((always_inline)) -> bool {
-        if (k - k0 >= (uint32_t)kSoOps) return false;
         locate(i, j);
         return cb == wb && ct == wt && cc == wc;
+    };
+    // the walk's view of the block, in registers: the quad's R row codes and 32 column codes (2 bits
+    // each), the tag column it stands in (W, the four sublanes' words) and the one to its left (NW,
+    // read ahead so that a diagonal or left move finds it ready)
+    uint64_t rowc = 0, colc = 0;
+    uint4 W = make_uint4(0, 0, 0, 0), NW = make_uint4(0, 0, 0, 0);
+    int wq = -1;
+    auto tagcol = [&](int q) __attribute__((always_inline)) -> uint4 {
+        uint4 w;
+        w.x = vw[q * 64 + quad * 4 + 0];
+        w.y = vw[q * 64 + quad * 4 + 1];
+        w.z = vw[q * 64 + quad * 4 + 2];
+        w.w = vw[q * 64 + quad * 4 + 3];
+        return w;
+    };
+    auto pack_codes = [&](int base) __attribute__((always_inline)) -> uint64_t {   // 32 bytes of 8 x code
+        uint64_t c = 0;
+#pragma unroll
+        for (int d = 0; d < 8; ++d) {
+            uint32_t x = (vw[(base >> 2) + d] >> 3) & 0x03030303u;   // four codes, one per byte
+            x = (x | (x >> 6)) & 0x000f000fu;
+            x = (x | (x >> 12)) & 0xffu;
+            c |= (uint64_t)x << (8 * d);
+        }
+        return c;
     };
     // recompute the block holding (i, j), columns up to j; every lane of a live quad takes part
     // (a finished or dead quad runs the same sub-step loop on a zero-width column range)
@@ -522,28 +540,36 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the edge DMA and the code stores
-        // sub-steps: sublane k at column qlo + u - k; its row above from sublane k-1 (DPP)
+        // sub-steps: sublane k at column qlo + u - k; its row above from sublane k-1 (DPP).  The
+        // column code and (sublane 0) the top row value of the next sub-step are read one sub-step
+        // ahead, so no sub-step waits on LDS.
         int hl = Hp[RS - 1];
         int prev_up = corner;
         int nmax = qhi - qlo + 1 + 3;   // sub-steps of this quad; the wave runs the most of any
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
+        auto rd_sym = [&](int q) __attribute__((always_inline)) -> uint32_t {
+            return act && q >= qlo && q <= qhi ? (uint32_t)vb[L::kColC + quad * 32 + q] : 0u;
+        };
+        auto rd_top = [&](int q) __attribute__((always_inline)) -> int {
+            if (sub != 0 || !act || !has_top || q < qlo || q > qhi) return 0;
+            const int s = slo + q;
+            const int d = (s >> 3) - pk0;
+            const int off = d < 4 ? L::kEdge + (quad * 4 + d) * 16 : L::kEdge2 + quad * 64;
+            return (int)((lds_u16*)(s_so + off + (s & 7) * 2))[0] << 2;
+        };
+        uint32_t nsym = rd_sym(qlo - sub);
+        int ntop = rd_top(qlo);
         for (int u = 0; u < nmax; ++u) {
             const int q = qlo + u - sub;
+            const uint32_t sym = nsym;
+            const int top = ntop;
+            nsym = rd_sym(q + 1);
+            ntop = rd_top(q + 1);
             int up_h = __builtin_amdgcn_mov_dpp(hl, 0x90, 0xf, 0xf, false);   // quad_perm [0,0,1,2]
             const bool on = act && q >= qlo && q <= qhi;
-            if (sub == 0) {
-                int top = 0;
-                if (on && has_top) {
-                    const int s = slo + q;
-                    const int d = (s >> 3) - pk0;
-                    const int off = d < 4 ? L::kEdge + (quad * 4 + d) * 16 : L::kEdge2 + quad * 64;
-                    top = (int)((lds_u16*)(s_so + off + (s & 7) * 2))[0] << 2;
-                }
-                up_h = top;
-            }
+            if (sub == 0) up_h = top;
             if (on) {
-                const uint32_t sym = vb[L::kColC + quad * 32 + q];
                 uint32_t dcur;
                 asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(dcur) : "v"(tab[0]), "v"(sym), "v"(prev_up));
                 uint32_t hu = (uint32_t)up_h, rec = 0;
@@ -569,13 +595,27 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
                 hl = Hp[RS - 1];
             }
         }
+        if (act) {   // (in-order LDS: these reads see the codes and tags stored above)
+            rowc = pack_codes(L::kRowC + quad * 32);
+            colc = pack_codes(L::kColC + quad * 32);
+            wq = qhi;
+            W = tagcol(qhi);
+            NW = qhi > 0 ? tagcol(qhi - 1) : make_uint4(0, 0, 0, 0);
+        }
     };
     auto tag = [&]() __attribute__((always_inline)) -> uint32_t {
-        return (vw[cq * 64 + quad * 4 + cr / RS] >> (2 * (cr % RS))) & 3u;
+        if (cq != wq) {   // one column left (a diagonal or left move): the word read ahead
+            W = NW;
+            wq = cq;
+            if (cq > 0) NW = tagcol(cq - 1);
+        }
+        const int sl = cr / RS;
+        const uint32_t w = sl == 0 ? W.x : sl == 1 ? W.y : sl == 2 ? W.z : W.w;
+        return (w >> (2 * (cr % RS))) & 3u;
     };
     auto cell_match = [&]() __attribute__((always_inline)) -> bool {
-        const uint32_t a = (vb[L::kRowC + quad * 32 + cr] >> 3) & 3u;
-        const uint32_t b = (vb[L::kColC + quad * 32 + cq] >> 3) & 3u;
+        const uint32_t a = (uint32_t)(rowc >> (2 * cr)) & 3u;
+        const uint32_t b = (uint32_t)(colc >> (2 * cq)) & 3u;
         return ((mt >> (a * 4 + b)) & 1u) != 0;
     };
 
@@ -585,7 +625,6 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
     for (;;) {
         if (__builtin_amdgcn_ballot_w64(!fin && !parked) == 0) {
             if (__builtin_amdgcn_ballot_w64(!fin) == 0) break;
-            if (!fin) flush();
             recompute(!fin, i, j);   // every lane: the sub-step loop uses DPP across the quad
             if (!fin) parked = false;
         }
@@ -606,7 +645,6 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         }
     }
     if (live) {
-        flush();
         if (sub == 0) {
             res.start_i = i;
             res.start_j = j;
