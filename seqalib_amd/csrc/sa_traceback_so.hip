@@ -365,6 +365,19 @@ __global__ __launch_bounds__(64) void traceback_so_kernel(TbParams P) {
 // (32 + 3) sub-steps x R/4 rows, and the wave's registers (R/4 rows of state) stay few, so the
 // traceback beside the next call's fill displaces fewer of its waves.
 constexpr int kSo4Pairs = 16;
+#ifdef SA_TB_STATS
+// Debug build only (-DSA_TB_STATS, tools/so4_stats.py), per wave summed: [rounds, walk-loop
+// iterations, moves, wave cycles, recompute: load-wait cycles, sub-step cycles, sub-steps, waves]
+__device__ unsigned long long g_so4_stats[8];
+extern "C" int sa_debug_so4_stats(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_so4_stats), sizeof(g_so4_stats)) != hipSuccess) return 1;
+    if (reset) {
+        unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_so4_stats), z, sizeof(z)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
 template <int R>
 struct So4Lds {
     static constexpr int kTags = 0;                         // [column q][lane] words
@@ -443,23 +456,16 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         cc = s >> 5;
         cq = s & 31;
     };
-    auto ready = [&](int i, int j) __attribute__((always_inline)) -> bool {
-        locate(i, j);
-        return cb == wb && ct == wt && cc == wc;
-    };
     // the walk's view of the block, in registers: the quad's R row codes and 32 column codes (2 bits
     // each), the tag column it stands in (W, the four sublanes' words) and the one to its left (NW,
     // read ahead so that a diagonal or left move finds it ready)
     uint64_t rowc = 0, colc = 0;
-    uint4 W = make_uint4(0, 0, 0, 0), NW = make_uint4(0, 0, 0, 0);
+    uint64_t W = 0, NW = 0, NNW = 0;   // tag columns wq, wq - 1, wq - 2: row r at bits 2r
     int wq = -1;
-    auto tagcol = [&](int q) __attribute__((always_inline)) -> uint4 {
-        uint4 w;
-        w.x = vw[q * 64 + quad * 4 + 0];
-        w.y = vw[q * 64 + quad * 4 + 1];
-        w.z = vw[q * 64 + quad * 4 + 2];
-        w.w = vw[q * 64 + quad * 4 + 3];
-        return w;
+    auto tagcol = [&](int q) __attribute__((always_inline)) -> uint64_t {   // the quad's 4 words, packed
+        const uint64_t w0 = vw[q * 64 + quad * 4 + 0], w1 = vw[q * 64 + quad * 4 + 1];
+        const uint64_t w2 = vw[q * 64 + quad * 4 + 2], w3 = vw[q * 64 + quad * 4 + 3];
+        return w0 | w1 << (2 * RS) | w2 << (4 * RS) | w3 << (6 * RS);
     };
     auto pack_codes = [&](int base) __attribute__((always_inline)) -> uint64_t {   // 32 bytes of 8 x code
         uint64_t c = 0;
@@ -474,7 +480,15 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
     };
     // recompute the block holding (i, j), columns up to j; every lane of a live quad takes part
     // (a finished or dead quad runs the same sub-step loop on a zero-width column range)
+#ifdef SA_TB_STATS
+    unsigned long long st_rounds = 0, st_iters = 0, st_wait = 0, st_sub = 0, st_nsub = 0;
+    const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
+    unsigned long long st_a = 0;
+#endif
     auto recompute = [&](bool act, int i, int j) __attribute__((always_inline)) {
+#ifdef SA_TB_STATS
+        st_a = __builtin_amdgcn_s_memtime();
+#endif
         int r0 = 0, j0 = 0, qlo = 0, qhi = -1, slo = 0, pk0 = 0, bp = 0, tp = 0;
         bool has_top = false, has_left = false;
         if (act) {
@@ -540,6 +554,13 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the edge DMA and the code stores
+#ifdef SA_TB_STATS
+        {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            st_wait += t - st_a;
+            st_a = t;
+        }
+#endif
         // sub-steps: sublane k at column qlo + u - k; its row above from sublane k-1 (DPP).  The
         // column code and (sublane 0) the top row value of the next sub-step are read one sub-step
         // ahead, so no sub-step waits on LDS.
@@ -556,14 +577,14 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
             const int s = slo + q;
             const int d = (s >> 3) - pk0;
             const int off = d < 4 ? L::kEdge + (quad * 4 + d) * 16 : L::kEdge2 + quad * 64;
-            return (int)((lds_u16*)(s_so + off + (s & 7) * 2))[0] << 2;
+            return (int)((lds_u16*)(s_so + off + (s & 7) * 2))[0];   // (x 4 at the use: no wait here)
         };
         uint32_t nsym = rd_sym(qlo - sub);
         int ntop = rd_top(qlo);
         for (int u = 0; u < nmax; ++u) {
             const int q = qlo + u - sub;
             const uint32_t sym = nsym;
-            const int top = ntop;
+            const int top = ntop << 2;
             nsym = rd_sym(q + 1);
             ntop = rd_top(q + 1);
             int up_h = __builtin_amdgcn_mov_dpp(hl, 0x90, 0xf, 0xf, false);   // quad_perm [0,0,1,2]
@@ -595,55 +616,82 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
                 hl = Hp[RS - 1];
             }
         }
+#ifdef SA_TB_STATS
+        st_sub += __builtin_amdgcn_s_memtime() - st_a;
+        st_nsub += (unsigned long long)nmax;
+#endif
         if (act) {   // (in-order LDS: these reads see the codes and tags stored above)
             rowc = pack_codes(L::kRowC + quad * 32);
             colc = pack_codes(L::kColC + quad * 32);
             wq = qhi;
             W = tagcol(qhi);
-            NW = qhi > 0 ? tagcol(qhi - 1) : make_uint4(0, 0, 0, 0);
+            NW = tagcol(max(qhi - 1, 0));
+            NNW = tagcol(max(qhi - 2, 0));
         }
-    };
-    auto tag = [&]() __attribute__((always_inline)) -> uint32_t {
-        if (cq != wq) {   // one column left (a diagonal or left move): the word read ahead
-            W = NW;
-            wq = cq;
-            if (cq > 0) NW = tagcol(cq - 1);
-        }
-        const int sl = cr / RS;
-        const uint32_t w = sl == 0 ? W.x : sl == 1 ? W.y : sl == 2 ? W.z : W.w;
-        return (w >> (2 * (cr % RS))) & 3u;
-    };
-    auto cell_match = [&]() __attribute__((always_inline)) -> bool {
-        const uint32_t a = (uint32_t)(rowc >> (2 * cr)) & 3u;
-        const uint32_t b = (uint32_t)(colc >> (2 * cq)) & 3u;
-        return ((mt >> (a * 4 + b)) & 1u) != 0;
     };
 
     int i = res.end_i, j = res.end_j, V = res.score;
     if (m == 0 || n == 0) { i = 0; j = 0; }
     bool fin = !live, parked = true;
+    // One move per iteration, branch-free (a lone wave pays for every divergent branch): every lane
+    // evaluates the move of its cell and applies it only when it may (mv).  A move lands in the
+    // walk's tag column or one to its left (W / NW); the column two to the left (NNW) is read a
+    // full iteration before it can be needed.
     for (;;) {
+#ifdef SA_TB_STATS
+        ++st_iters;
+#endif
         if (__builtin_amdgcn_ballot_w64(!fin && !parked) == 0) {
             if (__builtin_amdgcn_ballot_w64(!fin) == 0) break;
+#ifdef SA_TB_STATS
+            ++st_rounds;
+#endif
             recompute(!fin, i, j);   // every lane: the sub-step loop uses DPP across the quad
             if (!fin) parked = false;
         }
-        if (!fin && !parked) {
-            if (!(i > 0 && j > 0) || V == 0) {   // SASmithWaterman.h: stop on an edge or at H == 0
-                fin = true;
-            } else if (!ready(i, j)) {
-                parked = true;
-            } else {
-                const uint32_t f = tag();
-                const bool dg = f == 3u, up = f == 2u;
-                const bool v = dg && cell_match();
-                emit(dg ? (v ? 'M' : (allow ? 'S' : 'X')) : (up ? 'U' : 'L'));
-                V -= dg ? (v ? MA : MI) : G;
-                i -= (dg || up) ? 1 : 0;
-                j -= up ? 0 : 1;
-            }
-        }
+        // (cr, cq): the cell's row and column in the block, kept by the moves (recompute locates
+        // the entry cell); a move that takes either below 0 has left the block
+        const bool act = !fin && !parked;
+        const bool stop = !(i > 0 && j > 0) || V == 0;   // SASmithWaterman.h: an edge or H == 0
+        const bool inb = cr >= 0 && cq >= 0;
+        const bool mv = act && !stop && inb;
+        fin = fin || (act && stop);
+        parked = parked || (act && !stop && !inb);
+        const bool lft = cq != wq;
+        const uint64_t col = lft ? NW : W;
+        const uint32_t r2 = 2u * (uint32_t)(cr & 31), q2 = 2u * (uint32_t)(cq & 31);   // (bit pairs)
+        auto half = [](uint64_t x, uint32_t b) __attribute__((always_inline)) -> uint32_t {
+            return ((b < 32 ? (uint32_t)x : (uint32_t)(x >> 32)) >> (b & 31u)) & 3u;
+        };
+        const uint32_t f = half(col, r2);
+        const bool dg = f == 3u, up = f == 2u;
+        const bool v = dg & (((mt >> (half(rowc, r2) * 4 + half(colc, q2))) & 1u) != 0);
+        const uint8_t op = dg ? (v ? 'M' : (allow ? 'S' : 'X')) : (up ? 'U' : 'L');
+        if (mv) emit(op);
+        V -= mv ? (dg ? (v ? MA : MI) : G) : 0;
+        const int di = (mv && (dg || up)) ? 1 : 0, dj = (mv && !up) ? 1 : 0;
+        const bool sh = mv && lft;   // this cell lay one column left of W: it becomes the walk's column
+        W = sh ? NW : W;
+        NW = sh ? NNW : NW;
+        wq = sh ? cq : wq;
+        i -= di;
+        j -= dj;
+        cr -= di;
+        cq -= dj;
+        NNW = tagcol(max(wq - 2, 0));
     }
+#ifdef SA_TB_STATS
+    if (lane == __builtin_amdgcn_readfirstlane(lane)) {
+        atomicAdd(&g_so4_stats[0], st_rounds);
+        atomicAdd(&g_so4_stats[1], st_iters);
+        atomicAdd(&g_so4_stats[3], __builtin_amdgcn_s_memtime() - st_t0);
+        atomicAdd(&g_so4_stats[4], st_wait);
+        atomicAdd(&g_so4_stats[5], st_sub);
+        atomicAdd(&g_so4_stats[6], st_nsub);
+        atomicAdd(&g_so4_stats[7], 1ull);
+    }
+    if (live && sub == 0) atomicAdd(&g_so4_stats[2], (unsigned long long)k);
+#endif
     if (live) {
         if (sub == 0) {
             res.start_i = i;
