@@ -127,9 +127,19 @@ constexpr int fill_max_threads() { return (R >= 32 || (WIDE && R >= 16)) ? 256 :
 // load's s_waitcnt vmcnt also waits for every record store in flight (gfx9's vmcnt counts stores),
 // and a publish is an LDS read + wait + store.  With the 32-column chunks of round 2 a band ran
 // ~161 steps behind its producer (63 inherent, ~64 chunk quantisation, the rest latency).
-constexpr int kHandGran = 8;
+// Steps per hand-off granule: 16 for the linear-gap cell, 8 for the affine one (configs 2 / 4 on
+// one MI355X, tools/ab_split.py: SW 4096^2 fill 0.54 ms at 8, 0.49 at 16, 0.52 at 32, 0.63 at 4;
+// LocalGotoh 8192^2 1.61 ms at 8, 1.64 at 16, 1.73 at 32).  SA_HAND_GRAN overrides both (A/B).
+template <bool AFF>
+constexpr int hand_gran() {
+#ifdef SA_HAND_GRAN
+    return SA_HAND_GRAN;
+#else
+    return AFF ? 8 : 16;
+#endif
+}
 enum : int { kStepAny = 0, kStepSteady = 1, kStepStart = 2 };   // fill_kernel's step modes
-static_assert(kChunk % kHandGran == 0, "granules tile a chunk");
+static_assert(kChunk % hand_gran<false>() == 0 && kChunk % hand_gran<true>() == 0, "granules tile a chunk");
 
 #ifdef SA_TB_STATS
 // Debug build only (-DSA_TB_STATS, tools/split_stats.py): per SPLIT ticket {slot * bands + band,
@@ -181,6 +191,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     constexpr bool LUT = MM == kMatchLut;
     constexpr bool BITS = MM == kMatchBits;
     constexpr bool AFF = ALG >= SA_LOCAL_GOTOH;
+    constexpr int kHandGran = hand_gran<AFF>();   // SPLIT hand-off granule (steps)
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
     constexpr int FBITS = AFF ? 4 : 2;            // flag bits per cell
     constexpr int BPC = record_bpc(ALG, R, T16);  // record bits per cell (padding above the flags)
