@@ -156,11 +156,11 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
     }
 }
 
-// Score-only SW fill (sa_fill_impl.h SO): the fill tracked the odd rows at the odd steps of its
-// steady chunks (every cell of ramp chunks) and stored, per (band, chunk, lane), the lane's maximum
-// of its tracked cells; every cell is at most a tracked cell of the same lane and chunk - 2G, so S
-// lies in [smax, smax - 2G] and only the LANE BLOCKS (R rows x 32 columns) whose tracked maximum
-// reaches smax + 2G can hold it.  This kernel lists those blocks and recomputes each one alone,
+// Score-only SW fill (sa_fill_impl.h SO): the fill tracked the rows 3 mod 4 at the steps 3 mod 4
+// of its steady chunks (every cell of ramp chunks) and stored, per (band, chunk, lane), the lane's
+// maximum of its tracked cells; every cell is at most a tracked cell of the same lane and chunk -
+// kSoSlack G, so S lies in [smax, smax - kSoSlack G] and only the LANE BLOCKS (R rows x 32 columns)
+// whose tracked maximum reaches smax + kSoSlack G can hold it.  This kernel lists those blocks and recomputes each one alone,
 // as the score-only traceback recomputes a block on the path (sa_traceback_so.hip): its left
 // column from the snapshot of the chunk before, its top row from the edge stream (the last row of
 // the lane above, per step), one row per lane in a 32 + R - 1 step wavefront, 64 / R blocks per
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
     const int nch = (int)chunks_per_band((uint32_t)n);
     const uint32_t snch = P.snap_nch;
     const int G = P.gap;
-    const int thr = res.score + 2 * G;   // lane blocks whose tracked maximum reaches this may hold S
+    const int thr = res.score + kSoSlack * G;   // lane blocks whose tracked maximum reaches this may hold S
     const int32_t* cm = P.snap_m + (uint64_t)slot * P.snap_p_slot;   // [band][chunk][lane]
     const uint32_t* sh_base = P.snap_h + (uint64_t)slot * P.snap_h_slot;
     const int32_t* sp_base = P.snap_p + (uint64_t)slot * P.snap_p_slot;

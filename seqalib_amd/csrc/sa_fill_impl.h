@@ -566,7 +566,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     // lane inside; kStepStart, T16 local CMAX only: the band's first chunks, where lanes left of
     // their first column run the cell on garbage and are reset to the matrix border at it -- no
     // per-lane branch, so a lone SPLIT wave's first granule is not slowed by the band's start)
-    auto step = [&](auto mode, int q, int s, int vh, int vx, int vs, uint32_t (&rec)[RW], auto odd) {
+    auto step = [&](auto mode, int q, int s, int vh, int vx, int vs, uint32_t (&rec)[RW], auto phase) {
         constexpr int MODE = (int)decltype(mode)::value;
         constexpr bool STEADY = MODE == kStepSteady;
         constexpr bool START = MODE == kStepStart;
@@ -574,7 +574,8 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
         // pushes every step of every mode (a lane-step outside the matrix leaves a stale value in
         // the edge stream, which the traceback never reads)
         constexpr bool ACC = T16 && RB < 32 && (MODE != kStepAny || SO);
-        constexpr bool ODD = decltype(odd)::value;
+        constexpr int PH = decltype(phase)::value;   // the step's index in its chunk, mod 4
+        constexpr bool ODD = (PH & 1) != 0;
         const int up_h = shr1(vh, hl);
         int up_x = 0;
         if constexpr (AFF) up_x = shr1(vx, xl);
@@ -714,15 +715,19 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                             : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL));
                     }
                     // The lane's chunk maximum (H >= 0, one v_max3_u32 per two tracked cells).  Steady
-                    // chunks track only the odd rows at the odd steps: every cell (i, j) of the chunk
-                    // has the tracked cell (i | 1, j | 1) of the same lane and chunk with
-                    // H(i, j) <= H(i, j + 1) - G <= H(i + 1, j + 1) - 2G (its left / up candidates),
-                    // so the lane's true maximum is <= cml - 2G and the end-cell replay
-                    // (endcell_so_kernel) re-runs every chunk that could hold it.  Ramp chunks
-                    // (columns past the matrix edge) track every cell.
+                    // chunks track only the rows 3 mod 4 at the steps 3 mod 4: every cell (i, j) of
+                    // the chunk has the tracked cell (i | 3, j | 3) of the same lane and chunk, and a
+                    // cell is at most its right / lower neighbour - G (their left / up candidates), so
+                    // H(i, j) <= tracked - kSoSlack G (kSoSlack = 6): the lane's true maximum is at most
+                    // cml - 6G and the end-cell replay (endcell_so_kernel) recomputes every lane block
+                    // that could hold S.  Ramp chunks (columns past the matrix edge) track every cell.
                     if constexpr (STEADY) {
-                        if (ODD && (r & 3) == 3)
-                            asm("v_max3_u32 %0, %0, %1, %2" : "+v"(cml) : "v"(Hp[r >= 2 ? r - 2 : 0]), "v"(Hp[r]));
+                        if constexpr (R >= 8) {
+                            if (PH == 3 && (r & 7) == 7)
+                                asm("v_max3_u32 %0, %0, %1, %2" : "+v"(cml) : "v"(Hp[r >= 4 ? r - 4 : 0]), "v"(Hp[r]));
+                        } else if (PH == 3 && (r & 3) == 3) {
+                            asm("v_max_u32 %0, %0, %1" : "+v"(cml) : "v"(Hp[r]));
+                        }
                     } else if (r & 1) {
                         asm("v_max3_u32 %0, %0, %1, %2" : "+v"(cml) : "v"(Hp[r >= 1 ? r - 1 : 0]), "v"(Hp[r]));
                     }
@@ -980,12 +985,20 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                     // every lane pushes every step: the packet word fills from the top, step by
                     // step, into the same byte layout as the shifted-and-ORed records below
                     uint32_t(&acc_rec)[1] = *reinterpret_cast<uint32_t(*)[1]>(&pk[(g * BPS) / 4]);
-                    if (g & 1) step(steady, q, kC + q, vh, vx, vs, acc_rec, std::true_type{});
-                    else step(steady, q, kC + q, vh, vx, vs, acc_rec, std::false_type{});
+                    switch (g & 3) {   // (g is unrolled: one case remains)
+                        case 0: step(steady, q, kC + q, vh, vx, vs, acc_rec, std::integral_constant<int, 0>{}); break;
+                        case 1: step(steady, q, kC + q, vh, vx, vs, acc_rec, std::integral_constant<int, 1>{}); break;
+                        case 2: step(steady, q, kC + q, vh, vx, vs, acc_rec, std::integral_constant<int, 2>{}); break;
+                        default: step(steady, q, kC + q, vh, vx, vs, acc_rec, std::integral_constant<int, 3>{}); break;
+                    }
                 } else {
                     uint32_t rec[RW];
-                    if (g & 1) step(steady, q, kC + q, vh, vx, vs, rec, std::true_type{});
-                    else step(steady, q, kC + q, vh, vx, vs, rec, std::false_type{});
+                    switch (g & 3) {
+                        case 0: step(steady, q, kC + q, vh, vx, vs, rec, std::integral_constant<int, 0>{}); break;
+                        case 1: step(steady, q, kC + q, vh, vx, vs, rec, std::integral_constant<int, 1>{}); break;
+                        case 2: step(steady, q, kC + q, vh, vx, vs, rec, std::integral_constant<int, 2>{}); break;
+                        default: step(steady, q, kC + q, vh, vx, vs, rec, std::integral_constant<int, 3>{}); break;
+                    }
                     if constexpr (BPS >= 4) {
 #pragma unroll
                         for (int e = 0; e < RW; ++e) pk[g * RW + e] = rec[e];
@@ -1297,8 +1310,9 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                 // LocalGotoh reads M[0][0] = 0 there
                 r.score = (ALG == SA_SW) ? INT_MIN : 0;
             } else if constexpr (SO) {
-                // S >= smax and S <= smax - 2G: endcell_so_kernel finds S and the last row-major cell
-                h = (int)smax - 2 * G;   // (the retry test below: the largest S this pair may have)
+                // S >= smax and S <= smax - kSoSlack G: endcell_so_kernel finds S and the last
+                // row-major cell
+                h = (int)smax - kSoSlack * G;   // (the retry test below: the largest S this pair may have)
                 r.score = (int)smax; r.end_i = 0; r.end_j = 0;
                 r.reserved = 1;
             } else if constexpr (CMAX) {

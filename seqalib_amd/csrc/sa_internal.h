@@ -187,6 +187,9 @@ hipError_t launch_fill_gg(const FillVariant& v, const FillParams& p, uint32_t gr
 // Batch alphabet scan (presence bitmap of every byte of both sequence sets, 8 words) and the
 // device-side T16 decision.  aux layout (kAux* below): [bitmap 8][profile 4][sym_pack][sel].
 constexpr int kAuxProf = 8, kAuxSel = 13, kAuxWords = 64;
+// Score-only SW fill: steady chunks track the lane maximum at rows and steps 3 mod 4 only, so a
+// cell is at most its tracked cell - kSoSlack * gap (3 rows + 3 columns of gap moves)
+constexpr int kSoSlack = 6;
 hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uint8_t* d2,
                                 const uint64_t* o2, uint32_t npairs, uint32_t* aux, hipStream_t s);
 // decide_t16: from the bitmap, aux[kAuxSel] = 1 if the batch has <= 4 distinct symbols (then the
