@@ -4,7 +4,7 @@
 // Seq2 the Seq1 of pair p mutated (every third pair) or its own random sequence, length
 // 30 + (53p mod 270).  Prints, per pair, the FNV-1a 64 of the three printAlignment rows
 // (include/Test.cpp:10-31) joined by '\n' -- tests/test_dropin_cpp.py recomputes them from the oracle.
-//   dropin_chunks [pairs=4500]
+//   dropin_chunks [pairs=4500] [sw|nw|lg]
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -35,16 +35,30 @@ int main(int argc, char** argv) {
     }
     std::vector<std::pair<std::string*, std::string*>> pairs;
     for (uint32_t p = 0; p < P; ++p) pairs.push_back({&s1[p], &s2[p]});
-    SmithWatermanSA<std::string, char, '-'> sw(ScoringSystem(-1, 1, -1), equal<char>);
-    auto out = sw.getAlignments(pairs);
-    for (uint32_t p = 0; p < P; ++p) {
-        std::string r0, bars, r1;
-        for (auto& e : out[p].Data) {
-            r0 += e.get(0);
-            bars += e.match() ? '|' : ' ';
-            r1 += e.get(1);
+    auto print = [&](std::vector<AlignedSequence<char, '-'>>& out) {
+        for (uint32_t p = 0; p < P; ++p) {
+            std::string r0, bars, r1;
+            for (auto& e : out[p].Data) {
+                r0 += e.get(0);
+                bars += e.match() ? '|' : ' ';
+                r1 += e.get(1);
+            }
+            printf("%016llx\n", (unsigned long long)fnv(r0 + "\n" + bars + "\n" + r1));
         }
-        printf("%016llx\n", (unsigned long long)fnv(r0 + "\n" + bars + "\n" + r1));
+    };
+    const std::string algo = argc > 2 ? argv[2] : "sw";
+    if (algo == "sw") {
+        SmithWatermanSA<std::string, char, '-'> a(ScoringSystem(-1, 1, -1), equal<char>);
+        auto out = a.getAlignments(pairs);
+        print(out);
+    } else if (algo == "nw") {
+        NeedlemanWunschSA<std::string, char, '-'> a(ScoringSystem(-1, 2, -1), equal<char>);
+        auto out = a.getAlignments(pairs);
+        print(out);
+    } else {   // LocalGotoh: the size-hack split reports the whole batch at the end
+        LocalGotohSA<std::string, char, '-'> a(ScoringSystem(-3, -1, 1, -1), equal<char>);
+        auto out = a.getAlignments(pairs);
+        print(out);
     }
     return 0;
 }

@@ -96,17 +96,18 @@ def _fnv(s: str) -> int:
     return h
 
 
-def test_chunked_batch_lists_match_oracle(binaries, engine):
+@pytest.mark.parametrize("algo,code,args", [("sw", 0, (-1, 1, -1)), ("nw", 1, (-1, 2, -1)), ("lg", 2, (-3, -1, 1, -1))])
+def test_chunked_batch_lists_match_oracle(binaries, engine, algo, code, args):
     """tests/cpp/dropin_chunks: 4,500 pairs through getAlignments(), aligned as three chunks of one
-    sa_align_batch_cb call whose lists are built while later chunks run (SequenceAlignment.h run):
-    every pair's printAlignment rows must equal the full-matrix oracle's (SASmithWaterman.h
-    getAlignment incl. forceGlobal)."""
+    sa_align_batch_cb call whose lists are built while later chunks run (SequenceAlignment.h run;
+    LocalGotoh lands as one range after its size-hack split): every pair's printAlignment rows
+    must equal the full-matrix oracle's (getAlignment incl. forceGlobal for the local modes)."""
     import numpy as np
     import seqalib_amd as sa
     from util import oracle_batch, pack_bytes
     P = 4500
-    out = subprocess.run([os.path.join(CPP, "dropin_chunks"), str(P)], capture_output=True, text=True, timeout=240,
-                         check=True).stdout.split()
+    out = subprocess.run([os.path.join(CPP, "dropin_chunks"), str(P), algo], capture_output=True, text=True,
+                         timeout=240, check=True).stdout.split()
     assert len(out) == P
     pairs = []
     for p in range(P):
@@ -118,15 +119,15 @@ def test_chunked_batch_lists_match_oracle(binaries, engine):
                 if k % 11 != 5:
                     b[k] = a[k]
         pairs.append((a, bytes(b)))
-    sw = (-1, 1, -1)
     s1, o1, s2, o2 = pack_bytes(pairs)
-    res, ops = oracle_batch(0, sw, s1, o1, s2, o2, threads=16)
+    res, ops = oracle_batch(code, args, s1, o1, s2, o2, threads=16)
     bad = []
     for p, (a, b) in enumerate(pairs):
         off = int(o1[p] + o2[p]) + p
         r = sa.PairResult(int(res["score"][p]), int(res["end_i"][p]), int(res["end_j"][p]), int(res["start_i"][p]),
                           int(res["start_j"][p]), 0, ops[off:off + int(res["nops"][p])].tobytes())
-        rows = sa.expand_ops(sa.SA_SW, a.decode("latin-1"), b.decode("latin-1"), r).rows()
+        hack = code == 2 and (len(a), len(b)) in ((314, 288), (60, 57), (61, 58))   # SALocalGotoh.h:484-488
+        rows = sa.expand_ops(sa.SA_NW if hack else code, a.decode("latin-1"), b.decode("latin-1"), r).rows()
         if int(out[p], 16) != _fnv("\n".join(rows)):
             bad.append(p)
     assert not bad, (len(bad), bad[:10])
