@@ -111,6 +111,34 @@ __device__ __forceinline__ void hb_band16(const HbSweep& d, const uint8_t* s1, c
     };
     int32_t vup, nvup;
     uint32_t vsym, nvsym, sym = 0;
+    // the R cells of one step, updated in place: row r's block also forms row r+1's diagonal + s
+    // from the OLD Hp[r] before overwriting it, so the step needs no register copies
+    auto cells = [&](int32_t up_h) __attribute__((always_inline)) {
+        uint32_t dcur;
+        asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(dcur) : "v"(a[0]), "v"(sym), "v"(prev_up));
+        int32_t hu = up_h;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            uint32_t t0, dn = 0;
+            if (r + 1 < R) {
+                asm("v_max_i16 %[t0], %[hu], %[hp]\n\t"   // max(up, left) + gap
+                    "v_add_u16 %[t0], %[g], %[t0]\n\t"
+                    "v_bfe_i32 %[dn], %[an], %[sym], 8\n\t"   // next row: s + diagonal (old H)
+                    "v_add_u16 %[dn], %[hp], %[dn]\n\t"
+                    "v_max_i16 %[hp], %[dr], %[t0]"
+                    : [t0] "=&v"(t0), [dn] "=&v"(dn), [hp] "+v"(Hp[r])
+                    : [hu] "v"(hu), [g] "s"(g16), [an] "v"(a[r + 1 < R ? r + 1 : r]), [sym] "v"(sym), [dr] "v"(dcur));
+            } else {
+                asm("v_max_i16 %[t0], %[hu], %[hp]\n\t"
+                    "v_add_u16 %[t0], %[g], %[t0]\n\t"
+                    "v_max_i16 %[hp], %[dr], %[t0]"
+                    : [t0] "=&v"(t0), [hp] "+v"(Hp[r])
+                    : [hu] "v"(hu), [g] "s"(g16), [dr] "v"(dcur));
+            }
+            dcur = dn;
+            hu = Hp[r];
+        }
+    };
     // the lane and register holding the row this band hands on: its last row (lane 63, Hp[R-1]),
     // or in the last band row m of the sweep (lane tl, Hp[rl])
     const int src_lane = band < lastb ? 63 : tl;
@@ -126,21 +154,7 @@ __device__ __forceinline__ void hb_band16(const HbSweep& d, const uint8_t* s1, c
         for (int q = 0; q < 64; ++q) {
             const int32_t up_h = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vup, q), hl, 0x138, 0xf, 0xf, false);
             sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vsym, q), sym, 0x138, 0xf, 0xf, false);
-            int32_t hd = prev_up, hu = up_h;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                int32_t h, t;
-                asm("v_max_i16 %0, %2, %3\n\t"
-                    "v_add_u16 %0, %4, %0\n\t"
-                    "v_bfe_i32 %1, %5, %6, 8\n\t"
-                    "v_add_u16 %1, %7, %1\n\t"
-                    "v_max_i16 %0, %1, %0"
-                    : "=&v"(h), "=&v"(t)
-                    : "v"(hu), "v"(Hp[r]), "s"(g16), "v"(a[r]), "v"(sym), "v"(hd));
-                hd = Hp[r];
-                Hp[r] = h;
-                hu = h;
-            }
+            cells(up_h);
             prev_up = up_h;
             hl = Hp[R - 1];
             park[q] = Hp[SR];
@@ -168,21 +182,7 @@ __device__ __forceinline__ void hb_band16(const HbSweep& d, const uint8_t* s1, c
             sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vsym, q), sym, 0x138, 0xf, 0xf, false);
             const int j0 = s - lane;
             if (steady || (j0 >= 0 && j0 < n)) {
-                int32_t hd = prev_up, hu = up_h;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    int32_t h, t;
-                    asm("v_max_i16 %0, %2, %3\n\t"
-                        "v_add_u16 %0, %4, %0\n\t"
-                        "v_bfe_i32 %1, %5, %6, 8\n\t"
-                        "v_add_u16 %1, %7, %1\n\t"
-                        "v_max_i16 %0, %1, %0"
-                        : "=&v"(h), "=&v"(t)
-                        : "v"(hu), "v"(Hp[r]), "s"(g16), "v"(a[r]), "v"(sym), "v"(hd));
-                    hd = Hp[r];
-                    Hp[r] = h;
-                    hu = h;
-                }
+                cells(up_h);
                 prev_up = up_h;
                 hl = Hp[R - 1];
                 if (band < lastb) {

@@ -211,6 +211,49 @@ __device__ __forceinline__ void mm_band16(const MmSweep& d, const uint8_t* s1, c
     };
     int32_t vc, vd, nvc, nvd;
     uint32_t vs, nvs, sym = 0;
+    // the R cells of one step, updated in place (Cp, Ep): row r's block also forms row r+1's
+    // diagonal + s from the OLD Cp[r] before overwriting it, so the step needs no register copies;
+    // on_d(r, D) sees every row's new D; returns the last row's D
+    auto cells = [&](int32_t up_c, int32_t up_d, auto&& on_d) __attribute__((always_inline)) -> int32_t {
+        uint32_t tcur;
+        asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(tcur) : "v"(a[0]), "v"(sym), "v"(prev_up));
+        int32_t cu = up_c, du = up_d;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            uint32_t tmp, dd, tn = 0;
+            if (r + 1 < R) {
+                asm("v_add_u16 %[tmp], %[g], %[cp]\n\t"   // e = max(Ep, Cp + g) + h      (:202)
+                    "v_max_i16 %[ep], %[ep], %[tmp]\n\t"
+                    "v_add_u16 %[ep], %[h], %[ep]\n\t"
+                    "v_add_u16 %[dd], %[g], %[cu]\n\t"    // D = max(Du, Cu + g) + h      (:203)
+                    "v_max_i16 %[dd], %[du], %[dd]\n\t"
+                    "v_add_u16 %[dd], %[h], %[dd]\n\t"
+                    "v_bfe_i32 %[tn], %[an], %[sym], 8\n\t"   // next row: Cd + s(a, b) (old Cp)
+                    "v_add_u16 %[tn], %[cp], %[tn]\n\t"
+                    "v_max_i16 %[tmp], %[dd], %[ep]\n\t"  // C = max(max(D, e), diag)
+                    "v_max_i16 %[cp], %[tc], %[tmp]"
+                    : [tmp] "=&v"(tmp), [dd] "=&v"(dd), [tn] "=&v"(tn), [cp] "+v"(Cp[r]), [ep] "+v"(Ep[r])
+                    : [g] "s"(g16), [h] "s"(h16), [cu] "v"(cu), [du] "v"(du), [an] "v"(a[r + 1 < R ? r + 1 : r]),
+                      [sym] "v"(sym), [tc] "v"(tcur));
+            } else {
+                asm("v_add_u16 %[tmp], %[g], %[cp]\n\t"
+                    "v_max_i16 %[ep], %[ep], %[tmp]\n\t"
+                    "v_add_u16 %[ep], %[h], %[ep]\n\t"
+                    "v_add_u16 %[dd], %[g], %[cu]\n\t"
+                    "v_max_i16 %[dd], %[du], %[dd]\n\t"
+                    "v_add_u16 %[dd], %[h], %[dd]\n\t"
+                    "v_max_i16 %[tmp], %[dd], %[ep]\n\t"
+                    "v_max_i16 %[cp], %[tc], %[tmp]"
+                    : [tmp] "=&v"(tmp), [dd] "=&v"(dd), [cp] "+v"(Cp[r]), [ep] "+v"(Ep[r])
+                    : [g] "s"(g16), [h] "s"(h16), [cu] "v"(cu), [du] "v"(du), [tc] "v"(tcur));
+            }
+            tcur = tn;
+            cu = Cp[r];
+            du = (int32_t)dd;
+            on_d(r, (int32_t)dd);
+        }
+        return du;
+    };
     // Steady chunk (c0 >= 63, c0 + 64 <= n; as hb_band16): no per-lane branch; the handed-on row
     // (C and D of lane 63's last row, or of row m at lane tl / register rl in the last band) is
     // parked per step in LDS by every lane (others into a discard slot) and stored per chunk.
@@ -223,33 +266,10 @@ __device__ __forceinline__ void mm_band16(const MmSweep& d, const uint8_t* s1, c
             const int32_t up_c = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vc, q), cl, 0x138, 0xf, 0xf, false);
             const int32_t up_d = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vd, q), dl, 0x138, 0xf, 0xf, false);
             sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vs, q), sym, 0x138, 0xf, 0xf, false);
-            int32_t cd = prev_up, cu = up_c, du = up_d, dsel = 0;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                int32_t e, dd, c, t;
-                asm("v_add_u16 %0, %4, %5\n\t"
-                    "v_max_i16 %0, %6, %0\n\t"
-                    "v_add_u16 %0, %7, %0\n\t"
-                    "v_add_u16 %1, %4, %8\n\t"
-                    "v_max_i16 %1, %9, %1\n\t"
-                    "v_add_u16 %1, %7, %1\n\t"
-                    "v_bfe_i32 %3, %10, %11, 8\n\t"
-                    "v_add_u16 %3, %12, %3\n\t"
-                    "v_max_i16 %2, %1, %0\n\t"
-                    "v_max_i16 %2, %3, %2"
-                    : "=&v"(e), "=&v"(dd), "=&v"(c), "=&v"(t)
-                    : "s"(g16), "v"(Cp[r]), "v"(Ep[r]), "s"(h16), "v"(cu), "v"(du), "v"(a[r]), "v"(sym),
-                      "v"(cd));
-                cd = Cp[r];
-                Cp[r] = c;
-                Ep[r] = e;
-                cu = c;
-                du = dd;
-                if (r == SR) dsel = dd;
-            }
+            int32_t dsel = 0;
+            dl = cells(up_c, up_d, [&](int r, int32_t dd) __attribute__((always_inline)) { if (r == SR) dsel = dd; });
             prev_up = up_c;
             cl = Cp[R - 1];
-            dl = du;
             park[q] = Cp[SR];
             park[128 + q] = dsel;
         }
@@ -280,35 +300,14 @@ __device__ __forceinline__ void mm_band16(const MmSweep& d, const uint8_t* s1, c
             sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vs, q), sym, 0x138, 0xf, 0xf, false);
             const int j0 = s - lane;
             if (steady || (j0 >= 0 && j0 < n)) {
-                int32_t cd = prev_up, cu = up_c, du = up_d, dsel = 0;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    int32_t e, dd, c, t;
-                    asm("v_add_u16 %0, %4, %5\n\t"        // e = max(Ep, Cp + g) + h      (:202)
-                        "v_max_i16 %0, %6, %0\n\t"
-                        "v_add_u16 %0, %7, %0\n\t"
-                        "v_add_u16 %1, %4, %8\n\t"        // D = max(Du, Cu + g) + h      (:203)
-                        "v_max_i16 %1, %9, %1\n\t"
-                        "v_add_u16 %1, %7, %1\n\t"
-                        "v_bfe_i32 %3, %10, %11, 8\n\t"   // diag = Cd + s(a, b)
-                        "v_add_u16 %3, %12, %3\n\t"
-                        "v_max_i16 %2, %1, %0\n\t"        // C = max(max(D, e), diag)
-                        "v_max_i16 %2, %3, %2"
-                        : "=&v"(e), "=&v"(dd), "=&v"(c), "=&v"(t)
-                        : "s"(g16), "v"(Cp[r]), "v"(Ep[r]), "s"(h16), "v"(cu), "v"(du), "v"(a[r]), "v"(sym),
-                          "v"(cd));
-                    cd = Cp[r];
-                    Cp[r] = c;
-                    Ep[r] = e;
-                    cu = c;
-                    du = dd;
+                int32_t dsel = 0;
+                dl = cells(up_c, up_d, [&](int r, int32_t dd) __attribute__((always_inline)) {
                     if constexpr (LAST) {
                         if (r == rl) dsel = dd;
                     }
-                }
+                });
                 prev_up = up_c;
                 cl = Cp[R - 1];
-                dl = du;
                 if constexpr (!LAST) {
                     if (lane == 63) {                         // this band's last row, in place
                         outC[j0 + 1] = dc_unpack16(cl, delta);
