@@ -299,6 +299,7 @@ struct Dc16 {
     int32_t mismatch = 0;            // the profile's mismatch score
     int32_t park = 1;                // steady chunks park the handed-on row in LDS and store it per
                                      // chunk (SEQALIB_DC16_PARK=0: a lane-masked store per step)
+    int32_t seg16 = 0;               // this launch's 16-bit sweeps run in a two-per-wave kernel
 };
 // Host: is the 16-bit sweep exact for the batch's shapes and scoring?  lo / hi: bounds of every
 // row value and candidate of any sweep of at most max_m x max_n.

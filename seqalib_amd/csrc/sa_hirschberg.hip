@@ -209,6 +209,7 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
                                                       const DcLevel* lvl, int32_t* rows, const uint32_t* lutbits,
                                                       DcBits bits, HbScore sc, Dc16 d16) {
     constexpr bool LUT = MM == kMatchLut;
+    if (MM != kMatchBits && d16.seg16 && d16.aux && d16.aux[kAuxSel] == 1) return;   // (hb_sweep_seg16_kernel)
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];
     __shared__ int32_t s_park[128];   // Dc16 steady chunks: the handed-on row, parked per step
     const int lane = threadIdx.x;
@@ -303,6 +304,118 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
         __syncthreads();
     }
     if (lane == 0) out[0] = m * G;
+}
+
+// Deep levels of the 16-bit sweeps (Dc16): TWO sweeps per wave, 32 lanes x R rows each (a sweep
+// of at most 32 R rows, one band), instead of one 64-lane sweep per wave with R / 2 rows per lane:
+// the ramp is 31 steps instead of 63 and the per-step hand-off (two readlanes, two DPP moves) is
+// paid for twice the cells.  Lanes 0 and 32 take their segment's top row value and column symbol
+// (readlane of their own half of the chunk registers) where the other lanes take lane - 1's by
+// wave_shr:1.  The cells are hb_band16's (in place, 16-bit, value - delta).  Runs only when the
+// device's alphabet decision picked the 16-bit path; hb_sweep_kernel<R / 2> (launched beside it,
+// Dc16::seg16) returns at once then, and runs the int32 sweeps otherwise.
+template <int R>
+__global__ __launch_bounds__(64) void hb_sweep_seg16_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* split,
+                                                            const DcLevel* lvl, int32_t* rows, HbScore sc, Dc16 d16) {
+    if (!(d16.aux && d16.aux[kAuxSel] == 1)) return;   // the int32 sweeps run (hb_sweep_kernel)
+    const int lane = threadIdx.x;
+    const uint32_t nsw = 2 * lvl->nsplit;
+    if (blockIdx.x * 2 >= nsw) return;   // grid sized from an upper bound (uniform exit)
+    const int seg = lane >> 5, ls = lane & 31;
+    const uint32_t swi = blockIdx.x * 2 + seg;
+    const bool active = swi < nsw;
+    HbSweep d{};
+    if (active) d = hb_sweep_of(split[swi / 2], swi & 1);
+    const uint32_t* aux = d16.aux;
+    const int32_t delta = d16.delta;
+    const int m = d.alen, n = d.blen, G = sc.gap;
+    const uint32_t symp = aux[kAuxProf + 4];
+    const uint32_t g16 = (uint32_t)G & 0xffffu;
+    const int row0 = ls * R;
+    uint32_t a[R];
+    int32_t Hp[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int row = row0 + r;
+        a[r] = active && row < m ? aux[kAuxProf + (dc_code8(symp, d.rev ? s1[d.a - row] : s1[d.a + row]) >> 3)] : 0u;
+        Hp[r] = (row + 1) * G - delta;                      // H[i][0] = i * Gap (:37)
+    }
+    int32_t prev_up = row0 * G - delta;                      // H[row0][0]
+    const int tl = active ? (m - 1) / R : -1, rl = active ? (m - 1) % R : 0;   // owner of row m
+    int32_t* const out = rows + d.out;
+    uint32_t sym = 0;
+    auto cells = [&](int32_t up_h) __attribute__((always_inline)) {   // as hb_band16's
+        uint32_t dcur;
+        asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(dcur) : "v"(a[0]), "v"(sym), "v"(prev_up));
+        int32_t hu = up_h;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            uint32_t t0, dn = 0;
+            if (r + 1 < R) {
+                asm("v_max_i16 %[t0], %[hu], %[hp]\n\t"
+                    "v_add_u16 %[t0], %[g], %[t0]\n\t"
+                    "v_bfe_i32 %[dn], %[an], %[sym], 8\n\t"
+                    "v_add_u16 %[dn], %[hp], %[dn]\n\t"
+                    "v_max_i16 %[hp], %[dr], %[t0]"
+                    : [t0] "=&v"(t0), [dn] "=&v"(dn), [hp] "+v"(Hp[r])
+                    : [hu] "v"(hu), [g] "s"(g16), [an] "v"(a[r + 1 < R ? r + 1 : r]), [sym] "v"(sym), [dr] "v"(dcur));
+            } else {
+                asm("v_max_i16 %[t0], %[hu], %[hp]\n\t"
+                    "v_add_u16 %[t0], %[g], %[t0]\n\t"
+                    "v_max_i16 %[hp], %[dr], %[t0]"
+                    : [t0] "=&v"(t0), [hp] "+v"(Hp[r])
+                    : [hu] "v"(hu), [g] "s"(g16), [dr] "v"(dcur));
+            }
+            dcur = dn;
+            hu = Hp[r];
+        }
+    };
+    // per 32-step chunk, lane k of a segment holds its column c0 + k's top value and symbol
+    auto load_chunk = [&](int c0, int32_t& vu, uint32_t& vs) {
+        const int j = c0 + ls;
+        vu = 0;
+        vs = 0;
+        if (active && j < n) {
+            vu = (j + 1) * G - delta;                       // top row H[0][j+1] (:35)
+            vs = dc_code8(symp, d.rev ? s2[d.b - j] : s2[d.b + j]);
+        }
+    };
+    int steps = active ? n + 31 : 0;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) steps = max(steps, __shfl_xor(steps, off));
+    int32_t vup, nvup, hl = Hp[R - 1];
+    uint32_t vsym, nvsym;
+    load_chunk(0, vup, vsym);
+    for (int c0 = 0; c0 < steps; c0 += 32) {
+        load_chunk(c0 + 32, nvup, nvsym);
+        const int qn = min(32, steps - c0);
+        for (int q = 0; q < qn; ++q) {
+            int32_t up_h = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vup, q), hl, 0x138, 0xf, 0xf, false);
+            sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vsym, q), sym, 0x138, 0xf, 0xf, false);
+            const int32_t up_b = __builtin_amdgcn_readlane(vup, 32 + q);
+            const uint32_t sym_b = __builtin_amdgcn_readlane(vsym, 32 + q);
+            if (lane == 32) {   // the second segment's first lane: its own top row and symbol
+                up_h = up_b;
+                sym = sym_b;
+            }
+            const int j0 = c0 + q - ls;
+            if (active && j0 >= 0 && j0 < n) {
+                cells(up_h);
+                prev_up = up_h;
+                hl = Hp[R - 1];
+                if (ls == tl) {
+                    int32_t v = Hp[0];
+#pragma unroll
+                    for (int r = 1; r < R; ++r)
+                        if (r == rl) v = Hp[r];
+                    out[j0 + 1] = dc_unpack16(v, delta);   // row m of the sweep
+                }
+            }
+        }
+        vup = nvup;
+        vsym = nvsym;
+    }
+    if (active && ls == 0) out[0] = m * G;
 }
 
 // Packed sweeps for the deep levels (every sweep of the level has alen <= G = 8, 16 or 32 rows): 64 / G sweeps
@@ -575,8 +688,18 @@ struct HbLaunch {
 };
 
 template <int MM, bool ALLOW>
-void launch_sweeps_t(int R, int G, uint32_t count, const HbLaunch& a, hipStream_t st) {
+void launch_sweeps_t(int R, int G, uint32_t count, const HbLaunch& a_in, hipStream_t st) {
     const dim3 block(64);
+    HbLaunch a = a_in;
+    // 16-bit sweeps of <= 128 rows (whole-wave R = 1, 2): two per wave (hb_sweep_seg16_kernel, 2R rows per lane), the
+    // whole-wave kernel beside it for the int32 case ($SEQALIB_DC_SEG16=0: whole-wave only)
+    const bool seg16_on = !getenv("SEQALIB_DC_SEG16") || atoi(getenv("SEQALIB_DC_SEG16")) != 0;
+    if (MM != kMatchBits && a.d16.aux && G == 0 && R <= 2 && seg16_on) {
+        const dim3 grid2((count + 1) / 2);
+        if (R == 1) hipLaunchKernelGGL(hb_sweep_seg16_kernel<2>, grid2, block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.sc, a.d16);
+        else hipLaunchKernelGGL(hb_sweep_seg16_kernel<4>, grid2, block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.sc, a.d16);
+        a.d16.seg16 = 1;
+    }
 #define SA_HB_SEG(GG)                                                                                           \
     hipLaunchKernelGGL((hb_sweep_seg_kernel<GG, MM, ALLOW>), dim3((count + 64 / GG - 1) / (64 / GG)), block, 0, st, \
                        a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc)

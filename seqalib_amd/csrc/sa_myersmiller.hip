@@ -329,11 +329,146 @@ __device__ __forceinline__ void mm_band16(const MmSweep& d, const uint8_t* s1, c
     }
 }
 
+// Deep levels of the 16-bit sweeps (Dc16): TWO sweeps per wave, 32 lanes x R rows each (as
+// hb_sweep_seg16_kernel): a sweep of at most 32 R rows is one band; lanes 0 and 32 take their own
+// segment's top row (C, D) and column symbol.  Cells as mm_band16's.  Runs only when the device
+// picked the 16-bit path; mm_sweep_kernel (launched beside it, Dc16::seg16) returns at once then.
+template <int R>
+__global__ __launch_bounds__(64) void mm_sweep_seg16_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* split,
+                                                            const DcLevel* lvl, int32_t* rows, MmScore sc, Dc16 d16) {
+    if (!(d16.aux && d16.aux[kAuxSel] == 1)) return;   // the int32 sweeps run (mm_sweep_kernel)
+    const int lane = threadIdx.x;
+    if (blockIdx.x * 2 >= 2 * lvl->nsplit) return;   // grid sized from an upper bound (uniform exit)
+    const int seg = lane >> 5, ls = lane & 31;
+    const uint32_t swi = blockIdx.x * 2 + seg;
+    const bool active = swi < 2 * lvl->nsplit;
+    MmSweep d{};
+    if (active) d = mm_sweep_of(split[swi / 2], swi & 1);
+    const uint32_t* aux = d16.aux;
+    const int32_t delta = d16.delta;
+    const int m = d.alen, n = d.blen, g = sc.g, h = sc.h;
+    const uint32_t symp = aux[kAuxProf + 4];
+    const uint32_t g16 = (uint32_t)g & 0xffffu, h16 = (uint32_t)h & 0xffffu;
+    const int row0 = ls * R;
+    uint32_t a[R];
+    int32_t Cp[R], Ep[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int row = row0 + r;
+        a[r] = active && row < m ? aux[kAuxProf + (dc_code8(symp, d.rev ? s1[d.a - row] : s1[d.a + row]) >> 3)] : 0u;
+        Cp[r] = d.t0 + h * (row + 1) - delta;                // C[i][0] = t0 + i h (:192-197)
+        Ep[r] = Cp[r] + g;                                   // e = t + g (:198)
+    }
+    int32_t prev_up = (row0 == 0 ? 0 : d.t0 + h * row0) - delta;   // C[row0][0]; C[0][0] = 0 (:172)
+    const int tl = active ? (m - 1) / R : -1, rl = active ? (m - 1) % R : 0;   // owner of row m
+    int32_t* const outC = rows + d.out;
+    int32_t* const outD = outC + n + 1;
+    uint32_t sym = 0;
+    auto cells = [&](int32_t up_c, int32_t up_d, int32_t& dsel) __attribute__((always_inline)) -> int32_t {
+        uint32_t tcur;
+        asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(tcur) : "v"(a[0]), "v"(sym), "v"(prev_up));
+        int32_t cu = up_c, du = up_d;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            uint32_t tmp, dd, tn = 0;
+            if (r + 1 < R) {
+                asm("v_add_u16 %[tmp], %[g], %[cp]\n\t"
+                    "v_max_i16 %[ep], %[ep], %[tmp]\n\t"
+                    "v_add_u16 %[ep], %[h], %[ep]\n\t"
+                    "v_add_u16 %[dd], %[g], %[cu]\n\t"
+                    "v_max_i16 %[dd], %[du], %[dd]\n\t"
+                    "v_add_u16 %[dd], %[h], %[dd]\n\t"
+                    "v_bfe_i32 %[tn], %[an], %[sym], 8\n\t"
+                    "v_add_u16 %[tn], %[cp], %[tn]\n\t"
+                    "v_max_i16 %[tmp], %[dd], %[ep]\n\t"
+                    "v_max_i16 %[cp], %[tc], %[tmp]"
+                    : [tmp] "=&v"(tmp), [dd] "=&v"(dd), [tn] "=&v"(tn), [cp] "+v"(Cp[r]), [ep] "+v"(Ep[r])
+                    : [g] "s"(g16), [h] "s"(h16), [cu] "v"(cu), [du] "v"(du), [an] "v"(a[r + 1 < R ? r + 1 : r]),
+                      [sym] "v"(sym), [tc] "v"(tcur));
+            } else {
+                asm("v_add_u16 %[tmp], %[g], %[cp]\n\t"
+                    "v_max_i16 %[ep], %[ep], %[tmp]\n\t"
+                    "v_add_u16 %[ep], %[h], %[ep]\n\t"
+                    "v_add_u16 %[dd], %[g], %[cu]\n\t"
+                    "v_max_i16 %[dd], %[du], %[dd]\n\t"
+                    "v_add_u16 %[dd], %[h], %[dd]\n\t"
+                    "v_max_i16 %[tmp], %[dd], %[ep]\n\t"
+                    "v_max_i16 %[cp], %[tc], %[tmp]"
+                    : [tmp] "=&v"(tmp), [dd] "=&v"(dd), [cp] "+v"(Cp[r]), [ep] "+v"(Ep[r])
+                    : [g] "s"(g16), [h] "s"(h16), [cu] "v"(cu), [du] "v"(du), [tc] "v"(tcur));
+            }
+            tcur = tn;
+            cu = Cp[r];
+            du = (int32_t)dd;
+            if (r == rl) dsel = (int32_t)dd;
+        }
+        return du;
+    };
+    auto load_chunk = [&](int c0, int32_t& vc, int32_t& vd, uint32_t& vs) {
+        const int j = c0 + ls;
+        vc = 0;
+        vd = 0;
+        vs = 0;
+        if (active && j < n) {
+            vc = g + h * (j + 1);                            // CC[j] = g + j h, DD[j] = CC[j] + g (:183-188)
+            vd = vc + g;
+            vc -= delta;
+            vd -= delta;
+            vs = dc_code8(symp, d.rev ? s2[d.b - j] : s2[d.b + j]);
+        }
+    };
+    int steps = active ? n + 31 : 0;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) steps = max(steps, __shfl_xor(steps, off));
+    int32_t vc, vd, nvc, nvd, cl = Cp[R - 1], dl = Ep[R - 1];
+    uint32_t vs, nvs;
+    load_chunk(0, vc, vd, vs);
+    for (int c0 = 0; c0 < steps; c0 += 32) {
+        load_chunk(c0 + 32, nvc, nvd, nvs);
+        const int qn = min(32, steps - c0);
+        for (int q = 0; q < qn; ++q) {
+            int32_t up_c = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vc, q), cl, 0x138, 0xf, 0xf, false);
+            int32_t up_d = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vd, q), dl, 0x138, 0xf, 0xf, false);
+            sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vs, q), sym, 0x138, 0xf, 0xf, false);
+            const int32_t up_cb = __builtin_amdgcn_readlane(vc, 32 + q), up_db = __builtin_amdgcn_readlane(vd, 32 + q);
+            const uint32_t sym_b = __builtin_amdgcn_readlane(vs, 32 + q);
+            if (lane == 32) {   // the second segment's first lane: its own top row and symbol
+                up_c = up_cb;
+                up_d = up_db;
+                sym = sym_b;
+            }
+            const int j0 = c0 + q - ls;
+            if (active && j0 >= 0 && j0 < n) {
+                int32_t dsel = 0;
+                dl = cells(up_c, up_d, dsel);
+                prev_up = up_c;
+                cl = Cp[R - 1];
+                if (ls == tl) {
+                    int32_t csel = Cp[0];
+#pragma unroll
+                    for (int r = 1; r < R; ++r)
+                        if (r == rl) csel = Cp[r];
+                    outC[j0 + 1] = dc_unpack16(csel, delta);   // row m of the sweep
+                    outD[j0 + 1] = dc_unpack16(dsel, delta);
+                }
+            }
+        }
+        vc = nvc;
+        vd = nvd;
+        vs = nvs;
+    }
+    if (active && ls == 0) {
+        outC[0] = d.t0 + sc.h * m;
+        outD[0] = outC[0];                                    // DD[0] = CC[0] (:238)
+    }
+}
+
 template <int R, int MM, bool ALLOW>
 __global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const uint8_t* s2, const DcSub* split,
                                                       const DcLevel* lvl, int32_t* rows, const uint32_t* lutbits,
                                                       DcBits bits, MmScore sc, Dc16 d16) {
     constexpr bool LUT = MM == kMatchLut;
+    if (MM != kMatchBits && d16.seg16 && d16.aux && d16.aux[kAuxSel] == 1) return;   // (mm_sweep_seg16_kernel)
     __shared__ uint32_t s_lut[LUT ? 2048 : 1];
     __shared__ int32_t s_park[256];   // Dc16 steady chunks: the handed-on C and D rows, per step
     const int lane = threadIdx.x;
@@ -690,8 +825,18 @@ struct MmLaunch {
 };
 
 template <int MM, bool ALLOW>
-void launch_mm_sweeps_t(int R, int G, uint32_t count, const MmLaunch& a, hipStream_t st) {
+void launch_mm_sweeps_t(int R, int G, uint32_t count, const MmLaunch& a_in, hipStream_t st) {
     const dim3 block(64);
+    MmLaunch a = a_in;
+    // 16-bit sweeps of <= 128 rows (whole-wave R = 1, 2): two per wave (mm_sweep_seg16_kernel, 2R rows per lane), the
+    // whole-wave kernel beside it for the int32 case ($SEQALIB_DC_SEG16=0: whole-wave only)
+    const bool seg16_on = !getenv("SEQALIB_DC_SEG16") || atoi(getenv("SEQALIB_DC_SEG16")) != 0;
+    if (MM != kMatchBits && a.d16.aux && G == 0 && R <= 2 && seg16_on) {
+        const dim3 grid2((count + 1) / 2);
+        if (R == 1) hipLaunchKernelGGL(mm_sweep_seg16_kernel<2>, grid2, block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.sc, a.d16);
+        else hipLaunchKernelGGL(mm_sweep_seg16_kernel<4>, grid2, block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.sc, a.d16);
+        a.d16.seg16 = 1;
+    }
 #define SA_MM_SEG(GG)                                                                                           \
     hipLaunchKernelGGL((mm_sweep_seg_kernel<GG, MM, ALLOW>), dim3((count + 64 / GG - 1) / (64 / GG)), block, 0, st, \
                        a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc)

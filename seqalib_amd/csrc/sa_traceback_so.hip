@@ -444,7 +444,6 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         if (sub == 0) ops[k] = op;   // (a store in flight costs the walk nothing)
         ++k;
     };
-    int wb = -1, wt = 0, wc = 0;
     int cb = 0, ct = 0, cc = 0, cr = 0, cq = 0;
     auto locate = [&](int i, int j) __attribute__((always_inline)) {
         const int ii = i - 1;
@@ -493,7 +492,6 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         bool has_top = false, has_left = false;
         if (act) {
             locate(i, j);
-            wb = cb; wt = ct; wc = cc;
             r0 = cb * BAND + ct * R;
             j0 = 32 * cc - ct;
             qlo = j0 < 0 ? -j0 : 0;
