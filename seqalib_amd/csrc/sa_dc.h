@@ -301,6 +301,12 @@ struct Dc16 {
                                      // chunk (SEQALIB_DC16_PARK=0: a lane-masked store per step)
     int32_t seg16 = 0;               // this launch's 16-bit sweeps run in a two-per-wave kernel
 };
+// Grid cap of the whole-wave int32 sweep kernels launched beside a seg16 kernel: they usually
+// return at once, and otherwise grid-stride over the level's sweeps.
+constexpr uint32_t kDcSkipGrid = 8192;
+// Lanes per split in the midpoint kernels (hb_split_kernel / mm_split_kernel), from the level's
+// bound on the split rows: 64 (one per wave) for long rows, 16 or 8 at the deep levels.
+inline int dc_split_lanes(int maxm) { return maxm >= 256 ? 64 : maxm >= 64 ? 16 : 8; }
 // Host: is the 16-bit sweep exact for the batch's shapes and scoring?  lo / hi: bounds of every
 // row value and candidate of any sweep of at most max_m x max_n.
 inline Dc16 dc16_plan(bool affine, const sa_scoring* sc, uint32_t max_m, uint32_t max_n) {

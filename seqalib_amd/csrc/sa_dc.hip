@@ -44,32 +44,58 @@ __global__ __launch_bounds__(64) void dc_init_kernel(const uint64_t* o1, const u
 }
 
 // count = fixed (level 0) or mult * prev->nsplit; slots with m < 0 are empty (Myers–Miller's
-// type-1 midpoints leave their third child slot empty).
-__global__ __launch_bounds__(64) void dc_classify_kernel(const DcSub* cur, uint32_t fixed, const DcLevel* prev,
-                                                         uint32_t mult, int leaf_rows, int min_n, DcLevel* lvl,
-                                                         DcSub* split, DcSub* leaves, uint32_t* nleaf) {
-    const int lane = threadIdx.x;
+// type-1 midpoints leave their third child slot empty).  kClsPer x 256 subproblems per block and
+// ONE atomic per list per block: device-scope atomics on one address from every wave serialised
+// the deep levels (a level of 1.28 M subproblems took ~20 k of them per list); the lists'
+// order is free (the next level's slots and the leaves' outputs are placed by key).
+constexpr int kClsThreads = 256, kClsPer = 4, kClsWaves = kClsThreads / 64;
+__global__ __launch_bounds__(kClsThreads) void dc_classify_kernel(const DcSub* cur, uint32_t fixed, const DcLevel* prev,
+                                                                  uint32_t mult, int leaf_rows, int min_n, DcLevel* lvl,
+                                                                  DcSub* split, DcSub* leaves, uint32_t* nleaf) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t count = prev ? mult * prev->nsplit : fixed;
-    const uint32_t k = blockIdx.x * 64 + lane;
-    DcSub s{};
-    bool valid = k < count;
-    if (valid) {
-        s = cur[k];
-        valid = s.m >= 0;
+    const uint32_t base = blockIdx.x * (uint32_t)(kClsThreads * kClsPer);
+    if (base >= count) return;   // (uniform over the block)
+    __shared__ uint32_t s_ns[kClsPer * kClsWaves], s_nl[kClsPer * kClsWaves], s_base[2];
+    DcSub s[kClsPer];
+    uint64_t bs[kClsPer], bl[kClsPer];
+#pragma unroll
+    for (int it = 0; it < kClsPer; ++it) {
+        const uint32_t k = base + it * kClsThreads + threadIdx.x;
+        s[it] = DcSub{};
+        bool valid = k < count;
+        if (valid) {
+            s[it] = cur[k];
+            valid = s[it].m >= 0;
+        }
+        const bool is_split = valid && s[it].m > leaf_rows && s[it].n >= min_n;
+        bs[it] = __ballot(is_split);
+        bl[it] = __ballot(valid && !is_split);
+        if (lane == 0) {
+            s_ns[it * kClsWaves + wv] = (uint32_t)__popcll(bs[it]);
+            s_nl[it * kClsWaves + wv] = (uint32_t)__popcll(bl[it]);
+        }
     }
-    const bool is_split = valid && s.m > leaf_rows && s.n >= min_n;
-    const bool is_leaf = valid && !is_split;
-    const uint64_t bs = __ballot(is_split), bl = __ballot(is_leaf);
-    uint32_t base_s = 0, base_l = 0;
-    if (lane == 0) {
-        if (bs) base_s = atomicAdd(&lvl->nsplit, (uint32_t)__popcll(bs));
-        if (bl) base_l = atomicAdd(nleaf, (uint32_t)__popcll(bl));
+    __syncthreads();
+    if (threadIdx.x == 0) {   // exclusive offsets within the block, then one atomic per list
+        uint32_t ts = 0, tl = 0;
+        for (int q = 0; q < kClsPer * kClsWaves; ++q) {
+            const uint32_t a = s_ns[q], b = s_nl[q];
+            s_ns[q] = ts;
+            s_nl[q] = tl;
+            ts += a;
+            tl += b;
+        }
+        s_base[0] = ts ? atomicAdd(&lvl->nsplit, ts) : 0u;
+        s_base[1] = tl ? atomicAdd(nleaf, tl) : 0u;
     }
-    base_s = __shfl(base_s, 0);
-    base_l = __shfl(base_l, 0);
+    __syncthreads();
     const uint64_t below = (1ull << lane) - 1;
-    if (is_split) split[base_s + __popcll(bs & below)] = s;
-    if (is_leaf) leaves[base_l + __popcll(bl & below)] = s;
+#pragma unroll
+    for (int it = 0; it < kClsPer; ++it) {
+        if (bs[it] >> lane & 1) split[s_base[0] + s_ns[it * kClsWaves + wv] + __popcll(bs[it] & below)] = s[it];
+        if (bl[it] >> lane & 1) leaves[s_base[1] + s_nl[it * kClsWaves + wv] + __popcll(bl[it] & below)] = s[it];
+    }
 }
 
 __global__ __launch_bounds__(64) void dc_assemble_kernel(const uint64_t* o1, const uint64_t* o2, const int32_t* mark,
@@ -120,7 +146,8 @@ hipError_t dc_launch_classify(const DcSub* cur, uint32_t cap, uint32_t fixed, co
                               int leaf_rows, int min_n, DcLevel* lvl, DcSub* split, DcSub* leaves, uint32_t* nleaf,
                               hipStream_t st) {
     if (!cap) return hipSuccess;
-    hipLaunchKernelGGL(dc_classify_kernel, dim3((cap + 63) / 64), dim3(64), 0, st, cur, fixed, prev, mult, leaf_rows,
+    constexpr uint32_t per = kClsThreads * kClsPer;
+    hipLaunchKernelGGL(dc_classify_kernel, dim3((cap + per - 1) / per), dim3(kClsThreads), 0, st, cur, fixed, prev, mult, leaf_rows,
                        min_n, lvl, split, leaves, nleaf);
     return hipGetLastError();
 }

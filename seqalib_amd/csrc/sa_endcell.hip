@@ -169,6 +169,23 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
 // than kSoCand candidate blocks (an all-zero or low-scoring matrix: smax = 0 lists every block)
 // replays whole chunks instead (64 lanes, from the snapshots), as endcell_kernel does.
 constexpr int kSoCand = 1024;
+#ifndef SA_EC_SCAN
+#define SA_EC_SCAN 16
+#endif
+constexpr int kEcScan = SA_EC_SCAN;
+#ifdef SA_TB_STATS
+// Debug build only (-DSA_TB_STATS, tools/so4_stats.py): [pairs, candidate lane blocks, dense
+// fallbacks, wave cycles, scan cycles]
+__device__ unsigned long long g_ecso_stats[8];
+extern "C" int sa_debug_ecso_stats(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ecso_stats), sizeof(g_ecso_stats)) != hipSuccess) return 1;
+    if (reset) {
+        unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_ecso_stats), z, sizeof(z)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
 
 template <int R>
 __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
@@ -199,23 +216,26 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
         if (H > bv || (H == bv && (row > bi || (row == bi && col > bj)))) { bv = H; bi = row; bj = col; }
     };
 
+#ifdef SA_TB_STATS
+    const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
+#endif
     // ---- the candidate lane blocks, in [band][chunk][lane] order: 4 entries per lane per load
     __shared__ uint32_t s_cand[kSoCand];   // band << 22 | chunk << 6 | lane
-    // four (band, chunk) entries per iteration, one coalesced 256-B load each (issued together)
+    // kEcScan (band, chunk) entries per iteration, one coalesced 256-B load each (issued together)
     const uint32_t total = (uint32_t)B * snch;
     int cnt = 0;
-    for (uint32_t e0 = 0; e0 < total; e0 += 4) {
-        int v[4];
-        uint32_t bb[4], cc[4];
+    for (uint32_t e0 = 0; e0 < total; e0 += kEcScan) {
+        int v[kEcScan];
+        uint32_t bb[kEcScan], cc[kEcScan];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {   // (e0 + k is wave-uniform: scalar divide)
+        for (int k = 0; k < kEcScan; ++k) {   // (e0 + k is wave-uniform: scalar divide)
             const uint32_t e = e0 + k;
             bb[k] = e / snch;
             cc[k] = e - bb[k] * snch;
             v[k] = e < total && (int)cc[k] < nch ? cm[(uint64_t)e * kWave + lane] : INT_MIN;
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < kEcScan; ++k) {
             const bool hit = v[k] >= thr;
             const uint64_t hits = __builtin_amdgcn_ballot_w64(hit);
             if (hit) {
@@ -226,6 +246,14 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
         }
     }
     __syncthreads();
+#ifdef SA_TB_STATS
+    if (lane == 0) {
+        atomicAdd(&g_ecso_stats[0], 1ull);
+        atomicAdd(&g_ecso_stats[1], (unsigned long long)cnt);
+        atomicAdd(&g_ecso_stats[2], cnt > kSoCand ? 1ull : 0ull);
+        atomicAdd(&g_ecso_stats[4], __builtin_amdgcn_s_memtime() - st_t0);
+    }
+#endif
 
     if (cnt <= kSoCand) {
         // ---- lane blocks: 64 / R per round, lane = block g's row r
@@ -374,6 +402,9 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
         const int ov = __shfl_xor(bv, off), oi = __shfl_xor(bi, off), oj = __shfl_xor(bj, off);
         if (ov > bv || (ov == bv && (oi > bi || (oi == bi && oj > bj)))) { bv = ov; bi = oi; bj = oj; }
     }
+#ifdef SA_TB_STATS
+    if (lane == 0) atomicAdd(&g_ecso_stats[3], __builtin_amdgcn_s_memtime() - st_t0);
+#endif
     if (lane == 0) {   // (the other fields stay as the fill wrote them)
         sa_result* const o = P.res + pidx;
         o->score = bv;

@@ -214,96 +214,105 @@ __global__ __launch_bounds__(64) void hb_sweep_kernel(const uint8_t* s1, const u
     __shared__ int32_t s_park[128];   // Dc16 steady chunks: the handed-on row, parked per step
     const int lane = threadIdx.x;
     if (blockIdx.x / 2 >= lvl->nsplit) return;   // grid sized from an upper bound
-    const DcSub sub = split[blockIdx.x / 2];
-    const HbSweep d = hb_sweep_of(sub, blockIdx.x & 1);
     if constexpr (LUT) {
         for (int k = lane; k < 2048; k += 64) s_lut[k] = lutbits[k];
         __syncthreads();
     }
-    const DcSrc<MM> src = bits.src<MM>(s1, s2, s_lut, sub.pair, true);
-    int32_t* out = rows + d.out;
-    const int m = d.alen, n = d.blen, G = sc.gap;
-    if constexpr (MM != kMatchBits) {
-        if (d16.aux && d16.aux[kAuxSel] == 1) {
-            constexpr int BAND = 64 * R;
-            const int bands = (m + BAND - 1) / BAND;
-            const int tl = ((m - 1) % BAND) / R, rl = (m - 1) % R;
-            int32_t hl = 0;
-            for (int band = 0; band < bands; ++band) {
-                hb_band16<R>(d, s1, s2, d16.aux, d16.delta, G, band, bands - 1, tl, rl, out, hl, d16.park ? s_park : nullptr);
-                __threadfence_block();
-                __syncthreads();
+    // One sweep per block, or a grid-stride loop when the grid was capped (launched beside the
+    // 16-bit seg16 kernel, this kernel usually returns at once and a full grid would cost more
+    // than the skip itself).
+    auto one = [&](uint32_t bid) {
+        const DcSub sub = split[bid / 2];
+        const HbSweep d = hb_sweep_of(sub, bid & 1);
+        const DcSrc<MM> src = bits.src<MM>(s1, s2, s_lut, sub.pair, true);
+        int32_t* out = rows + d.out;
+        const int m = d.alen, n = d.blen, G = sc.gap;
+        if constexpr (MM != kMatchBits) {
+            if (d16.aux && d16.aux[kAuxSel] == 1) {
+                constexpr int BAND = 64 * R;
+                const int bands = (m + BAND - 1) / BAND;
+                const int tl = ((m - 1) % BAND) / R, rl = (m - 1) % R;
+                int32_t hl = 0;
+                for (int band = 0; band < bands; ++band) {
+                    hb_band16<R>(d, s1, s2, d16.aux, d16.delta, G, band, bands - 1, tl, rl, out, hl, d16.park ? s_park : nullptr);
+                    __threadfence_block();
+                    __syncthreads();
+                }
+                if (lane == 0) out[0] = m * G;
+                return;
             }
-            if (lane == 0) out[0] = m * G;
-            return;
         }
-    }
-    auto symA = [&](int k) -> uint32_t { return src.a(d.rev ? d.a - k : d.a + k); };
-    auto symB = [&](int k) -> uint32_t { return src.b(d.rev ? d.b - k : d.b + k); };
-    constexpr int BAND = 64 * R;
-    const int bands = (m + BAND - 1) / BAND;
-    const int lastb = bands - 1;
-    const int tl = ((m - 1) % BAND) / R, rl = (m - 1) % R;   // owner of row m-1 in the last band
-    int hl = 0;
-    for (int band = 0; band < bands; ++band) {
-        const int row0 = band * BAND + lane * R;
-        uint32_t a[R];
-        int32_t Hp[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            a[r] = row0 + r < m ? symA(row0 + r) : 0u;
-            Hp[r] = (row0 + r + 1) * G;                      // H[i][0] = i * Gap (:37)
-        }
-        int32_t prev_up = row0 * G;                          // H[row0][0]
-        // Per 64-step chunk, lane k holds column c0+k's row-above value (for lane 0) and Seq2
-        // symbol, loaded one chunk ahead; both reach their lane by DPP wave_shr:1 like the fill.
-        auto load_chunk = [&](int c0, int32_t& vu, uint32_t& vs) {
-            const int j = c0 + lane;
-            vu = 0;
-            vs = 0;
-            if (j < n) {
-                vu = band == 0 ? (j + 1) * G : out[j + 1];
-                vs = symB(j);
+        auto symA = [&](int k) -> uint32_t { return src.a(d.rev ? d.a - k : d.a + k); };
+        auto symB = [&](int k) -> uint32_t { return src.b(d.rev ? d.b - k : d.b + k); };
+        constexpr int BAND = 64 * R;
+        const int bands = (m + BAND - 1) / BAND;
+        const int lastb = bands - 1;
+        const int tl = ((m - 1) % BAND) / R, rl = (m - 1) % R;   // owner of row m-1 in the last band
+        int hl = 0;
+        for (int band = 0; band < bands; ++band) {
+            const int row0 = band * BAND + lane * R;
+            uint32_t a[R];
+            int32_t Hp[R];
+    #pragma unroll
+            for (int r = 0; r < R; ++r) {
+                a[r] = row0 + r < m ? symA(row0 + r) : 0u;
+                Hp[r] = (row0 + r + 1) * G;                      // H[i][0] = i * Gap (:37)
             }
-        };
-        int32_t vup, nvup;
-        uint32_t vsym, nvsym, sym = 0;
-        load_chunk(0, vup, vsym);
-        for (int c0 = 0; c0 < n + 63; c0 += 64) {
-            load_chunk(c0 + 64, nvup, nvsym);
-            const int steps = min(64, n + 63 - c0);
-            const bool steady = c0 >= 63 && c0 + 64 <= n;   // every lane inside (as the 16-bit sweep)
-            for (int q = 0; q < steps; ++q) {
-                const int s = c0 + q;
-                const int32_t up_h = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vup, q), hl, 0x138, 0xf,
-                                                                 0xf, false);
-                sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vsym, q), sym, 0x138, 0xf, 0xf, false);
-                const int j0 = s - lane;
-                if (steady || (j0 >= 0 && j0 < n)) {
-                    int32_t hd = prev_up, hu = up_h;
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        const int32_t h = hb_cell_v<ALLOW>(hd, hu, Hp[r], src.match(a[r], sym), sc);
-                        hd = Hp[r];
-                        Hp[r] = h;
-                        hu = h;
-                    }
-                    prev_up = up_h;
-                    hl = Hp[R - 1];
-                    if (band < lastb) {
-                        if (lane == 63) out[j0 + 1] = hl;    // this band's last row, in place
-                    } else if (lane == tl) {
-                        out[j0 + 1] = Hp[rl];                // row m of the sweep (uniform index)
+            int32_t prev_up = row0 * G;                          // H[row0][0]
+            // Per 64-step chunk, lane k holds column c0+k's row-above value (for lane 0) and Seq2
+            // symbol, loaded one chunk ahead; both reach their lane by DPP wave_shr:1 like the fill.
+            auto load_chunk = [&](int c0, int32_t& vu, uint32_t& vs) {
+                const int j = c0 + lane;
+                vu = 0;
+                vs = 0;
+                if (j < n) {
+                    vu = band == 0 ? (j + 1) * G : out[j + 1];
+                    vs = symB(j);
+                }
+            };
+            int32_t vup, nvup;
+            uint32_t vsym, nvsym, sym = 0;
+            load_chunk(0, vup, vsym);
+            for (int c0 = 0; c0 < n + 63; c0 += 64) {
+                load_chunk(c0 + 64, nvup, nvsym);
+                const int steps = min(64, n + 63 - c0);
+                const bool steady = c0 >= 63 && c0 + 64 <= n;   // every lane inside (as the 16-bit sweep)
+                for (int q = 0; q < steps; ++q) {
+                    const int s = c0 + q;
+                    const int32_t up_h = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vup, q), hl, 0x138, 0xf,
+                                                                     0xf, false);
+                    sym = __builtin_amdgcn_update_dpp(__builtin_amdgcn_readlane(vsym, q), sym, 0x138, 0xf, 0xf, false);
+                    const int j0 = s - lane;
+                    if (steady || (j0 >= 0 && j0 < n)) {
+                        int32_t hd = prev_up, hu = up_h;
+    #pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const int32_t h = hb_cell_v<ALLOW>(hd, hu, Hp[r], src.match(a[r], sym), sc);
+                            hd = Hp[r];
+                            Hp[r] = h;
+                            hu = h;
+                        }
+                        prev_up = up_h;
+                        hl = Hp[R - 1];
+                        if (band < lastb) {
+                            if (lane == 63) out[j0 + 1] = hl;    // this band's last row, in place
+                        } else if (lane == tl) {
+                            out[j0 + 1] = Hp[rl];                // row m of the sweep (uniform index)
+                        }
                     }
                 }
+                vup = nvup;
+                vsym = nvsym;
             }
-            vup = nvup;
-            vsym = nvsym;
+            __threadfence_block();
+            __syncthreads();
         }
-        __threadfence_block();
+        if (lane == 0) out[0] = m * G;
+    };
+    for (uint32_t bid = blockIdx.x; bid / 2 < lvl->nsplit; bid += gridDim.x) {
+        one(bid);
         __syncthreads();
     }
-    if (lane == 0) out[0] = m * G;
 }
 
 // Deep levels of the 16-bit sweeps (Dc16): TWO sweeps per wave, 32 lanes x R rows each (a sweep
@@ -486,32 +495,38 @@ __global__ __launch_bounds__(64) void hb_sweep_seg_kernel(const uint8_t* s1, con
 }
 
 // ---------------------------------------------------------------------------- split
+template <int GS>
 __global__ __launch_bounds__(64) void hb_split_kernel(const DcSub* split, const DcLevel* lvl, const int32_t* rows,
                                                       DcSub* next, sa_result* res) {
-    const int lane = threadIdx.x;
-    if (blockIdx.x >= lvl->nsplit) return;
-    const DcSub d = split[blockIdx.x];
+    // GS lanes per split, 64 / GS splits per wave (deep levels: short rows, many splits)
+    const int lane = threadIdx.x, sl = lane % GS;
+    const uint32_t k = blockIdx.x * (64 / GS) + lane / GS;
+    const uint32_t ns = lvl->nsplit;
+    if (blockIdx.x * (64 / GS) >= ns) return;   // (uniform)
+    const bool act = k < ns;
+    DcSub d{};
+    if (act) d = split[k];
     const int32_t* F = rows + 2 * (d.a0 + d.b0);
-    const int n = d.n;
+    const int n = act ? d.n : 0;
     const int32_t* B = F + n + 1;
     int32_t best = INT_MIN;
     int idx = 0;
-    for (int i = lane; i < n; i += 64) {
+    for (int i = sl; i < n; i += GS) {
         const int32_t s = F[i] + B[n - i];
         if (s >= best) { best = s; idx = i; }
     }
     // lexicographic (sum, i) maximum = the reference's last maximum (S >= MaxScore, :144)
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
+    for (int off = GS / 2; off >= 1; off >>= 1) {
         const int32_t ob = __shfl_xor(best, off);
         const int oi = __shfl_xor(idx, off);
         if (ob > best || (ob == best && oi > idx)) { best = ob; idx = oi; }
     }
-    if (lane == 0) {
+    if (act && sl == 0) {
         if (d.top) res[d.pair].score = max(best, F[n] + B[0]);   // NW H[m][n] over i in [0, n]
         const int mid = d.m / 2;
-        next[2 * blockIdx.x] = DcSub{d.a0, d.b0, mid, idx, 0, 0, d.pair, 0};
-        next[2 * blockIdx.x + 1] = DcSub{d.a0 + (uint64_t)mid, d.b0 + (uint64_t)idx, d.m - mid, n - idx, 0, 0, d.pair, 0};
+        next[2 * k] = DcSub{d.a0, d.b0, mid, idx, 0, 0, d.pair, 0};
+        next[2 * k + 1] = DcSub{d.a0 + (uint64_t)mid, d.b0 + (uint64_t)idx, d.m - mid, n - idx, 0, 0, d.pair, 0};
     }
 }
 
@@ -704,7 +719,7 @@ void launch_sweeps_t(int R, int G, uint32_t count, const HbLaunch& a_in, hipStre
     hipLaunchKernelGGL((hb_sweep_seg_kernel<GG, MM, ALLOW>), dim3((count + 64 / GG - 1) / (64 / GG)), block, 0, st, \
                        a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc)
 #define SA_HB_SW(RR) \
-    hipLaunchKernelGGL((hb_sweep_kernel<RR, MM, ALLOW>), dim3(count), block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc, a.d16)
+    hipLaunchKernelGGL((hb_sweep_kernel<RR, MM, ALLOW>), dim3(a.d16.seg16 ? std::min(count, kDcSkipGrid) : count), block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc, a.d16)
     if (G == 8) SA_HB_SEG(8);
     else if (G == 16) SA_HB_SEG(16);
     else if (G == 32) SA_HB_SEG(32);
@@ -774,8 +789,18 @@ int hirschberg_run(DcWork& w, hipEvent_t prev, const sa_scoring* scoring, const 
         const int G = !seg_sweeps ? 0 : maxa <= 8 ? 8 : maxa <= 16 ? 16 : maxa <= 32 ? 32 : 0;
         const HbLaunch a{in.d1, in.d2, w.split.p, w.lvl.p + l, w.rows.p, in.lutbits, in.bits, sc, d16};
         SA_DC_HIP(launch_sweeps(R, G, 2 * splits, a, st));
-        hipLaunchKernelGGL(hb_split_kernel, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p, w.next.p,
-                           d_res);
+        // lanes per split: the level's rows bound the split's columns only loosely (n ~ m for
+        // similar pairs), any n is exact, a wider one just loops
+        const int gs = dc_split_lanes(maxm);
+        if (gs == 64)
+            hipLaunchKernelGGL(hb_split_kernel<64>, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p,
+                               w.next.p, d_res);
+        else if (gs == 16)
+            hipLaunchKernelGGL(hb_split_kernel<16>, dim3((splits + 3) / 4), dim3(64), 0, st, w.split.p, w.lvl.p + l,
+                               w.rows.p, w.next.p, d_res);
+        else
+            hipLaunchKernelGGL(hb_split_kernel<8>, dim3((splits + 7) / 8), dim3(64), 0, st, w.split.p, w.lvl.p + l,
+                               w.rows.p, w.next.p, d_res);
         SA_DC_HIP(hipGetLastError());
         w.cur.swap(w.next);
         cap = 2 * splits;

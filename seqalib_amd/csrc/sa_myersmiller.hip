@@ -473,44 +473,51 @@ __global__ __launch_bounds__(64) void mm_sweep_kernel(const uint8_t* s1, const u
     __shared__ int32_t s_park[256];   // Dc16 steady chunks: the handed-on C and D rows, per step
     const int lane = threadIdx.x;
     if (blockIdx.x / 2 >= lvl->nsplit) return;   // grid sized from an upper bound
-    const DcSub sub = split[blockIdx.x / 2];
-    const MmSweep d = mm_sweep_of(sub, blockIdx.x & 1);
     if constexpr (LUT) {
         for (int k = lane; k < 2048; k += 64) s_lut[k] = lutbits[k];
         __syncthreads();
     }
-    const DcSrc<MM> src = bits.src<MM>(s1, s2, s_lut, sub.pair, true);
-    const int m = d.alen, n = d.blen;
-    int32_t* outC = rows + d.out;
-    int32_t* outD = outC + n + 1;
-    constexpr int BAND = 64 * R;
-    const int bands = (m + BAND - 1) / BAND;
-    const int tl = ((m - 1) % BAND) / R, rl = (m - 1) % R;   // owner of row m-1 in the last band
-    int32_t cl = 0, dl = 0;                                   // this lane's last row: C, D
-    bool b16 = false;
-    if constexpr (MM != kMatchBits) b16 = d16.aux && d16.aux[kAuxSel] == 1;   // uniform over the grid
-    for (int band = 0; band < bands; ++band) {
-        if constexpr (MM != kMatchBits) {
-            if (b16) {
-                if (band < bands - 1)
-                    mm_band16<R, false>(d, s1, s2, d16.aux, d16.delta, sc, band, outC, outD, tl, rl, cl, dl, d16.park ? s_park : nullptr);
-                else
-                    mm_band16<R, true>(d, s1, s2, d16.aux, d16.delta, sc, band, outC, outD, tl, rl, cl, dl, d16.park ? s_park : nullptr);
-                __threadfence_block();
-                __syncthreads();
-                continue;
+    // One sweep per block, or a grid-stride loop over a capped grid (kDcSkipGrid).
+    auto one = [&](uint32_t bid) {
+        const DcSub sub = split[bid / 2];
+        const MmSweep d = mm_sweep_of(sub, bid & 1);
+        const DcSrc<MM> src = bits.src<MM>(s1, s2, s_lut, sub.pair, true);
+        const int m = d.alen, n = d.blen;
+        int32_t* outC = rows + d.out;
+        int32_t* outD = outC + n + 1;
+        constexpr int BAND = 64 * R;
+        const int bands = (m + BAND - 1) / BAND;
+        const int tl = ((m - 1) % BAND) / R, rl = (m - 1) % R;   // owner of row m-1 in the last band
+        int32_t cl = 0, dl = 0;                                   // this lane's last row: C, D
+        bool b16 = false;
+        if constexpr (MM != kMatchBits) b16 = d16.aux && d16.aux[kAuxSel] == 1;   // uniform over the grid
+        for (int band = 0; band < bands; ++band) {
+            if constexpr (MM != kMatchBits) {
+                if (b16) {
+                    if (band < bands - 1)
+                        mm_band16<R, false>(d, s1, s2, d16.aux, d16.delta, sc, band, outC, outD, tl, rl, cl, dl, d16.park ? s_park : nullptr);
+                    else
+                        mm_band16<R, true>(d, s1, s2, d16.aux, d16.delta, sc, band, outC, outD, tl, rl, cl, dl, d16.park ? s_park : nullptr);
+                    __threadfence_block();
+                    __syncthreads();
+                    continue;
+                }
             }
+            if (band < bands - 1)
+                mm_band<R, MM, ALLOW, false>(d, src, sc, band, outC, outD, tl, rl, cl, dl);
+            else
+                mm_band<R, MM, ALLOW, true>(d, src, sc, band, outC, outD, tl, rl, cl, dl);
+            __threadfence_block();
+            __syncthreads();
         }
-        if (band < bands - 1)
-            mm_band<R, MM, ALLOW, false>(d, src, sc, band, outC, outD, tl, rl, cl, dl);
-        else
-            mm_band<R, MM, ALLOW, true>(d, src, sc, band, outC, outD, tl, rl, cl, dl);
-        __threadfence_block();
+        if (lane == 0) {
+            outC[0] = d.t0 + sc.h * m;
+            outD[0] = outC[0];                                    // DD[0] = CC[0] (:238)
+        }
+    };
+    for (uint32_t bid = blockIdx.x; bid / 2 < lvl->nsplit; bid += gridDim.x) {
+        one(bid);
         __syncthreads();
-    }
-    if (lane == 0) {
-        outC[0] = d.t0 + sc.h * m;
-        outD[0] = outC[0];                                    // DD[0] = CC[0] (:238)
     }
 }
 
@@ -595,19 +602,25 @@ __global__ __launch_bounds__(64) void mm_sweep_seg_kernel(const uint8_t* s1, con
 }
 
 // ---------------------------------------------------------------------------- split
+template <int GS>
 __global__ __launch_bounds__(64) void mm_split_kernel(const DcSub* split, const DcLevel* lvl, const int32_t* rows,
                                                       DcSub* next, sa_result* res, int32_t g) {
-    const int lane = threadIdx.x;
-    if (blockIdx.x >= lvl->nsplit) return;
-    const DcSub d = split[blockIdx.x];
-    const int n = d.n;
+    // GS lanes per split, 64 / GS splits per wave (dc_split_lanes)
+    const int lane = threadIdx.x, sl = lane % GS;
+    const uint32_t k = blockIdx.x * (64 / GS) + lane / GS;
+    const uint32_t ns = lvl->nsplit;
+    if (blockIdx.x * (64 / GS) >= ns) return;   // (uniform)
+    const bool act = k < ns;
+    DcSub d{};
+    if (act) d = split[k];
+    const int n = act ? d.n : -1;
     const int32_t* C = rows + 4 * (d.a0 + d.b0);
     const int32_t* D = C + n + 1;
     const int32_t* Cr = D + n + 1;
     const int32_t* Dr = Cr + n + 1;
     int32_t best = INT_MIN;
     int idx = 0, ty = 0;
-    for (int j = lane; j <= n; j += 64) {
+    for (int j = sl; j <= n; j += GS) {
         const int32_t c1 = C[j] + Cr[n - j];
         const int32_t c2 = D[j] + Dr[n - j] - g;
         const int32_t t = max(c1, c2);
@@ -615,16 +628,16 @@ __global__ __launch_bounds__(64) void mm_split_kernel(const DcSub* split, const 
     }
     // lexicographic (max, -j): the reference keeps the FIRST maximum (temp > max, :326)
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
+    for (int off = GS / 2; off >= 1; off >>= 1) {
         const int32_t ob = __shfl_xor(best, off);
         const int oi = __shfl_xor(idx, off);
         const int ot = __shfl_xor(ty, off);
         if (ob > best || (ob == best && oi < idx)) { best = ob; idx = oi; ty = ot; }
     }
-    if (lane == 0) {
+    if (act && sl == 0) {
         if (d.top) res[d.pair].score = best;
         const int mid = d.m / 2, j = idx;
-        DcSub* c = next + 3 * blockIdx.x;
+        DcSub* c = next + 3 * k;
         if (!ty) {   // type 1 (:358-374)
             c[0] = DcSub{d.a0, d.b0, mid, j, d.tb, g, d.pair, 0};
             c[1] = DcSub{d.a0 + (uint64_t)mid, d.b0 + (uint64_t)j, d.m - mid, n - j, g, d.te, d.pair, 0};
@@ -841,7 +854,7 @@ void launch_mm_sweeps_t(int R, int G, uint32_t count, const MmLaunch& a_in, hipS
     hipLaunchKernelGGL((mm_sweep_seg_kernel<GG, MM, ALLOW>), dim3((count + 64 / GG - 1) / (64 / GG)), block, 0, st, \
                        a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc)
 #define SA_MM_SW(RR) \
-    hipLaunchKernelGGL((mm_sweep_kernel<RR, MM, ALLOW>), dim3(count), block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc, a.d16)
+    hipLaunchKernelGGL((mm_sweep_kernel<RR, MM, ALLOW>), dim3(a.d16.seg16 ? std::min(count, kDcSkipGrid) : count), block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.lut, a.bits, a.sc, a.d16)
     if (G == 8) SA_MM_SEG(8);
     else if (G == 16) SA_MM_SEG(16);
     else if (G == 32) SA_MM_SEG(32);
@@ -911,8 +924,16 @@ int myersmiller_run(DcWork& w, hipEvent_t prev, const sa_scoring* scoring, const
         const int G = !seg_sweeps ? 0 : maxa <= 8 ? 8 : maxa <= 16 ? 16 : maxa <= 32 ? 32 : 0;
         const MmLaunch a{in.d1, in.d2, w.split.p, w.lvl.p + l, w.rows.p, in.lutbits, in.bits, sc, d16};
         SA_DC_HIP(launch_mm_sweeps(R, G, 2 * splits, a, st));
-        hipLaunchKernelGGL(mm_split_kernel, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p, w.next.p,
-                           d_res, sc.g);
+        const int gs = dc_split_lanes(maxm);
+        if (gs == 64)
+            hipLaunchKernelGGL(mm_split_kernel<64>, dim3(splits), dim3(64), 0, st, w.split.p, w.lvl.p + l, w.rows.p,
+                               w.next.p, d_res, sc.g);
+        else if (gs == 16)
+            hipLaunchKernelGGL(mm_split_kernel<16>, dim3((splits + 3) / 4), dim3(64), 0, st, w.split.p, w.lvl.p + l,
+                               w.rows.p, w.next.p, d_res, sc.g);
+        else
+            hipLaunchKernelGGL(mm_split_kernel<8>, dim3((splits + 7) / 8), dim3(64), 0, st, w.split.p, w.lvl.p + l,
+                               w.rows.p, w.next.p, d_res, sc.g);
         SA_DC_HIP(hipGetLastError());
         w.cur.swap(w.next);
         cap = 3 * splits;

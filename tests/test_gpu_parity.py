@@ -166,6 +166,24 @@ def test_dc_level_loop_variants_vs_oracle(engine, monkeypatch, algo, leaf, seg):
         compare_with_oracle(engine, sa.SA_MYERS_MILLER, (-3, -1, 1, -1, True), pairs)
 
 
+@pytest.mark.parametrize("algo", ["hb", "mm"])
+def test_dc_int32_sweeps_grid_stride(engine, algo):
+    """Five-symbol batch (N wildcards): the int32 whole-wave sweeps run beside the 16-bit two-per-
+    wave kernel, on a grid capped at kDcSkipGrid (sa_dc.h) blocks, each block looping over the
+    level's sweeps -- 2500 pairs give levels of more than 8192 sweeps."""
+    pairs = []
+    for k in range(2500):
+        m, n = 180 + k % 97, 170 + (k * 7) % 113
+        a = sa.synth_dna(120_000 + 2 * k, m)
+        b = sa.synth_mutate(a, k)[:n] if k % 2 else sa.synth_dna(120_001 + 2 * k, n)
+        b = bytes(ord("N") if (x % 11 == 5) else c for x, c in enumerate(b))
+        pairs.append((a, b))
+    if algo == "hb":
+        compare_with_oracle(engine, sa.SA_HIRSCHBERG, (-3, 2, -2), pairs, "nwild")
+    else:
+        compare_with_oracle(engine, sa.SA_MYERS_MILLER, (-5, -2, 3, -2, True), pairs, "nwild")
+
+
 def compare_with_oracle(engine, algo, args, pairs, match=None):
     lut = named_lut(match)
     res = engine.align(algo, sc_obj(args), pairs, lut)

@@ -4,7 +4,8 @@ the wave's cycles go (recompute load wait, sub-step loop, the rest = walk).
     python3 tools/so4_stats.py [pairs=10000]"""
 import ctypes as C, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["SEQALIB_HIP_LIB"] = os.path.join(ROOT, "tools", "bin", "libstats.so")
+os.environ["SEQALIB_HIP_LIB"] = os.path.join(ROOT, "tools", "bin", os.environ.get("SO4_STATS_LIB", "libstats.so"))
+os.environ.setdefault("SEQALIB_KERNEL_TIMING", "1")
 sys.path.insert(0, ROOT)
 import numpy as np, torch
 import seqalib_amd as sa
@@ -17,13 +18,20 @@ d1, do1, d2, do2 = t(s1), t(o1), t(s2), t(o2)
 res = torch.zeros(P * 32, dtype=torch.uint8, device=dev); ops = torch.zeros(len(s1) + len(s2) + P, dtype=torch.uint8, device=dev)
 eng = sa.Engine(0)
 out = (C.c_ulonglong * 8)()
+ec = (C.c_ulonglong * 8)()
 for it in range(2):
     L.sa_debug_so4_stats(out, 1)
+    L.sa_debug_ecso_stats(ec, 1)
     eng.align_device(0, sa.ScoringSystem(-1, 1, -1), d1.data_ptr(), do1.data_ptr(), d2.data_ptr(), do2.data_ptr(), P, n, n,
                      res.data_ptr(), ops.data_ptr(), 0)
     torch.cuda.synchronize()
     f, tb, _ = eng.last_timings()
     L.sa_debug_so4_stats(out, 1)
+    L.sa_debug_ecso_stats(ec, 1)
+    ep = max(ec[0], 1)
+    kf, ks = eng.last_kernel_timings()
+    print(f"end cell: {ks - kf:.3f} ms, {ec[0]} pairs, {ec[1] / ep:.1f} candidate lane blocks per pair, {ec[2]} dense fallbacks, "
+          f"{ec[3] / ep:.0f} cycles per wave of which scan {ec[4] / ep:.0f}")
     rounds, iters, moves, cyc, wait, sub, nsub, waves = list(out)
     w = max(waves, 1)
     print(f"pairs {P} fill {f:.2f} ms tb {tb:.2f} ms | per wave: rounds {rounds / w:.0f} iters {iters / w:.0f} "
