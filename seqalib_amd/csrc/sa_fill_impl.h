@@ -130,6 +130,12 @@ constexpr int fill_max_threads() { return (R >= 32 || (WIDE && R >= 16)) ? 256 :
 // Steps per hand-off granule: 16 for the linear-gap cell, 8 for the affine one (configs 2 / 4 on
 // one MI355X, tools/ab_split.py: SW 4096^2 fill 0.54 ms at 8, 0.49 at 16, 0.52 at 32, 0.63 at 4;
 // LocalGotoh 8192^2 1.61 ms at 8, 1.64 at 16, 1.73 at 32).  SA_HAND_GRAN overrides both (A/B).
+// Score-only SW cell form (A/B): 1 = the shared-gap form, 4 fast ops + v_bfe_i32 (default);
+// 0 = separate left / up candidates, 5 fast ops + v_bfe_i32 (round 4's first score-only cell).
+#ifndef SA_SO_CELL5
+#define SA_SO_CELL5 1
+#endif
+
 template <bool AFF>
 constexpr int hand_gran() {
 #ifdef SA_HAND_GRAN
@@ -693,6 +699,31 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                     // zero clamp is free, as in the tagged cell), two v_max_i16.  5 fast-class 16-bit
                     // ops + v_bfe_i32 (tools/microbench_so.hip: 1.33x the tagged cell's rate).
                     uint32_t t0, t1;
+#if SA_SO_CELL5
+                    // Both gap candidates share G: max(U + G, L + G, 0) = max(U, L) - (-G) with
+                    // unsigned saturation (U, L = H >= 0), so the cell is max(D, sat(max(U, L) - CU)):
+                    // 4 fast-class ops + v_bfe_i32 for the next row's diagonal (one add fewer).
+                    (void)t0;
+                    if (r + 1 < R) {
+                        uint32_t dn;
+                        const uint32_t tabn = (uint32_t)a[r + 1 < R ? r + 1 : r];
+                        asm("v_max_i16 %[t1], %[hu], %[hp]\n\t"
+                            "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\t"
+                            "v_add_u16 %[dn], %[hp], %[dn]\n\t"
+                            "v_sub_u16_e64 %[t1], %[t1], %[cu] clamp\n\t"
+                            "v_max_i16 %[hp], %[dr], %[t1]"
+                            : [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r])
+                            : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [tabn] "v"(tabn), [sym] "v"(sym));
+                        dcur = dn;
+                    } else {
+                        asm("v_max_i16 %[t1], %[hu], %[hp]\n\t"
+                            "v_sub_u16_e64 %[t1], %[t1], %[cu] clamp\n\t"
+                            "v_max_i16 %[hp], %[dr], %[t1]"
+                            : [t1] "=&v"(t1), [hp] "+v"(Hp[r])
+                            : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU));
+                    }
+                    (void)CL;
+#else
                     if (r + 1 < R) {
                         uint32_t dn;
                         const uint32_t tabn = (uint32_t)a[r + 1 < R ? r + 1 : r];
@@ -714,6 +745,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                             : [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r])
                             : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL));
                     }
+#endif
                     // The lane's chunk maximum (H >= 0, one v_max3_u32 per two tracked cells).  Steady
                     // chunks track only the rows 3 mod 4 at the steps 3 mod 4: every cell (i, j) of
                     // the chunk has the tracked cell (i | 3, j | 3) of the same lane and chunk, and a
