@@ -743,6 +743,10 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         const uint64_t hand_x_off = any_split ? (uint64_t)cnt * sp_bands * std::max<uint32_t>(max_n, 1) : 0;
         // fill parameters of variant k (k == nv: the SPLIT fallback)
         FillParams fps[3];
+        // $SEQALIB_STAGE_SEQ2=0: read Seq2 from global memory in every plan (tests the unstaged
+        // path that batches with max_n > kMaxStagedSeq2 take)
+        const char* stage_env = getenv("SEQALIB_STAGE_SEQ2");
+        const bool no_stage = stage_env && stage_env[0] == '0';
         auto make_fp = [&](int k) {
             const Variant& v = vars[k];
             const Plan& pl = v.pl;
@@ -768,7 +772,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fp.gap_open = sc->gap_open; fp.gap_extend = sc->gap_extend;
             fp.waves = pl.W;
             fp.count = cnt;
-            fp.stage_seq2 = max_n <= kMaxStagedSeq2 ? 1 : 0;
+            fp.stage_seq2 = (max_n <= kMaxStagedSeq2 && !no_stage) ? 1 : 0;
             fp.prof = prof;
             const bool fb = k == nv;
             fp.sel = fb ? nullptr : sel; fp.sel_want = v.t16 ? 1u : 0u;

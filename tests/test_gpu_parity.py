@@ -232,6 +232,21 @@ def test_many_pairs_plan_vs_oracle(engine, algo):
     compare_with_oracle(engine, algo, SCORINGS[algo][0], pairs)
 
 
+@pytest.mark.parametrize("algo,tall", [(0, False), (0, True), (1, False), (2, False), (3, False)])
+def test_many_pairs_unstaged_seq2_vs_oracle(engine, algo, tall, monkeypatch):
+    """The many-pairs plans with Seq2 read from global memory per chunk instead of staged in LDS
+    (what a batch with max_n > kMaxStagedSeq2 = 48 KiB takes; $SEQALIB_STAGE_SEQ2=0 forces it):
+    SW runs the score-only fill, at R = 4 and (tall) R = 32."""
+    monkeypatch.setenv("SEQALIB_STAGE_SEQ2", "0")
+    pairs = []
+    for k in range(1100):
+        m, n = (2100 + (k % 29), 120 + (k % 31)) if tall else (150 + (k % 37), 140 + (k % 53))
+        a = sa.synth_dna(40_000 + 2 * k, m)
+        b = sa.synth_mutate(a, k)[:n] if k % 2 else sa.synth_dna(40_001 + 2 * k, n)
+        pairs.append((a, b))
+    compare_with_oracle(engine, algo, SCORINGS[algo][0], pairs)
+
+
 @pytest.mark.parametrize("algo", [0, 1, 2, 3])
 def test_multiband_wrap_vs_oracle(engine, algo, monkeypatch):
     """More bands than waves (m > 64*R*W): bands wrap round-robin over the waves of one
