@@ -224,15 +224,19 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
     // kEcScan (band, chunk) entries per iteration, one coalesced 256-B load each (issued together)
     const uint32_t total = (uint32_t)B * snch;
     int cnt = 0;
+    uint32_t bnext = 0, cnext = 0;   // (band, chunk) of entry e0, stepped (no scalar divide)
     for (uint32_t e0 = 0; e0 < total; e0 += kEcScan) {
         int v[kEcScan];
         uint32_t bb[kEcScan], cc[kEcScan];
 #pragma unroll
-        for (int k = 0; k < kEcScan; ++k) {   // (e0 + k is wave-uniform: scalar divide)
+        for (int k = 0; k < kEcScan; ++k) {   // (wave-uniform: scalar)
             const uint32_t e = e0 + k;
-            bb[k] = e / snch;
-            cc[k] = e - bb[k] * snch;
-            v[k] = e < total && (int)cc[k] < nch ? cm[(uint64_t)e * kWave + lane] : INT_MIN;
+            bb[k] = bnext;
+            cc[k] = cnext;
+            v[k] = e < total && (int)cnext < nch ? cm[(uint64_t)e * kWave + lane] : INT_MIN;
+            const bool wrap = cnext + 1 == snch;
+            bnext += wrap ? 1u : 0u;
+            cnext = wrap ? 0u : cnext + 1;
         }
 #pragma unroll
         for (int k = 0; k < kEcScan; ++k) {
