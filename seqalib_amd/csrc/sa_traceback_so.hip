@@ -364,7 +364,10 @@ __global__ __launch_bounds__(64) void traceback_so_kernel(TbParams P) {
 // A lone wave's serial recompute per block drops from 32 columns x R rows of dependent cells to
 // (32 + 3) sub-steps x R/4 rows, and the wave's registers (R/4 rows of state) stay few, so the
 // traceback beside the next call's fill displaces fewer of its waves.
-constexpr int kSo4Pairs = 16;
+// Lanes per pair by default: 8 at R = 32 (headline, 10,000 x 4096^2: traceback 6.50 -> 6.30 ms,
+// pipelined step 19.50 -> 19.35 ms), 4 below (R = 16, 10,000 x 1024^2: 1.80 ms at 4, 1.84 at 8);
+// profiles/tb_lp_ab_r04.txt.  $SEQALIB_TB_LP overrides.
+constexpr int so4_default_lp(int R) { return R >= 32 ? 8 : 4; }
 #ifdef SA_TB_STATS
 // Debug build only (-DSA_TB_STATS, tools/so4_stats.py), per wave summed: [rounds, walk-loop
 // iterations, moves, wave cycles, recompute: load-wait cycles, sub-step cycles, sub-steps, waves]
@@ -378,31 +381,33 @@ extern "C" int sa_debug_so4_stats(unsigned long long* out, int reset) {
     return 0;
 }
 #endif
-template <int R>
+// LP lanes per pair (a "quad" of LP sublanes; LP = 8 halves the sub-steps' rows per lane and the
+// pairs per wave -- twice the waves for the same batch).
+template <int R, int LP>
 struct So4Lds {
-    static constexpr int kTags = 0;                         // [column q][lane] words
-    static constexpr int kEdge = kTags + 32 * 64 * 4;       // [lane] 16 B: packet (lane & 3) of quad
-    static constexpr int kEdge2 = kEdge + 64 * 16;          // [lane] 16 B: packet 4 (sublane 0)
-    static constexpr int kRowC = kEdge2 + 64 * 16;          // [quad][32] row codes (8 x code)
-    static constexpr int kColC = kRowC + kSo4Pairs * 32;    // [quad][32] column codes
-    static constexpr int kOps = kColC + kSo4Pairs * 32;     // [quad][kSoOps] op bytes of a round
-    static constexpr int kBytes = kOps + kSo4Pairs * kSoOps;
+    static constexpr int kPairs = kWave / LP;                 // pairs per wave
+    static constexpr int kTags = 0;                           // [column q][lane] words
+    static constexpr int kEdge = kTags + 32 * 64 * 4;         // [lane] 16 B: packet (sub) of the quad
+    static constexpr int kEdge2 = kEdge + 64 * 16;            // LP = 4: [lane] 16 B: packet 4 (sublane 0)
+    static constexpr int kRowC = kEdge2 + (LP < 5 ? 64 * 16 : 0);   // [quad][32] row codes (8 x code)
+    static constexpr int kColC = kRowC + kPairs * 32;         // [quad][32] column codes
+    static constexpr int kBytes = kColC + kPairs * 32;
 };
 
-template <int R>
+template <int R, int LP>
 __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
-    using L = So4Lds<R>;
-    constexpr int RS = R / 4;   // rows per sublane
+    using L = So4Lds<R, LP>;
+    constexpr int RS = R / LP;   // rows per sublane
     constexpr int BAND = kWave * R;
-    static_assert(R >= 4 && R % 4 == 0 && RS <= 16, "four sublanes of <= 16 rows");
+    static_assert((LP == 4 || LP == 8) && R >= LP && R % LP == 0 && RS <= 16, "LP sublanes of <= 16 rows");
     __shared__ __attribute__((aligned(16))) uint8_t s_so[L::kBytes];
     typedef volatile uint8_t __attribute__((address_space(3))) lds_u8;
     typedef volatile uint32_t __attribute__((address_space(3))) lds_u32;
     typedef volatile uint16_t __attribute__((address_space(3))) lds_u16;
     lds_u8* const vb = (lds_u8*)s_so;
     lds_u32* const vw = (lds_u32*)s_so;
-    const int lane = threadIdx.x, quad = lane >> 2, sub = lane & 3;
-    const uint32_t slot = blockIdx.x * kSo4Pairs + quad;
+    const int lane = threadIdx.x, quad = lane / LP, sub = lane % LP;
+    const uint32_t slot = blockIdx.x * L::kPairs + quad;
     // a quad whose pair is not walked here leaves as a whole (the four lanes agree)
     bool live = slot < P.count;
     const uint32_t pidx = P.pair_base + (live ? slot : 0);
@@ -461,10 +466,11 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
     uint64_t rowc = 0, colc = 0;
     uint64_t W = 0, NW = 0, NNW = 0;   // tag columns wq, wq - 1, wq - 2: row r at bits 2r
     int wq = -1;
-    auto tagcol = [&](int q) __attribute__((always_inline)) -> uint64_t {   // the quad's 4 words, packed
-        const uint64_t w0 = vw[q * 64 + quad * 4 + 0], w1 = vw[q * 64 + quad * 4 + 1];
-        const uint64_t w2 = vw[q * 64 + quad * 4 + 2], w3 = vw[q * 64 + quad * 4 + 3];
-        return w0 | w1 << (2 * RS) | w2 << (4 * RS) | w3 << (6 * RS);
+    auto tagcol = [&](int q) __attribute__((always_inline)) -> uint64_t {   // the quad's LP words, packed
+        uint64_t t = 0;
+#pragma unroll
+        for (int k = 0; k < LP; ++k) t |= (uint64_t)vw[q * 64 + quad * LP + k] << (2 * RS * k);
+        return t;
     };
     auto pack_codes = [&](int base) __attribute__((always_inline)) -> uint64_t {   // 32 bytes of 8 x code
         uint64_t c = 0;
@@ -502,16 +508,18 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
             slo = j0 + tp;
             pk0 = slo >> 3;
             has_left = cc > 0 && j0 >= 1;
-            if (has_top) {   // the top row's five packets: sublane k loads packet k, sublane 0 also packet 4
+            if (has_top) {   // the top row's five packets: sublane k loads packet k (LP = 4: sublane 0 also packet 4)
                 const uint8_t* base = dir + (uint64_t)bp * band_stride;
                 const int pk = pk0 + sub;
-                if (pk >= 0 && (uint32_t)pk < npk)
+                if (sub < 5 && pk >= 0 && (uint32_t)pk < npk)
                     __builtin_amdgcn_global_load_lds((so_gptr)(base + ((uint64_t)pk * kWave + tp) * 16),
                                                      (so_lptr)(s_so + L::kEdge), 16, 0, 0);
-                const int pk4 = pk0 + 4;
-                if (sub == 0 && pk4 >= 0 && (uint32_t)pk4 < npk)
-                    __builtin_amdgcn_global_load_lds((so_gptr)(base + ((uint64_t)pk4 * kWave + tp) * 16),
-                                                     (so_lptr)(s_so + L::kEdge2), 16, 0, 0);
+                if constexpr (LP < 5) {
+                    const int pk4 = pk0 + 4;
+                    if (sub == 0 && pk4 >= 0 && (uint32_t)pk4 < npk)
+                        __builtin_amdgcn_global_load_lds((so_gptr)(base + ((uint64_t)pk4 * kWave + tp) * 16),
+                                                         (so_lptr)(s_so + L::kEdge2), 16, 0, 0);
+                }
             }
         }
         // this sublane's rows: left column, corner (the row above its first row, column j0 - 1)
@@ -546,8 +554,8 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
                 vb[L::kRowC + quad * 32 + rs0 + r] = (uint8_t)c8;
             }
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int q = sub * 8 + e, jj = j0 + q;
+            for (int e = 0; e < 32 / LP; ++e) {
+                const int q = sub * (32 / LP) + e, jj = j0 + q;
                 vb[L::kColC + quad * 32 + q] = (uint8_t)(q >= qlo && q <= qhi && jj < n ? so_code8(symp, s2[jj]) : 0u);
             }
         }
@@ -564,7 +572,7 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         // ahead, so no sub-step waits on LDS.
         int hl = Hp[RS - 1];
         int prev_up = corner;
-        int nmax = qhi - qlo + 1 + 3;   // sub-steps of this quad; the wave runs the most of any
+        int nmax = qhi - qlo + 1 + (LP - 1);   // sub-steps of this quad; the wave runs the most of any
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
         auto rd_sym = [&](int q) __attribute__((always_inline)) -> uint32_t {
@@ -574,7 +582,7 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
             if (sub != 0 || !act || !has_top || q < qlo || q > qhi) return 0;
             const int s = slo + q;
             const int d = (s >> 3) - pk0;
-            const int off = d < 4 ? L::kEdge + (quad * 4 + d) * 16 : L::kEdge2 + quad * 64;
+            const int off = (LP >= 5 || d < 4) ? L::kEdge + (quad * LP + d) * 16 : L::kEdge2 + quad * 64;
             return (int)((lds_u16*)(s_so + off + (s & 7) * 2))[0];   // (x 4 at the use: no wait here)
         };
         uint32_t nsym = rd_sym(qlo - sub);
@@ -585,7 +593,10 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
             const int top = ntop << 2;
             nsym = rd_sym(q + 1);
             ntop = rd_top(q + 1);
-            int up_h = __builtin_amdgcn_mov_dpp(hl, 0x90, 0xf, 0xf, false);   // quad_perm [0,0,1,2]
+            // the row above from sublane k-1: quad_perm [0,0,1,2] (LP = 4) / row_shr:1 (LP = 8; the
+            // sublane 0 lanes, which take lane 7 of the previous group, use the top row instead)
+            int up_h = LP == 4 ? __builtin_amdgcn_mov_dpp(hl, 0x90, 0xf, 0xf, false)
+                               : __builtin_amdgcn_mov_dpp(hl, 0x111, 0xf, 0xf, false);
             const bool on = act && q >= qlo && q <= qhi;
             if (sub == 0) up_h = top;
             if (on) {
@@ -715,12 +726,25 @@ hipError_t launch_traceback_so(int R, const TbParams& p, hipStream_t stream) {
         }
         return hipGetLastError();
     }
-    const dim3 grid((p.count + kSo4Pairs - 1) / kSo4Pairs);
+    // lanes per pair: $SEQALIB_TB_LP (4 or 8), else so4_default_lp
+    int lp = so4_default_lp(R);
+    if (const char* l = getenv("SEQALIB_TB_LP")) lp = (atoi(l) == 8 && R >= 8) ? 8 : 4;
+    const uint32_t ppw = (uint32_t)(kWave / lp);
+    const dim3 grid((p.count + ppw - 1) / ppw);
+    if (lp == 8) {
+        switch (R) {
+            case 8: hipLaunchKernelGGL((traceback_so4_kernel<8, 8>), grid, block, 0, stream, p); break;
+            case 16: hipLaunchKernelGGL((traceback_so4_kernel<16, 8>), grid, block, 0, stream, p); break;
+            case 32: hipLaunchKernelGGL((traceback_so4_kernel<32, 8>), grid, block, 0, stream, p); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (R) {
-        case 4: hipLaunchKernelGGL(traceback_so4_kernel<4>, grid, block, 0, stream, p); break;
-        case 8: hipLaunchKernelGGL(traceback_so4_kernel<8>, grid, block, 0, stream, p); break;
-        case 16: hipLaunchKernelGGL(traceback_so4_kernel<16>, grid, block, 0, stream, p); break;
-        case 32: hipLaunchKernelGGL(traceback_so4_kernel<32>, grid, block, 0, stream, p); break;
+        case 4: hipLaunchKernelGGL((traceback_so4_kernel<4, 4>), grid, block, 0, stream, p); break;
+        case 8: hipLaunchKernelGGL((traceback_so4_kernel<8, 4>), grid, block, 0, stream, p); break;
+        case 16: hipLaunchKernelGGL((traceback_so4_kernel<16, 4>), grid, block, 0, stream, p); break;
+        case 32: hipLaunchKernelGGL((traceback_so4_kernel<32, 4>), grid, block, 0, stream, p); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -247,6 +247,22 @@ def test_many_pairs_unstaged_seq2_vs_oracle(engine, algo, tall, monkeypatch):
     compare_with_oracle(engine, algo, SCORINGS[algo][0], pairs)
 
 
+@pytest.mark.parametrize("lp", ["4", "8"])
+@pytest.mark.parametrize("tall", [False, True])
+def test_so_traceback_lanes_per_pair_vs_oracle(engine, lp, tall, monkeypatch):
+    """Score-only traceback (traceback_so4_kernel) at 4 and 8 lanes per pair ($SEQALIB_TB_LP; the
+    default is 8 at R = 32, 4 below): R = 16 and (tall) R = 32 many-pairs batches, every op stream
+    against the full-matrix oracle."""
+    monkeypatch.setenv("SEQALIB_TB_LP", lp)
+    pairs = []
+    for k in range(1100):
+        m, n = (2050 + (k % 41), 150 + (k % 37)) if tall else (600 + (k % 43), 300 + (k % 29))
+        a = sa.synth_dna(50_000 + 2 * k, m)
+        b = sa.synth_mutate(a, k)[:n] if k % 2 else sa.synth_dna(50_001 + 2 * k, n)
+        pairs.append((a, b))
+    compare_with_oracle(engine, 0, SCORINGS[0][0], pairs)
+
+
 @pytest.mark.parametrize("algo", [0, 1, 2, 3])
 def test_multiband_wrap_vs_oracle(engine, algo, monkeypatch):
     """More bands than waves (m > 64*R*W): bands wrap round-robin over the waves of one
