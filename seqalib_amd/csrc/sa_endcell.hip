@@ -187,7 +187,11 @@ extern "C" int sa_debug_ecso_stats(unsigned long long* out, int reset) {
 }
 #endif
 
-template <int R>
+// DENSE = false: the candidate scan and the lane-block replay; a pair with more than kSoCand
+// candidate blocks is left pending (reserved != 0) for the DENSE = true launch behind it, which
+// replays whole chunks -- a kernel of its own so that its R-row register arrays do not set the
+// common kernel's occupancy (121 -> fewer VGPRs, more resident waves).
+template <int R, bool DENSE>
 __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
     if (sa_skip(P.sel, P.sel_want)) return;
     const int lane = threadIdx.x;
@@ -219,10 +223,10 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
 #ifdef SA_TB_STATS
     const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
 #endif
-    // ---- the candidate lane blocks, in [band][chunk][lane] order: 4 entries per lane per load
-    __shared__ uint32_t s_cand[kSoCand];   // band << 22 | chunk << 6 | lane
+    // ---- the candidate lane blocks, in [band][chunk][lane] order: kEcScan entries per lane per load
+    __shared__ uint32_t s_cand[DENSE ? 1 : kSoCand];   // band << 22 | chunk << 6 | lane
     // kEcScan (band, chunk) entries per iteration, one coalesced 256-B load each (issued together)
-    const uint32_t total = (uint32_t)B * snch;
+    const uint32_t total = DENSE ? 0u : (uint32_t)B * snch;
     int cnt = 0;
     uint32_t bnext = 0, cnext = 0;   // (band, chunk) of entry e0, stepped (no scalar divide)
     for (uint32_t e0 = 0; e0 < total; e0 += kEcScan) {
@@ -259,13 +263,58 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
     }
 #endif
 
-    if (cnt <= kSoCand) {
+    if (!DENSE && cnt > kSoCand) return;   // (uniform) pending: the DENSE launch takes the pair
+    if constexpr (!DENSE) {
         // ---- lane blocks: 64 / R per round, lane = block g's row r
         constexpr int NB = kWave / R;
         const int g = lane / R, r = lane % R;
         __shared__ uint32_t s_pk[NB][kChunk + 1];   // per block, q = -1 .. 31: top H | column code << 16
         const uint8_t* const dir = P.dirs + (uint64_t)slot * P.dir_slot;
         const uint64_t bst = P.band_stride;
+        // Round k+1's loads (left word, top values, Seq2 / Seq1 bytes) are issued before round k's
+        // steps and consumed after them, so a round's dependent global reads do not stall it; the
+        // profile words are registers (no load behind the Seq1 byte).
+        constexpr int QN = (kChunk + R) / R;   // q = r - 1 + R k < kChunk: at most QN per lane
+        const uint32_t pf0 = P.prof[0], pf1 = P.prof[1], pf2 = P.prof[2], pf3 = P.prof[3];
+        struct Pre {
+            uint32_t w, s1c;
+            uint32_t top[QN], s2c[QN];
+        };
+        auto fetch = [&](int c0, Pre& x) __attribute__((always_inline)) {
+            const int ci = c0 + g;
+            const bool act = ci < cnt;
+            const uint32_t cd = act ? s_cand[ci] : 0u;
+            const int b = (int)(cd >> 22), c = (int)((cd >> 6) & 0xffffu), t = (int)(cd & 63u);
+            const int i = b * BAND + t * R + r;
+            const int j0 = kChunk * c - t;
+            x.w = 0;
+            if (act && j0 >= 1 && i < m) x.w = sh_base[(((uint64_t)b * snch + (c - 1)) * (R / 2) + (r >> 1)) * kWave + t];
+            // the top row (row i0 - 1, the last row of lane t - 1, or of lane 63 of band b - 1) and the
+            // column codes: lane tp computed column jj at step jj + tp of its band's edge stream
+            const bool has_top = !(b == 0 && t == 0);
+            const int bp = t > 0 ? b : b - 1, tp = t > 0 ? t - 1 : kWave - 1;
+#pragma unroll
+            for (int k = 0; k < QN; ++k) {
+                const int q = r - 1 + R * k, jj = j0 + q;
+                x.top[k] = 0;
+                x.s2c[k] = 0;
+                if (q < kChunk && act && jj >= 0 && jj < n) {
+                    if (has_top) {
+                        if (q < 0 && j0 >= 1) {
+                            x.top[k] = (uint32_t)sp_base[((uint64_t)b * snch + (c - 1)) * kWave + t] & 0xffffu;
+                        } else {
+                            const int st = jj + tp;
+                            x.top[k] = *reinterpret_cast<const uint16_t*>(dir + (uint64_t)bp * bst +
+                                                                        ((uint64_t)(st >> 3) * kWave + tp) * 16 + (st & 7) * 2);
+                        }
+                    }
+                    x.s2c[k] = s2[jj];
+                }
+            }
+            x.s1c = act && i < m ? s1[i] : 0u;
+        };
+        Pre cur, nxt;
+        fetch(0, cur);
         for (int c0 = 0; c0 < cnt; c0 += NB) {
             const int ci = c0 + g;
             const bool act = ci < cnt;
@@ -273,33 +322,17 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
             const int b = (int)(cd >> 22), c = (int)((cd >> 6) & 0xffffu), t = (int)(cd & 63u);
             const int i = b * BAND + t * R + r;   // this lane's row (0-based)
             const int j0 = kChunk * c - t;        // the block's first column
-            int h = 0;                            // H at column j0 - 1 (left of the block)
-            if (act && j0 >= 1 && i < m) {
-                const uint32_t w = sh_base[(((uint64_t)b * snch + (c - 1)) * (R / 2) + (r >> 1)) * kWave + t];
-                h = (int)((r & 1) ? (w >> 16) : (w & 0xffffu));
+            // H at column j0 - 1 (left of the block)
+            int h = (int)((r & 1) ? (cur.w >> 16) : (cur.w & 0xffffu));
+#pragma unroll
+            for (int k = 0; k < QN; ++k) {
+                const int q = r - 1 + R * k, jj = j0 + q;
+                const uint32_t code = (act && jj >= 0 && jj < n) ? ec_code8(symp, cur.s2c[k]) : 0u;
+                if (q < kChunk) s_pk[g][q + 1] = cur.top[k] | code << 16;
             }
-            // the top row (row i0 - 1, the last row of lane t - 1, or of lane 63 of band b - 1) and the
-            // column codes: lane tp computed column jj at step jj + tp of its band's edge stream
-            const bool has_top = !(b == 0 && t == 0);
-            const int bp = t > 0 ? b : b - 1, tp = t > 0 ? t - 1 : kWave - 1;
-            for (int q = r - 1; q < kChunk; q += R) {
-                const int jj = j0 + q;
-                uint32_t top = 0, code = 0;
-                if (act && jj >= 0 && jj < n) {
-                    if (has_top) {
-                        if (q < 0 && j0 >= 1) {
-                            top = (uint32_t)sp_base[((uint64_t)b * snch + (c - 1)) * kWave + t] & 0xffffu;
-                        } else {
-                            const int st = jj + tp;
-                            top = *reinterpret_cast<const uint16_t*>(dir + (uint64_t)bp * bst +
-                                                                     ((uint64_t)(st >> 3) * kWave + tp) * 16 + (st & 7) * 2);
-                        }
-                    }
-                    code = ec_code8(symp, s2[jj]);
-                }
-                s_pk[g][q + 1] = top | code << 16;
-            }
-            const uint32_t tab = act && i < m ? P.prof[ec_code8(symp, s1[i]) >> 3] : 0u;
+            const uint32_t c8 = ec_code8(symp, cur.s1c);
+            const uint32_t tab = act && i < m ? (c8 == 0 ? pf0 : c8 == 8 ? pf1 : c8 == 16 ? pf2 : pf3) : 0u;
+            if (c0 + NB < cnt) fetch(c0 + NB, nxt);
             __syncthreads();
             uint32_t pk = 0;            // (top H | column code << 16) of this lane's current column
             int up_prev = (int)(s_pk[g][0] & 0xffffu);   // row 0: the corner; other rows: set below
@@ -326,6 +359,7 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
                 }
             }
             __syncthreads();   // (s_pk and s_cand reads of this round)
+            cur = nxt;
         }
     } else {
         // ---- dense: whole chunks holding a candidate lane, all 64 lanes from the snapshots
@@ -631,13 +665,19 @@ hipError_t launch_split_reduce(int algo, const SplitReduceParams& p, hipStream_t
 
 hipError_t launch_endcell_so(int R, const EndcellParams& p, hipStream_t stream) {
     const dim3 grid(p.count), block(64);
+    // the lane-block kernel, then the dense one for the pairs it left pending (most return at once)
+#define SA_EC_SO(RR)                                                                       \
+    hipLaunchKernelGGL((endcell_so_kernel<RR, false>), grid, block, 0, stream, p);          \
+    if (hipPeekAtLastError() == hipSuccess)                                                 \
+        hipLaunchKernelGGL((endcell_so_kernel<RR, true>), grid, block, 0, stream, p);
     switch (R) {
-        case 4: hipLaunchKernelGGL(endcell_so_kernel<4>, grid, block, 0, stream, p); break;
-        case 8: hipLaunchKernelGGL(endcell_so_kernel<8>, grid, block, 0, stream, p); break;
-        case 16: hipLaunchKernelGGL(endcell_so_kernel<16>, grid, block, 0, stream, p); break;
-        case 32: hipLaunchKernelGGL(endcell_so_kernel<32>, grid, block, 0, stream, p); break;
+        case 4: SA_EC_SO(4) break;
+        case 8: SA_EC_SO(8) break;
+        case 16: SA_EC_SO(16) break;
+        case 32: SA_EC_SO(32) break;
         default: return hipErrorInvalidValue;
     }
+#undef SA_EC_SO
     return hipGetLastError();
 }
 

@@ -522,7 +522,8 @@ def test_t16_global_gotoh_screened_lut(engine):
 
 def test_endcell_replay_vs_oracle(engine, monkeypatch):
     """>= 1024 DNA SW pairs take the T16 plan with per-chunk maxima and the end-cell replay
-    (sa_endcell.hip): one pair per wave at R = 32 (max_m 4200 -> 3 bands).  Cases: all-zero matrices (end cell = last cell), periodic sequences (many
+    (sa_endcell.hip): one pair per wave at R = 32 (max_m 4200 -> 3 bands).  Cases: all-zero matrices (end cell = last cell; a
+    2500 x 2000 one takes the dense launch), periodic sequences (many
     tied maxima across rows and chunks), identical sequences, multi-band pairs."""
     rng = np.random.default_rng(5)
     pairs = []
@@ -542,6 +543,8 @@ def test_endcell_replay_vs_oracle(engine, monkeypatch):
     pairs[7] = (sa.synth_dna(1, 4200), sa.synth_dna(2, 3100))
     pairs[11] = (sa.synth_dna(3, 2100), sa.synth_mutate(sa.synth_dna(3, 2100), 9))
     pairs[13] = (b"ACGT" * 1050, b"ACGT" * 700)
+    # all-zero and 2 bands: every lane block is a candidate (> kSoCand), the dense end-cell launch
+    pairs[17] = (b"A" * 2500, b"C" * 2000)
     for args in [(-1, 1, -1), (-3, 2, -2), (-1, 2, -1)]:
         compare_with_oracle(engine, 0, args, pairs)
         assert engine.last_plan()[:2] == (sa.SA_KERNEL_T16_ENDCELL, 32), args
