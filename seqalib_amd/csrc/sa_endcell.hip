@@ -255,7 +255,7 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
     }
     __syncthreads();
 #ifdef SA_TB_STATS
-    if (lane == 0) {
+    if (!DENSE && lane == 0) {
         atomicAdd(&g_ecso_stats[0], 1ull);
         atomicAdd(&g_ecso_stats[1], (unsigned long long)cnt);
         atomicAdd(&g_ecso_stats[2], cnt > kSoCand ? 1ull : 0ull);
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
         if (ov > bv || (ov == bv && (oi > bi || (oi == bi && oj > bj)))) { bv = ov; bi = oi; bj = oj; }
     }
 #ifdef SA_TB_STATS
-    if (lane == 0) atomicAdd(&g_ecso_stats[3], __builtin_amdgcn_s_memtime() - st_t0);
+    if (!DENSE && lane == 0) atomicAdd(&g_ecso_stats[3], __builtin_amdgcn_s_memtime() - st_t0);
 #endif
     if (lane == 0) {   // (the other fields stay as the fill wrote them)
         sa_result* const o = P.res + pidx;
