@@ -169,6 +169,10 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
 // than kSoCand candidate blocks (an all-zero or low-scoring matrix: smax = 0 lists every block)
 // replays whole chunks instead (64 lanes, from the snapshots), as endcell_kernel does.
 constexpr int kSoCand = 1024;
+#ifndef SA_EC_SCAN
+#define SA_EC_SCAN 16
+#endif
+constexpr int kEcScan = SA_EC_SCAN;
 #ifdef SA_TB_STATS
 // Debug build only (-DSA_TB_STATS, tools/so4_stats.py): [pairs, candidate lane blocks, dense
 // fallbacks, wave cycles, scan cycles]
@@ -219,31 +223,34 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
 #ifdef SA_TB_STATS
     const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
 #endif
-    // ---- the candidate lane blocks, in [band][chunk][lane] order
+    // ---- the candidate lane blocks, in [band][chunk][lane] order: kEcScan entries per lane per load
     __shared__ uint32_t s_cand[DENSE ? 1 : kSoCand];   // band << 22 | chunk << 6 | lane
+    // kEcScan (band, chunk) entries per iteration, one coalesced 256-B load each (issued together)
     const uint32_t total = DENSE ? 0u : (uint32_t)B * snch;
     int cnt = 0;
-    // 64 (band, chunk) entries per load: entry e's wave maximum is the high half of lane (e & 63)'s
-    // snapshot word of e (the fill stores it there, sa_fill_impl.h SO); only the chunks whose
-    // maximum reaches thr have their 64 lane maxima read (one coalesced 256 B load each)
-    for (uint32_t e0 = 0; e0 < total; e0 += kWave) {
-        const uint32_t e = e0 + lane;
-        const uint32_t be = e / snch;
-        int wmax = INT_MIN;
-        if (e < total && (int)(e - be * snch) < nch) wmax = (int)((uint32_t)sp_base[(uint64_t)e * kWave + lane] >> 16);
-        uint64_t hits = __builtin_amdgcn_ballot_w64(wmax >= thr);
-        while (hits) {
-            const uint32_t k = (uint32_t)__builtin_ctzll(hits);
-            hits &= hits - 1;
-            const uint32_t eh = e0 + k;                     // (wave-uniform)
-            const uint32_t bb = eh / snch, cc = eh - bb * snch;
-            const bool hit = cm[(uint64_t)eh * kWave + lane] >= thr;
-            const uint64_t hl = __builtin_amdgcn_ballot_w64(hit);
+    uint32_t bnext = 0, cnext = 0;   // (band, chunk) of entry e0, stepped (no scalar divide)
+    for (uint32_t e0 = 0; e0 < total; e0 += kEcScan) {
+        int v[kEcScan];
+        uint32_t bb[kEcScan], cc[kEcScan];
+#pragma unroll
+        for (int k = 0; k < kEcScan; ++k) {   // (wave-uniform: scalar)
+            const uint32_t e = e0 + k;
+            bb[k] = bnext;
+            cc[k] = cnext;
+            v[k] = e < total && (int)cnext < nch ? cm[(uint64_t)e * kWave + lane] : INT_MIN;
+            const bool wrap = cnext + 1 == snch;
+            bnext += wrap ? 1u : 0u;
+            cnext = wrap ? 0u : cnext + 1;
+        }
+#pragma unroll
+        for (int k = 0; k < kEcScan; ++k) {
+            const bool hit = v[k] >= thr;
+            const uint64_t hits = __builtin_amdgcn_ballot_w64(hit);
             if (hit) {
-                const int pos = cnt + (int)__builtin_popcountll(hl & ((1ull << lane) - 1));
-                if (pos < kSoCand) s_cand[pos] = bb << 22 | cc << 6 | (uint32_t)lane;
+                const int pos = cnt + (int)__builtin_popcountll(hits & ((1ull << lane) - 1));
+                if (pos < kSoCand) s_cand[pos] = bb[k] << 22 | cc[k] << 6 | (uint32_t)lane;
             }
-            cnt += (int)__builtin_popcountll(hl);
+            cnt += (int)__builtin_popcountll(hits);
         }
     }
     __syncthreads();

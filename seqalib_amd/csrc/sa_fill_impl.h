@@ -550,7 +550,6 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     // t16_ok, chunks < 4096 since n < 65535): highest score, then last chunk
     uint32_t lkey = 0;
     uint32_t smax = 0;   // SO: the lane's largest tracked cell (the wave's: a lower bound of S)
-    uint32_t so_wmax = 0;   // SO: the current chunk's wave maximum << 16 (snapshot word high half)
     int hl = 0, xl = 0, sym = 0, prev_up = 0;
     int row0 = 0;
     // Running best of this lane over its bands: (score, i, j), 1-based cell.
@@ -1224,13 +1223,6 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                         // end-cell replay then recomputes only the lane blocks that may hold S
                         P.snap_m[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = (int32_t)cml;
                         smax = max(smax, cml);   // (per lane; reduced over the wave at the end)
-                        // the chunk's wave maximum rides in the high half of lane (e & 63)'s snapshot
-                        // word of entry e (H < 2^16; readers mask the low half): the end-cell scan
-                        // reads 64 entries per load and the lane maxima of the hit chunks only
-                        uint32_t wm = cml;
-#pragma unroll
-                        for (int off = 32; off >= 1; off >>= 1) wm = max(wm, (uint32_t)__shfl_xor((int)wm, off));
-                        so_wmax = wm << 16;
                     } else {
                         P.snap_m[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = (int32_t)cml;
                         lkey = max(lkey, (cml >> CSH) << 12 | ck);
@@ -1250,10 +1242,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                                 sh[(R / 2 + q) * kWave] = ((uint32_t)Yp[2 * q] & 0xffffu) | ((uint32_t)Yp[2 * q + 1] << 16);
                             sh[R * kWave] = (uint32_t)xl;
                         }
-                        P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] =
-                            SO ? (int32_t)((uint32_t)prev_up | (lane == (int)(e & 63) ? so_wmax : 0u)) : prev_up;
-                    } else if constexpr (SO) {   // the band's last chunk: its wave maximum only
-                        if (lane == (int)(e & 63)) P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = (int32_t)so_wmax;
+                        P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = prev_up;
                     }
                 }
                 // ---------------------------------------------------------------- band end
