@@ -6,7 +6,8 @@ assembly) over one batch of synthetic DNA pairs that is already resident in HBM.
 N=1 (north_star headline): 10,000 pairs of 4,096 x 4,096, ScoringSystem(-1, 1, -1) with
 equal<char> — the same pairs the reference's SmithWatermanSA would see.
 
-Multi-GPU: one process per GPU (torchrun); rank r aligns its own 10,000-pair shard of a global
+Multi-GPU: one process per GPU -- started by torch.distributed.run, or, when `--gpus N` is given
+without a launcher, spawned by this script itself (spawn_ranks); rank r aligns its own 10,000-pair shard of a global
 batch (pair p uses seeds base+2p+1 / base+2p+2), with no data-path collective (pairs are
 independent); timing is barrier-bracketed (gloo, host memory: no RCCL anywhere) and the max over
 ranks is reported.  scaling = weak.
@@ -79,10 +80,52 @@ def parse():
     return ap.parse_args()
 
 
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE): start N rank processes of
+    this script, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), as
+    torch.distributed.run would.  This process touches no GPU and imports no torch: it only waits
+    for the ranks (rank 0 prints the JSON line) and returns the first non-zero exit code; when one
+    rank fails, the others are terminated instead of being left at a barrier."""
+    import subprocess
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        # a line for N GPUs must come from N ranks: never report one rank's work as --gpus N
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} "
+                         "(launch with torch.distributed.run --nproc-per-node N, or without a launcher)")
     import torch
 
     if world > 1:
@@ -251,8 +294,22 @@ def issue_model(label: str):
         return None
 
 
+def gather_parity(par: dict, world: int):
+    """Every rank's parity summary (gloo, host memory), in rank order."""
+    if world == 1:
+        return [par]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, par)
+    return out
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     # HIP events around each fill kernel alone (sa_last_kernel_timings): the roofline's launch time
     os.environ.setdefault("SEQALIB_KERNEL_TIMING", "1")
     world, rank, local = dist_setup(args)
@@ -341,6 +398,7 @@ def main():
     ops = d_ops[last].cpu().numpy()
     cores = host_cores()["usable"]
     par = parity_sw_batch(s1, o1, s2, o2, res, ops, args.parity_ops, cores, 10)
+    par_ranks = gather_parity(par, world)
     configs = None
     if rank == 0 and world == 1 and args.configs:
         from bench_configs import measure
@@ -413,10 +471,14 @@ def main():
                      "piece k), fill, end cell, traceback, download of results and op streams into the caller's "
                      "(reused) buffers piece by piece",
         "pipelined": pipelined, "serial_ms_per_step": round(serial_ms, 2) if serial_ms else None,
-        "parity": (f"{par['end_cells']} pairs' (MaxScore, MaxRow, MaxCol) bit-exact vs oracle; {par['rescored']} "
-                   f"alignments re-score to MaxScore; {par['op_streams']} full op streams bit-exact; "
-                   f"{par['flagged']} flagged"),
-        "parity_exact": par["exact"],
+        "parity": "; ".join(
+            (f"rank {r}: " if world > 1 else "")
+            + (f"{q['end_cells']} pairs' (MaxScore, MaxRow, MaxCol) bit-exact vs oracle; {q['rescored']} "
+               f"alignments re-score to MaxScore; {q['op_streams']} full op streams bit-exact; {q['flagged']} flagged")
+            for r, q in enumerate(par_ranks)),
+        "parity_exact": all(q["exact"] for q in par_ranks),
+        "parity_ranks": [{"rank": r, "exact": q["exact"], "end_cells": q["end_cells"], "op_streams": q["op_streams"]}
+                         for r, q in enumerate(par_ranks)] if world > 1 else None,
         "configs": configs,
     }
     if world == 1:

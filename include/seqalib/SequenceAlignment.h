@@ -191,6 +191,9 @@ std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std
     auto build = [&](size_t p0, size_t p1) {
         for (size_t p = p0; p < p1; ++p) {
             const sa_result& r = res[p];
+            // a diverged or timed-out pair has no valid end cell / op stream: never expand it
+            // (align() throws for it once the GPU call returns)
+            if (r.flags & (SA_FLAG_DIVERGED | SA_FLAG_TIMEOUT)) continue;
             build_from_ops<Ty, Blank>(*pairs[p].first, *pairs[p].second, r, ops.data() + off[p], out[p]);
             const bool local = (ALGO == SA_SW || ALGO == SA_LOCAL_GOTOH) && !(r.flags & SA_FLAG_SIZE_HACK);
             if (local)

@@ -51,6 +51,9 @@ struct sa_ctx {
     int nvar = 0, var_kernel[2] = {0, 0}, var_R[2] = {0, 0}, var_W[2] = {0, 0}, var_records[2] = {0, 0};
     uint32_t* h_sel = nullptr;
     hipEvent_t ev_sel = nullptr;
+    // the last call's selection when the host decided it (host_alphabet), else -1: then the
+    // device's word arrives in h_sel (a host write there could race with a pending download)
+    int host_sel = -1;
     // cross-call pipeline of the device API (sa_set_pipeline): fills on s_fill, tracebacks on
     // s_tb, two workspace slots; ev_slot[k] = traceback of the last call that used slot k done
     int pipeline = 0;
@@ -558,6 +561,9 @@ struct HostSeqs {   // a host API batch's sequences (and host match table) for h
     // copy (up_bytes from up_src to up_dst; dhdr is where the header lands) before any kernel.
     uint32_t* hhdr = nullptr;
     const uint32_t* dhdr = nullptr;
+    // otherwise (pipelined chunks of one host call) the chunk's own pinned slot of 6 words for the
+    // profile upload: the chunks are enqueued without a host wait, so they must not share one
+    uint32_t* hprof = nullptr;
     void* up_dst = nullptr;
     const void* up_src = nullptr;
     uint64_t up_bytes = 0;
@@ -608,9 +614,10 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         // the host decided the alphabet (align_host): upload the profile; enqueue the chosen variant
         // alone -- plus the int32 re-run when T16 may overflow (SW / LocalGotoh retry_above, the
         // screened GlobalGotoh), which then reads the selection word as usual
-        *c->h_sel = (uint32_t)ha->sel;
+        c->host_sel = ha->sel;
         const bool in_hdr = hs->hhdr != nullptr;   // (small call: travels with the inputs)
-        uint32_t* const hp = in_hdr ? hs->hhdr : c->h_sel + 8;   // pinned (the host API call is synchronous)
+        if (!in_hdr && !hs->hprof) return fail(c, SA_ERR_ARG, "internal: no pinned profile slot");
+        uint32_t* const hp = in_hdr ? hs->hhdr : hs->hprof;   // pinned, this call's / chunk's own
         for (int k = 0; k < 5; ++k) hp[k] = ha->prof[k];
         hp[5] = (uint32_t)ha->sel;
         if (in_hdr) prof = hs->dhdr;
@@ -624,6 +631,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     if (host_sel) {
         SA_HIP(c, hipEventRecord(c->ev_sel, stream));
     } else if (t16) {
+        c->host_sel = -1;
         SA_HIP(c, launch_alphabet_scan(d1, o1, d2, o2, npairs, aux, stream));
         SA_HIP(c, launch_decide_t16(d_lutbits, sc->match, tm.mismatch, is_affine(algo) ? 1 : 0, aux, stream));
         SA_HIP(c, hipMemcpyAsync(c->h_sel, aux + kAuxSel, 4, hipMemcpyDeviceToHost, stream));
@@ -706,8 +714,10 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     if (pipe && (((c->ws_bytes / 2) & ~(uint64_t)255) < need || (any_split && ((c->split_bytes / 2) & ~(uint64_t)255) < sp_slot)))
         return fail(c, SA_ERR_HIP, "internal: pipeline slots overlap");
 
-    // reset timing
+    // reset timing (kernel timings describe this call only: a call without
+    // SEQALIB_KERNEL_TIMING leaves none, and sa_last_kernel_timings then fails)
     c->launches = 0;
+    c->kvars.clear();
     c->timed_stream = stream;
     hipStream_t sf = stream, stb = stream;
     if (pipe) {
@@ -1152,7 +1162,9 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     const uint64_t b_s1 = al(t1 + 1), b_s2 = al(t2 + 1), b_o = al(8 * n_off);
     const uint64_t b_res = al(sizeof(sa_result) * (uint64_t)npairs);
     const uint64_t b_ops = al(ops_total + 1), b_lut = al(65536), b_bits = al(8192);
-    constexpr uint64_t b_hdr = 256;   // small calls: the host-decided T16 profile (HostSeqs::hhdr)
+    // small calls: the host-decided T16 profile (HostSeqs::hhdr); chunked calls: one 32-byte
+    // profile slot per chunk (HostSeqs::hprof)
+    const uint64_t b_hdr = al(std::max<uint64_t>(256, 32ull * G));
     const uint64_t io_need = b_hdr + b_s1 + b_s2 + 2 * b_o + b_res + b_ops + b_lut + b_bits;
     if (int rc = ensure_io(c, io_need)) return rc;
     uint8_t* p = c->io;
@@ -1264,6 +1276,7 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         } else {
             // small batches: the alphabet is decided here, on the host (no scan / decide kernels)
             HostSeqs hs{seq1 + a1, n1, seq2 + a2, n2, use_lut ? lut : nullptr};
+            hs.hprof = shdr + 8 * g;
             if (small) {
                 hs.hhdr = shdr;
                 hs.dhdr = dhdr;
@@ -1654,9 +1667,9 @@ int sa_last_kernel_timings(sa_ctx* c, float* fill_kernel_ms, float* fill_stream_
 int sa_last_plan_ex(sa_ctx* c, int* kernel, int* R, int* W, int* records) {
     if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
     int k = 0;
-    if (c->nvar == 2) {   // T16 and int32 were both enqueued: the device's choice decides
+    if (c->nvar == 2) {   // T16 and int32 were both enqueued: the host's or the device's choice decides
         SA_HIP(c, hipEventSynchronize(c->ev_sel));
-        k = *c->h_sel == 1 ? 0 : 1;
+        k = (c->host_sel >= 0 ? (uint32_t)c->host_sel : *c->h_sel) == 1 ? 0 : 1;
     }
     if (kernel) *kernel = c->var_kernel[k];
     if (R) *R = c->var_R[k];

@@ -88,3 +88,28 @@ def test_slice_batch_rebases_offsets():
     a, oa, b, ob = slice_batch(s1, o1, s2, o2, 2, 4)
     assert list(oa) == [0, 10, 20] and list(ob) == [0, 7, 14]
     assert a.tobytes() == s1[20:40].tobytes() and b.tobytes() == s2[14:28].tobytes()
+
+
+def _run_bench(args, env_extra, timeout=240):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, "bench.py"] + args, cwd=root, env=env, capture_output=True, text=True,
+                          timeout=timeout)
+
+
+def test_bench_refuses_world_size_mismatch():
+    """A line for N GPUs must come from N ranks: --gpus 2 under a launcher's WORLD_SIZE=3 fails loudly."""
+    r = _run_bench(["--gpus", "2", "--steps", "1"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "--gpus 2 but WORLD_SIZE=3" in r.stderr
+
+
+def test_bench_gpus_n_spawns_n_ranks_without_launcher():
+    """`bench.py --gpus 2` with no launcher starts two rank processes that rendezvous over gloo on
+    127.0.0.1 (here, without a GPU, each rank then stops at the GPU check after the rendezvous)."""
+    r = _run_bench(["--gpus", "2", "--steps", "1"], {"CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""})
+    assert r.returncode != 0
+    assert r.stderr.count("bench.py needs a GPU") == 2, r.stderr[-2000:]

@@ -259,3 +259,30 @@ def test_multi_engine_four_contexts_stage_concurrently(engine, capfd, monkeypatc
     inflight = max(int(ln.split("max ")[1].split(" copy jobs")[0]) for ln in lines)
     print("\n".join(lines))
     assert inflight >= 2, lines
+
+
+@pytest.mark.parametrize("algo,args", [(0, (-1, 1, -1)), (1, (-1, 2, -1)), (2, (-3, -1, 1, -1)),
+                                       (3, (-3, -1, 1, -1, True))])
+def test_host_chunks_with_distinct_small_alphabets(engine, monkeypatch, algo, args):
+    """A host call cut into pipelined chunks (SEQALIB_HOST_CHUNKS) whose chunks are small enough for
+    the host to decide each chunk's T16 alphabet, and whose alphabets differ (ACGT / ACGN / TWXY,
+    <= 4 symbols each): every chunk must run with its OWN profile and symbol pack (each chunk has
+    its own pinned profile slot; round-4 advisor finding), so every pair equals the oracle."""
+    from util import oracle_batch
+    rng = np.random.default_rng(100 + algo)
+    pairs = []
+    for alph in (b"ACGT", b"ACGN", b"TWXY"):
+        sym = np.frombuffer(alph, dtype=np.uint8)
+        for _ in range(700):   # equal cells per pair: the three chunks are exactly the three groups
+            pairs.append((sym[rng.integers(0, 4, 24)].tobytes(), sym[rng.integers(0, 4, 20)].tobytes()))
+    s1, o1, s2, o2 = sa.pack_pairs(pairs)
+    monkeypatch.setenv("SEQALIB_HOST_CHUNKS", "3")
+    res, ops = engine.align_packed(algo, sa.ScoringSystem(*args), s1, o1, s2, o2)
+    ores, oops = oracle_batch(algo, args, s1, o1, s2, o2, threads=THREADS)
+    for p in range(len(pairs)):
+        off = int(o1[p] + o2[p]) + p
+        got = (int(res["score"][p]), int(res["end_i"][p]), int(res["end_j"][p]), int(res["start_i"][p]),
+               int(res["start_j"][p]), ops[off:off + int(res["nops"][p])].tobytes())
+        exp = (int(ores["score"][p]), int(ores["end_i"][p]), int(ores["end_j"][p]), int(ores["start_i"][p]),
+               int(ores["start_j"][p]), oops[off:off + int(ores["nops"][p])].tobytes())
+        assert got == exp, (p, got, exp)

@@ -47,3 +47,33 @@ def test_two_hip_ranks_gloo(tmp_path, length):
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
     assert abs(line["ms_per_step"] - slowest / steps * 1e3) < 0.01
     assert line["value"] > 0
+
+
+@pytest.mark.timeout(900)
+def test_bench_gpus2_spawns_two_ranks(tmp_path):
+    """`python3 bench.py --gpus 2 --steps 2 --warmup 1` exactly as the driver starts it for N = 2 --
+    no launcher, no WORLD_SIZE -- must run two ranks (bench.py spawns them), each aligning its own
+    10,000-pair shard of the 4096 x 4096 headline workload, and report n_gpus = 2, the max-over-ranks
+    time and exact parity on both shards.  Both ranks share GPU 0 here (SEQALIB_BENCH_DEVICE=0)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(SEQALIB_BENCH_DEVICE="0")
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--rank-out", str(tmp_path), "--out", str(tmp_path / "line.json")]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=840)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]   # rank 0 alone prints the line
+    line = json.loads(lines[0])
+    assert line == json.loads(open(tmp_path / "line.json").read())
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "pair-shard x2"
+    assert line["config"]["workload"] == "sw_batch_10000x4096x4096"
+    assert line["parity_exact"] is True
+    assert [q["rank"] for q in line["parity_ranks"]] == [0, 1]
+    for q in line["parity_ranks"]:
+        assert q["exact"] and q["end_cells"] == "10000/10000", q
+    ranks = [json.load(open(tmp_path / f"rank{k}.json")) for k in (0, 1)]
+    assert [rr["world"] for rr in ranks] == [2, 2]
+    assert ranks[0]["seed_base"] != ranks[1]["seed_base"]
+    slowest = max(rr["own_s"] for rr in ranks)
+    assert abs(line["ms_per_step"] - slowest / 2 * 1e3) < 0.01
+    assert line["value"] == pytest.approx(2 * 10000 * 4096 * 4096 * 2 / slowest / 1e9, rel=1e-3)

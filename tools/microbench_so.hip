@@ -7,6 +7,9 @@
 //   SO4  SO with the lane maximum over every other row only (max3 per 4 rows)               (6.25)
 //   SO0  SO without the lane maximum (lower bound)                                          (6)
 //   SOB  SO + the lane's last row packed per step into a 16-bit stream (v_perm every 2 steps)
+//   SG   shipped round-4 shared-gap cell: max(U, L), bfe + add (next diag), sub clamp, max      (5)
+//   SD   shared-gap cell with the substitution by v_dot4_i32_i8 (profile bytes . one-hot column
+//        code + Hp = next diag in one op): max, dot4, sub clamp, max                          (4)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -22,18 +25,37 @@ __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, i
     uint32_t tab[R], Hp[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) { tab[r] = in[(lane * 7 + r) & 1023]; Hp[r] = 0; }
-    uint32_t hl = 0, sym = (lane & 3) * 8, prev_up = 0, rec = 0, acc = 0, cml = 0, bot = 0;
+    uint32_t hl = 0, sym = (lane & 3) * 8, prev_up = 0, rec = 0, acc = 0, cml = 0, bot = 0, oh = 1u << ((lane & 3) * 8);
     const uint32_t CU = 2, CL = 0xfffd, CU1 = 1, CL1 = 0xffff;
     for (int s = 0; s < steps; ++s) {
         const uint32_t up_h = shr1(in[s & 1023], hl);
-        sym = shr1((uint32_t)((s * 7) & 3) * 8, sym);
+        if constexpr (V == 6) oh = shr1(1u << (((s * 7) & 3) * 8), oh);
+        else sym = shr1((uint32_t)((s * 7) & 3) * 8, sym);
         uint32_t hu = up_h, dcur;
         asm volatile("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(dcur) : "v"(tab[0]), "v"(sym), "v"(prev_up));
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             uint32_t t0, t1, dn = 0;
             const uint32_t tabn = tab[r + 1 < R ? r + 1 : r];
-            if constexpr (V == 0) {
+            if constexpr (V == 5) {
+                asm volatile("v_max_i16 %[t1], %[hu], %[hp]\n\t"
+                             "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\tv_add_u16 %[dn], %[hp], %[dn]\n\t"
+                             "v_sub_u16_e64 %[t1], %[t1], %[cu] clamp\n\t"
+                             "v_max_i16 %[hp], %[dr], %[t1]"
+                             : [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r])
+                             : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU1), [tabn] "v"(tabn), [sym] "v"(sym));
+                (void)t0;
+                if (r % 8 == 7 && (s & 3) == 3) asm volatile("v_max3_u32 %0, %0, %1, %2" : "+v"(cml) : "v"(Hp[r - 4]), "v"(Hp[r]));
+            } else if constexpr (V == 6) {
+                asm volatile("v_max_i16 %[t1], %[hu], %[hp]\n\t"
+                             "v_dot4_i32_i8 %[dn], %[tabn], %[oh], %[hp]\n\t"
+                             "v_sub_u16_e64 %[t1], %[t1], %[cu] clamp\n\t"
+                             "v_max_i16 %[hp], %[dr], %[t1]"
+                             : [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r])
+                             : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU1), [tabn] "v"(tabn), [oh] "v"(oh));
+                (void)t0;
+                if (r % 8 == 7 && (s & 3) == 3) asm volatile("v_max3_u32 %0, %0, %1, %2" : "+v"(cml) : "v"(Hp[r - 4]), "v"(Hp[r]));
+            } else if constexpr (V == 0) {
                 asm volatile("v_add_u16 %[t0], %[cl], %[hp]\n\t"
                              "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\tv_add_u16 %[dn], %[hp], %[dn]\n\t"
                              "v_sub_u16_e64 %[t1], %[hu], %[cu] clamp\n\t"
@@ -69,7 +91,7 @@ __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, i
         }
         acc ^= rec;
     }
-    uint32_t x = acc ^ hl ^ cml;
+    uint32_t x = acc ^ hl ^ cml ^ oh;
 #pragma unroll
     for (int r = 0; r < R; ++r) x ^= Hp[r];
     out[blockIdx.x * 64 + lane] = x;
@@ -88,6 +110,9 @@ int main(int argc, char** argv) {
         {"SO4 score-only R32 max/4 (6.25)", cells<2, 32>, 32},
         {"SO0 score-only R32 no max (6)", cells<3, 32>, 32},
         {"SOB SO + bottom-row stream R32", cells<4, 32>, 32},
+        {"SG shared-gap shipped R32 (5)", cells<5, 32>, 32},
+        {"SD shared-gap dot4 R32 (4)", cells<6, 32>, 32},
+        {"SD shared-gap dot4 R16 (4)", cells<6, 16>, 16},
         {"SO score-only R16 (6.5)", cells<1, 16>, 16},
         {"SO score-only R64 (6.5)", cells<1, 64>, 64},
     };
