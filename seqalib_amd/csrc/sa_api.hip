@@ -220,18 +220,21 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
     v.cmax = t16 && v.pl.W == 1 && v.pl.R >= 2 &&
              ((algo == SA_SW && v.pl.R <= 32) || (algo == SA_LOCAL_GOTOH && v.pl.R <= 16));
     if (const char* ec = getenv("SEQALIB_CMAX")) if (ec[0] == '0') v.cmax = false;
-    if (v.cmax) {
+    // Score-only fill (T16 many-pairs plans): no per-cell records; the traceback recomputes the
+    // blocks along its path from per-chunk snapshots and the edge stream.  SW with the chunk-max end
+    // cell; NW (whose walk starts at (m, n)) from the plain T16 plan.  SEQALIB_SO=0 keeps the tagged
+    // records (A/B, tests).
+    const bool so_plan = !v.pl.split && v.pl.W == 1 && v.pl.R >= 4 && v.pl.R <= 32;
+    v.so = so_plan && ((algo == SA_SW && v.cmax) || (algo == SA_NW && t16));
+    if (const char* e = getenv("SEQALIB_SO")) if (e[0] == '0') v.so = false;
+    if (v.cmax || v.so) {
         v.snap_nch = chunks_per_band(max_n);
         v.snap_p_slot = (uint64_t)v.pl.g.bands * v.snap_nch * kWave;
         // per lane: R 16-bit values (LocalGotoh: M, then Iy, then the last row's Ix: R + 1 words)
         v.snap_h_slot = v.snap_p_slot * (is_affine(algo) ? v.pl.R + 1 : v.pl.R / 2);
-        v.pl.rowbuf_elems = (uint64_t)(is_affine(algo) ? 2 : 1) * v.pl.g.bands * std::max<uint32_t>(max_n, 1);
+        // the end-cell replay reads every band's top row (the SO NW fill reuses one row)
+        if (v.cmax) v.pl.rowbuf_elems = (uint64_t)(is_affine(algo) ? 2 : 1) * v.pl.g.bands * std::max<uint32_t>(max_n, 1);
     }
-    // Score-only fill (T16 SW chunk-max, many-pairs plans): no per-cell records; the traceback
-    // recomputes the blocks along its path from the snapshots and the edge stream.
-    // SEQALIB_SO=0 keeps the tagged records (A/B, tests).
-    v.so = v.cmax && algo == SA_SW && !v.pl.split && v.pl.R >= 4 && v.pl.R <= 32;
-    if (const char* e = getenv("SEQALIB_SO")) if (e[0] == '0') v.so = false;
     if (v.so) v.pl.g = make_geom(algo, v.pl.R, max_m, max_n, kGeomEdge);
     if (v.pl.split) v.pl.rowbuf_elems = 0;   // hand-off granules live in c->split
     v.kernel = v.cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
@@ -720,8 +723,14 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     c->kvars.clear();
     c->timed_stream = stream;
     hipStream_t sf = stream, stb = stream;
+    // A/B (round 5): SEQALIB_FILL2=1 runs the fills of pipeline slot 1 on the context's own stream
+    // (idle in the device API), so call k+1's fill may start in call k's fill tail;
+    // SEQALIB_ENDCELL_TB=1 runs the end-cell replay on the traceback stream
+    const char* e_f2 = getenv("SEQALIB_FILL2");
+    const char* e_etb = getenv("SEQALIB_ENDCELL_TB");
+    const bool endcell_tb = pipe && e_etb && e_etb[0] == '1';
     if (pipe) {
-        sf = c->s_fill;
+        sf = (slot == 1 && e_f2 && e_f2[0] == '1') ? c->stream : c->s_fill;
         stb = c->s_tb;
         SA_HIP(c, hipEventRecord(c->ev_in, stream));
         SA_HIP(c, hipStreamWaitEvent(sf, c->ev_in, 0));
@@ -753,6 +762,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         const uint64_t hand_x_off = any_split ? (uint64_t)cnt * sp_bands * std::max<uint32_t>(max_n, 1) : 0;
         // fill parameters of variant k (k == nv: the SPLIT fallback)
         FillParams fps[3];
+        EndcellParams eps[3];
+        bool ep_set[3] = {false, false, false};
         // $SEQALIB_STAGE_SEQ2=0: read Seq2 from global memory in every plan (tests the unstaged
         // path that batches with max_n > kMaxStagedSeq2 take)
         const char* stage_env = getenv("SEQALIB_STAGE_SEQ2");
@@ -848,12 +859,23 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 ep.dirs = fp.dirs; ep.dir_slot = fp.dir_slot; ep.band_stride = fp.band_stride;
                 // on the fill stream, right after the fill: run beside the next call's fill (on the
                 // traceback stream) its 10,000 short waves slowed that fill by 4 % (measured)
+                if (endcell_tb) {
+                    eps[k] = ep;
+                    ep_set[k] = true;
+                    continue;
+                }
                 e = v.so ? launch_endcell_so(pl.R, ep, sf) : launch_endcell(algo, pl.R, ep, sf);
                 if (e != hipSuccess) return hip_fail(c, e, "end-cell kernel launch");
             }
         }
         SA_HIP(c, hipEventRecord(ev[1], sf));
         if (pipe) SA_HIP(c, hipStreamWaitEvent(stb, ev[1], 0));
+        for (int k = 0; k < nv; ++k) {
+            if (!ep_set[k]) continue;
+            const hipError_t e = vars[k].so ? launch_endcell_so(vars[k].pl.R, eps[k], stb)
+                                            : launch_endcell(algo, vars[k].pl.R, eps[k], stb);
+            if (e != hipSuccess) return hip_fail(c, e, "end-cell kernel launch");
+        }
         auto make_tp = [&](int k) {
             const Variant& v = vars[k];
             TbParams tp{};
@@ -874,6 +896,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             tp.snap_h = fps[k].snap_h; tp.snap_p = fps[k].snap_p;
             tp.snap_h_slot = v.snap_h_slot; tp.snap_p_slot = v.snap_p_slot; tp.snap_nch = v.snap_nch;
             tp.prof = fps[k].prof;
+            tp.t16_delta = fps[k].t16_delta;
             return tp;
         };
         for (int k = 0; k < nv; ++k) {
@@ -904,7 +927,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                     }
                 }
             }
-            hipError_t e = v.so ? launch_traceback_so(v.pl.R, tp, stb)
+            hipError_t e = v.so ? launch_traceback_so(algo, v.pl.R, tp, stb)
                          : tb_wave(cnt) ? launch_traceback_wave(algo, v.pl.R, lut, tp, stb)
                                         : launch_traceback(algo, v.pl.R, lut, tp, stb);
             if (e != hipSuccess) return hip_fail(c, e, "traceback kernel launch");

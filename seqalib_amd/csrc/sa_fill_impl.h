@@ -173,11 +173,25 @@ constexpr int kEvCol = 2048;
         }                                                                                           \
         return 0;                                                                                   \
     }
+// many-pairs plans: per workgroup (slot) {start, end} in s_memrealtime ticks and {HW_ID, XCC_ID}
+// (tools/fill_timeline.py: the fill's schedule -- generations, per-SIMD residency, the tail)
+static __device__ unsigned long long g_fill_stats[32768][3];
+#define SA_FILL_STATS_ACCESSOR(NAME)                                                               \
+    extern "C" int NAME(unsigned long long* out, int reset) {                                       \
+        if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fill_stats), sizeof(g_fill_stats)) != hipSuccess) \
+            return 1;                                                                               \
+        if (reset) {                                                                                \
+            static unsigned long long z[32768][3];                                                  \
+            if (hipMemcpyToSymbol(HIP_SYMBOL(g_fill_stats), z, sizeof(g_fill_stats)) != hipSuccess) return 1; \
+        }                                                                                           \
+        return 0;                                                                                   \
+    }
 #define SA_EV(k, cond) do { if (ev[k] == 0 && (cond)) ev[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define SA_EV_FLUSH() do { const uint64_t id_ = (uint64_t)slot * P.split_bands + band0;            \
     if (id_ < 4096 && lane == 0) for (int k_ = 0; k_ < 12; ++k_) if (ev[k_]) g_split_ev[id_][k_] = ev[k_]; } while (0)
 #else
 #define SA_SPLIT_STATS_ACCESSOR(NAME)
+#define SA_FILL_STATS_ACCESSOR(NAME)
 #define SA_EV(k, cond) do {} while (0)
 #define SA_EV_FLUSH() do {} while (0)
 #endif
@@ -214,7 +228,11 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                   "T16: allow-mismatch, profile");
     static_assert(!T16 || !LOCAL || KEYED, "T16 local mode tracks its maximum with keys");
     constexpr int SC = SO ? 1 : T16 ? (AFF ? 8 : 4) : 1;   // score scale of the register values
-    static_assert(!SO || (T16 && CMAX && ALG == SA_SW && !SPLIT), "SO: T16 SW chunk-max, many pairs");
+    // SO: T16, many pairs; SW with the chunk-max end cell, or NW (which ends at (m, n))
+    static_assert(!SO || (T16 && !SPLIT && ((ALG == SA_SW && CMAX) || (ALG == SA_NW && !CMAX))),
+                  "SO: T16 SW chunk-max or NW, many pairs");
+    // per-chunk snapshots of every lane's state (the end-cell replay and the SO traceback read them)
+    constexpr bool SNAP = CMAX || SO;
     constexpr int CSH = SO ? 0 : (AFF ? 3 : 2);   // CMAX: chunk maxima are H << CSH
     static_assert(!CMAX || (T16 && LOCAL && R % 2 == 0), "CMAX: T16 Smith-Waterman / LocalGotoh");
 
@@ -265,6 +283,9 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
 #ifdef SA_TB_STATS
     const unsigned long long st_t0 = __builtin_amdgcn_s_memrealtime();
     unsigned long long st_wait = 0;
+    // s_getreg HW_REG_HW_ID (4) and HW_REG_XCC_ID (20), all 32 bits
+    const uint32_t st_hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const uint32_t st_xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
 #endif
     const uint64_t o1 = P.off1[pidx];
     const uint64_t o2 = P.off2[pidx];
@@ -376,7 +397,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     // which also applies the zero clamp of the cell: max(D, max(U, 0), L) == max(D, U, L, 0).
     const uint32_t CU = SO ? ((uint32_t)(-G) & 0xffffu)
                        : LOCAL ? ((uint32_t)(-(4 * G + 2)) & 0xffffu) : (uint32_t)(4 * G + 2);
-    const uint32_t CL = SO ? ((uint32_t)G & 0xffffu) : (uint32_t)(4 * G + 1);
+    const uint32_t CL = SO ? ((uint32_t)G & 0xffffu) : (uint32_t)(4 * G + 1);   // (SO NW: the shared gap term)
     // T16 affine: class / extend tagged gap terms (u16 arithmetic, sa_fill_impl.h header).  The
     // LocalGotoh Ix open term is max(Mu + 8GOE + 4, 0) = Mu - CXO with unsigned saturation (Mu >= 0,
     // CXO = -(8GOE + 4) > 0 since t16_mode demands GOE < 0).
@@ -692,6 +713,30 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                             asm("v_max3_u32 %0, %0, %1, %2" : "+v"(cml) : "v"(Hp[r >= 1 ? r - 1 : 0]), "v"(Hp[r]));
                     }
                     xu = (int)xs;
+                    Hc = Hp[r];
+                } else if constexpr (SO && ALG == SA_NW) {
+                    // Score-only NW cell (Hp = H - delta, no tags, no clamp): both gap candidates
+                    // share G, so max(U + G, L + G) = max(U, L) + G; the cell is max(D, that), the
+                    // next row's diagonal Hp_old + s from the profile (SANeedlemanWunsch.h:69-86)
+                    uint32_t t1;
+                    if (r + 1 < R) {
+                        uint32_t dn;
+                        const uint32_t tabn = (uint32_t)a[r + 1 < R ? r + 1 : r];
+                        asm("v_max_i16 %[t1], %[hu], %[hp]\n\t"
+                            "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\t"
+                            "v_add_u16 %[dn], %[hp], %[dn]\n\t"
+                            "v_add_u16 %[t1], %[cg], %[t1]\n\t"
+                            "v_max_i16 %[hp], %[dr], %[t1]"
+                            : [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r])
+                            : [dr] "v"(dcur), [hu] "v"(hu), [cg] "s"(CL), [tabn] "v"(tabn), [sym] "v"(sym));
+                        dcur = dn;
+                    } else {
+                        asm("v_max_i16 %[t1], %[hu], %[hp]\n\t"
+                            "v_add_u16 %[t1], %[cg], %[t1]\n\t"
+                            "v_max_i16 %[hp], %[dr], %[t1]"
+                            : [t1] "=&v"(t1), [hp] "+v"(Hp[r])
+                            : [dr] "v"(dcur), [hu] "v"(hu), [cg] "s"(CL));
+                    }
                     Hc = Hp[r];
                 } else if constexpr (SO) {
                     // Score-only cell (Hp = H, no tags): left = Hp + G, the next row's diagonal
@@ -1112,7 +1157,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                         const int row = row0 + r;
                         // CMAX: rows past m get substitution -128 (with gap < 0 their values stay
                         // below the matrix maximum, so they never win the lane's chunk maximum)
-                        if constexpr (SO) a[r] = row < m ? (int)so_profile(P.prof[t16_code8(symp, s1[row]) >> 3]) : (int)0x80808080u;
+                        if constexpr (SO) a[r] = row < m ? (int)so_profile(P.prof[t16_code8(symp, s1[row]) >> 3]) : (CMAX ? (int)0x80808080u : 0);
                         else if constexpr (T16) a[r] = row < m ? (int)P.prof[t16_code8(symp, s1[row]) >> 3] : (CMAX ? (int)0x80808080u : 0);
                         else a[r] = row < m ? (int)s1[row] : 0;
                         const int i = row + 1;
@@ -1213,19 +1258,21 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                     }
                 }
                 // ------------------------------------------------ CMAX: chunk maxima, snapshot
-                if constexpr (CMAX) {
-                    // (start mode: a lane that has not reached its first column holds garbage)
-                    if (kC + kChunk - 1 < lane) cml = 0;
-                    const uint32_t ck = chunk + 1;
+                if constexpr (SNAP) {
                     const uint64_t e = (uint64_t)band * P.snap_nch + chunk;
-                    if constexpr (SO) {
+                    if constexpr (!CMAX) {
+                        // (SO NW: snapshots only)
+                    } else if constexpr (SO) {
                         // per (band, chunk, lane): the lane's maximum of its tracked cells -- the
                         // end-cell replay then recomputes only the lane blocks that may hold S
+                        if (kC + kChunk - 1 < lane) cml = 0;   // (a lane that has not reached its first column)
                         P.snap_m[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = (int32_t)cml;
                         smax = max(smax, cml);   // (per lane; reduced over the wave at the end)
                     } else {
+                        // (start mode: a lane that has not reached its first column holds garbage)
+                        if (kC + kChunk - 1 < lane) cml = 0;
                         P.snap_m[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = (int32_t)cml;
-                        lkey = max(lkey, (cml >> CSH) << 12 | ck);
+                        lkey = max(lkey, (cml >> CSH) << 12 | (chunk + 1));
                     }
                     cml = 0;
                     if (chunk + 1 < nch) {   // state entering chunk + 1, for the end-cell replay
@@ -1315,6 +1362,13 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
 #endif
         }
     } else if constexpr (LOCAL) {
+#ifdef SA_TB_STATS
+        if (threadIdx.x == 0 && slot < 32768) {
+            g_fill_stats[slot][0] = st_t0;
+            g_fill_stats[slot][1] = __builtin_amdgcn_s_memrealtime();
+            g_fill_stats[slot][2] = (unsigned long long)st_hwid | ((unsigned long long)st_xcc << 32);
+        }
+#endif
         if constexpr (SO) {
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, off));
@@ -1384,16 +1438,17 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
 // The score-only kernel (one wave per workgroup): 4 waves per SIMD.  Its cell needs no record
 // registers, and the fourth wave hides the cell's dependent 16-bit chain (tools/microbench_so.hip:
 // 8,054 vs 7,520 GCUPS-equivalent at 4 vs 3 waves per SIMD).
-template <int R>
+template <int ALG, int R>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void fill_so_kernel(FillParams P) {
-    fill_body<SA_SW, R, kMatchEq, true, true, true, true, false, true>(P);
+    if constexpr (ALG == SA_SW) fill_body<SA_SW, R, kMatchEq, true, true, true, true, false, true>(P);
+    else fill_body<SA_NW, R, kMatchEq, true, false, true, false, false, true>(P);
 }
 
 template <int ALG>
 hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream) {
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
     const int R = v.R;
-    if (v.so && (ALG != SA_SW || !v.t16 || !v.cmax || v.split)) return hipErrorInvalidValue;
+    if (v.so && (!v.t16 || v.split || !((ALG == SA_SW && v.cmax) || (ALG == SA_NW && !v.cmax)))) return hipErrorInvalidValue;
     const bool lut = (v.t16 || v.bits) ? false : v.lut, allow = v.allow;
     const bool keyed = LOCAL && v.keyed;
     // SPLIT: the compute wave + its poller and publisher waves (see kHandGran); LDS for one
@@ -1410,9 +1465,9 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
                 return hipErrorInvalidConfiguration;
 #define SA_LAUNCH16S(RR, SP)                                                                         \
     if (R == RR && split == SP) {                                                                    \
-        if constexpr (ALG == SA_SW && !SP && RR <= 32) {                                              \
-            if (v.cmax && v.so) {                                                                    \
-                hipLaunchKernelGGL((fill_so_kernel<RR>), dim3(grid), block, lds, stream, p);            \
+        if constexpr ((ALG == SA_SW || ALG == SA_NW) && !SP && RR <= 32) {                            \
+            if (v.so) {                                                                              \
+                hipLaunchKernelGGL((fill_so_kernel<ALG, RR>), dim3(grid), block, lds, stream, p);       \
                 return hipGetLastError();                                                            \
             }                                                                                        \
         }                                                                                            \

@@ -6,4 +6,5 @@ hipError_t launch_fill_sw(const FillVariant& v, const FillParams& p, uint32_t gr
     return launch_fill_alg<SA_SW>(v, p, grid, s);
 }
 SA_SPLIT_STATS_ACCESSOR(sa_debug_split_stats_sw)
+SA_FILL_STATS_ACCESSOR(sa_debug_fill_stats_sw)
 }  // namespace sa

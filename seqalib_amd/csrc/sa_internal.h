@@ -166,6 +166,7 @@ struct TbParams {
     uint64_t snap_h_slot, snap_p_slot;
     uint32_t snap_nch;
     const uint32_t* prof;
+    int32_t t16_delta;         // score-only NW: the fill's values are H - t16_delta (the borders)
 };
 // SA_FLAG_TIMEOUT: a SPLIT band's bounded wait for its producer expired (results invalid)
 
@@ -241,8 +242,8 @@ hipError_t launch_traceback(int algo, int R, bool lut, const TbParams& p, hipStr
 // One wave per pair (sa_traceback_wave.hip): the few-pairs traceback.
 hipError_t launch_traceback_wave(int algo, int R, bool lut, const TbParams& p, hipStream_t stream);
 hipError_t launch_endcell(int algo, int R, const EndcellParams& p, hipStream_t stream);
-// Score-only SW fills: the block-recompute traceback (sa_traceback_so.hip), R in {4, 8, 16, 32}.
-hipError_t launch_traceback_so(int R, const TbParams& p, hipStream_t stream);
+// Score-only SW / NW fills: the block-recompute traceback (sa_traceback_so.hip), R in {4, 8, 16, 32}.
+hipError_t launch_traceback_so(int algo, int R, const TbParams& p, hipStream_t stream);
 // Score-only SW fills: the end cell from the per-(band, chunk) maxima of the tracked cells.
 hipError_t launch_endcell_so(int R, const EndcellParams& p, hipStream_t stream);
 }  // namespace sa

@@ -394,8 +394,12 @@ struct So4Lds {
     static constexpr int kBytes = kColC + kPairs * 32;
 };
 
-template <int R, int LP>
+// ALG: SA_SW (SASmithWaterman.h:220-339, from the end cell, stops at H == 0) or SA_NW
+// (SANeedlemanWunsch.h:155-231: from (m, n) to (0, 0); the recompute's borders are the NW borders
+// i * Gap / j * Gap, the fill's values H - t16_delta, and the cell has no zero clamp).
+template <int ALG, int R, int LP>
 __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
+    constexpr bool NWK = ALG == SA_NW;
     using L = So4Lds<R, LP>;
     constexpr int RS = R / LP;   // rows per sublane
     constexpr int BAND = kWave * R;
@@ -441,8 +445,13 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         }
     const bool allow = P.allow != 0;
     const int G = P.gap, MA = P.match, MI = P.mismatch;
-    const uint32_t CU = (uint32_t)(-(4 * G + 2)) & 0xffffu;
+    // up term: SW max(4U + 2, 0) by unsigned saturation, NW 4U + 2 (no clamp)
+    const uint32_t CU = (uint32_t)(NWK ? 4 * G + 2 : -(4 * G + 2)) & 0xffffu;
     const uint32_t CL = (uint32_t)(4 * G + 1) & 0xffffu;
+    const int D0 = P.t16_delta;
+    auto border = [&](int x) __attribute__((always_inline)) -> int {   // NW: 4 (H - delta) of a border cell x * Gap
+        return 4 * (x * G - D0);
+    };
 
     uint32_t k = 0;
     auto emit = [&](uint8_t op) __attribute__((always_inline)) {
@@ -530,6 +539,17 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         for (int r = 0; r < RS; ++r) { Hp[r] = 0; tab[r] = pf0; }
         if (act) {
             const int rs0 = sub * RS;   // block-relative first row
+            if constexpr (NWK) {
+                // NW borders (SANeedlemanWunsch.h:59-62): the left column j0 <= 0 is column 0 (row i
+                // holds i * Gap), the corner of a first row r0 = 0 is H(0, j0) = j0 * Gap
+                if (!has_left) {
+#pragma unroll
+                    for (int r = 0; r < RS; ++r) Hp[r] = border(r0 + rs0 + r + 1);
+                    corner = border(r0 + rs0);
+                } else if (rs0 == 0 && r0 == 0) {
+                    corner = border(j0);
+                }
+            }
             if (has_left) {
                 const uint64_t e = (uint64_t)cb * snap_nch + (cc - 1);
                 const uint32_t* sh = sh_base + e * (R / 2) * kWave + ct;
@@ -579,18 +599,19 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
             return act && q >= qlo && q <= qhi ? (uint32_t)vb[L::kColC + quad * 32 + q] : 0u;
         };
         auto rd_top = [&](int q) __attribute__((always_inline)) -> int {
-            if (sub != 0 || !act || !has_top || q < qlo || q > qhi) return 0;
+            if (sub != 0 || !act || q < qlo || q > qhi) return 0;
+            if (!has_top) return NWK ? border(j0 + q + 1) : 0;   // row 0: H(0, j) = j * Gap (NW), 0 (SW)
             const int s = slo + q;
             const int d = (s >> 3) - pk0;
             const int off = (LP >= 5 || d < 4) ? L::kEdge + (quad * LP + d) * 16 : L::kEdge2 + quad * 64;
-            return (int)((lds_u16*)(s_so + off + (s & 7) * 2))[0];   // (x 4 at the use: no wait here)
+            return (int)((lds_u16*)(s_so + off + (s & 7) * 2))[0] << 2;
         };
         uint32_t nsym = rd_sym(qlo - sub);
         int ntop = rd_top(qlo);
         for (int u = 0; u < nmax; ++u) {
             const int q = qlo + u - sub;
             const uint32_t sym = nsym;
-            const int top = ntop << 2;
+            const int top = ntop;
             nsym = rd_sym(q + 1);
             ntop = rd_top(q + 1);
             // the row above from sublane k-1: quad_perm [0,0,1,2] (LP = 4) / row_shr:1 (LP = 8; the
@@ -606,17 +627,20 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
 #pragma unroll
                 for (int r = 0; r < RS; ++r) {
                     uint32_t a0, a1, adn;
-                    asm("v_add_u16 %[a0], %[cl], %[hp]\n\t"
-                        "v_bfe_i32 %[adn], %[tabn], %[sym], 8\n\t"
-                        "v_add_u16 %[adn], %[hp], %[adn]\n\t"
-                        "v_sub_u16_e64 %[a1], %[hu], %[cu] clamp\n\t"
-                        "v_max_i16 %[a0], %[dr], %[a0]\n\t"
-                        "v_max_i16 %[a0], %[a1], %[a0]\n\t"
-                        "v_and_b32 %[hp], -4, %[a0]\n\t"
-                        "v_alignbit_b32 %[rec], %[a0], %[rec], 2"
-                        : [a0] "=&v"(a0), [a1] "=&v"(a1), [adn] "=&v"(adn), [hp] "+v"(Hp[r]), [rec] "+v"(rec)
-                        : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL),
-                          [tabn] "v"(tab[r + 1 < RS ? r + 1 : r]), [sym] "v"(sym));
+#define SO4_CELL(UP)                                                                               \
+    asm("v_add_u16 %[a0], %[cl], %[hp]\n\t"                                                         \
+        "v_bfe_i32 %[adn], %[tabn], %[sym], 8\n\t"                                                  \
+        "v_add_u16 %[adn], %[hp], %[adn]\n\t" UP                                                   \
+        "v_max_i16 %[a0], %[dr], %[a0]\n\t"                                                         \
+        "v_max_i16 %[a0], %[a1], %[a0]\n\t"                                                         \
+        "v_and_b32 %[hp], -4, %[a0]\n\t"                                                            \
+        "v_alignbit_b32 %[rec], %[a0], %[rec], 2"                                                  \
+        : [a0] "=&v"(a0), [a1] "=&v"(a1), [adn] "=&v"(adn), [hp] "+v"(Hp[r]), [rec] "+v"(rec)       \
+        : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL),                                 \
+          [tabn] "v"(tab[r + 1 < RS ? r + 1 : r]), [sym] "v"(sym))
+                    if constexpr (NWK) SO4_CELL("v_add_u16 %[a1], %[cu], %[hu]\n\t");
+                    else SO4_CELL("v_sub_u16_e64 %[a1], %[hu], %[cu] clamp\n\t");
+#undef SO4_CELL
                     dcur = adn;
                     hu = (uint32_t)Hp[r];
                 }
@@ -640,7 +664,7 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
     };
 
     int i = res.end_i, j = res.end_j, V = res.score;
-    if (m == 0 || n == 0) { i = 0; j = 0; }
+    if (!NWK && (m == 0 || n == 0)) { i = 0; j = 0; }
     bool fin = !live, parked = true;
     // One move per iteration, branch-free (a lone wave pays for every divergent branch): every lane
     // evaluates the move of its cell and applies it only when it may (mv).  A move lands in the
@@ -661,7 +685,8 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         // (cr, cq): the cell's row and column in the block, kept by the moves (recompute locates
         // the entry cell); a move that takes either below 0 has left the block
         const bool act = !fin && !parked;
-        const bool stop = !(i > 0 && j > 0) || V == 0;   // SASmithWaterman.h: an edge or H == 0
+        // SASmithWaterman.h: an edge or H == 0; NW: the walk leaves the interior (border moves below)
+        const bool stop = !(i > 0 && j > 0) || (!NWK && V == 0);
         const bool inb = cr >= 0 && cq >= 0;
         const bool mv = act && !stop && inb;
         fin = fin || (act && stop);
@@ -701,6 +726,14 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
     }
     if (live && sub == 0) atomicAdd(&g_so4_stats[2], (unsigned long long)k);
 #endif
+    if constexpr (NWK) {
+        // on the border the reference moves up while i > 0 (H[i][0] == H[i-1][0] + Gap), then left
+        // (SANeedlemanWunsch.h:216-229)
+        if (live) {
+            for (; i > 0; --i) emit('U');
+            for (; j > 0; --j) emit('L');
+        }
+    }
     if (live) {
         if (sub == 0) {
             res.start_i = i;
@@ -712,10 +745,32 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
 }
 
 // SEQALIB_TB_SO=1: one lane per pair (traceback_so_kernel); default four lanes per pair.
-hipError_t launch_traceback_so(int R, const TbParams& p, hipStream_t stream) {
+template <int ALG>
+hipError_t launch_so4(int R, int lp, dim3 grid, dim3 block, const TbParams& p, hipStream_t stream) {
+    if (lp == 8) {
+        switch (R) {
+            case 8: hipLaunchKernelGGL((traceback_so4_kernel<ALG, 8, 8>), grid, block, 0, stream, p); break;
+            case 16: hipLaunchKernelGGL((traceback_so4_kernel<ALG, 16, 8>), grid, block, 0, stream, p); break;
+            case 32: hipLaunchKernelGGL((traceback_so4_kernel<ALG, 32, 8>), grid, block, 0, stream, p); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    switch (R) {
+        case 4: hipLaunchKernelGGL((traceback_so4_kernel<ALG, 4, 4>), grid, block, 0, stream, p); break;
+        case 8: hipLaunchKernelGGL((traceback_so4_kernel<ALG, 8, 4>), grid, block, 0, stream, p); break;
+        case 16: hipLaunchKernelGGL((traceback_so4_kernel<ALG, 16, 4>), grid, block, 0, stream, p); break;
+        case 32: hipLaunchKernelGGL((traceback_so4_kernel<ALG, 32, 4>), grid, block, 0, stream, p); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_traceback_so(int algo, int R, const TbParams& p, hipStream_t stream) {
     const dim3 block(64);
+    if (algo != SA_SW && algo != SA_NW) return hipErrorInvalidValue;
     const char* e = getenv("SEQALIB_TB_SO");
-    if (e && e[0] == '1') {
+    if (algo == SA_SW && e && e[0] == '1') {   // (the one-lane walker is SW only)
         const dim3 grid((p.count + 63) / 64);
         switch (R) {
             case 4: hipLaunchKernelGGL(traceback_so_kernel<4>, grid, block, 0, stream, p); break;
@@ -731,23 +786,7 @@ hipError_t launch_traceback_so(int R, const TbParams& p, hipStream_t stream) {
     if (const char* l = getenv("SEQALIB_TB_LP")) lp = (atoi(l) == 8 && R >= 8) ? 8 : 4;
     const uint32_t ppw = (uint32_t)(kWave / lp);
     const dim3 grid((p.count + ppw - 1) / ppw);
-    if (lp == 8) {
-        switch (R) {
-            case 8: hipLaunchKernelGGL((traceback_so4_kernel<8, 8>), grid, block, 0, stream, p); break;
-            case 16: hipLaunchKernelGGL((traceback_so4_kernel<16, 8>), grid, block, 0, stream, p); break;
-            case 32: hipLaunchKernelGGL((traceback_so4_kernel<32, 8>), grid, block, 0, stream, p); break;
-            default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
-    switch (R) {
-        case 4: hipLaunchKernelGGL((traceback_so4_kernel<4, 4>), grid, block, 0, stream, p); break;
-        case 8: hipLaunchKernelGGL((traceback_so4_kernel<8, 4>), grid, block, 0, stream, p); break;
-        case 16: hipLaunchKernelGGL((traceback_so4_kernel<16, 4>), grid, block, 0, stream, p); break;
-        case 32: hipLaunchKernelGGL((traceback_so4_kernel<32, 4>), grid, block, 0, stream, p); break;
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
+    return algo == SA_SW ? launch_so4<SA_SW>(R, lp, grid, block, p, stream) : launch_so4<SA_NW>(R, lp, grid, block, p, stream);
 }
 
 }  // namespace sa

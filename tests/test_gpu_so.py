@@ -25,14 +25,14 @@ THREADS = 16
 FIELDS = ("score", "end_i", "end_j", "start_i", "start_j", "nops", "flags")
 
 
-def run(engine, so, *batch, scoring=SW, lut=None, tb="4"):
+def run(engine, so, *batch, scoring=SW, lut=None, tb="4", algo=0):
     """so: score-only fill (else SEQALIB_SO=0, tagged records); tb: SEQALIB_TB_SO, the score-only
     traceback with four lanes per pair ("4", default) or one ("1")."""
     old = {k: os.environ.get(k) for k in ("SEQALIB_SO", "SEQALIB_TB_SO")}
     os.environ["SEQALIB_SO"] = "1" if so else "0"
     os.environ["SEQALIB_TB_SO"] = tb
     try:
-        res, ops = engine.align_packed(0, sa.ScoringSystem(*scoring), *batch, lut=lut)
+        res, ops = engine.align_packed(algo, sa.ScoringSystem(*scoring), *batch, lut=lut)
         plan = engine.last_plan()
     finally:
         for k, v in old.items():
@@ -166,4 +166,82 @@ def test_headline_batch_every_pair(engine):
         assert (int(res["start_i"][p]), int(res["start_j"][p])) == (int(ores["start_i"][q]), int(ores["start_j"][q]))
         assert ops[off:off + int(res["nops"][p])].tobytes() == oops[ooff:ooff + int(ores["nops"][q])].tobytes(), int(p)
     tg = run(engine, False, s1, o1, s2, o2)
+    assert_same(so, tg, o1, o2)
+
+
+NW = (-1, 2, -1)   # NeedlemanWunschSA::getDefaultScoring (SANeedlemanWunsch.h:244-247)
+
+
+def check_vs_oracle(algo, scoring, got, batch, idx, lut=None):
+    """Full results and op streams of pairs idx against the full-matrix oracle."""
+    s1, o1, s2, o2 = batch
+    res, ops = got[0], got[1]
+    for p in idx:
+        a, b = s1[o1[p]:o1[p + 1]].tobytes(), s2[o2[p]:o2[p + 1]].tobytes()
+        o = oracle_align(algo, scoring, a, b, lut=lut)
+        off = int(o1[p] + o2[p]) + int(p)
+        g = (int(res["score"][p]), int(res["end_i"][p]), int(res["end_j"][p]), int(res["start_i"][p]),
+             int(res["start_j"][p]), ops[off:off + int(res["nops"][p])].tobytes())
+        assert g == (o["score"], o["end_i"], o["end_j"], o["start_i"], o["start_j"], o["ops"]), (scoring, int(p))
+
+
+@pytest.mark.parametrize("maxlen,R", [(200, 4), (500, 8), (1000, 16), (2000, 32), (3000, 32)])
+def test_so_nw_ragged_matches_tagged_and_oracle(engine, maxlen, R):
+    """Score-only NeedlemanWunsch (no records; the walk from (m, n) recomputes its blocks with the NW
+    borders i * Gap / j * Gap and the fill's offset delta, then follows the border to (0, 0)):
+    ragged batches on every plan, identical to the tagged path on every pair, a sample (and every
+    edge shape, empty sides included) against the full-matrix oracle."""
+    batch = ragged_batch(80 + maxlen, 1100, maxlen)
+    so = run(engine, True, *batch, scoring=NW, algo=1)
+    recs = engine.last_plan_ex()[3]
+    tg = run(engine, False, *batch, scoring=NW, algo=1)
+    assert so[2] == (sa.SA_KERNEL_T16, R, 1) and tg[2] == so[2]
+    assert recs == sa.SA_RECORDS_SCORE_ONLY
+    s1, o1, s2, o2 = batch
+    assert (so[0]["flags"] == 0).all()
+    assert_same(so, tg, o1, o2)
+    assert (linear_rescore(NW, so[0], so[1], o1, o2) == so[0]["score"]).all()
+    idx = np.unique(np.concatenate([np.arange(11), np.random.default_rng(maxlen).choice(len(o1) - 1, 40, replace=False)]))
+    check_vs_oracle(1, NW, so, batch, idx)
+
+
+def test_so_nw_scorings_and_lut(engine):
+    """Score-only NW with other scorings -- the reference's 2-argument (Gap, Match) form
+    (!AllowMismatch, test/Test.cpp's (-1, 2)), (-2, 1, -1, false), (-2, 2, -3) -- and a non-identity
+    match table: identical to the tagged path, a sample against the oracle."""
+    batch = ragged_batch(9, 1030, 700)
+    lut = np.zeros((256, 256), np.uint8)
+    for x in b"ACGT":
+        lut[x, x] = 1
+    for x, y in (b"AG", b"GA", b"CT", b"TC"):
+        lut[x, y] = 1
+    for scoring, lt in (((-1, 2), None), ((-2, 1, -1, False), None), ((-2, 2, -3), None), (NW, lut)):
+        so = run(engine, True, *batch, scoring=scoring, lut=lt, algo=1)
+        assert engine.last_plan_ex()[3] == sa.SA_RECORDS_SCORE_ONLY, scoring
+        tg = run(engine, False, *batch, scoring=scoring, lut=lt, algo=1)
+        assert_same(so, tg, batch[1], batch[3])
+        check_vs_oracle(1, scoring, so, batch, [0, 1, 2, 3, 4, 5, 11, 12, 13, 14, 15, 1029], lut=lt)
+
+
+def test_so_nw_batch_1024_every_pair(engine):
+    """10,000 x 1024^2 NeedlemanWunsch (-1, 2, -1), the configs leg of bench.py: every pair's score
+    re-scored from its op stream and consuming all of both sequences, 128 pairs against the oracle,
+    every pair identical to the tagged path."""
+    s1, o1, s2, o2 = sa.synth_dna_batch(6_000_000_000, 10000, 1024, 1024, threads=THREADS)
+    so = run(engine, True, s1, o1, s2, o2, scoring=NW, algo=1)
+    assert so[2] == (sa.SA_KERNEL_T16, 16, 1)
+    res, ops = so[0], so[1]
+    assert (res["flags"] == 0).all()
+    assert (linear_rescore(NW, res, ops, o1, o2) == res["score"]).all()
+    assert (res["start_i"] == 0).all() and (res["start_j"] == 0).all()
+    assert (res["end_i"] == 1024).all() and (res["end_j"] == 1024).all()
+    jdx = np.sort(np.random.default_rng(6).choice(10000, 128, replace=False))
+    sub = subset(s1, o1, s2, o2, jdx)
+    ores, oops = oracle_batch(1, NW, *sub, threads=THREADS)
+    for q, p in enumerate(jdx):
+        off = int(o1[p] + o2[p]) + int(p)
+        ooff = int(sub[1][q] + sub[3][q]) + q
+        assert int(res["score"][p]) == int(ores["score"][q]), int(p)
+        assert ops[off:off + int(res["nops"][p])].tobytes() == oops[ooff:ooff + int(ores["nops"][q])].tobytes(), int(p)
+    tg = run(engine, False, s1, o1, s2, o2, scoring=NW, algo=1)
     assert_same(so, tg, o1, o2)
