@@ -71,7 +71,7 @@ def parse():
                     help="run steps back to back without overlapping step k's traceback with step k+1's fill")
     ap.add_argument("--serial-steps", type=int, default=3,
                     help="after the timed run, also time this many non-pipelined steps (reported, not the value)")
-    ap.add_argument("--configs", default="2,3,4,5",
+    ap.add_argument("--configs", default="2,3,4,5,nw,lg,gg",
                     help="BASELINE.json configs measured after the headline (tools/bench_configs.py); '' = none")
     ap.add_argument("--parity-ops", type=int, default=16,
                     help="headline parity: full op streams checked against the full-matrix oracle "
@@ -243,6 +243,22 @@ def dropin_e2e(args):
         return {"error": str(e)[:200]}
 
 
+def small_call_phases(stderr: str):
+    """Host phases of the library's small-call path from its SEQALIB_HOST_TIMING lines
+    ("... small-call kernel: T us = pinned buffer A + staging in B + launch C + kernel and sync D +
+    copies out E"): the first call's, and the medians of the others."""
+    import re
+    names = ("total", "pinned_buffer", "staging_in", "launch", "kernel_and_sync", "copies_out")
+    pat = re.compile(r"small-call kernel: ([\d.]+) us = pinned buffer ([\d.]+) \+ staging in ([\d.]+) \+ "
+                     r"launch ([\d.]+) \+ kernel and sync ([\d.]+) \+ copies out ([\d.]+)")
+    rows = [tuple(float(x) for x in m.groups()) for m in pat.finditer(stderr)]
+    if not rows:
+        return None
+    rest = rows[1:] or rows
+    med = [sorted(r[k] for r in rest)[len(rest) // 2] for k in range(len(names))]
+    return {"first_call": dict(zip(names, rows[0])), "median": dict(zip(names, med)), "calls": len(rows)}
+
+
 def dropin_latency(args):
     """Single-call latency of the C++ drop-in (tests/cpp/dropin_latency: getAlignment per call on
     test/Test.cpp's 11 x 8 NW pair and on one 1024^2 SW pair), beside the reference's own per-call
@@ -256,6 +272,11 @@ def dropin_latency(args):
         out = subprocess.run([exe, str(args.latency_reps)], capture_output=True, text=True, timeout=300,
                              check=True).stdout
         d = json.loads(out.strip().splitlines()[-1])
+        # host phases of the small call (a second run: printing them costs time per call)
+        env = dict(os.environ, SEQALIB_HOST_TIMING="1")
+        err = subprocess.run([exe, "100", "nw"], capture_output=True, text=True, timeout=300, check=True,
+                             env=env).stderr
+        d["nw_11x8"]["host_phases_us"] = small_call_phases(err)
     except Exception as e:   # reported, never fatal for the bench line
         return {"error": str(e)[:200]}
     ref = os.path.join(ROOT, "oracle", "_ref", "libsaref.so")

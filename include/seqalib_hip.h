@@ -209,6 +209,11 @@ int sa_last_kernel_timings(sa_ctx* ctx, float* fill_kernel_ms, float* fill_strea
 #define SA_KERNEL_INT32 0
 #define SA_KERNEL_T16 1
 #define SA_KERNEL_T16_ENDCELL 2   /* T16 SW / LocalGotoh with per-chunk maxima + end-cell replay */
+/* Host-buffer calls of at most 64 pairs with m <= 256, n <= 1024, m * n <= 32768 (SW / NW /
+ * LocalGotoh / GlobalGotoh): one kernel fills and walks each pair in one wave (int32 cells, flags
+ * in LDS), reading and writing pinned host memory.  Such a call reports 0 fill launches to
+ * sa_last_timings.  Environment: SEQALIB_TINY=0 sends them through the batch kernels. */
+#define SA_KERNEL_TINY 3
 int sa_last_plan(sa_ctx* ctx, int* kernel, int* rows_per_lane, int* waves);
 /* sa_last_plan plus what the fill stored for the traceback: SA_RECORDS_FLAGS (int32 equality
  * flags), SA_RECORDS_TAGS (T16 move tags per cell) or SA_RECORDS_SCORE_ONLY (score-only T16 SW fill:

@@ -37,7 +37,7 @@ SA_SW, SA_NW, SA_LOCAL_GOTOH, SA_GLOBAL_GOTOH, SA_HIRSCHBERG, SA_MYERS_MILLER = 
 ALGO_NAMES = {SA_SW: "sw", SA_NW: "nw", SA_LOCAL_GOTOH: "local_gotoh", SA_GLOBAL_GOTOH: "global_gotoh",
               SA_HIRSCHBERG: "hirschberg", SA_MYERS_MILLER: "myers_miller"}
 SA_FLAG_DIVERGED, SA_FLAG_BAD_SHAPE, SA_FLAG_SIZE_HACK, SA_FLAG_TIMEOUT = 1, 2, 4, 8
-SA_KERNEL_INT32, SA_KERNEL_T16, SA_KERNEL_T16_ENDCELL = 0, 1, 2
+SA_KERNEL_INT32, SA_KERNEL_T16, SA_KERNEL_T16_ENDCELL, SA_KERNEL_TINY = 0, 1, 2, 3
 SA_RECORDS_FLAGS, SA_RECORDS_TAGS, SA_RECORDS_SCORE_ONLY = 0, 1, 2
 INT32_MIN = -(2 ** 31)
 

@@ -57,6 +57,7 @@ struct sa_ctx {
     // cross-call pipeline of the device API (sa_set_pipeline): fills on s_fill, tracebacks on
     // s_tb, two workspace slots; ev_slot[k] = traceback of the last call that used slot k done
     int pipeline = 0;
+    uint32_t fill_epoch = 0;   // score-only fills: per-launch tag of their hand-off granules
     hipStream_t s_fill = nullptr, s_tb = nullptr;
     hipEvent_t ev_in = nullptr, ev_slot[2] = {nullptr, nullptr};
     uint64_t pipe_k = 0;
@@ -66,6 +67,10 @@ struct sa_ctx {
     // HirschbergSA / MyersMillerSA level-loop buffers and the host API's pinned upload staging
     sa::DcWork dc;
     sa::HostBuf<uint8_t> stage, ostage;
+    // the small-call path (align_tiny): coherent pinned inputs and outputs the kernel reads and
+    // writes in place (host pointer, device pointer)
+    uint8_t* tiny_io = nullptr;
+    uint8_t* tiny_dev = nullptr;
     // host API: download stream and per-chunk events (align_host)
     hipStream_t s_out = nullptr;
     std::vector<hipEvent_t> host_ev;
@@ -207,6 +212,7 @@ struct Variant {
     bool so = false;   // score-only fill + block-recompute traceback (sa_traceback_so.hip)
     uint32_t snap_nch = 0;
     uint64_t snap_h_slot = 0, snap_p_slot = 0;   // 32-bit words per pair
+    uint64_t part_slot = 0;   // score-only band units: 64-bit per-band maxima per pair
     uint64_t slot_bytes = 0;
     int kernel = SA_KERNEL_INT32;
 };
@@ -225,20 +231,25 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
     // cell; NW (whose walk starts at (m, n)) from the plain T16 plan.  SEQALIB_SO=0 keeps the tagged
     // records (A/B, tests).
     const bool so_plan = !v.pl.split && v.pl.W == 1 && v.pl.R >= 4 && v.pl.R <= 32;
-    v.so = so_plan && ((algo == SA_SW && v.cmax) || (algo == SA_NW && t16));
+    const bool local = algo == SA_SW || algo == SA_LOCAL_GOTOH;
+    v.so = so_plan && t16 && (local ? v.cmax : true) && algo <= SA_GLOBAL_GOTOH;
     if (const char* e = getenv("SEQALIB_SO")) if (e[0] == '0') v.so = false;
     if (v.cmax || v.so) {
         v.snap_nch = chunks_per_band(max_n);
         v.snap_p_slot = (uint64_t)v.pl.g.bands * v.snap_nch * kWave;
         // per lane: R 16-bit values (LocalGotoh: M, then Iy, then the last row's Ix: R + 1 words)
         v.snap_h_slot = v.snap_p_slot * (is_affine(algo) ? v.pl.R + 1 : v.pl.R / 2);
-        // the end-cell replay reads every band's top row (the SO NW fill reuses one row)
-        if (v.cmax) v.pl.rowbuf_elems = (uint64_t)(is_affine(algo) ? 2 : 1) * v.pl.g.bands * std::max<uint32_t>(max_n, 1);
+        // every band's top row: the end-cell replay reads them, and the score-only fill's band units
+        // hand them over
+        v.pl.rowbuf_elems = (uint64_t)(is_affine(algo) ? 2 : 1) * v.pl.g.bands * std::max<uint32_t>(max_n, 1);
     }
-    if (v.so) v.pl.g = make_geom(algo, v.pl.R, max_m, max_n, kGeomEdge);
+    if (v.so) {
+        v.pl.g = make_geom(algo, v.pl.R, max_m, max_n, kGeomEdge);
+        v.part_slot = v.pl.g.bands;
+    }
     if (v.pl.split) v.pl.rowbuf_elems = 0;   // hand-off granules live in c->split
     v.kernel = v.cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
-    v.slot_bytes = v.pl.g.dir_slot + v.pl.rowbuf_elems * 4 + (v.snap_h_slot + 2 * v.snap_p_slot) * 4;
+    v.slot_bytes = v.pl.g.dir_slot + v.pl.rowbuf_elems * 4 + (v.snap_h_slot + 2 * v.snap_p_slot) * 4 + v.part_slot * 8;
     return v;
 }
 
@@ -723,14 +734,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     c->kvars.clear();
     c->timed_stream = stream;
     hipStream_t sf = stream, stb = stream;
-    // A/B (round 5): SEQALIB_FILL2=1 runs the fills of pipeline slot 1 on the context's own stream
-    // (idle in the device API), so call k+1's fill may start in call k's fill tail;
-    // SEQALIB_ENDCELL_TB=1 runs the end-cell replay on the traceback stream
-    const char* e_f2 = getenv("SEQALIB_FILL2");
-    const char* e_etb = getenv("SEQALIB_ENDCELL_TB");
-    const bool endcell_tb = pipe && e_etb && e_etb[0] == '1';
     if (pipe) {
-        sf = (slot == 1 && e_f2 && e_f2[0] == '1') ? c->stream : c->s_fill;
+        sf = c->s_fill;
         stb = c->s_tb;
         SA_HIP(c, hipEventRecord(c->ev_in, stream));
         SA_HIP(c, hipStreamWaitEvent(sf, c->ev_in, 0));
@@ -762,8 +767,6 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         const uint64_t hand_x_off = any_split ? (uint64_t)cnt * sp_bands * std::max<uint32_t>(max_n, 1) : 0;
         // fill parameters of variant k (k == nv: the SPLIT fallback)
         FillParams fps[3];
-        EndcellParams eps[3];
-        bool ep_set[3] = {false, false, false};
         // $SEQALIB_STAGE_SEQ2=0: read Seq2 from global memory in every plan (tests the unstaged
         // path that batches with max_n > kMaxStagedSeq2 take)
         const char* stage_env = getenv("SEQALIB_STAGE_SEQ2");
@@ -803,14 +806,18 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fp.retry_above = v.t16 ? tm.retry_above : INT_MAX;
             fp.t16_sent = v.t16 ? tm.sent : -10000;
             fp.snap_h = snap_h; fp.snap_p = snap_p; fp.snap_m = snap_p + per_launch * v.snap_p_slot;
+            if (v.so) {   // band units: launch epoch, per-band maxima (after the chunk maxima); ticket below
+                fp.epoch = ++c->fill_epoch;
+                fp.band_part = reinterpret_cast<unsigned long long*>(fp.snap_m + per_launch * v.snap_p_slot);
+                fp.part_bands = (uint32_t)v.part_slot;
+            }
             fp.snap_h_slot = v.snap_h_slot; fp.snap_p_slot = v.snap_p_slot; fp.snap_nch = v.snap_nch;
             fp.split_bands = (uint32_t)sp_bands;
-            fp.ticket = pl.split ? reinterpret_cast<uint32_t*>(vblk) : nullptr;
+            fp.ticket = pl.split ? reinterpret_cast<uint32_t*>(vblk) : v.so ? aux + kAuxTicket : nullptr;
             fp.hand = pl.split ? reinterpret_cast<unsigned long long*>(vblk + 256) : nullptr;
             fp.hand_x_off = pl.split ? hand_x_off : 0;
             fp.part = pl.split ? reinterpret_cast<int32_t*>(spbase + sp_part) : nullptr;
             fp.wait_ticks = wait_ticks;
-            fp.no_start = getenv("SEQALIB_NO_START") ? 1 : 0;
             FillVariant fv{pl.R, lut, allow || v.t16, keyed, v.t16, v.cmax, pl.split, bits};
             fv.so = v.so;
             return fv;
@@ -821,8 +828,13 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             const FillVariant fv = make_fp(k);
             const FillParams& fp = fps[k];
             if (pl.split) SA_HIP(c, hipMemsetAsync(fp.ticket, 0, 256 + hand_x_off * 8 * aff2, sf));
+            if (v.so && !is_affine(algo)) SA_HIP(c, hipMemsetAsync(fp.ticket, 0, 4, sf));
             if (kev) SA_HIP(c, hipEventRecord(kev[2 * k], sf));
-            hipError_t e = launch_fill(algo, fv, fp, pl.split ? (uint32_t)(cnt * sp_bands) : cnt, sf);
+            // grid: SPLIT one workgroup per (pair, band) slot; score-only SW / NW one per (pair,
+            // band) unit (band units, sa_fill_impl.h BU); otherwise one per pair
+            const bool units = v.so && !is_affine(algo);
+            const uint32_t grid = pl.split ? (uint32_t)(cnt * sp_bands) : units ? cnt * pl.g.bands : cnt;
+            hipError_t e = launch_fill(algo, fv, fp, grid, sf);
             if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
             if (kev) SA_HIP(c, hipEventRecord(kev[2 * k + 1], sf));
             if (pl.split) {
@@ -858,24 +870,14 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 ep.hshift = v.so ? 0 : 2;
                 ep.dirs = fp.dirs; ep.dir_slot = fp.dir_slot; ep.band_stride = fp.band_stride;
                 // on the fill stream, right after the fill: run beside the next call's fill (on the
-                // traceback stream) its 10,000 short waves slowed that fill by 4 % (measured)
-                if (endcell_tb) {
-                    eps[k] = ep;
-                    ep_set[k] = true;
-                    continue;
-                }
-                e = v.so ? launch_endcell_so(pl.R, ep, sf) : launch_endcell(algo, pl.R, ep, sf);
+                // traceback stream) its 10,000 short waves slowed that fill by 4 % in round 4, and
+                // the whole pipelined step by 12 % in round 5 (21.4 vs 19.1 ms per step)
+                e = (v.so && algo == SA_SW) ? launch_endcell_so(pl.R, ep, sf) : launch_endcell(algo, pl.R, ep, sf);
                 if (e != hipSuccess) return hip_fail(c, e, "end-cell kernel launch");
             }
         }
         SA_HIP(c, hipEventRecord(ev[1], sf));
         if (pipe) SA_HIP(c, hipStreamWaitEvent(stb, ev[1], 0));
-        for (int k = 0; k < nv; ++k) {
-            if (!ep_set[k]) continue;
-            const hipError_t e = vars[k].so ? launch_endcell_so(vars[k].pl.R, eps[k], stb)
-                                            : launch_endcell(algo, vars[k].pl.R, eps[k], stb);
-            if (e != hipSuccess) return hip_fail(c, e, "end-cell kernel launch");
-        }
         auto make_tp = [&](int k) {
             const Variant& v = vars[k];
             TbParams tp{};
@@ -897,6 +899,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             tp.snap_h_slot = v.snap_h_slot; tp.snap_p_slot = v.snap_p_slot; tp.snap_nch = v.snap_nch;
             tp.prof = fps[k].prof;
             tp.t16_delta = fps[k].t16_delta;
+            tp.t16_sent = fps[k].t16_sent;
             return tp;
         };
         for (int k = 0; k < nv; ++k) {
@@ -913,19 +916,6 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 SA_HIP(c, hipMemsetAsync(tp.seg_fin, 0xff, (uint64_t)cnt * 16, stb));
                 hipError_t e = launch_traceback_seg(algo, v.pl.R, lut, tp, stb, seg_inject);
                 if (e != hipSuccess) return hip_fail(c, e, "segmented traceback kernel launch");
-                if (const char* dump = getenv("SEQALIB_SEG_DUMP")) {   // debugging aid: exit records
-                    const uint64_t nrec = (uint64_t)cnt * sp_bands * seg_rs;
-                    std::vector<int4> h(nrec + cnt);
-                    SA_HIP(c, hipStreamSynchronize(stb));
-                    SA_HIP(c, hipMemcpy(h.data(), tp.seg_rec, nrec * 16, hipMemcpyDeviceToHost));
-                    SA_HIP(c, hipMemcpy(h.data() + nrec, tp.seg_fin, (uint64_t)cnt * 16, hipMemcpyDeviceToHost));
-                    if (FILE* f = fopen(dump, "wb")) {
-                        const uint64_t hdr[4] = {cnt, sp_bands, seg_rs, (uint64_t)v.pl.R};
-                        fwrite(hdr, 8, 4, f);
-                        fwrite(h.data(), 16, h.size(), f);
-                        fclose(f);
-                    }
-                }
             }
             hipError_t e = v.so ? launch_traceback_so(algo, v.pl.R, tp, stb)
                          : tb_wave(cnt) ? launch_traceback_wave(algo, v.pl.R, lut, tp, stb)
@@ -1155,6 +1145,113 @@ std::vector<uint32_t> cut_by_cells(const uint64_t* off1, const uint64_t* off2, u
     return cut;
 }
 
+// The small-call path (sa_tiny.hip): a host call of few short pairs -- the reference's one
+// getAlignment() per pair -- is one kernel launch and one stream synchronisation.  The inputs are
+// copied into coherent pinned memory the kernel reads in place, and the kernel writes the results
+// and op streams there (no device buffers, no copies, no workspace).  *max_m: the longest Seq1.
+bool tiny_call(int algo, const uint64_t* off1, const uint64_t* off2, uint32_t npairs, int* max_m) {
+    if (algo < SA_SW || algo > SA_GLOBAL_GOTOH || npairs == 0 || npairs > (uint32_t)kTinyPairs) return false;
+    if (const char* e = getenv("SEQALIB_TINY"))
+        if (e[0] == '0') return false;
+    uint64_t mm = 0;
+    for (uint32_t p = 0; p < npairs; ++p) {
+        const uint64_t m = off1[p + 1] - off1[p], n = off2[p + 1] - off2[p];
+        if (m > (uint64_t)kTinyM || n > (uint64_t)kTinyN || m * n > (uint64_t)kTinyCells) return false;
+        mm = std::max(mm, m);
+    }
+    *max_m = (int)mm;
+    return true;
+}
+
+// tiny_io: inputs [seq1][seq2][off1][off2][lut bits] from 0, outputs [results][ops] from kTinyOut
+constexpr uint64_t kTinyOut = 128ull << 10, kTinyIo = 256ull << 10;
+
+int align_tiny(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, const uint64_t* off1,
+               const uint8_t* seq2, const uint64_t* off2, uint32_t npairs, const uint8_t* lut,
+               sa_result* results, uint8_t* ops, int max_m) {
+    const bool timing = getenv("SEQALIB_HOST_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::micro>(b - a).count();
+    };
+    if (!c->tiny_io) {   // once per context
+        SA_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->tiny_io), kTinyIo, hipHostMallocCoherent));
+        void* dp = nullptr;
+        SA_HIP(c, hipHostGetDevicePointer(&dp, c->tiny_io, 0));
+        c->tiny_dev = static_cast<uint8_t*>(dp);
+    }
+    const auto t_alloc = std::chrono::steady_clock::now();
+    auto al = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
+    const uint64_t t1 = off1[npairs], t2 = off2[npairs];
+    const uint64_t b1 = al(t1 + 1), b2 = al(t2 + 1), bo = al(8ull * (npairs + 1));
+    const uint64_t x_s2 = b1, x_o1 = x_s2 + b2, x_o2 = x_o1 + bo, x_lut = x_o2 + bo;
+    static_assert((uint64_t)kTinyPairs * (kTinyM + kTinyN) + 4 * 256 + 2 * 8 * (kTinyPairs + 1) + 8192 <= kTinyOut,
+                  "tiny inputs overflow their region");
+    static_assert(kTinyOut + sizeof(sa_result) * kTinyPairs + (uint64_t)kTinyPairs * (kTinyM + kTinyN + 1) <= kTinyIo,
+                  "tiny outputs overflow their region");
+    uint8_t* const h = c->tiny_io;
+    memcpy(h, seq1, t1);
+    memcpy(h + x_s2, seq2, t2);
+    memcpy(h + x_o1, off1, 8ull * (npairs + 1));
+    memcpy(h + x_o2, off2, 8ull * (npairs + 1));
+    const bool use_lut = lut && !lut_identity_on(lut, seq1, t1, seq2, t2);
+    if (use_lut) {   // bit rows of the Seq1 symbols present (the kernel reads no other row)
+        uint32_t* bits = reinterpret_cast<uint32_t*>(h + x_lut);
+        bool u1[256] = {};
+        for (uint64_t k = 0; k < t1; ++k) u1[seq1[k]] = true;
+        for (int a = 0; a < 256; ++a) {
+            if (!u1[a]) continue;
+            for (int w = 0; w < 8; ++w) {
+                uint32_t word = 0;
+                for (int b = 0; b < 32; ++b) word |= (lut[a * 256 + w * 32 + b] ? 1u : 0u) << b;
+                bits[a * 8 + w] = word;
+            }
+        }
+    }
+    TinyParams tp;
+    tp.seq1 = c->tiny_dev;
+    tp.seq2 = c->tiny_dev + x_s2;
+    tp.off1 = reinterpret_cast<const uint64_t*>(c->tiny_dev + x_o1);
+    tp.off2 = reinterpret_cast<const uint64_t*>(c->tiny_dev + x_o2);
+    tp.lutbits = use_lut ? reinterpret_cast<const uint32_t*>(c->tiny_dev + x_lut) : nullptr;
+    tp.res = reinterpret_cast<sa_result*>(c->tiny_dev + kTinyOut);
+    tp.ops = c->tiny_dev + kTinyOut + al(sizeof(sa_result) * npairs);
+    tp.npairs = npairs;
+    tp.gap = sc->gap;
+    tp.match = sc->match;
+    tp.mismatch = sc->mismatch;
+    tp.gap_open = sc->gap_open;
+    tp.gap_extend = sc->gap_extend;
+    tp.allow = sc->allow_mismatch;
+    const auto t_stage = std::chrono::steady_clock::now();
+    SA_HIP(c, launch_tiny(algo, use_lut, max_m, tp, c->stream));
+    const auto t_launch = std::chrono::steady_clock::now();
+    SA_HIP(c, hipStreamSynchronize(c->stream));
+    const auto t_sync = std::chrono::steady_clock::now();
+    const sa_result* hres = reinterpret_cast<const sa_result*>(h + kTinyOut);
+    const uint8_t* hops = h + kTinyOut + al(sizeof(sa_result) * npairs);
+    memcpy(results, hres, sizeof(sa_result) * npairs);
+    for (uint32_t p = 0; p < npairs; ++p) {
+        const uint64_t o = off1[p] + off2[p] + p;
+        memcpy(ops + o, hops + o, results[p].nops);
+    }
+    // the plan of this call (sa_last_plan_ex); no fill launch of the batch kernels
+    c->nvar = 1;
+    c->host_sel = -1;
+    c->var_kernel[0] = SA_KERNEL_TINY;
+    c->var_R[0] = max_m > kWave ? 4 : 1;
+    c->var_W[0] = 1;
+    c->var_records[0] = SA_RECORDS_FLAGS;
+    c->launches = 0;
+    c->kvars.clear();
+    if (timing)
+        fprintf(stderr, "[seqalib host api] %u pairs, small-call kernel: %.1f us = pinned buffer %.1f + staging in %.1f + "
+                "launch %.1f + kernel and sync %.1f + copies out %.1f\n",
+                npairs, us(t0, std::chrono::steady_clock::now()), us(t0, t_alloc), us(t_alloc, t_stage),
+                us(t_stage, t_launch), us(t_launch, t_sync), us(t_sync, std::chrono::steady_clock::now()));
+    return SA_OK;
+}
+
 int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, const uint64_t* off1,
                const uint8_t* seq2, const uint64_t* off2, uint32_t npairs, const uint8_t* lut,
                sa_result* results, uint8_t* ops, uint64_t ops_cap, uint32_t chunks = 0,
@@ -1172,8 +1269,15 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     const uint64_t ops_total = t1 + t2 + npairs;
     if (ops_cap < ops_total) return fail(c, SA_ERR_CAPACITY, "ops buffer needs " + std::to_string(ops_total) + " bytes");
     if (!npairs) return SA_OK;
-    const bool use_lut = lut && !lut_is_identity(lut) &&
-                         !(t1 + t2 <= kHostScanBytes && lut_identity_on(lut, seq1, t1, seq2, t2));
+    int tiny_m = 0;
+    if (chunks <= 1 && tiny_call(algo, off1, off2, npairs, &tiny_m)) {
+        const int rc = align_tiny(c, algo, sc, seq1, off1, seq2, off2, npairs, lut, results, ops, tiny_m);
+        if (rc == SA_OK && cb) cb(cb_user, 0, npairs);
+        return rc;
+    }
+    // (identity on the symbols present implies nothing for large batches, whose scan costs more)
+    const bool use_lut = lut && !(t1 + t2 <= kHostScanBytes ? lut_identity_on(lut, seq1, t1, seq2, t2)
+                                                            : lut_is_identity(lut));
     const bool dc = algo == SA_HIRSCHBERG || algo == SA_MYERS_MILLER;
     const uint32_t G = chunks && !dc ? std::min(chunks, npairs) : host_chunks(algo, npairs);
     const std::vector<uint32_t> cut = cut_by_cells(off1, off2, npairs, G);
@@ -1477,6 +1581,7 @@ void sa_destroy(sa_ctx* c) {
     if (c->io) (void)hipFree(c->io);
     if (c->aux) (void)hipFree(c->aux);
     if (c->h_sel) (void)hipHostFree(c->h_sel);
+    if (c->tiny_io) (void)hipHostFree(c->tiny_io);
     if (c->split) (void)hipFree(c->split);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;

@@ -398,7 +398,7 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
                 }
                 if (lane < kChunk) {
                     const int j = cc * kChunk + lane;
-                    s_top[lane] = (top && j < n) ? ec_top(top + j) : 0;
+                    s_top[lane] = (top && j < n) ? (ec_top(top + j) & 0xffff) : 0;   // ({epoch, H} granules)
                 }
                 __syncthreads();
                 int hl = Hp[R - 1];
@@ -458,7 +458,9 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
 // open term floored it); the band's top row holds M and Ix.  Replayed Ix values may differ from
 // the reference's below 0 (the fill keeps max(Ix, 0) there), which leaves every M unchanged:
 // M = max(D, Ix, Iy, 0) and max(max(Ix, 0) + GE, GE) keeps max(., 0) of the chain (GE < 0).
-template <int R>
+// SO (score-only LocalGotoh fill, hshift 0): the snapshots and top rows hold M, B = Iy - (GO + GE)
+// and A = Ix - (GO + GE) unscaled and exact (sa_fill_impl.h, the SO affine cell); the chunk maxima M.
+template <int R, bool SO>
 __global__ __launch_bounds__(64) void endcell_lg_kernel(EndcellParams P) {
     if (sa_skip(P.sel, P.sel_want)) return;
     const int lane = threadIdx.x;
@@ -507,7 +509,7 @@ __global__ __launch_bounds__(64) void endcell_lg_kernel(EndcellParams P) {
     __shared__ int s_top[2 * kChunk];   // M, then Ix, of the band's top row at the chunk's columns
     for (int base = 0; base <= c; base += kWave) {   // candidate chunks, as endcell_kernel
         const int ccl = base + lane;
-        uint64_t hits = __builtin_amdgcn_ballot_w64(ccl <= c && lmax[(uint64_t)ccl * kWave] == 8 * S);
+        uint64_t hits = __builtin_amdgcn_ballot_w64(ccl <= c && lmax[(uint64_t)ccl * kWave] == (SO ? S : 8 * S));
         while (hits) {
         const int cc = base + (int)__builtin_ctzll(hits);
         hits &= hits - 1;
@@ -518,16 +520,18 @@ __global__ __launch_bounds__(64) void endcell_lg_kernel(EndcellParams P) {
         if (cc > 0) {
             const uint64_t e = (uint64_t)b * P.snap_nch + (cc - 1);
             const uint32_t* sh = P.snap_h + (uint64_t)slot * P.snap_h_slot + e * (R + 1) * kWave + lane;
+            constexpr int SH = SO ? 0 : 3;   // SO: M, B, A unscaled; tagged: 8M, 8Iy + 2, 8Ix + 4
+            const int off = SO ? GOE : 0;
 #pragma unroll
             for (int q = 0; q < R / 2; ++q) {
                 const uint32_t w = sh[q * kWave], y = sh[(R / 2 + q) * kWave];
-                Mp[2 * q] = (int)(w & 0xffffu) >> 3;   // 8M, non-negative
-                Mp[2 * q + 1] = (int)(w >> 16) >> 3;
-                Yp[2 * q] = (int)(int16_t)(y & 0xffffu) >> 3;   // 8Iy + 2 (the border: far below)
-                Yp[2 * q + 1] = (int)(int16_t)(y >> 16) >> 3;
+                Mp[2 * q] = (int)(w & 0xffffu) >> SH;   // M >= 0
+                Mp[2 * q + 1] = (int)(w >> 16) >> SH;
+                Yp[2 * q] = ((int)(int16_t)(y & 0xffffu) >> SH) + off;   // Iy (the border: far below)
+                Yp[2 * q + 1] = ((int)(int16_t)(y >> 16) >> SH) + off;
             }
-            xl = (int)(int16_t)(sh[R * kWave] & 0xffffu) >> 3;
-            prev_up = (int)(P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] & 0xffff) >> 3;
+            xl = ((int)(int16_t)(sh[R * kWave] & 0xffffu) >> SH) + off;
+            prev_up = (int)(P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] & 0xffff) >> SH;
         }
         __syncthreads();
         for (int k = lane; k < kWave + kChunk; k += kWave) {
@@ -537,8 +541,8 @@ __global__ __launch_bounds__(64) void endcell_lg_kernel(EndcellParams P) {
         if (lane < kChunk) {
             const int j = cc * kChunk + lane;
             const bool t = top && j < n;
-            s_top[lane] = t ? (ec_top(top + (uint64_t)j * rs) >> 3) : 0;
-            s_top[kChunk + lane] = t ? ((int)(int16_t)(ec_top(topx + (uint64_t)j * rs) & 0xffff) >> 3) : kNeg;
+            s_top[lane] = t ? ((ec_top(top + (uint64_t)j * rs) & (SO ? 0xffff : -1)) >> (SO ? 0 : 3)) : 0;
+            s_top[kChunk + lane] = t ? (((int)(int16_t)(ec_top(topx + (uint64_t)j * rs) & 0xffff) >> (SO ? 0 : 3)) + (SO ? GOE : 0)) : kNeg;
         }
         __syncthreads();
         int hl = Mp[R - 1];
@@ -684,11 +688,15 @@ hipError_t launch_endcell_so(int R, const EndcellParams& p, hipStream_t stream) 
 hipError_t launch_endcell(int algo, int R, const EndcellParams& p, hipStream_t stream) {
     const dim3 grid(p.count), block(64);
     if (algo == SA_LOCAL_GOTOH) {
+        const bool so = p.hshift == 0;   // the score-only fill's unscaled snapshots
         switch (R) {
-            case 2: hipLaunchKernelGGL(endcell_lg_kernel<2>, grid, block, 0, stream, p); break;
-            case 4: hipLaunchKernelGGL(endcell_lg_kernel<4>, grid, block, 0, stream, p); break;
-            case 8: hipLaunchKernelGGL(endcell_lg_kernel<8>, grid, block, 0, stream, p); break;
-            case 16: hipLaunchKernelGGL(endcell_lg_kernel<16>, grid, block, 0, stream, p); break;
+            case 2: if (so) return hipErrorInvalidValue; hipLaunchKernelGGL((endcell_lg_kernel<2, false>), grid, block, 0, stream, p); break;
+            case 4: if (so) hipLaunchKernelGGL((endcell_lg_kernel<4, true>), grid, block, 0, stream, p);
+                    else hipLaunchKernelGGL((endcell_lg_kernel<4, false>), grid, block, 0, stream, p); break;
+            case 8: if (so) hipLaunchKernelGGL((endcell_lg_kernel<8, true>), grid, block, 0, stream, p);
+                    else hipLaunchKernelGGL((endcell_lg_kernel<8, false>), grid, block, 0, stream, p); break;
+            case 16: if (so) hipLaunchKernelGGL((endcell_lg_kernel<16, true>), grid, block, 0, stream, p);
+                     else hipLaunchKernelGGL((endcell_lg_kernel<16, false>), grid, block, 0, stream, p); break;
             default: return hipErrorInvalidValue;
         }
         return hipGetLastError();

@@ -90,11 +90,15 @@ __device__ __forceinline__ uint32_t t16_code8(uint32_t sp, uint32_t b) {
            (b == (sp >> 24) ? 24u : 0u);
 }
 
-// SO profile word: the tagged profile bytes 4s + 3 (decide_t16) back to s, byte by byte.
+// SO profile word: the tagged profile bytes 4s + 3 (8s + 6 affine; decide_t16) back to s, byte by
+// byte.
+template <bool AFF = false>
 __device__ __forceinline__ uint32_t so_profile(uint32_t w) {
     uint32_t o = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) o |= ((uint32_t)(((int)(int8_t)(w >> (8 * k)) - 3) >> 2) & 255u) << (8 * k);
+    for (int k = 0; k < 4; ++k)
+        o |= ((uint32_t)(AFF ? (((int)(int8_t)(w >> (8 * k)) - 6) >> 3) : (((int)(int8_t)(w >> (8 * k)) - 3) >> 2)) & 255u)
+             << (8 * k);
     return o;
 }
 
@@ -130,11 +134,6 @@ constexpr int fill_max_threads() { return (R >= 32 || (WIDE && R >= 16)) ? 256 :
 // Steps per hand-off granule: 16 for the linear-gap cell, 8 for the affine one (configs 2 / 4 on
 // one MI355X, tools/ab_split.py: SW 4096^2 fill 0.54 ms at 8, 0.49 at 16, 0.52 at 32, 0.63 at 4;
 // LocalGotoh 8192^2 1.61 ms at 8, 1.64 at 16, 1.73 at 32).  SA_HAND_GRAN overrides both (A/B).
-// Score-only SW cell form (A/B): 1 = the shared-gap form, 4 fast ops + v_bfe_i32 (default);
-// 0 = separate left / up candidates, 5 fast ops + v_bfe_i32 (round 4's first score-only cell).
-#ifndef SA_SO_CELL5
-#define SA_SO_CELL5 1
-#endif
 
 template <bool AFF>
 constexpr int hand_gran() {
@@ -215,7 +214,8 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
     constexpr int FBITS = AFF ? 4 : 2;            // flag bits per cell
     constexpr int BPC = record_bpc(ALG, R, T16);  // record bits per cell (padding above the flags)
-    constexpr int RB = SO ? 16 : R * BPC;      // bits per record (SO: the lane's last row, 16 bits)
+    // bits per record (SO: the lane's last row, 16 bits; affine: its M and Ix - (GO + GE), 32 bits)
+    constexpr int RB = SO ? (AFF ? 32 : 16) : R * BPC;
     constexpr int BPS = RB / 8;                // bytes per record
     constexpr int RW = (RB + 31) / 32;         // words per record
     constexpr int RPW = (RB < 32 ? RB : 32) / BPC;  // rows per record word
@@ -228,11 +228,26 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                   "T16: allow-mismatch, profile");
     static_assert(!T16 || !LOCAL || KEYED, "T16 local mode tracks its maximum with keys");
     constexpr int SC = SO ? 1 : T16 ? (AFF ? 8 : 4) : 1;   // score scale of the register values
-    // SO: T16, many pairs; SW with the chunk-max end cell, or NW (which ends at (m, n))
-    static_assert(!SO || (T16 && !SPLIT && ((ALG == SA_SW && CMAX) || (ALG == SA_NW && !CMAX))),
-                  "SO: T16 SW chunk-max or NW, many pairs");
+    // SO: T16, many pairs; SW / LocalGotoh with the chunk-max end cell, or NW / GlobalGotoh (which
+    // end at (m, n))
+    static_assert(!SO || (T16 && !SPLIT && (LOCAL ? CMAX : !CMAX)), "SO: T16 chunk-max local or global, many pairs");
     // per-chunk snapshots of every lane's state (the end-cell replay and the SO traceback read them)
     constexpr bool SNAP = CMAX || SO;
+    // BAND UNITS (SO): every (pair, band) is a work unit of its own -- one single-wave workgroup per
+    // unit, units handed out by a ticket counter band-major (all bands 0, then all bands 1, ...), so
+    // a unit's producer band started earlier and, at the batch sizes that fill the chip, has long
+    // finished.  The launch tail is then the duration of one band, not of a whole pair (a 4096-row
+    // pair is two R = 32 bands: 10,000 x 4096^2 fill 16.55 -> 15.23 ms measured as 20,000 x
+    // 2048 x 4096, tools/fill_sweep.py).  The band's last row goes to the next band as 32-bit
+    // {epoch, value} granules in the row buffer (written and read as agent-scope atomics, i.e.
+    // coherent across the XCDs' L2s); a consumer re-reads a chunk's granules until they carry this
+    // launch's epoch (rare: see above).  The bands' score maxima meet in epoch-tagged partials
+    // that the last band folds into the pair's result.
+    constexpr bool BU = SO && !AFF;
+    // SOMAX (SO SW): the chunk maxima track only sampled cells (see the SW SO cell), the pair reports
+    // their maximum smax and endcell_so_kernel finds S; SO LocalGotoh keeps the exact chunk maxima
+    // of CMAX
+    constexpr bool SOMAX = SO && ALG == SA_SW;
     constexpr int CSH = SO ? 0 : (AFF ? 3 : 2);   // CMAX: chunk maxima are H << CSH
     static_assert(!CMAX || (T16 && LOCAL && R % 2 == 0), "CMAX: T16 Smith-Waterman / LocalGotoh");
 
@@ -265,7 +280,13 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     // ticket counter in the order workgroups actually start, so band b's producer (ticket - 1)
     // is always already running or done: no wait can deadlock whatever the residency.
     uint32_t slot, band0 = 0;
-    if constexpr (SPLIT) {
+    if constexpr (BU) {
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(P.ticket, 1u);
+        t = __builtin_amdgcn_readlane(t, 0);
+        band0 = t / P.count;
+        slot = t - band0 * P.count;
+    } else if constexpr (SPLIT) {
         if (threadIdx.x == 0) {
             s_ticket = atomicAdd(P.ticket, 1u);
             s_sync[0] = 0; s_sync[1] = 0; s_sync[2] = 0; s_sync[3] = 0; s_sync[4] = 0;
@@ -276,6 +297,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
         band0 = t - slot * P.split_bands;
     } else {
         slot = blockIdx.x;
+        if (slot >= P.count) return;   // (uniform) a grid larger than the launch's pairs
     }
     const uint32_t pidx = P.pair_base + slot;
     if (redo && !(P.res[pidx].flags & kFlagRetry)) return;   // uniform over the workgroup
@@ -293,7 +315,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     const int n = (int)(P.off2[pidx + 1] - o2);
 
     if ((uint32_t)m > P.max_m || (uint32_t)n > P.max_n) {  // whole block leaves together
-        if (!SPLIT && threadIdx.x == 0) {   // SPLIT: split_reduce_kernel reports it
+        if (!SPLIT && threadIdx.x == 0 && band0 == 0) {   // SPLIT: split_reduce_kernel reports it
             sa_result r = {};
             r.flags = SA_FLAG_BAD_SHAPE;
             P.res[pidx] = r;
@@ -404,14 +426,19 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     const uint32_t CXO = (uint32_t)(LOCAL ? -(8 * GOE + 4) : 8 * GOE + 4) & 0xffffu;
     const uint32_t CXE = (uint32_t)(8 * GE + 1) & 0xffffu;
     const uint32_t CYO = (uint32_t)(8 * GOE + 2) & 0xffffu;
+    // SO affine: CGE = GE; CGOE = -(GO + GE) (LocalGotoh, by saturation) or GO + GE (GlobalGotoh)
+    const uint32_t CGE = (uint32_t)GE & 0xffffu;
+    const uint32_t CGOE = (uint32_t)(LOCAL ? -GOE : GOE) & 0xffffu;
     // Ix / Iy borders (the reference's -10000): T16 affine uses a value below every candidate
     const int XB = (T16 && AFF) ? P.t16_sent : -10000;
 
     const int B = (m > 0 && n > 0) ? (m + BAND - 1) / BAND : 0;
     if (SPLIT && (int)band0 >= B) return;   // uniform: this pair has fewer bands
+    if (BU && (int)band0 >= (B > 0 ? B : 1)) return;   // (an empty pair: unit 0 reports it)
     const uint32_t nch = chunks_per_band((uint32_t)n);
     const uint32_t period = sched_period(nch, W);
-    const uint32_t total = SPLIT ? nch : total_phases((uint32_t)B, (uint32_t)n, W);
+    const uint32_t total = SPLIT ? nch : BU ? (B > 0 ? nch : 0u) : total_phases((uint32_t)B, (uint32_t)n, W);
+    const uint32_t epoch16 = ((P.epoch % 65535u) + 1u) << 16;   // BU: this launch's granule tag
     // SPLIT hand-off: band b's last row as 8-byte {tag = 1, value} granules written
     // write-through (sc1) per column, polled by band b+1 with sc1 loads; the data is its own flag
     // (cdna_hip_programming.md Guideline 16, R2).  The host zeroes them before every launch.
@@ -439,24 +466,15 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
             auto issue = [&](int b, unsigned long long& x, unsigned long long& y) {
                 const int cl = min(b + lane, n - 1);
                 gu64* const pa = src + cl;
-#ifdef SA_POLL_CXX
-                x = __hip_atomic_load(pa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                y = 1ull << 32;
-                if constexpr (AFF) y = __hip_atomic_load(pa + P.hand_x_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
                 asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=&v"(x) : "v"(pa) : "memory");
                 y = 1ull << 32;
                 if constexpr (AFF) {
                     gu64* const px = pa + P.hand_x_off;
                     asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=&v"(y) : "v"(px) : "memory");
                 }
-#endif
             };
             // the older window's loads are done once only the newer window's remain in flight
             auto settle = [&](unsigned long long& x, unsigned long long& y) {
-#ifdef SA_POLL_CXX
-                return;
-#endif
                 if constexpr (AFF) asm volatile("s_waitcnt vmcnt(2)" : "+v"(x), "+v"(y) :: "memory");
                 else asm volatile("s_waitcnt vmcnt(1)" : "+v"(x) :: "memory");
             };
@@ -555,9 +573,11 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     int32_t* const rb_h = P.rowbuf + (uint64_t)slot * P.rowbuf_slot;
     // affine: [M rows][Ix rows], the halves of the slot
     int32_t* const rb_x = rb_h + P.rowbuf_slot / 2;
-    // CMAX keeps every band's top row (row buffer = bands x max_n per component); otherwise one
-    // row is reused
-    const uint64_t rbs = CMAX ? P.max_n : 0;
+    // CMAX (the end-cell replay) and BU (the units of a pair run concurrently) keep every band's
+    // top row (row buffer = bands x max_n per component); otherwise one row is reused
+    const uint64_t rbs = (CMAX || BU) ? P.max_n : 0;
+    typedef uint32_t __attribute__((address_space(1))) gu32;
+    gu32* const rb_g = (gu32*)rb_h;   // BU: the granules
 
     // Per-lane state for the current band.
     int a[R];      // Seq1 symbols of my rows
@@ -641,7 +661,52 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
             for (int r = 0; r < R; ++r) {
                 uint32_t& rw = rec[r / RPW];
                 int Hc;
-                if constexpr (T16 && AFF) {
+                if constexpr (SO && AFF) {
+                    // Score-only affine cell (SALocalGotoh.h:108-130, SAGlobalGotoh.h:98-126), no tags.
+                    // Registers hold A = Ix - (GO + GE) (down the rows: xu) and B = Iy - (GO + GE) (Yp):
+                    //   A = max(Mu, Au + GE), B = max(Ml, Bl + GE), M = max(D, max(A, B) + GO + GE)
+                    // (LocalGotoh: max(., 0) of the second term by unsigned saturation: A, B >= M >= 0),
+                    // D = Md + s from the profile: 8 fast 16-bit ops + v_bfe_i32, against 16 for the
+                    // tagged cell.
+#define SA_SOA_HEAD                                                                                \
+    "v_add_u16 %[xa], %[cge], %[xu]\n\t"                                                            \
+    "v_add_u16 %[yb], %[cge], %[yp]\n\t"                                                            \
+    "v_max_i16 %[xa], %[hu], %[xa]\n\t"                                                             \
+    "v_max_i16 %[yp], %[hp], %[yb]\n\t"
+#define SA_SOA_NEXT "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\tv_add_u16 %[dn], %[hp], %[dn]\n\t"
+#define SA_SOA_TAIL_L "v_max_i16 %[t], %[xa], %[yp]\n\tv_sub_u16_e64 %[t], %[t], %[cgoe] clamp\n\tv_max_i16 %[hp], %[dr], %[t]"
+#define SA_SOA_TAIL_G "v_max_i16 %[t], %[xa], %[yp]\n\tv_add_u16 %[t], %[cgoe], %[t]\n\tv_max_i16 %[hp], %[dr], %[t]"
+#define SA_SOA_OUT [xa] "=&v"(xa), [yb] "=&v"(yb), [t] "=&v"(tt), [hp] "+v"(Hp[r]), [yp] "+v"(Yp[r])
+#define SA_SOA_IN [dr] "v"(dcur), [hu] "v"(hu), [xu] "v"(xu), [cge] "s"(CGE), [cgoe] "s"(CGOE)
+                    uint32_t xa, yb, tt;
+                    if (r + 1 < R) {
+                        uint32_t dn;
+                        const uint32_t tabn = (uint32_t)a[r + 1 < R ? r + 1 : r];
+                        if constexpr (LOCAL)
+                            asm(SA_SOA_HEAD SA_SOA_NEXT SA_SOA_TAIL_L : SA_SOA_OUT, [dn] "=&v"(dn)
+                                : SA_SOA_IN, [tabn] "v"(tabn), [sym] "v"(sym));
+                        else
+                            asm(SA_SOA_HEAD SA_SOA_NEXT SA_SOA_TAIL_G : SA_SOA_OUT, [dn] "=&v"(dn)
+                                : SA_SOA_IN, [tabn] "v"(tabn), [sym] "v"(sym));
+                        dcur = dn;
+                    } else {
+                        if constexpr (LOCAL) asm(SA_SOA_HEAD SA_SOA_TAIL_L : SA_SOA_OUT : SA_SOA_IN);
+                        else asm(SA_SOA_HEAD SA_SOA_TAIL_G : SA_SOA_OUT : SA_SOA_IN);
+                    }
+#undef SA_SOA_HEAD
+#undef SA_SOA_NEXT
+#undef SA_SOA_TAIL_L
+#undef SA_SOA_TAIL_G
+#undef SA_SOA_OUT
+#undef SA_SOA_IN
+                    (void)yb;
+                    if constexpr (CMAX) {   // the lane's chunk maximum of M (>= 0), one v_max3_u32 per two rows
+                        if (r & 1)
+                            asm("v_max3_u32 %0, %0, %1, %2" : "+v"(cml) : "v"(Hp[r >= 1 ? r - 1 : 0]), "v"(Hp[r]));
+                    }
+                    xu = (int)xa;
+                    Hc = Hp[r];
+                } else if constexpr (T16 && AFF) {
                     // One asm block per cell (see the header): Ix and Iy terms, M's max, the three
                     // record pushes and strips, the next row's diagonal candidate from Hp[r] before
                     // Hp[r] is updated, and (LocalGotoh) the (M, column) key: Hp = 8M, so
@@ -739,16 +804,13 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                     }
                     Hc = Hp[r];
                 } else if constexpr (SO) {
-                    // Score-only cell (Hp = H, no tags): left = Hp + G, the next row's diagonal
-                    // Hp_old + s from the profile, up = max(Hu + G, 0) by unsigned saturation (so the
-                    // zero clamp is free, as in the tagged cell), two v_max_i16.  5 fast-class 16-bit
-                    // ops + v_bfe_i32 (tools/microbench_so.hip: 1.33x the tagged cell's rate).
-                    uint32_t t0, t1;
-#if SA_SO_CELL5
-                    // Both gap candidates share G: max(U + G, L + G, 0) = max(U, L) - (-G) with
-                    // unsigned saturation (U, L = H >= 0), so the cell is max(D, sat(max(U, L) - CU)):
-                    // 4 fast-class ops + v_bfe_i32 for the next row's diagonal (one add fewer).
-                    (void)t0;
+                    // Score-only cell (Hp = H, no tags).  Both gap candidates share G: max(U + G,
+                    // L + G, 0) = max(U, L) - (-G) with unsigned saturation (U, L = H >= 0, so the zero
+                    // clamp is free), and the cell is max(D, sat(max(U, L) - CU)): 4 fast-class 16-bit
+                    // ops + v_bfe_i32 for the next row's diagonal Hp_old + s from the profile.  No
+                    // single fast-class op does the 4-symbol lookup (round 5, tools/microbench_ops3.hip:
+                    // v_perm / dot4 / sdwa forms issue at the v_bfe rate or slower).
+                    uint32_t t1;
                     if (r + 1 < R) {
                         uint32_t dn;
                         const uint32_t tabn = (uint32_t)a[r + 1 < R ? r + 1 : r];
@@ -768,29 +830,6 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                             : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU));
                     }
                     (void)CL;
-#else
-                    if (r + 1 < R) {
-                        uint32_t dn;
-                        const uint32_t tabn = (uint32_t)a[r + 1 < R ? r + 1 : r];
-                        asm("v_add_u16 %[t0], %[cl], %[hp]\n\t"
-                            "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\t"
-                            "v_add_u16 %[dn], %[hp], %[dn]\n\t"
-                            "v_sub_u16_e64 %[t1], %[hu], %[cu] clamp\n\t"
-                            "v_max_i16 %[t0], %[dr], %[t0]\n\t"
-                            "v_max_i16 %[hp], %[t1], %[t0]"
-                            : [t0] "=&v"(t0), [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r])
-                            : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL), [tabn] "v"(tabn),
-                              [sym] "v"(sym));
-                        dcur = dn;
-                    } else {
-                        asm("v_add_u16 %[t0], %[cl], %[hp]\n\t"
-                            "v_sub_u16_e64 %[t1], %[hu], %[cu] clamp\n\t"
-                            "v_max_i16 %[t0], %[dr], %[t0]\n\t"
-                            "v_max_i16 %[hp], %[t1], %[t0]"
-                            : [t0] "=&v"(t0), [t1] "=&v"(t1), [hp] "+v"(Hp[r])
-                            : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL));
-                    }
-#endif
                     // The lane's chunk maximum (H >= 0, one v_max3_u32 per two tracked cells).  Steady
                     // chunks track only the rows 3 mod 4 at the steps 3 mod 4: every cell (i, j) of
                     // the chunk has the tracked cell (i | 3, j | 3) of the same lane and chunk, and a
@@ -946,7 +985,8 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
         }
         // SO: the step's record is the lane's last row, pushed into the packet word from the top
         // (two steps per word)
-        if constexpr (SO) rec[0] = __builtin_amdgcn_alignbit((uint32_t)hl, rec[0], 16u);
+        if constexpr (SO && AFF) rec[0] = __builtin_amdgcn_perm((uint32_t)xl, (uint32_t)hl, 0x05040100u);   // M | A << 16
+        else if constexpr (SO) rec[0] = __builtin_amdgcn_alignbit((uint32_t)hl, rec[0], 16u);
     };
 
     // SPLIT compute wave, before the group of SG steps at step q of the chunk at kC: back-pressure
@@ -1130,6 +1170,8 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                 else if constexpr (ALG == SA_GLOBAL_GOTOH) vh = SC * (GO + J * GE - P.t16_delta);
             } else if constexpr (SPLIT) {
                 // polled per granule group inside the chunk (split_sub)
+            } else if constexpr (BU) {
+                vh = (int)__hip_atomic_load(rb_g + (uint64_t)(band - 1) * rbs + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else if (band % W != 0) {
                 vh = ring(band % W, 0)[c % kRing];
                 if constexpr (AFF) vx = ring(band % W, 1)[c % kRing];
@@ -1140,14 +1182,26 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
         }
         // SPLIT, band > 0: the lane-0 inputs are polled per granule group inside the chunk
         // (split_sub); the values written to s_step here are placeholders
+        if constexpr (BU) {
+            if (band > 0) {   // (uniform) the producer band's granules of this chunk, this launch's
+                const bool want = lane < kChunk && c < n;
+                while (__builtin_amdgcn_ballot_w64(want && ((uint32_t)vh & 0xffff0000u) != epoch16) != 0) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (want)
+                        vh = (int)__hip_atomic_load(rb_g + (uint64_t)(band - 1) * rbs + c, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+                }
+                vh &= 0xffff;
+            }
+        }
     };
 
     for (uint32_t ph = 0; ph < total; ++ph) {
         const int rel = (int)ph - w * kLagPhases;
-        if (SPLIT || rel >= 0) {
-            const uint32_t k = SPLIT ? 0u : (uint32_t)rel / period;
-            const uint32_t chunk = SPLIT ? ph : (uint32_t)rel - k * period;
-            const int band = SPLIT ? (int)band0 : w + (int)k * W;
+        if (SPLIT || BU || rel >= 0) {
+            const uint32_t k = (SPLIT || BU) ? 0u : (uint32_t)rel / period;
+            const uint32_t chunk = (SPLIT || BU) ? ph : (uint32_t)rel - k * period;
+            const int band = (SPLIT || BU) ? (int)band0 : w + (int)k * W;
             if (chunk < nch && band < B) {
                 // ---------------------------------------------------------------- band start
                 if (chunk == 0) {
@@ -1157,7 +1211,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                         const int row = row0 + r;
                         // CMAX: rows past m get substitution -128 (with gap < 0 their values stay
                         // below the matrix maximum, so they never win the lane's chunk maximum)
-                        if constexpr (SO) a[r] = row < m ? (int)so_profile(P.prof[t16_code8(symp, s1[row]) >> 3]) : (CMAX ? (int)0x80808080u : 0);
+                        if constexpr (SO) a[r] = row < m ? (int)so_profile<AFF>(P.prof[t16_code8(symp, s1[row]) >> 3]) : (CMAX ? (int)0x80808080u : 0);
                         else if constexpr (T16) a[r] = row < m ? (int)P.prof[t16_code8(symp, s1[row]) >> 3] : (CMAX ? (int)0x80808080u : 0);
                         else a[r] = row < m ? (int)s1[row] : 0;
                         const int i = row + 1;
@@ -1230,7 +1284,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                 }
                 if (steady) {
                     run_chunk(std::integral_constant<int, kStepSteady>{}, band, kC, bch, bcx, symc, acc_h, acc_x);
-                } else if (T16 && LOCAL && CMAX && SPLIT && !P.no_start && n >= kWave && kC < kWave - 1) {
+                } else if (T16 && LOCAL && CMAX && SPLIT && n >= kWave && kC < kWave - 1) {
                     // a band's first chunks (n >= 64: every lane reaches its first column inside
                     // them, so none starts from start-mode garbage in a kStepAny chunk).  SPLIT
                     // only: a third chunk body costs the many-pairs R = 32 kernel 31 VGPRs (138 ->
@@ -1248,6 +1302,9 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                         const int nw = (band + 1) % W;
                         if constexpr (SPLIT) {
                             // stored by the publisher wave from the park ring
+                        } else if constexpr (BU) {
+                            __hip_atomic_store(rb_g + (uint64_t)band * rbs + cc, epoch16 | ((uint32_t)acc_h & 0xffffu),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         } else if (nw != 0) {
                             ring(nw, 0)[cc % kRing] = acc_h;
                             if constexpr (AFF) ring(nw, 1)[cc % kRing] = acc_x;
@@ -1262,7 +1319,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                     const uint64_t e = (uint64_t)band * P.snap_nch + chunk;
                     if constexpr (!CMAX) {
                         // (SO NW: snapshots only)
-                    } else if constexpr (SO) {
+                    } else if constexpr (SOMAX) {
                         // per (band, chunk, lane): the lane's maximum of its tracked cells -- the
                         // end-cell replay then recomputes only the lane blocks that may hold S
                         if (kC + kChunk - 1 < lane) cml = 0;   // (a lane that has not reached its first column)
@@ -1362,6 +1419,27 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
 #endif
         }
     } else if constexpr (LOCAL) {
+        if constexpr (BU) {
+            // this band's maximum of its tracked cells; the pair's last band folds the partials
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, off));
+            typedef unsigned long long __attribute__((address_space(1))) gu64p;
+            gu64p* const part = (gu64p*)(P.band_part + (uint64_t)slot * P.part_bands);
+            if (B > 1 && (int)band0 < B - 1) {
+                if (lane == 0)
+                    __hip_atomic_store(part + band0, (unsigned long long)P.epoch << 32 | smax, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
+            // (the last band: every earlier band finished its last chunk before this one's last
+            // chunk could read it, so its partial is at most a few instructions away)
+            for (int b = lane; b < B - 1; b += kWave) {
+                unsigned long long x;
+                while (((x = __hip_atomic_load(part + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != P.epoch)
+                    __builtin_amdgcn_s_sleep(2);
+                smax = max(smax, (uint32_t)x);
+            }
+        }
 #ifdef SA_TB_STATS
         if (threadIdx.x == 0 && slot < 32768) {
             g_fill_stats[slot][0] = st_t0;
@@ -1369,7 +1447,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
             g_fill_stats[slot][2] = (unsigned long long)st_hwid | ((unsigned long long)st_xcc << 32);
         }
 #endif
-        if constexpr (SO) {
+        if constexpr (SOMAX) {
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, off));
         }
@@ -1395,7 +1473,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                 // empty input: SW keeps MaxScore = INT_MIN, (MaxRow, MaxCol) = (0, 0);
                 // LocalGotoh reads M[0][0] = 0 there
                 r.score = (ALG == SA_SW) ? INT_MIN : 0;
-            } else if constexpr (SO) {
+            } else if constexpr (SOMAX) {
                 // S >= smax and S <= smax - kSoSlack G: endcell_so_kernel finds S and the last
                 // row-major cell
                 h = (int)smax - kSoSlack * G;   // (the retry test below: the largest S this pair may have)
@@ -1413,6 +1491,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
             P.res[pidx] = r;
         }
     } else {
+        if (BU && B > 0 && (int)band0 != (m - 1) / BAND) return;   // (uniform) the unit holding row m reports
         if (threadIdx.x == 0) {   // the phase loop's last barrier orders the owner's s_score store
             sa_result r = {};
             r.end_i = m;
@@ -1440,15 +1519,15 @@ __global__ __launch_bounds__((fill_max_threads<R, (T16 && ALG >= SA_LOCAL_GOTOH)
 // 8,054 vs 7,520 GCUPS-equivalent at 4 vs 3 waves per SIMD).
 template <int ALG, int R>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void fill_so_kernel(FillParams P) {
-    if constexpr (ALG == SA_SW) fill_body<SA_SW, R, kMatchEq, true, true, true, true, false, true>(P);
-    else fill_body<SA_NW, R, kMatchEq, true, false, true, false, false, true>(P);
+    constexpr bool LOCAL = ALG == SA_SW || ALG == SA_LOCAL_GOTOH;
+    fill_body<ALG, R, kMatchEq, true, LOCAL, true, LOCAL, false, true>(P);
 }
 
 template <int ALG>
 hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream) {
     constexpr bool LOCAL = (ALG == SA_SW || ALG == SA_LOCAL_GOTOH);
     const int R = v.R;
-    if (v.so && (!v.t16 || v.split || !((ALG == SA_SW && v.cmax) || (ALG == SA_NW && !v.cmax)))) return hipErrorInvalidValue;
+    if (v.so && (!v.t16 || v.split || v.cmax != LOCAL)) return hipErrorInvalidValue;
     const bool lut = (v.t16 || v.bits) ? false : v.lut, allow = v.allow;
     const bool keyed = LOCAL && v.keyed;
     // SPLIT: the compute wave + its poller and publisher waves (see kHandGran); LDS for one
@@ -1507,6 +1586,13 @@ hipError_t launch_fill_alg(const FillVariant& v, const FillParams& p, uint32_t g
                 return hipErrorInvalidConfiguration;
 #define SA_LAUNCH16A(RR, SP)                                                                           \
     if (R == RR && split == SP) {                                                                      \
+        if constexpr (!SP && RR >= 4) {                                                                \
+            if (v.so) {                                                                                \
+                hipLaunchKernelGGL((fill_so_kernel<ALG, RR>), dim3(grid), block, lds, stream, p);         \
+                return hipGetLastError();                                                              \
+            }                                                                                          \
+        }                                                                                              \
+        if (v.so) return hipErrorInvalidValue;                                                         \
         if constexpr (LOCAL && RR % 2 == 0) {                                                          \
             if (v.cmax) {                                                                              \
                 hipLaunchKernelGGL((fill_kernel<ALG, RR, kMatchEq, true, true, true, true, SP>), dim3(grid), block, \

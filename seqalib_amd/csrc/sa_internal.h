@@ -80,7 +80,12 @@ struct FillParams {
     uint64_t wait_ticks;       // SPLIT: bounded wait for the producer band (s_memrealtime ticks)
     // the fallback launch: re-runs only the pairs a SPLIT fill flagged SA_FLAG_TIMEOUT
     int rerun;
-    int no_start;              // debugging aid (SEQALIB_NO_START): no start-mode steps
+    // score-only fills (band units, sa_fill_impl.h BU): ticket = the unit counter (zeroed before
+    // the launch), epoch = this launch's tag of the row-buffer granules and of the per-band maxima
+    // band_part (part_bands 64-bit words per slot: epoch << 32 | the band's maximum)
+    uint32_t epoch;
+    unsigned long long* band_part;
+    uint32_t part_bands;
 };
 
 // SPLIT fills: per-pair fold of the per-band partials into sa_result (split_reduce_kernel).
@@ -167,6 +172,7 @@ struct TbParams {
     uint32_t snap_nch;
     const uint32_t* prof;
     int32_t t16_delta;         // score-only NW: the fill's values are H - t16_delta (the borders)
+    int32_t t16_sent;          // score-only Gotoh: the tagged Ix / Iy border (FillParams::t16_sent)
 };
 // SA_FLAG_TIMEOUT: a SPLIT band's bounded wait for its producer expired (results invalid)
 
@@ -188,6 +194,7 @@ hipError_t launch_fill_gg(const FillVariant& v, const FillParams& p, uint32_t gr
 // Batch alphabet scan (presence bitmap of every byte of both sequence sets, 8 words) and the
 // device-side T16 decision.  aux layout (kAux* below): [bitmap 8][profile 4][sym_pack][sel].
 constexpr int kAuxProf = 8, kAuxSel = 13, kAuxWords = 64;
+constexpr int kAuxTicket = 32;   // the score-only fill's unit ticket (zeroed before each launch)
 // Score-only SW fill: steady chunks track the lane maximum at rows and steps 3 mod 4 only, so a
 // cell is at most its tracked cell - kSoSlack * gap (3 rows + 3 columns of gap moves)
 constexpr int kSoSlack = 6;
@@ -246,4 +253,22 @@ hipError_t launch_endcell(int algo, int R, const EndcellParams& p, hipStream_t s
 hipError_t launch_traceback_so(int algo, int R, const TbParams& p, hipStream_t stream);
 // Score-only SW fills: the end cell from the per-(band, chunk) maxima of the tracked cells.
 hipError_t launch_endcell_so(int R, const EndcellParams& p, hipStream_t stream);
+
+// The small-call path (sa_tiny.hip): one single-wave workgroup per pair fills, keeps the flags
+// in LDS and walks the traceback; inputs and outputs are pinned host memory mapped into the GPU.
+// Shapes: m <= kTinyM, n <= kTinyN, m * n <= kTinyCells, at most kTinyPairs pairs per call.
+constexpr int kTinyM = 256, kTinyN = 1024, kTinyCells = 32768, kTinyPairs = 64;
+struct TinyParams {
+    const uint8_t* seq1;
+    const uint64_t* off1;      // npairs + 1 offsets (prefix sums)
+    const uint8_t* seq2;
+    const uint64_t* off2;
+    const uint32_t* lutbits;   // 2048 words, or NULL (identity)
+    sa_result* res;
+    uint8_t* ops;              // pair p's ops at off1[p] + off2[p] + p
+    uint32_t npairs;
+    int32_t gap, match, mismatch, gap_open, gap_extend;
+    int allow;
+};
+hipError_t launch_tiny(int algo, bool lut, int max_m, const TinyParams& p, hipStream_t stream);
 }  // namespace sa

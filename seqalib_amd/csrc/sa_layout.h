@@ -101,7 +101,7 @@ struct Geom {
     uint64_t dir_slot;     // bytes per pair
     int tagged;            // 0 equality flags; 1 max tags (T16 kernels); 2 score-only edge stream
 };
-constexpr int kGeomEdge = 2;   // Geom::tagged of a score-only (SO) fill: 16 bits per lane-step
+constexpr int kGeomEdge = 2;   // Geom::tagged of a score-only (SO) fill: 16 bits per lane-step (affine: 32)
 
 SA_HD uint32_t round_up(uint32_t x, uint32_t a) { return (x + a - 1) / a * a; }
 
@@ -111,7 +111,7 @@ SA_HD Geom make_geom(int algo, int R, uint32_t max_m, uint32_t max_n, int tagged
     g.tagged = tagged;
     g.bpc = record_bpc(algo, R, tagged != 0);
     // score-only fills (sa_fill_impl.h SO) store the lane's last row per step instead of flags
-    g.bps = tagged == kGeomEdge ? 2 : R * g.bpc / 8;
+    g.bps = tagged == kGeomEdge ? (is_affine(algo) ? 4 : 2) : R * g.bpc / 8;   // (affine: M and Ix)
     g.spp = g.bps >= 16 ? 1 : 16 / g.bps;
     g.pps = g.bps > 16 ? g.bps / 16 : 1;
     g.steps_pad = round_up(max_n + 63, kChunk);

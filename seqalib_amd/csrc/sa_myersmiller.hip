@@ -842,9 +842,8 @@ void launch_mm_sweeps_t(int R, int G, uint32_t count, const MmLaunch& a_in, hipS
     const dim3 block(64);
     MmLaunch a = a_in;
     // 16-bit sweeps of <= 128 rows (whole-wave R = 1, 2): two per wave (mm_sweep_seg16_kernel, 2R rows per lane), the
-    // whole-wave kernel beside it for the int32 case ($SEQALIB_DC_SEG16=0: whole-wave only)
-    const bool seg16_on = !getenv("SEQALIB_DC_SEG16") || atoi(getenv("SEQALIB_DC_SEG16")) != 0;
-    if (MM != kMatchBits && a.d16.aux && G == 0 && R <= 2 && seg16_on) {
+    // whole-wave kernel beside it for the int32 case
+    if (MM != kMatchBits && a.d16.aux && G == 0 && R <= 2) {
         const dim3 grid2((count + 1) / 2);
         if (R == 1) hipLaunchKernelGGL(mm_sweep_seg16_kernel<2>, grid2, block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.sc, a.d16);
         else hipLaunchKernelGGL(mm_sweep_seg16_kernel<4>, grid2, block, 0, st, a.d1, a.d2, a.split, a.lvl, a.rows, a.sc, a.d16);
@@ -889,8 +888,7 @@ int myersmiller_run(DcWork& w, hipEvent_t prev, const sa_scoring* scoring, const
     if (const char* lr = getenv("SEQALIB_MM_LEAF")) leaf_rows = std::min(4096, std::max(2, atoi(lr)));
     const char* segenv = getenv("SEQALIB_DC_SEG");   // 0: whole-wave sweeps only (A/B, tests)
     const bool seg_sweeps = !segenv || atoi(segenv) != 0;
-    int rmax = 32;                                   // tuning: SEQALIB_DC_RMAX caps the sweep's R
-    if (const char* r = getenv("SEQALIB_DC_RMAX")) rmax = std::min(32, std::max(1, atoi(r)));
+    constexpr int rmax = 32;                         // the sweep's largest R
     const uint32_t npairs = in.npairs;
     MmScore sc;
     sc.g = scoring->gap_open;

@@ -745,6 +745,298 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
 }
 
 // SEQALIB_TB_SO=1: one lane per pair (traceback_so_kernel); default four lanes per pair.
+// ------------------------------------------------------------------------------------------------
+// Score-only LocalGotoh / GlobalGotoh (sa_fill_impl.h, the SO affine cell): buildResult
+// (SALocalGotoh.h:275-470, SAGlobalGotoh.h:235-421) on flags recomputed block by block.  Four lanes
+// per pair (16 pairs per wave), sublane k owning rows k R/4 .. of the block, swept as a four-lane
+// anti-diagonal wavefront as in traceback_so4_kernel.  The recompute runs the tagged affine cell of
+// the T16 fill (8 V + class / extend bits: one v_max_i16 chain per state gives the value and the
+// reference's tie order -- diag, then Ix, then Iy; extend before open), from the fill's exact
+// unscaled M, B = Iy - (GO + GE) and A = Ix - (GO + GE): the left column and corner from the chunk
+// snapshot, the top row (M and A of the lane above) from the 32-bit edge stream.  Per cell it keeps
+// the four flags of the int32 records (bit 3 M == diag, bit 2 M == Ix, bit 1 Ix extends, bit 0 Iy
+// extends; sa_layout.h t16a_flags) and the walk is sa_traceback.hip's three-state machine.
+template <int ALG, int R>
+__global__ __launch_bounds__(64) void traceback_soa_kernel(TbParams P) {
+    constexpr int LP = 4, RS = R / LP, BAND = kWave * R;
+    constexpr bool LG = ALG == SA_LOCAL_GOTOH;
+    static_assert(R >= 4 && R <= 16 && R % LP == 0, "R in {4, 8, 16}");
+    // LDS: flags [column q][lane] words (RS rows x 4 bits); the top row's <= 9 edge packets in three
+    // regions of 64 lanes x 16 B (sublane k loads packets k, k + 4, k + 8); row / column codes
+    constexpr int kTags = 0, kEdge = kTags + 32 * 64 * 4, kRowC = kEdge + 3 * 1024, kColC = kRowC + 16 * 32;
+    constexpr int kBytes = kColC + 16 * 32;
+    __shared__ __attribute__((aligned(16))) uint8_t s_so[kBytes];
+    typedef volatile uint8_t __attribute__((address_space(3))) lds_u8;
+    typedef volatile uint32_t __attribute__((address_space(3))) lds_u32;
+    lds_u8* const vb = (lds_u8*)s_so;
+    lds_u32* const vw = (lds_u32*)s_so;
+    const int lane = threadIdx.x, quad = lane / LP, sub = lane % LP;
+    const uint32_t slot = blockIdx.x * (kWave / LP) + quad;
+    bool live = slot < P.count;
+    const uint32_t pidx = P.pair_base + (live ? slot : 0);
+    sa_result res = P.res[pidx];
+    live = live && !(res.flags & SA_FLAG_BAD_SHAPE) && tb_mine(P, res.flags);
+    if (__builtin_amdgcn_ballot_w64(live) == 0) return;
+    res.flags &= ~(kFlagRetry | kFlagRedo | kFlagRerun);
+    uint32_t flags = res.flags;
+    const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
+    const int m = (int)(P.off1[pidx + 1] - o1);
+    const int n = (int)(P.off2[pidx + 1] - o2);
+    const uint8_t* s1 = P.seq1 + o1;
+    const uint8_t* s2 = P.seq2 + o2;
+    typedef uint8_t __attribute__((address_space(1))) glb_u8;
+    glb_u8* ops = (glb_u8*)(P.ops + o1 + o2 + pidx);
+    const uint8_t* const dir = P.dirs + (uint64_t)(live ? slot : 0) * P.dir_slot;
+    const uint64_t band_stride = P.band_stride;
+    const uint32_t npk = (uint32_t)(band_stride / (kWave * 16));   // edge packets (4 steps each) per band
+    const uint32_t* const sh_base = P.snap_h + (uint64_t)(live ? slot : 0) * P.snap_h_slot;
+    const int32_t* const sp_base = P.snap_p + (uint64_t)(live ? slot : 0) * P.snap_p_slot;
+    const uint32_t snap_nch = P.snap_nch;
+    const uint32_t symp = P.prof[4];
+    const uint32_t pf0 = P.prof[0], pf1 = P.prof[1], pf2 = P.prof[2], pf3 = P.prof[3];
+    uint32_t mt = 0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t sa_ = (symp >> (8 * a)) & 255u, sb_ = (symp >> (8 * b)) & 255u;
+            const bool v = P.lutbits ? ((P.lutbits[(sa_ << 3) | (sb_ >> 5)] >> (sb_ & 31u)) & 1u) != 0 : sa_ == sb_;
+            mt |= (v ? 1u : 0u) << (a * 4 + b);
+        }
+    const bool allow = P.allow != 0;
+    const int MA = P.match, MI = P.mismatch, GO = P.gap_open, GE = P.gap_extend, GOE = GO + GE;
+    const int D0 = LG ? 0 : P.t16_delta;
+    const int SENT = P.t16_sent;   // the tagged Ix / Iy border (below every candidate)
+    // the tagged affine cell's constants (sa_fill_impl.h, T16 affine)
+    const uint32_t CXO = (uint32_t)(LG ? -(8 * GOE + 4) : 8 * GOE + 4) & 0xffffu;
+    const uint32_t CXE = (uint32_t)(8 * GE + 1) & 0xffffu;
+    const uint32_t CYO = (uint32_t)(8 * GOE + 2) & 0xffffu;
+    // 8 (M - delta) of a border cell with index x (row i of column 0, or column j of row 0)
+    auto mb = [&](int x) __attribute__((always_inline)) -> int { return LG ? 0 : 8 * ((x < 1 ? 0 : GO + x * GE) - D0); };
+
+    uint32_t k = 0;
+    auto emit = [&](uint8_t op) __attribute__((always_inline)) {
+        if (sub == 0) ops[k] = op;
+        ++k;
+    };
+    int cb = 0, ct = 0, cc = 0, cr = 0, cq = 0;
+    auto locate = [&](int i, int j) __attribute__((always_inline)) {
+        const int ii = i - 1;
+        cb = ii / BAND;
+        const int rem = ii - cb * BAND;
+        ct = rem / R;
+        cr = rem - ct * R;
+        const int s = j - 1 + ct;
+        cc = s >> 5;
+        cq = s & 31;
+    };
+    auto recompute = [&](bool act, int i, int j) __attribute__((always_inline)) {
+        int r0 = 0, j0 = 0, qlo = 0, qhi = -1, slo = 0, pk0 = 0, bp = 0, tp = 0;
+        bool has_top = false, has_left = false;
+        if (act) {
+            locate(i, j);
+            r0 = cb * BAND + ct * R;
+            j0 = 32 * cc - ct;
+            qlo = j0 < 0 ? -j0 : 0;
+            qhi = j - 1 - j0;
+            has_top = !(cb == 0 && ct == 0);
+            bp = ct > 0 ? cb : cb - 1;
+            tp = ct > 0 ? ct - 1 : kWave - 1;
+            slo = j0 + tp;
+            pk0 = slo >> 2;   // (arithmetic)
+            has_left = cc > 0 && j0 >= 1;
+            if (has_top) {
+                const uint8_t* base = dir + (uint64_t)bp * band_stride;
+#pragma unroll
+                for (int d = 0; d < 3; ++d) {
+                    const int pk = pk0 + sub + 4 * d;
+                    if (sub + 4 * d < 9 && pk >= 0 && (uint32_t)pk < npk)
+                        __builtin_amdgcn_global_load_lds((so_gptr)(base + ((uint64_t)pk * kWave + tp) * 16),
+                                                         (so_lptr)(s_so + kEdge + d * 1024), 16, 0, 0);
+                }
+            }
+        }
+        const int rs0 = sub * RS;   // block-relative first row of this sublane
+        int Mp[RS], Yp[RS];
+        uint32_t tab[RS];
+        int corner = 0;
+#pragma unroll
+        for (int r = 0; r < RS; ++r) { Mp[r] = 0; Yp[r] = SENT; tab[r] = pf0; }
+        if (act) {
+            if (has_left) {
+                const uint64_t e = (uint64_t)cb * snap_nch + (cc - 1);
+                const uint32_t* sh = sh_base + e * (R + 1) * kWave + ct;
+#pragma unroll
+                for (int r = 0; r < RS; ++r) {
+                    const int rr = rs0 + r;
+                    const uint32_t w = sh[(rr >> 1) * kWave], y = sh[(R / 2 + (rr >> 1)) * kWave];
+                    const int mv = (int)((rr & 1) ? (w >> 16) : (w & 0xffffu));
+                    const int bv = (int)(int16_t)((rr & 1) ? (y >> 16) : (y & 0xffffu));
+                    Mp[r] = mv << 3;                  // 8 (M - delta)
+                    Yp[r] = ((bv + GOE) << 3) + 2;    // 8 (Iy - delta) + class 1
+                }
+                if (rs0 > 0) {
+                    const uint32_t w = sh[((rs0 - 1) >> 1) * kWave];
+                    corner = (int)(((rs0 - 1) & 1) ? (w >> 16) : (w & 0xffffu)) << 3;
+                } else if (r0 > 0) {
+                    corner = (sp_base[e * kWave + ct] & 0xffff) << 3;
+                } else {
+                    corner = mb(j0);                  // M(0, j0)
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < RS; ++r) Mp[r] = mb(r0 + rs0 + r + 1);   // M(i, 0)
+                corner = mb(r0 + rs0);
+            }
+#pragma unroll
+            for (int r = 0; r < RS; ++r) {
+                const int row = r0 + rs0 + r;
+                const uint32_t c8 = row < m ? so_code8(symp, s1[row]) : 0u;
+                tab[r] = c8 == 0 ? pf0 : c8 == 8 ? pf1 : c8 == 16 ? pf2 : pf3;
+                vb[kRowC + quad * 32 + rs0 + r] = (uint8_t)c8;
+            }
+#pragma unroll
+            for (int e = 0; e < 32 / LP; ++e) {
+                const int q = sub * (32 / LP) + e, jj = j0 + q;
+                vb[kColC + quad * 32 + q] = (uint8_t)(q >= qlo && q <= qhi && jj < n ? so_code8(symp, s2[jj]) : 0u);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the edge DMA and the code stores
+        int hl = Mp[RS - 1], xl = SENT;
+        int prev_up = corner;
+        int nmax = qhi - qlo + 1 + (LP - 1);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
+        for (int u = 0; u < nmax; ++u) {
+            const int q = qlo + u - sub;
+            const bool on = act && q >= qlo && q <= qhi;
+            // the row above: from sublane k - 1 (quad_perm [0,0,1,2]); sublane 0: the top row
+            int up_h = __builtin_amdgcn_mov_dpp(hl, 0x90, 0xf, 0xf, false);
+            int up_x = __builtin_amdgcn_mov_dpp(xl, 0x90, 0xf, 0xf, false);
+            if (sub == 0) {
+                up_h = 0;
+                up_x = SENT;
+                if (on) {
+                    if (!has_top) {
+                        up_h = mb(j0 + q + 1);    // M(0, j)
+                    } else {
+                        const int st = slo + q;
+                        const int p = (st >> 2) - pk0;
+                        const uint32_t w = vw[(kEdge >> 2) + (p >> 2) * 256 + (quad * LP + (p & 3)) * 4 + (st & 3)];
+                        up_h = (int)(w & 0xffffu) << 3;
+                        up_x = (((int)(int16_t)(w >> 16) + GOE) << 3) + 4;   // 8 (Ix - delta) + class 2
+                    }
+                }
+            }
+            if (on) {
+                const uint32_t sym = vb[kColC + quad * 32 + q];
+                uint32_t dcur;
+                asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(dcur) : "v"(tab[0]), "v"(sym), "v"(prev_up));
+                uint32_t hu = (uint32_t)up_h, xu = (uint32_t)up_x, rec = 0;
+#pragma unroll
+                for (int r = 0; r < RS; ++r) {
+                    uint32_t t0, t1, xr, yr, dn;
+                    const uint32_t tabn = tab[r + 1 < RS ? r + 1 : r];
+                    if constexpr (LG) asm("v_sub_u16_e64 %[t0], %[hu], %[cxo] clamp" : [t0] "=v"(t0) : [hu] "v"(hu), [cxo] "s"(CXO));
+                    else asm("v_add_u16 %[t0], %[cxo], %[hu]" : [t0] "=v"(t0) : [hu] "v"(hu), [cxo] "s"(CXO));
+                    asm("v_add_u16 %[t1], %[cyo], %[hp]\n\t"
+                        "v_add_u16 %[xr], %[cxe], %[xu]\n\t"
+                        "v_add_u16 %[yr], %[cxe], %[yp]\n\t"
+                        "v_max_i16 %[xr], %[t0], %[xr]\n\t"
+                        "v_max_i16 %[yr], %[t1], %[yr]\n\t"
+                        "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\t"
+                        "v_add_u16 %[dn], %[hp], %[dn]\n\t"
+                        "v_max_i16 %[t1], %[dr], %[xr]\n\t"
+                        "v_max_i16 %[t1], %[yr], %[t1]"
+                        : [t1] "=&v"(t1), [xr] "=&v"(xr), [yr] "=&v"(yr), [dn] "=&v"(dn)
+                        : [t0] "v"(t0), [hp] "v"(Mp[r]), [xu] "v"(xu), [yp] "v"(Yp[r]), [dr] "v"(dcur),
+                          [cxe] "s"(CXE), [cyo] "s"(CYO), [tabn] "v"(tabn), [sym] "v"(sym));
+                    const uint32_t cls = (t1 >> 1) & 3u;
+                    rec |= ((cls == 3u ? 8u : 0u) | (cls == 2u ? 4u : 0u) | ((xr & 1u) << 1) | (yr & 1u)) << (4 * r);
+                    xu = xr & ~1u;            // Ix keeps its class bits (8 Ix + 4)
+                    Yp[r] = (int)(yr & ~1u);  // 8 Iy + 2
+                    Mp[r] = (int)(t1 & ~7u);  // 8 M
+                    hu = (uint32_t)Mp[r];
+                    dcur = dn;
+                }
+                vw[q * 64 + lane] = rec;
+                prev_up = up_h;
+                hl = Mp[RS - 1];
+                xl = (int)xu;
+            }
+        }
+    };
+    auto flag_of = [&](int r, int q) __attribute__((always_inline)) -> uint32_t {
+        return (vw[q * 64 + quad * LP + r / RS] >> (4 * (r % RS))) & 15u;
+    };
+    auto match_of = [&](int r, int q) __attribute__((always_inline)) -> bool {
+        const uint32_t a = (vb[kRowC + quad * 32 + r] >> 3) & 3u, b = (vb[kColC + quad * 32 + q] >> 3) & 3u;
+        return ((mt >> (a * 4 + b)) & 1u) != 0;
+    };
+
+    int i, j, V = 0, st = 0;
+    if constexpr (LG) { i = res.end_i; j = res.end_j; V = res.score; }
+    else { i = m; j = n; }
+    bool fin = !live, parked = true;
+    for (;;) {
+        if (__builtin_amdgcn_ballot_w64(!fin && !parked) == 0) {
+            if (__builtin_amdgcn_ballot_w64(!fin) == 0) break;
+            recompute(!fin, i, j);   // every lane: the sub-step loop uses DPP across the quad
+            if (!fin) parked = false;
+        }
+        if (fin || parked) continue;
+        if (!(i > 0 && j > 0)) { fin = true; continue; }     // LG: an edge ends the walk; GG: the edge tail below
+        if (LG && st == 0 && V <= 0) { fin = true; continue; }   // M == max(D, 0) <= 0
+        if (cr < 0 || cq < 0) { parked = true; continue; }     // the walk left the block
+        const uint32_t f = flag_of(cr, cq);
+        if (st == 0) {
+            if (f & 8u) {
+                const bool v = match_of(cr, cq);
+                emit(v ? 'M' : (allow ? 'S' : 'X'));
+                V -= v ? MA : MI;
+                --i; --j; --cr; --cq;
+            } else {
+                st = (f & 4u) ? 1 : 2;   // M == Ix, else M == Iy (the same value)
+            }
+        } else if (st == 1) {
+            if constexpr (LG) {
+                if (f & 2u) { emit('U'); V -= GE; --i; --cr; }
+                else if (V > 0) { emit('U'); V -= GOE; --i; --cr; st = 0; }
+                else if (V == 0) { emit('u'); fin = true; }
+                else { flags |= SA_FLAG_DIVERGED; fin = true; }
+            } else {
+                emit('U'); --i; --cr;
+                if (!(f & 2u)) st = 0;   // gap open: Ix == M[i-1][j] + GO + GE
+            }
+        } else {
+            if constexpr (LG) {
+                if (f & 1u) { emit('L'); V -= GE; --j; --cq; }
+                else if (V > 0) { emit('L'); V -= GOE; --j; --cq; st = 0; }
+                else if (V == 0) { emit('l'); fin = true; }
+                else { flags |= SA_FLAG_DIVERGED; fin = true; }
+            } else {
+                emit('L'); --j; --cq;
+                if (!(f & 1u)) st = 0;
+            }
+        }
+    }
+    if constexpr (!LG) {
+        // SAGlobalGotoh.h:312-319, :370-377: on the edge j == 0 the walk moves up, on i == 0 left,
+        // whatever its state
+        if (live) {
+            for (; i > 0; --i) emit('U');
+            for (; j > 0; --j) emit('L');
+        }
+    }
+    if (live && sub == 0) {
+        res.start_i = i;
+        res.start_j = j;
+        res.nops = k;
+        res.flags = flags;
+        P.res[pidx] = res;
+    }
+}
+
 template <int ALG>
 hipError_t launch_so4(int R, int lp, dim3 grid, dim3 block, const TbParams& p, hipStream_t stream) {
     if (lp == 8) {
@@ -768,6 +1060,22 @@ hipError_t launch_so4(int R, int lp, dim3 grid, dim3 block, const TbParams& p, h
 
 hipError_t launch_traceback_so(int algo, int R, const TbParams& p, hipStream_t stream) {
     const dim3 block(64);
+    if (algo == SA_LOCAL_GOTOH || algo == SA_GLOBAL_GOTOH) {   // four lanes per pair
+        const dim3 grid((p.count + 15) / 16);
+#define SA_TB_SOA(RR)                                                                                       \
+    case RR:                                                                                                \
+        if (algo == SA_LOCAL_GOTOH) hipLaunchKernelGGL((traceback_soa_kernel<SA_LOCAL_GOTOH, RR>), grid, block, 0, stream, p); \
+        else hipLaunchKernelGGL((traceback_soa_kernel<SA_GLOBAL_GOTOH, RR>), grid, block, 0, stream, p);     \
+        break;
+        switch (R) {
+            SA_TB_SOA(4)
+            SA_TB_SOA(8)
+            SA_TB_SOA(16)
+            default: return hipErrorInvalidValue;
+        }
+#undef SA_TB_SOA
+        return hipGetLastError();
+    }
     if (algo != SA_SW && algo != SA_NW) return hipErrorInvalidValue;
     const char* e = getenv("SEQALIB_TB_SO");
     if (algo == SA_SW && e && e[0] == '1') {   // (the one-lane walker is SW only)

@@ -20,3 +20,12 @@ def engine():
     eng = seqalib_amd.Engine(0)
     yield eng
     eng.close()
+
+
+@pytest.fixture(autouse=True)
+def _batch_kernels(request, monkeypatch):
+    """Modules that test the batch kernels (BATCH_KERNELS = True) keep their small host calls off
+    the small-call kernel (SEQALIB_TINY=0, sa_tiny.hip); a test may set it back.  The small-call
+    kernel has its own tests (test_gpu_tiny.py) and runs by default everywhere else."""
+    if getattr(request.module, "BATCH_KERNELS", False):
+        monkeypatch.setenv("SEQALIB_TINY", "0")

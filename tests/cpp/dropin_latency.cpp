@@ -4,8 +4,11 @@
 //   * config 1: NeedlemanWunschSA<std::string,char,'-'>(ScoringSystem(-1,2), equal<char>) on
 //     test/Test.cpp's pair "AAAGAATGCAT" / "AAACTCAT";
 //   * one 1024 x 1024 SmithWatermanSA (default scoring) DNA pair.
-// The first call (HIP context, workspace) is reported apart; then `reps` calls are timed one by one.
-// Prints one JSON line.   dropin_latency [reps=200] [nw|sw: that call only]
+// The first-call costs are reported apart: "context_us" opens the drop-in's HIP context (runtime
+// start-up + stream), each call's "first_call_us" is its first getAlignment (code-object load at
+// the first launch, pinned buffers); then `reps` calls are timed one by one.  With
+// SEQALIB_HOST_TIMING set the library prints each call's host phases to stderr (bench.py reads
+// them).  Prints one JSON line.   dropin_latency [reps=200] [nw|sw: that call only]
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -44,7 +47,11 @@ int main(int argc, char** argv) {
     std::string x(1024, 'A'), y(1024, 'A');
     sa_synth_dna(1000000001ull, 1024, reinterpret_cast<uint8_t*>(&x[0]));   // config 1 x 1e9 seeds
     sa_synth_dna(1000000002ull, 1024, reinterpret_cast<uint8_t*>(&y[0]));
+    const auto c0 = std::chrono::steady_clock::now();
+    seqalib::detail::context();
+    const double ctx_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c0).count();
     printf("{\"what\": \"C++ drop-in getAlignment per call (aligner constructed per call, as include/Test.cpp:98-107)\", ");
+    printf("\"context_us\": %.1f, ", ctx_us);
     if (only != "sw") timed("nw_11x8", reps, [&] {
         AlignedSequence<char, '-'> r = NeedlemanWunschSA<std::string, char, '-'>(ScoringSystem(-1, 2), equal<char>).getAlignment(a, b);
         return r.Data.size();

@@ -15,6 +15,7 @@ import seqalib_amd as sa
 from util import linear_rescore, oracle_batch, oracle_sw_scores, subset
 
 pytestmark = pytest.mark.gpu
+BATCH_KERNELS = True   # small host calls stay on the batch kernels (conftest.py)
 
 SW = (-1, 1, -1)   # SmithWatermanSA::getDefaultScoring (SASmithWaterman.h:352)
 THREADS = 16       # the GPU box's host share

@@ -61,7 +61,7 @@ def check(engine, algo, args, pairs, match):
         got = (r.score, r.end_i, r.end_j, r.start_i, r.start_j, r.ops)
         exp = (o["score"], o["end_i"], o["end_j"], o["start_i"], o["start_j"], o["ops"])
         assert got == exp, (algo, args, len(a), len(b))
-        assert r.flags & ~sa.SA_FLAG_SIZE_HACK == 0
+        assert (r.flags & ~sa.SA_FLAG_SIZE_HACK) == 0
 
 
 @pytest.mark.parametrize("algo", [0, 1, 2, 3, 4, 5])

@@ -13,6 +13,7 @@ import seqalib_amd as sa
 from util import ALGOS, golden_sequences, load_golden, named_lut, oracle_align, rows_digest
 
 pytestmark = pytest.mark.gpu
+BATCH_KERNELS = True   # small host calls stay on the batch kernels (conftest.py)
 
 
 def sc_obj(args):
@@ -39,7 +40,7 @@ def check_golden(engine, entries):
         pairs = [golden_sequences(e) for e in es]
         res = run_group(engine, ALGOS[algo], args, match, pairs)
         for e, (a, b), r in zip(es, pairs, res):
-            assert r.flags & (sa.SA_FLAG_DIVERGED | sa.SA_FLAG_BAD_SHAPE) == 0, e["id"]
+            assert (r.flags & (sa.SA_FLAG_DIVERGED | sa.SA_FLAG_BAD_SHAPE)) == 0, e["id"]
             if e["score"] is not None:   # None: the reference exposes no score (MyersMillerSA)
                 assert r.score == e["score"], e["id"]
             assert (r.end_i, r.end_j) == (e["max_row"], e["max_col"]), e["id"]
@@ -66,6 +67,24 @@ def test_golden_kat(engine):
 
 def test_golden_random(engine):
     assert check_golden(engine, load_golden("random.jsonl")) > 200
+
+
+def test_golden_small_calls(engine, monkeypatch):
+    """The known-answer and random vectors of the unmodified reference, one getAlignment() per
+    pair as its tests call it: every pair within the small-call limits is its own host call on
+    the small-call kernel (sa_tiny.hip)."""
+    monkeypatch.setenv("SEQALIB_TINY", "1")
+    n = 0
+    for name in ("kat.jsonl", "random.jsonl"):
+        for e in load_golden(name):
+            if ALGOS[e["algo"]] > 3:
+                continue
+            a, b = golden_sequences(e)
+            if len(a) > 256 or len(b) > 1024 or len(a) * len(b) > 32768:
+                continue
+            n += check_golden(engine, [e])
+            assert engine.last_plan()[0] == sa.SA_KERNEL_TINY, e["id"]
+    assert n > 1000
 
 
 def test_golden_hirschberg(engine):
@@ -307,7 +326,7 @@ def test_split_plan_vs_oracle(engine, algo, monkeypatch):
     for args in SCORINGS[algo]:
         compare_with_oracle(engine, algo, args, pairs)
         assert engine.last_plan()[1:] == (R0, 0), args
-        assert all(r.flags & sa.SA_FLAG_TIMEOUT == 0 for r in engine.align(algo, sc_obj(args), pairs[:2]))
+        assert all((r.flags & sa.SA_FLAG_TIMEOUT) == 0 for r in engine.align(algo, sc_obj(args), pairs[:2]))
     for r in (1, 2, 4, 8):
         monkeypatch.setenv("SEQALIB_PLAN", f"{r},0")
         for args in SCORINGS[algo][:2]:
@@ -807,3 +826,34 @@ def test_segmented_traceback_vs_oracle(engine, algo, monkeypatch):
     long_pairs = [(a, sa.synth_mutate(a, 99)), (sa.synth_dna(42_100, 2900), sa.synth_dna(42_101, 3100))]
     for args in SCORINGS[algo][:2]:
         compare_with_oracle(engine, algo, args, long_pairs)
+
+
+@pytest.mark.parametrize("algo", [0, 2])
+def test_keyed_end_cell_vs_oracle(engine, algo, monkeypatch):
+    """SEQALIB_CMAX=0: the local modes' T16 fills keep per-cell (score, column) keys instead of the
+    chunk maxima + end-cell replay; same results as the oracle on a many-pairs batch."""
+    pairs = dna_pairs(60 + algo, 1100, 300)
+    monkeypatch.setenv("SEQALIB_CMAX", "0")
+    compare_with_oracle(engine, algo, SCORINGS[algo][0], pairs[:200] + pairs[-30:])
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    big = [(sa.synth_dna(61_000 + k, 700), sa.synth_mutate(sa.synth_dna(61_000 + k, 700), k)) for k in range(1100)]
+    res = engine.align(algo, sc_obj(SCORINGS[algo][0]), big)
+    assert engine.last_plan()[0] == sa.SA_KERNEL_T16
+    for k in (0, 1, 517, 1099):
+        o = oracle_align(algo, SCORINGS[algo][0], *big[k])
+        assert (res[k].score, res[k].end_i, res[k].end_j, res[k].ops) == (o["score"], o["end_i"], o["end_j"], o["ops"])
+
+
+def test_kernel_timing_switch(engine, monkeypatch):
+    """SEQALIB_KERNEL_TIMING: sa_last_kernel_timings reports the fill kernels alone (<= the fill
+    stream span) for a call made with it, and fails for a call made without it."""
+    pairs = dna_pairs(70, 1100, 400)
+    monkeypatch.setenv("SEQALIB_KERNEL_TIMING", "1")
+    engine.align(0, sc_obj((-1, 1, -1)), pairs)
+    fk, fs = engine.last_kernel_timings()
+    assert 0 < fk <= fs * 1.001 + 1e-3
+    assert fs <= engine.last_timings()[0] * 1.001 + 1e-3
+    monkeypatch.delenv("SEQALIB_KERNEL_TIMING")
+    engine.align(0, sc_obj((-1, 1, -1)), pairs)
+    with pytest.raises(sa.SeqalibError):
+        engine.last_kernel_timings()

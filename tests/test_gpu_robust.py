@@ -16,6 +16,7 @@ from test_gpu_parity import SCORINGS, compare_with_oracle, sc_obj
 from util import oracle_align
 
 pytestmark = pytest.mark.gpu
+BATCH_KERNELS = True   # small host calls stay on the batch kernels (conftest.py)
 SA_FLAG_RECOVERED = 16
 
 

@@ -19,6 +19,7 @@ import seqalib_amd as sa
 from util import linear_rescore, oracle_align, oracle_batch, oracle_sw_scores, subset
 
 pytestmark = pytest.mark.gpu
+BATCH_KERNELS = True   # small host calls stay on the batch kernels (conftest.py)
 
 SW = (-1, 1, -1)   # SmithWatermanSA::getDefaultScoring (SASmithWaterman.h:352)
 THREADS = 16
@@ -244,4 +245,73 @@ def test_so_nw_batch_1024_every_pair(engine):
         assert int(res["score"][p]) == int(ores["score"][q]), int(p)
         assert ops[off:off + int(res["nops"][p])].tobytes() == oops[ooff:ooff + int(ores["nops"][q])].tobytes(), int(p)
     tg = run(engine, False, s1, o1, s2, o2, scoring=NW, algo=1)
+    assert_same(so, tg, o1, o2)
+
+
+LG_SIZE_HACK = {(314, 288), (60, 57), (61, 58)}   # SALocalGotoh.h:484-488 (parity unpinned there)
+AFF = [(2, (-3, -1, 1, -1, True)), (2, (-3, -1, 1, -1, False)), (3, (-3, -1, 1, -1, True))]
+
+
+@pytest.mark.parametrize("algo,scoring", AFF)
+@pytest.mark.parametrize("maxlen,R", [(200, 4), (500, 8), (1000, 16), (2000, 16)])
+def test_so_affine_ragged_matches_tagged_and_oracle(engine, algo, scoring, maxlen, R):
+    """Score-only LocalGotoh / GlobalGotoh (the SO affine cell: A = Ix - GOE, B = Iy - GOE, 8 fast ops
+    + v_bfe per cell, no records; the traceback recomputes its blocks with the tagged affine cell
+    from the snapshots and the 32-bit edge stream): ragged batches on every plan (R = 4, 8, 16; one
+    and two bands), identical to the tagged path on every pair, a sample and every edge shape against
+    the full-matrix oracle."""
+    batch = ragged_batch(120 + maxlen + algo, 1100, maxlen)
+    so = run(engine, True, *batch, scoring=scoring, algo=algo)
+    recs = engine.last_plan_ex()[3]
+    tg = run(engine, False, *batch, scoring=scoring, algo=algo)
+    kern = sa.SA_KERNEL_T16_ENDCELL if algo == 2 else sa.SA_KERNEL_T16
+    assert so[2] == (kern, R, 1) and tg[2] == so[2]
+    assert recs == sa.SA_RECORDS_SCORE_ONLY
+    s1, o1, s2, o2 = batch
+    assert ((so[0]["flags"] & np.uint32(0xffffffff ^ sa.SA_FLAG_SIZE_HACK)) == 0).all()
+    assert_same(so, tg, o1, o2)
+    idx = np.unique(np.concatenate([np.arange(11), np.random.default_rng(maxlen + algo).choice(len(o1) - 1, 40, replace=False)]))
+    idx = [int(p) for p in idx if (int(o1[p + 1] - o1[p]), int(o2[p + 1] - o2[p])) not in LG_SIZE_HACK]
+    check_vs_oracle(algo, scoring, so, batch, idx)
+
+
+def test_so_affine_lut(engine):
+    """Score-only Gotoh with a non-identity match table (A~G, C~T) and (-2, -1, 2, -1): identical to
+    the tagged path, a sample against the oracle."""
+    batch = ragged_batch(13, 1030, 700)
+    lut = np.zeros((256, 256), np.uint8)
+    for x in b"ACGT":
+        lut[x, x] = 1
+    for x, y in (b"AG", b"GA", b"CT", b"TC"):
+        lut[x, y] = 1
+    for algo in (2, 3):
+        for scoring, lt in (((-2, -1, 2, -1, True), None), ((-3, -1, 1, -1, True), lut)):
+            so = run(engine, True, *batch, scoring=scoring, lut=lt, algo=algo)
+            assert engine.last_plan_ex()[3] == sa.SA_RECORDS_SCORE_ONLY, (algo, scoring)
+            tg = run(engine, False, *batch, scoring=scoring, lut=lt, algo=algo)
+            assert_same(so, tg, batch[1], batch[3])
+            check_vs_oracle(algo, scoring, so, batch, [0, 1, 2, 3, 4, 5, 11, 12, 13, 14, 15, 1029], lut=lt)
+
+
+@pytest.mark.parametrize("algo", [2, 3])
+def test_so_affine_batch_1024(engine, algo):
+    """10,000 x 1024^2 LocalGotoh / GlobalGotoh (-3, -1, 1, -1, true), the configs legs of bench.py:
+    every pair identical to the tagged path, 96 pairs against the full-matrix oracle."""
+    scoring = (-3, -1, 1, -1, True)
+    s1, o1, s2, o2 = sa.synth_dna_batch(7_000_000_000 + algo, 10000, 1024, 1024, threads=THREADS)
+    so = run(engine, True, s1, o1, s2, o2, scoring=scoring, algo=algo)
+    assert so[2][1:] == (16, 1)
+    assert (so[0]["flags"] == 0).all()
+    jdx = np.sort(np.random.default_rng(algo).choice(10000, 96, replace=False))
+    sub = subset(s1, o1, s2, o2, jdx)
+    ores, oops = oracle_batch(algo, scoring, *sub, threads=THREADS)
+    res, ops = so[0], so[1]
+    for q, p in enumerate(jdx):
+        off = int(o1[p] + o2[p]) + int(p)
+        ooff = int(sub[1][q] + sub[3][q]) + q
+        got = tuple(int(res[f][p]) for f in ("score", "end_i", "end_j", "start_i", "start_j"))
+        exp = tuple(int(ores[f][q]) for f in ("score", "end_i", "end_j", "start_i", "start_j"))
+        assert got == exp, (int(p), got, exp)
+        assert ops[off:off + int(res["nops"][p])].tobytes() == oops[ooff:ooff + int(ores["nops"][q])].tobytes(), int(p)
+    tg = run(engine, False, s1, o1, s2, o2, scoring=scoring, algo=algo)
     assert_same(so, tg, o1, o2)

@@ -10,6 +10,8 @@ one JSON line per config.
   config 4  1 x 8192^2 LocalGotoh (-3,-1,1,-1,false)   one pair (and the 4-argument scoring's
                                                        allowMismatch = true); ref 1 thread
   config 5  12,500 x 2048^2 SW                         one GPU's shard of 100,000 pairs over 8
+  nw/lg/gg  10,000 x 1024^2 NW (-1,2,-1), LocalGotoh / GlobalGotoh (-3,-1,1,-1,true): the score-only
+            fill and the tagged one beside it, every pair vs the full-matrix oracle
   gotoh     10,000 x 1024^2 Local/GlobalGotoh          T16 affine vs int32 kernel (tuning, not in bench)
 
 Seeds: config c uses base c x 1e9.  Reference semantics: SASmithWaterman.h:358-366
@@ -231,6 +233,54 @@ def measure(sa, torch, eng, dev, only=("2", "3", "4", "5"), threads=16):
             g, cdt = ref_batch_sw(s1, o1, s2, o2, 8 * threads, threads)
             line["cpu_reference"] = {"gcups": round(g, 3), "cores": threads, "speedup": round(cells / dtp / 1e9 / g, 1),
                                      "sample": f"first {8 * threads} pairs, {cdt:.2f} s"}
+        out.append(line)
+        del d, outs
+    for key, algo, name, args in (("nw", sa.SA_NW, "NeedlemanWunsch", (-1, 2, -1)),
+                                  ("lg", sa.SA_LOCAL_GOTOH, "LocalGotoh", (-3, -1, 1, -1, True)),
+                                  ("gg", sa.SA_GLOBAL_GOTOH, "GlobalGotoh", (-3, -1, 1, -1, True))):
+        if key not in only:
+            continue
+        # 10,000 x 1024^2 batches of the other three aligners: the score-only fill (pipelined steps,
+        # as the headline), the tagged-record fill beside it (SEQALIB_SO=0, serial calls), every
+        # pair's full result and op stream against the full-matrix oracle, the reference beside it
+        P = 10000
+        s1, o1, s2, o2 = sa.synth_dna_batch(6 * 10 ** 9 + algo, P, 1024, 1024, threads=threads)
+        d, outs, n = r.put(s1, o1, s2, o2)
+        sc = sa.ScoringSystem(*args)
+        cells = P * 1024 * 1024
+        dtp, k, fill_ms, tb_ms = r.time_calls(algo, sc, d, outs, n, 1024, 1024, 10, True)
+        fk_so = r.fill_kernel_ms
+        plan = list(eng.last_plan_ex())
+        res, ops = r.results(outs, k)
+        os.environ["SEQALIB_SO"] = "0"
+        try:
+            dtt, _, _, _ = r.time_calls(algo, sc, d, outs, n, 1024, 1024, 3, False)
+            fk_tag = r.fill_kernel_ms
+        finally:
+            os.environ.pop("SEQALIB_SO")
+        t0 = time.perf_counter()
+        ok = parity_full(algo, args, s1, o1, s2, o2, res, ops, np.arange(P), threads)
+        line = {"config": key, "workload": f"10,000 x 1024^2 {name} ({','.join(str(x).lower() for x in args)})",
+                "gcups": round(cells / dtp / 1e9, 1), "ms_per_step": round(dtp * 1e3, 3),
+                "fill_ms": round(fill_ms, 3), "fill_gcups": round(cells / (fk_so or fill_ms) / 1e6, 1),
+                "traceback_ms": round(tb_ms, 3), "fill_kernel_ms": round(fk_so, 3) if fk_so else None,
+                "plan": plan, "records": "score-only" if plan[3] == sa.SA_RECORDS_SCORE_ONLY else "tagged",
+                "tagged_fill_kernel_ms": round(fk_tag, 3) if fk_tag else None,
+                "tagged_fill_gcups": round(cells / fk_tag / 1e6, 1) if fk_tag else None,
+                "parity": {"pairs_bit_exact": f"{ok}/{P}", "what": "score, end cell, start cell and op stream of every "
+                           "pair vs the full-matrix oracle", "check_s": round(time.perf_counter() - t0, 1),
+                           "exact": ok == P}}
+        if have_ref:
+            from concurrent.futures import ThreadPoolExecutor
+            ks = 16 * threads
+            t0 = time.perf_counter()
+            with ThreadPoolExecutor(threads) as ex:   # (ctypes releases the GIL)
+                list(ex.map(lambda p: ref_one(algo, args, s1[o1[p]:o1[p + 1]].tobytes(), s2[o2[p]:o2[p + 1]].tobytes()),
+                            range(ks)))
+            cdt = time.perf_counter() - t0
+            g = ks * 1024 * 1024 / cdt / 1e9
+            line["cpu_reference"] = {"gcups": round(g, 3), "cores": threads, "speedup": round(cells / dtp / 1e9 / g, 1),
+                                     "sample": f"first {ks} pairs, getAlignment per pair, {cdt:.2f} s"}
         out.append(line)
         del d, outs
     if "gotoh" in only:   # batched affine: T16 affine kernel vs the int32 kernel (SEQALIB_T16=0)

@@ -29,7 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="4096,8192,10000,12288")
     ap.add_argument("--len", type=int, default=4096)
-    ap.add_argument("--variants", default="base;SEQALIB_ENDCELL_TB=1;SEQALIB_FILL2=1;SEQALIB_FILL2=1,SEQALIB_ENDCELL_TB=1")
+    ap.add_argument("--variants", default="base")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=2)
     a = ap.parse_args()
