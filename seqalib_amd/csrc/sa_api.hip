@@ -822,6 +822,37 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fv.so = v.so;
             return fv;
         };
+        auto make_tp = [&](int k) {
+            const Variant& v = vars[k];
+            TbParams tp{};
+            tp.seq1 = d1; tp.off1 = o1; tp.seq2 = d2; tp.off2 = o2;
+            tp.lutbits = lut ? d_lutbits : nullptr;
+            tp.vrec = bits ? 1 : 0;
+            tp.dirs = fps[k].dirs; tp.dir_slot = v.pl.g.dir_slot;
+            tp.ops = d_ops; tp.res = d_res;
+            tp.pair_base = (uint32_t)base; tp.count = cnt;
+            tp.max_m = max_m; tp.max_n = max_n;
+            tp.gap = fps[k].gap; tp.match = fps[k].match; tp.mismatch = fps[k].mismatch;
+            tp.gap_open = fps[k].gap_open; tp.gap_extend = fps[k].gap_extend;
+            tp.allow = (allow || v.t16) ? 1 : 0;
+            tp.tagged = v.t16 ? 1 : 0;
+            tp.sel = fps[k].sel; tp.sel_want = fps[k].sel_want;
+            tp.rerun = fps[k].rerun;
+            tp.band_stride = v.pl.g.band_stride;
+            tp.snap_h = fps[k].snap_h; tp.snap_p = fps[k].snap_p;
+            tp.snap_h_slot = v.snap_h_slot; tp.snap_p_slot = v.snap_p_slot; tp.snap_nch = v.snap_nch;
+            tp.prof = fps[k].prof;
+            tp.t16_delta = fps[k].t16_delta;
+            tp.t16_sent = fps[k].t16_sent;
+            return tp;
+        };
+        // Pipelined calls: the int32 variant of a T16 batch (it re-runs only the pairs the T16 fill
+        // flagged, or every pair when the device chose int32) walks its traceback on the fill stream
+        // right after its fill.  On the traceback stream, behind the score-only traceback, its
+        // workgroups waited for the next call's fill to be dispatched (up to 9.6 ms, round 4 rocprof)
+        // and delayed the slot's release to the call after it.
+        const char* e_sk = getenv("SEQALIB_SKIPTB_STB");   // A/B (round 5), removed after measuring
+        const bool tb_on_fill = pipe && nv == 2 && !vars[1].t16 && !vars[1].pl.split && !(e_sk && e_sk[0] == '1');
         for (int k = 0; k < nv; ++k) {
             const Variant& v = vars[k];
             const Plan& pl = v.pl;
@@ -875,35 +906,17 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 e = (v.so && algo == SA_SW) ? launch_endcell_so(pl.R, ep, sf) : launch_endcell(algo, pl.R, ep, sf);
                 if (e != hipSuccess) return hip_fail(c, e, "end-cell kernel launch");
             }
+            if (tb_on_fill && k == 1) {
+                const TbParams tp = make_tp(k);
+                e = tb_wave(cnt) ? launch_traceback_wave(algo, pl.R, lut, tp, sf) : launch_traceback(algo, pl.R, lut, tp, sf);
+                if (e != hipSuccess) return hip_fail(c, e, "traceback kernel launch");
+            }
         }
         SA_HIP(c, hipEventRecord(ev[1], sf));
         if (pipe) SA_HIP(c, hipStreamWaitEvent(stb, ev[1], 0));
-        auto make_tp = [&](int k) {
-            const Variant& v = vars[k];
-            TbParams tp{};
-            tp.seq1 = d1; tp.off1 = o1; tp.seq2 = d2; tp.off2 = o2;
-            tp.lutbits = lut ? d_lutbits : nullptr;
-            tp.vrec = bits ? 1 : 0;
-            tp.dirs = fps[k].dirs; tp.dir_slot = v.pl.g.dir_slot;
-            tp.ops = d_ops; tp.res = d_res;
-            tp.pair_base = (uint32_t)base; tp.count = cnt;
-            tp.max_m = max_m; tp.max_n = max_n;
-            tp.gap = fps[k].gap; tp.match = fps[k].match; tp.mismatch = fps[k].mismatch;
-            tp.gap_open = fps[k].gap_open; tp.gap_extend = fps[k].gap_extend;
-            tp.allow = (allow || v.t16) ? 1 : 0;
-            tp.tagged = v.t16 ? 1 : 0;
-            tp.sel = fps[k].sel; tp.sel_want = fps[k].sel_want;
-            tp.rerun = fps[k].rerun;
-            tp.band_stride = v.pl.g.band_stride;
-            tp.snap_h = fps[k].snap_h; tp.snap_p = fps[k].snap_p;
-            tp.snap_h_slot = v.snap_h_slot; tp.snap_p_slot = v.snap_p_slot; tp.snap_nch = v.snap_nch;
-            tp.prof = fps[k].prof;
-            tp.t16_delta = fps[k].t16_delta;
-            tp.t16_sent = fps[k].t16_sent;
-            return tp;
-        };
         for (int k = 0; k < nv; ++k) {
             const Variant& v = vars[k];
+            if (tb_on_fill && k == 1) continue;   // walked on the fill stream (above)
             TbParams tp = make_tp(k);
             if (seg_on && v.pl.split && tb_wave(cnt)) {
                 tp.seg_mode = seg_mode;

@@ -469,18 +469,9 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         cc = s >> 5;
         cq = s & 31;
     };
-    // the walk's view of the block, in registers: the quad's R row codes and 32 column codes (2 bits
-    // each), the tag column it stands in (W, the four sublanes' words) and the one to its left (NW,
-    // read ahead so that a diagonal or left move finds it ready)
+    // the walk's view of the block: the quad's R row codes and 32 column codes (2 bits each) in
+    // registers; the move tags stay in LDS ([column q][lane] words, sublane r / RS, bits 2 (r % RS))
     uint64_t rowc = 0, colc = 0;
-    uint64_t W = 0, NW = 0, NNW = 0;   // tag columns wq, wq - 1, wq - 2: row r at bits 2r
-    int wq = -1;
-    auto tagcol = [&](int q) __attribute__((always_inline)) -> uint64_t {   // the quad's LP words, packed
-        uint64_t t = 0;
-#pragma unroll
-        for (int k = 0; k < LP; ++k) t |= (uint64_t)vw[q * 64 + quad * LP + k] << (2 * RS * k);
-        return t;
-    };
     auto pack_codes = [&](int base) __attribute__((always_inline)) -> uint64_t {   // 32 bytes of 8 x code
         uint64_t c = 0;
 #pragma unroll
@@ -539,6 +530,21 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         for (int r = 0; r < RS; ++r) { Hp[r] = 0; tab[r] = pf0; }
         if (act) {
             const int rs0 = sub * RS;   // block-relative first row
+            // Every load of the block's inputs is issued before any value is used, so a round pays one
+            // memory round trip, not one per load (round 5: 9.4K -> ? cycles of load wait per round)
+            // (unconditional loads at clamped addresses: a recompute runs only for a cell (i, j) >= (1,
+            // 1), so m, n >= 1; without a left column the snapshot words are read from the slot's first)
+            uint32_t w[RS], b1[RS], b2[32 / LP];
+            const uint64_t e = has_left ? (uint64_t)cb * snap_nch + (cc - 1) : 0;
+            const uint32_t* sh = sh_base + e * (R / 2) * kWave + ct;
+#pragma unroll
+            for (int r = 0; r < RS; ++r) w[r] = sh[((rs0 + r) >> 1) * kWave];
+            const uint32_t wc = sh[(rs0 > 0 ? (rs0 - 1) >> 1 : 0) * kWave];
+            const int32_t pc = sp_base[e * kWave + ct];
+#pragma unroll
+            for (int r = 0; r < RS; ++r) b1[r] = s1[min(r0 + rs0 + r, m - 1)];
+#pragma unroll
+            for (int x = 0; x < 32 / LP; ++x) b2[x] = s2[min(max(j0 + sub * (32 / LP) + x, 0), n - 1)];
             if constexpr (NWK) {
                 // NW borders (SANeedlemanWunsch.h:59-62): the left column j0 <= 0 is column 0 (row i
                 // holds i * Gap), the corner of a first row r0 = 0 is H(0, j0) = j0 * Gap
@@ -551,32 +557,21 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
                 }
             }
             if (has_left) {
-                const uint64_t e = (uint64_t)cb * snap_nch + (cc - 1);
-                const uint32_t* sh = sh_base + e * (R / 2) * kWave + ct;
 #pragma unroll
-                for (int r = 0; r < RS; ++r) {
-                    const int rr = rs0 + r;
-                    const uint32_t w = sh[(rr >> 1) * kWave];
-                    Hp[r] = (int)((rr & 1) ? (w >> 16) : (w & 0xffffu)) << 2;
-                }
-                if (rs0 > 0) {
-                    const uint32_t w = sh[((rs0 - 1) >> 1) * kWave];
-                    corner = (int)(((rs0 - 1) & 1) ? (w >> 16) : (w & 0xffffu)) << 2;
-                } else if (r0 > 0) {
-                    corner = (sp_base[e * kWave + ct] & 0xffff) << 2;
-                }
+                for (int r = 0; r < RS; ++r) Hp[r] = (int)(((rs0 + r) & 1) ? (w[r] >> 16) : (w[r] & 0xffffu)) << 2;
+                if (rs0 > 0) corner = (int)(((rs0 - 1) & 1) ? (wc >> 16) : (wc & 0xffffu)) << 2;
+                else if (r0 > 0) corner = (pc & 0xffff) << 2;
             }
 #pragma unroll
             for (int r = 0; r < RS; ++r) {
-                const int row = r0 + rs0 + r;
-                const uint32_t c8 = row < m ? so_code8(symp, s1[row]) : 0u;
+                const uint32_t c8 = r0 + rs0 + r < m ? so_code8(symp, b1[r]) : 0u;
                 tab[r] = c8 == 0 ? pf0 : c8 == 8 ? pf1 : c8 == 16 ? pf2 : pf3;
                 vb[L::kRowC + quad * 32 + rs0 + r] = (uint8_t)c8;
             }
 #pragma unroll
-            for (int e = 0; e < 32 / LP; ++e) {
-                const int q = sub * (32 / LP) + e, jj = j0 + q;
-                vb[L::kColC + quad * 32 + q] = (uint8_t)(q >= qlo && q <= qhi && jj < n ? so_code8(symp, s2[jj]) : 0u);
+            for (int x = 0; x < 32 / LP; ++x) {
+                const int q = sub * (32 / LP) + x, jj = j0 + q;
+                vb[L::kColC + quad * 32 + q] = (uint8_t)(q >= qlo && q <= qhi && jj < n ? so_code8(symp, b2[x]) : 0u);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the edge DMA and the code stores
@@ -588,32 +583,28 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         }
 #endif
         // sub-steps: sublane k at column qlo + u - k; its row above from sublane k-1 (DPP).  The
-        // column code and (sublane 0) the top row value of the next sub-step are read one sub-step
-        // ahead, so no sub-step waits on LDS.
+        // column codes come from the quad's packed 2-bit codes (registers), sublane 0's top-row value
+        // of the next sub-step is read one sub-step ahead from an always-valid LDS address, so a
+        // sub-step neither branches round an LDS read nor waits for one.
+        if (act) colc = pack_codes(L::kColC + quad * 32);   // (in-order LDS: the codes stored above)
         int hl = Hp[RS - 1];
         int prev_up = corner;
         int nmax = qhi - qlo + 1 + (LP - 1);   // sub-steps of this quad; the wave runs the most of any
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
-        auto rd_sym = [&](int q) __attribute__((always_inline)) -> uint32_t {
-            return act && q >= qlo && q <= qhi ? (uint32_t)vb[L::kColC + quad * 32 + q] : 0u;
-        };
-        auto rd_top = [&](int q) __attribute__((always_inline)) -> int {
-            if (sub != 0 || !act || q < qlo || q > qhi) return 0;
-            if (!has_top) return NWK ? border(j0 + q + 1) : 0;   // row 0: H(0, j) = j * Gap (NW), 0 (SW)
+        auto rd_top = [&](int q) __attribute__((always_inline)) -> int {   // (used by sublane 0 only)
             const int s = slo + q;
-            const int d = (s >> 3) - pk0;
+            const int d = min(max((s >> 3) - pk0, 0), 4);
             const int off = (LP >= 5 || d < 4) ? L::kEdge + (quad * LP + d) * 16 : L::kEdge2 + quad * 64;
-            return (int)((lds_u16*)(s_so + off + (s & 7) * 2))[0] << 2;
+            const int v = (int)((lds_u16*)(s_so + off + (s & 7) * 2))[0] << 2;
+            return has_top ? v : NWK ? border(j0 + q + 1) : 0;   // row 0: H(0, j) = j * Gap (NW), 0 (SW)
         };
-        uint32_t nsym = rd_sym(qlo - sub);
         int ntop = rd_top(qlo);
         for (int u = 0; u < nmax; ++u) {
             const int q = qlo + u - sub;
-            const uint32_t sym = nsym;
             const int top = ntop;
-            nsym = rd_sym(q + 1);
-            ntop = rd_top(q + 1);
+            ntop = rd_top(qlo + u + 1);
+            const uint32_t sym = (uint32_t)((colc >> (2 * (q & 31))) & 3u) << 3;
             // the row above from sublane k-1: quad_perm [0,0,1,2] (LP = 4) / row_shr:1 (LP = 8; the
             // sublane 0 lanes, which take lane 7 of the previous group, use the top row instead)
             int up_h = LP == 4 ? __builtin_amdgcn_mov_dpp(hl, 0x90, 0xf, 0xf, false)
@@ -653,66 +644,66 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         st_sub += __builtin_amdgcn_s_memtime() - st_a;
         st_nsub += (unsigned long long)nmax;
 #endif
-        if (act) {   // (in-order LDS: these reads see the codes and tags stored above)
-            rowc = pack_codes(L::kRowC + quad * 32);
-            colc = pack_codes(L::kColC + quad * 32);
-            wq = qhi;
-            W = tagcol(qhi);
-            NW = tagcol(max(qhi - 1, 0));
-            NNW = tagcol(max(qhi - 2, 0));
-        }
+        if (act) rowc = pack_codes(L::kRowC + quad * 32);
     };
 
     int i = res.end_i, j = res.end_j, V = res.score;
     if (!NWK && (m == 0 || n == 0)) { i = 0; j = 0; }
     bool fin = !live, parked = true;
-    // One move per iteration, branch-free (a lone wave pays for every divergent branch): every lane
-    // evaluates the move of its cell and applies it only when it may (mv).  A move lands in the
-    // walk's tag column or one to its left (W / NW); the column two to the left (NNW) is read a
-    // full iteration before it can be needed.
+    auto half = [](uint64_t x, uint32_t b) __attribute__((always_inline)) -> uint32_t {
+        return ((b < 32 ? (uint32_t)x : (uint32_t)(x >> 32)) >> (b & 31u)) & 3u;
+    };
+    // the tag of block cell (r, q): word [q][quad * LP + r / RS], bits 2 (r % RS)
+    const uint32_t tag_base = (uint32_t)(quad * LP);
+    auto tag_at = [&](int r, int q) __attribute__((always_inline)) -> uint32_t {
+        const uint32_t w = vw[(uint32_t)q * 64u + tag_base + (uint32_t)r / RS];
+        return (w >> (2u * ((uint32_t)r % RS))) & 3u;
+    };
+    // Rounds: recompute the block of every unfinished walk (all lanes: the sub-steps use DPP across
+    // the quad), then each quad's sublane 0 walks its block alone, one move per iteration from the
+    // tags in LDS.  The three cells a move can reach next (up, left, diagonal) are read while the
+    // current move is decided, so an iteration waits for one LDS round trip at most, not for the
+    // quad's LP tag words of a whole column.
+    const int lead = quad * LP;
     for (;;) {
-#ifdef SA_TB_STATS
-        ++st_iters;
-#endif
+        // the walk's state lives in sublane 0: the quad's other lanes take it for the recompute
+        i = __shfl(i, lead);
+        j = __shfl(j, lead);
+        fin = __shfl((int)fin, lead) != 0;
+        parked = __shfl((int)parked, lead) != 0;
         if (__builtin_amdgcn_ballot_w64(!fin && !parked) == 0) {
             if (__builtin_amdgcn_ballot_w64(!fin) == 0) break;
 #ifdef SA_TB_STATS
             ++st_rounds;
 #endif
-            recompute(!fin, i, j);   // every lane: the sub-step loop uses DPP across the quad
+            recompute(!fin && i > 0 && j > 0, i, j);   // (a walk that stops at once needs no block)
             if (!fin) parked = false;
         }
-        // (cr, cq): the cell's row and column in the block, kept by the moves (recompute locates
-        // the entry cell); a move that takes either below 0 has left the block
-        const bool act = !fin && !parked;
-        // SASmithWaterman.h: an edge or H == 0; NW: the walk leaves the interior (border moves below)
-        const bool stop = !(i > 0 && j > 0) || (!NWK && V == 0);
-        const bool inb = cr >= 0 && cq >= 0;
-        const bool mv = act && !stop && inb;
-        fin = fin || (act && stop);
-        parked = parked || (act && !stop && !inb);
-        const bool lft = cq != wq;
-        const uint64_t col = lft ? NW : W;
-        const uint32_t r2 = 2u * (uint32_t)(cr & 31), q2 = 2u * (uint32_t)(cq & 31);   // (bit pairs)
-        auto half = [](uint64_t x, uint32_t b) __attribute__((always_inline)) -> uint32_t {
-            return ((b < 32 ? (uint32_t)x : (uint32_t)(x >> 32)) >> (b & 31u)) & 3u;
-        };
-        const uint32_t f = half(col, r2);
-        const bool dg = f == 3u, up = f == 2u;
-        const bool v = dg & (((mt >> (half(rowc, r2) * 4 + half(colc, q2))) & 1u) != 0);
-        const uint8_t op = dg ? (v ? 'M' : (allow ? 'S' : 'X')) : (up ? 'U' : 'L');
-        if (mv) emit(op);
-        V -= mv ? (dg ? (v ? MA : MI) : G) : 0;
-        const int di = (mv && (dg || up)) ? 1 : 0, dj = (mv && !up) ? 1 : 0;
-        const bool sh = mv && lft;   // this cell lay one column left of W: it becomes the walk's column
-        W = sh ? NW : W;
-        NW = sh ? NNW : NW;
-        wq = sh ? cq : wq;
-        i -= di;
-        j -= dj;
-        cr -= di;
-        cq -= dj;
-        NNW = tagcol(max(wq - 2, 0));
+        if (sub != 0 || fin || parked) continue;
+        // (cr, cq): the walk's cell in the block (recompute located it); a move that takes either
+        // below 0 leaves the block
+        uint32_t f = (cr >= 0 && cq >= 0) ? tag_at(cr, cq) : 0u;
+        for (;;) {
+#ifdef SA_TB_STATS
+            ++st_iters;
+#endif
+            // SASmithWaterman.h: an edge or H == 0; NW: the walk leaves the interior (border moves below)
+            if (!(i > 0 && j > 0) || (!NWK && V == 0)) { fin = true; break; }
+            if (cr < 0 || cq < 0) { parked = true; break; }
+            // the three cells the next move may reach (clamped into the block: a move out of it parks)
+            const int ru = cr > 0 ? cr - 1 : 0, ql = cq > 0 ? cq - 1 : 0;
+            const uint32_t fu = tag_at(ru, cq), fl = tag_at(cr, ql), fd = tag_at(ru, ql);
+            const bool dg = f == 3u, up = f == 2u;
+            const bool v = dg & (((mt >> (half(rowc, 2u * (uint32_t)cr) * 4 + half(colc, 2u * (uint32_t)cq))) & 1u) != 0);
+            emit(dg ? (v ? 'M' : (allow ? 'S' : 'X')) : (up ? 'U' : 'L'));
+            V -= dg ? (v ? MA : MI) : G;
+            const int di = (dg || up) ? 1 : 0, dj = up ? 0 : 1;
+            i -= di;
+            j -= dj;
+            cr -= di;
+            cq -= dj;
+            f = dg ? fd : up ? fu : fl;
+        }
     }
 #ifdef SA_TB_STATS
     if (lane == __builtin_amdgcn_readfirstlane(lane)) {
@@ -1089,7 +1080,9 @@ hipError_t launch_traceback_so(int algo, int R, const TbParams& p, hipStream_t s
         }
         return hipGetLastError();
     }
-    // lanes per pair: $SEQALIB_TB_LP (4 or 8), else so4_default_lp
+    // lanes per pair: $SEQALIB_TB_LP (4 or 8), else so4_default_lp (16 lanes per pair, round 5:
+    // 5 % fewer cycles per walk but twice the waves, traceback 6.01 -> 6.29 ms and pipelined step
+    // 18.9 -> 20.4 ms)
     int lp = so4_default_lp(R);
     if (const char* l = getenv("SEQALIB_TB_LP")) lp = (atoi(l) == 8 && R >= 8) ? 8 : 4;
     const uint32_t ppw = (uint32_t)(kWave / lp);

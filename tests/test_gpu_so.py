@@ -315,3 +315,24 @@ def test_so_affine_batch_1024(engine, algo):
         assert ops[off:off + int(res["nops"][p])].tobytes() == oops[ooff:ooff + int(ores["nops"][q])].tobytes(), int(p)
     tg = run(engine, False, s1, o1, s2, o2, scoring=scoring, algo=algo)
     assert_same(so, tg, o1, o2)
+
+
+def test_so_retry_pair_leaves_neighbours_intact(engine):
+    """A score-only SW batch (R = 32 plan) with two pairs above the int16 headroom (identical
+    9,000-long sequences: score 9,000) at the front: the int32 variant re-runs exactly those, and
+    every other pair -- whose score-only edges and snapshots share the launch's workspace with
+    the int32 records -- still equals the tagged path and the oracle."""
+    rng = np.random.default_rng(77)
+    hot = sa.synth_dna(81_000, 9000)
+    pairs = [(hot, hot), (hot[:8800], sa.synth_mutate(hot, 5)[:8900])]
+    for k in range(1100):
+        a = sa.synth_dna(82_000 + 2 * k, int(rng.integers(600, 1300)))
+        b = sa.synth_mutate(a, k) if k % 3 == 0 else sa.synth_dna(82_001 + 2 * k, int(rng.integers(600, 1300)))
+        pairs.append((a, b))
+    batch = sa.pack_pairs(pairs)
+    so = run(engine, True, *batch)
+    assert engine.last_plan_ex()[3] == sa.SA_RECORDS_SCORE_ONLY
+    tg = run(engine, False, *batch)
+    assert_same(so, tg, batch[1], batch[3])
+    assert int(so[0]["score"][0]) == 9000
+    check_vs_oracle(0, SW, so, batch, [0, 1, 2, 3, 4, 5, 50, 100, 500, 1000, 1101])
