@@ -348,10 +348,11 @@ def main():
     s1, o1, s2, o2 = sa.synth_dna_batch(shard_seed_base(rank, world, P), P, Lq, Lq, threads=16)
     as_t = lambda x: torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)
     d1, do1, d2, do2 = as_t(s1), as_t(o1), as_t(s2), as_t(o2)
-    # two output sets: with the cross-call pipeline, step k's traceback still writes its results
-    # while step k+1 fills, so consecutive steps must not share result buffers
-    d_res = [torch.zeros(P * 32, dtype=torch.uint8, device=dev) for _ in range(2)]
-    d_ops = [torch.zeros(len(s1) + len(s2) + P, dtype=torch.uint8, device=dev) for _ in range(2)]
+    # SA_PIPELINE_DEPTH output sets: with the cross-call pipeline, step k's traceback still writes
+    # its results while steps k+1 and k+2 fill, so those steps must not share result buffers
+    NSET = sa.SA_PIPELINE_DEPTH
+    d_res = [torch.zeros(P * 32, dtype=torch.uint8, device=dev) for _ in range(NSET)]
+    d_ops = [torch.zeros(len(s1) + len(s2) + P, dtype=torch.uint8, device=dev) for _ in range(NSET)]
     eng = sa.Engine(gpu)
     scoring = sa.ScoringSystem(*SCORING)
     stream = torch.cuda.current_stream(dev)
@@ -360,7 +361,7 @@ def main():
 
     def step(k):
         eng.align_device(sa.SA_SW, scoring, d1.data_ptr(), do1.data_ptr(), d2.data_ptr(), do2.data_ptr(), P, Lq, Lq,
-                         d_res[k % 2].data_ptr(), d_ops[k % 2].data_ptr(), stream.cuda_stream)
+                         d_res[k % NSET].data_ptr(), d_ops[k % NSET].data_ptr(), stream.cuda_stream)
 
     for k in range(args.warmup):
         step(k)
@@ -379,7 +380,7 @@ def main():
     elapsed = max_over_ranks(own, world)
     fill_ms, tb_ms, launches = eng.last_timings()   # HIP events of the last step (fill stream / traceback stream)
     fill_kernel_ms, _ = eng.last_kernel_timings()    # the fill kernel alone (without the end-cell replay)
-    last = (args.steps - 1) % 2
+    last = (args.steps - 1) % NSET
     serial_ms = None
     if pipelined and args.serial_steps > 0:
         # the same steps without overlap, for reference (outside the timed region above)
@@ -387,7 +388,7 @@ def main():
         torch.cuda.synchronize()
         ts = time.perf_counter()
         for k in range(args.serial_steps):
-            step(last + 1 + 2 * k)   # the other output set: keeps the checked one intact
+            step(last + 1 + NSET * k)   # another output set: keeps the checked one intact
         torch.cuda.synchronize()
         serial_ms = max_over_ranks(time.perf_counter() - ts, world) / args.serial_steps * 1e3
     kernel, plan_R, plan_W = eng.last_plan()

@@ -119,11 +119,13 @@ int sa_trim(sa_ctx* ctx);                                   /* free the cached w
 
 /* Cross-call pipeline of the device API (off by default).  When enabled, consecutive
  * sa_align_batch_device calls overlap: call k's traceback runs on an internal stream while call
- * k+1's fill runs on another, with two workspace slots (twice the HBM).  A call is ordered after
- * work already enqueued on the caller's stream, but the caller's stream is NOT ordered after
- * the call's results: wait with sa_wait(ctx) (or a device-wide synchronize) before reading
- * d_results / d_ops, and give calls that may overlap distinct output buffers.  Disabling waits
- * for pipelined work.  The host API (sa_align_batch) never pipelines. */
+ * k+1's fill runs on another, with SA_PIPELINE_DEPTH workspace slots (that many times the HBM).
+ * A call is ordered after work
+ * already enqueued on the caller's stream, but the caller's stream is NOT ordered after the
+ * call's results: wait with sa_wait(ctx) (or a device-wide synchronize) before reading
+ * d_results / d_ops, and give any SA_PIPELINE_DEPTH consecutive calls distinct output buffers.
+ * Disabling waits for pipelined work.  The host API (sa_align_batch) never pipelines. */
+#define SA_PIPELINE_DEPTH 2
 int sa_set_pipeline(sa_ctx* ctx, int enable);
 int sa_wait(sa_ctx* ctx);
 
@@ -237,7 +239,7 @@ int sa_plan_query(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs,
  * plan), and the device workspace one pair occupies (direction records + row buffers + end-cell
  * snapshots; the larger of the T16 and int32 variants when the scoring admits T16, since the
  * variant is chosen on the device and both are provisioned).  A pipelined context
- * (sa_set_pipeline) holds two such slots per pair of a launch. */
+ * (sa_set_pipeline) holds SA_PIPELINE_DEPTH such slots per pair of a launch. */
 int sa_plan_query_ex(int algo, const sa_scoring* scoring, uint32_t max_m, uint32_t max_n,
                      uint32_t npairs, int nsym, int* kernel, int* rows_per_lane, int* waves,
                      uint64_t* workspace_bytes_per_pair);

@@ -38,6 +38,7 @@ ALGO_NAMES = {SA_SW: "sw", SA_NW: "nw", SA_LOCAL_GOTOH: "local_gotoh", SA_GLOBAL
               SA_HIRSCHBERG: "hirschberg", SA_MYERS_MILLER: "myers_miller"}
 SA_FLAG_DIVERGED, SA_FLAG_BAD_SHAPE, SA_FLAG_SIZE_HACK, SA_FLAG_TIMEOUT = 1, 2, 4, 8
 SA_KERNEL_INT32, SA_KERNEL_T16, SA_KERNEL_T16_ENDCELL, SA_KERNEL_TINY = 0, 1, 2, 3
+SA_PIPELINE_DEPTH = 2   # pipelined device calls that may run at once (distinct output buffers)
 SA_RECORDS_FLAGS, SA_RECORDS_TAGS, SA_RECORDS_SCORE_ONLY = 0, 1, 2
 INT32_MIN = -(2 ** 31)
 

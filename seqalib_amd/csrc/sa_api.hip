@@ -23,6 +23,10 @@
 using namespace sa;
 
 constexpr int kKEv = 6;   // SEQALIB_KERNEL_TIMING events per fill launch (two per variant, <= 3)
+// Cross-call pipeline: workspace slots (call k's fill waits for call k-2's traceback).  Three slots
+// with the fills alternating between two streams (call k+1's fill starting in call k's fill tail)
+// measured slower, 19.5 vs 18.2 ms per headline step (round 5, profiles/pipe_slots_ab_r05.txt).
+constexpr int kPipeSlots = SA_PIPELINE_DEPTH;
 
 struct sa_ctx {
     int device = 0;
@@ -55,11 +59,11 @@ struct sa_ctx {
     // device's word arrives in h_sel (a host write there could race with a pending download)
     int host_sel = -1;
     // cross-call pipeline of the device API (sa_set_pipeline): fills on s_fill, tracebacks on
-    // s_tb, two workspace slots; ev_slot[k] = traceback of the last call that used slot k done
+    // s_tb, kPipeSlots workspace slots; ev_slot[k] = traceback of the last call that used slot k done
     int pipeline = 0;
     uint32_t fill_epoch = 0;   // score-only fills: per-launch tag of their hand-off granules
     hipStream_t s_fill = nullptr, s_tb = nullptr;
-    hipEvent_t ev_in = nullptr, ev_slot[2] = {nullptr, nullptr};
+    hipEvent_t ev_in = nullptr, ev_slot[kPipeSlots] = {};
     uint64_t pipe_k = 0;
     // SPLIT plans (few pairs, one workgroup per band): [ticket, pad to 256 B][granules][partials]
     uint8_t* split = nullptr;
@@ -213,6 +217,7 @@ struct Variant {
     uint32_t snap_nch = 0;
     uint64_t snap_h_slot = 0, snap_p_slot = 0;   // 32-bit words per pair
     uint64_t part_slot = 0;   // score-only band units: 64-bit per-band maxima per pair
+    uint64_t snap_c_slot = 0; // score-only SW: 32-bit (band, chunk) maxima per pair (FillParams::snap_c)
     uint64_t slot_bytes = 0;
     int kernel = SA_KERNEL_INT32;
 };
@@ -246,10 +251,12 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
     if (v.so) {
         v.pl.g = make_geom(algo, v.pl.R, max_m, max_n, kGeomEdge);
         v.part_slot = v.pl.g.bands;
+        if (algo == SA_SW) v.snap_c_slot = (uint64_t)v.pl.g.bands * v.snap_nch;
     }
     if (v.pl.split) v.pl.rowbuf_elems = 0;   // hand-off granules live in c->split
     v.kernel = v.cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
-    v.slot_bytes = v.pl.g.dir_slot + v.pl.rowbuf_elems * 4 + (v.snap_h_slot + 2 * v.snap_p_slot) * 4 + v.part_slot * 8;
+    v.slot_bytes = v.pl.g.dir_slot + v.pl.rowbuf_elems * 4 + (v.snap_h_slot + 2 * v.snap_p_slot) * 4 + v.part_slot * 8 +
+                   v.snap_c_slot * 4;
     return v;
 }
 
@@ -604,7 +611,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     const T16Mode tm = bits ? T16Mode{} : t16_candidate(algo, sc, max_m, max_n, npairs);
     const bool t16 = tm.ok;
     const bool kernel_timing = getenv("SEQALIB_KERNEL_TIMING") != nullptr;
-    if (!c->aux) SA_HIP(c, hipMalloc(&c->aux, 2 * kAuxWords * 4));
+    if (!c->aux) SA_HIP(c, hipMalloc(&c->aux, kPipeSlots * kAuxWords * 4));
     if (!c->h_sel) {
         SA_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_sel), 64, hipHostMallocDefault));
         SA_HIP(c, hipEventCreateWithFlags(&c->ev_sel, hipEventDisableTiming));
@@ -613,7 +620,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         SA_HIP(c, hipStreamSynchronize(c->s_fill));
         SA_HIP(c, hipStreamSynchronize(c->s_tb));
     }
-    const int slot = pipe ? (int)(c->pipe_k & 1) : 0;
+    constexpr int nslots = kPipeSlots;
+    const int slot = pipe ? (int)(c->pipe_k % (uint64_t)nslots) : 0;
     uint32_t* aux = c->aux + kAuxWords * slot;
     if (pipe && c->ev_slot[slot]) SA_HIP(c, hipStreamWaitEvent(stream, c->ev_slot[slot], 0));   // slot free
     const uint32_t* sel = nullptr;
@@ -672,7 +680,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             sp_bands = std::max<uint64_t>(sp_bands, vars[k].pl.g.bands);
         }
     }
-    const uint64_t budget = pipe ? ws_budget(c) / 2 : ws_budget(c);
+    const uint64_t budget = pipe ? ws_budget(c) / nslots : ws_budget(c);
     uint64_t per_launch = slot_bytes ? std::max<uint64_t>(1, budget / std::max<uint64_t>(slot_bytes, 1)) : npairs;
     per_launch = std::min<uint64_t>(per_launch, npairs ? npairs : 1);
     per_launch = std::min<uint64_t>(per_launch, 1u << 30);
@@ -680,7 +688,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     if (need > budget && per_launch == 1 && c->ws_limit)
         return fail(c, SA_ERR_NOMEM, "one pair needs " + std::to_string(slot_bytes) +
                                          " bytes of workspace, above the limit");
-    int rc = ensure_ws(c, std::max<uint64_t>(pipe ? 2 * need : need, 4096));
+    int rc = ensure_ws(c, std::max<uint64_t>(pipe ? nslots * need : need, 4096));
     if (rc) return rc;
     // SPLIT scratch, per variant: [ticket][hand-off granules] (zeroed before its fill; the
     // segmented traceback reads the granules after both variants' fills), then the per-band
@@ -705,7 +713,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     // so an unaligned slot size let slot 0's last exit records and slot 1's ticket share bytes --
     // the pipelined calls then corrupted each other's scratch now and then)
     const uint64_t sp_slot = (sp_seg + (seg_on ? (per_launch * sp_bands * seg_rs + per_launch) * 16 : 0) + 255) & ~(uint64_t)255;
-    const uint64_t sp_need = any_split ? sp_slot * (pipe ? 2 : 1) : 0;
+    const uint64_t sp_need = any_split ? sp_slot * (pipe ? nslots : 1) : 0;
     if (any_split && c->split_bytes < sp_need) {
         if (c->split) {
             if (int rc = drain(c)) return rc;
@@ -721,11 +729,11 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     }
     // A pipeline slot is one contiguous half of the workspace holding everything its calls
     // write (dirs, row buffers, snapshots), so calls on the other slot never touch it.
-    uint8_t* const wbase = c->ws + (pipe ? slot * ((c->ws_bytes / 2) & ~(uint64_t)255) : 0);
+    uint8_t* const wbase = c->ws + (pipe ? slot * ((c->ws_bytes / nslots) & ~(uint64_t)255) : 0);
     // (fixed halves of the scratch, as the workspace: a slot's block never moves with the shape)
-    uint8_t* const spbase = any_split ? c->split + (pipe ? slot * ((c->split_bytes / 2) & ~(uint64_t)255) : 0) : nullptr;
-    // the two pipeline slots must not share a byte (each holds what its calls write)
-    if (pipe && (((c->ws_bytes / 2) & ~(uint64_t)255) < need || (any_split && ((c->split_bytes / 2) & ~(uint64_t)255) < sp_slot)))
+    uint8_t* const spbase = any_split ? c->split + (pipe ? slot * ((c->split_bytes / nslots) & ~(uint64_t)255) : 0) : nullptr;
+    // the pipeline slots must not share a byte (each holds what its calls write)
+    if (pipe && (((c->ws_bytes / nslots) & ~(uint64_t)255) < need || (any_split && ((c->split_bytes / nslots) & ~(uint64_t)255) < sp_slot)))
         return fail(c, SA_ERR_HIP, "internal: pipeline slots overlap");
 
     // reset timing (kernel timings describe this call only: a call without
@@ -810,6 +818,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 fp.epoch = ++c->fill_epoch;
                 fp.band_part = reinterpret_cast<unsigned long long*>(fp.snap_m + per_launch * v.snap_p_slot);
                 fp.part_bands = (uint32_t)v.part_slot;
+                fp.snap_c = reinterpret_cast<int32_t*>(fp.band_part + per_launch * v.part_slot);
             }
             fp.snap_h_slot = v.snap_h_slot; fp.snap_p_slot = v.snap_p_slot; fp.snap_nch = v.snap_nch;
             fp.split_bands = (uint32_t)sp_bands;
@@ -899,6 +908,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 ep.res = d_res; ep.pair_base = (uint32_t)base; ep.count = cnt;
                 ep.gap = sc->gap; ep.gap_open = sc->gap_open; ep.gap_extend = sc->gap_extend;
                 ep.hshift = v.so ? 0 : 2;
+                ep.snap_c = fp.snap_c; ep.snap_c_slot = v.snap_c_slot;
                 ep.dirs = fp.dirs; ep.dir_slot = fp.dir_slot; ep.band_stride = fp.band_stride;
                 // on the fill stream, right after the fill: run beside the next call's fill (on the
                 // traceback stream) its 10,000 short waves slowed that fill by 4 % in round 4, and

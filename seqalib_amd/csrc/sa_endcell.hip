@@ -223,24 +223,43 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
 #ifdef SA_TB_STATS
     const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
 #endif
-    // ---- the candidate lane blocks, in [band][chunk][lane] order: kEcScan entries per lane per load
+    // ---- the candidate lane blocks, in [band][chunk][lane] order.  First level: the fill's
+    // (band, chunk) maxima of the lane maxima (FillParams::snap_c), kEcScan x 64 entries per round of
+    // loads issued together; second level: the 64 lane maxima of each (band, chunk) that reaches thr
     __shared__ uint32_t s_cand[DENSE ? 1 : kSoCand];   // band << 22 | chunk << 6 | lane
-    // kEcScan (band, chunk) entries per iteration, one coalesced 256-B load each (issued together)
+    __shared__ uint32_t s_hit[DENSE ? 1 : kSoCand];    // (band, chunk) entries whose maximum reaches thr
     const uint32_t total = DENSE ? 0u : (uint32_t)B * snch;
-    int cnt = 0;
-    uint32_t bnext = 0, cnext = 0;   // (band, chunk) of entry e0, stepped (no scalar divide)
-    for (uint32_t e0 = 0; e0 < total; e0 += kEcScan) {
+    const int32_t* const sc = P.snap_c + (uint64_t)slot * P.snap_c_slot;
+    int nhit = 0;
+    for (uint32_t e0 = 0; e0 < total; e0 += kWave * kEcScan) {
         int v[kEcScan];
-        uint32_t bb[kEcScan], cc[kEcScan];
 #pragma unroll
-        for (int k = 0; k < kEcScan; ++k) {   // (wave-uniform: scalar)
-            const uint32_t e = e0 + k;
-            bb[k] = bnext;
-            cc[k] = cnext;
-            v[k] = e < total && (int)cnext < nch ? cm[(uint64_t)e * kWave + lane] : INT_MIN;
-            const bool wrap = cnext + 1 == snch;
-            bnext += wrap ? 1u : 0u;
-            cnext = wrap ? 0u : cnext + 1;
+        for (int k = 0; k < kEcScan; ++k) {
+            const uint32_t e = e0 + (uint32_t)(k * kWave + lane);
+            v[k] = e < total && (int)(e % snch) < nch ? sc[e] : INT_MIN;
+        }
+#pragma unroll
+        for (int k = 0; k < kEcScan; ++k) {
+            const bool hit = v[k] >= thr;
+            const uint64_t hits = __builtin_amdgcn_ballot_w64(hit);
+            if (hit) {
+                const int pos = nhit + (int)__builtin_popcountll(hits & ((1ull << lane) - 1));
+                if (pos < kSoCand) s_hit[pos] = e0 + (uint32_t)(k * kWave + lane);
+            }
+            nhit += (int)__builtin_popcountll(hits);
+        }
+    }
+    const bool over = nhit > kSoCand;   // (uniform) more chunks than the list holds: the DENSE launch
+    nhit = min(nhit, kSoCand);
+    __syncthreads();
+    int cnt = over ? kSoCand + 1 : 0;
+    for (int h0 = 0; h0 < (over ? 0 : nhit); h0 += kEcScan) {
+        int v[kEcScan];
+        uint32_t ee[kEcScan];
+#pragma unroll
+        for (int k = 0; k < kEcScan; ++k) {   // (wave-uniform)
+            ee[k] = h0 + k < nhit ? s_hit[h0 + k] : 0u;
+            v[k] = h0 + k < nhit ? cm[(uint64_t)ee[k] * kWave + lane] : INT_MIN;
         }
 #pragma unroll
         for (int k = 0; k < kEcScan; ++k) {
@@ -248,7 +267,8 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
             const uint64_t hits = __builtin_amdgcn_ballot_w64(hit);
             if (hit) {
                 const int pos = cnt + (int)__builtin_popcountll(hits & ((1ull << lane) - 1));
-                if (pos < kSoCand) s_cand[pos] = bb[k] << 22 | cc[k] << 6 | (uint32_t)lane;
+                const uint32_t bb = ee[k] / snch, cc = ee[k] - bb * snch;
+                if (pos < kSoCand) s_cand[pos] = bb << 22 | cc << 6 | (uint32_t)lane;
             }
             cnt += (int)__builtin_popcountll(hits);
         }

@@ -1325,6 +1325,16 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                         if (kC + kChunk - 1 < lane) cml = 0;   // (a lane that has not reached its first column)
                         P.snap_m[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = (int32_t)cml;
                         smax = max(smax, cml);   // (per lane; reduced over the wave at the end)
+                        // the wave's maximum of the chunk (DPP row prefix maxima, then the row
+                        // broadcasts: lane 63 holds it), for the end-cell replay's first-level scan
+                        uint32_t wm = cml;
+                        wm = max(wm, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x111, 0xf, 0xf, false));
+                        wm = max(wm, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x112, 0xf, 0xf, false));
+                        wm = max(wm, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x114, 0xf, 0xf, false));
+                        wm = max(wm, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x118, 0xf, 0xf, false));
+                        wm = max(wm, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x142, 0xa, 0xf, false));
+                        wm = max(wm, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)wm, 0x143, 0xc, 0xf, false));
+                        if (lane == kWave - 1) P.snap_c[(uint64_t)slot * P.part_bands * P.snap_nch + e] = (int32_t)wm;
                     } else {
                         // (start mode: a lane that has not reached its first column holds garbage)
                         if (kC + kChunk - 1 < lane) cml = 0;
@@ -1429,6 +1439,14 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                 if (lane == 0)
                     __hip_atomic_store(part + band0, (unsigned long long)P.epoch << 32 | smax, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+#ifdef SA_TB_STATS
+                const uint64_t sid = (uint64_t)band0 * P.count + slot;
+                if (threadIdx.x == 0 && sid < 32768) {
+                    g_fill_stats[sid][0] = st_t0;
+                    g_fill_stats[sid][1] = __builtin_amdgcn_s_memrealtime();
+                    g_fill_stats[sid][2] = (unsigned long long)st_hwid | ((unsigned long long)st_xcc << 32);
+                }
+#endif
                 return;
             }
             // (the last band: every earlier band finished its last chunk before this one's last
@@ -1441,10 +1459,11 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
             }
         }
 #ifdef SA_TB_STATS
-        if (threadIdx.x == 0 && slot < 32768) {
-            g_fill_stats[slot][0] = st_t0;
-            g_fill_stats[slot][1] = __builtin_amdgcn_s_memrealtime();
-            g_fill_stats[slot][2] = (unsigned long long)st_hwid | ((unsigned long long)st_xcc << 32);
+        const uint64_t sid = BU ? (uint64_t)band0 * P.count + slot : slot;   // (BU: one entry per unit)
+        if (threadIdx.x == 0 && sid < 32768) {
+            g_fill_stats[sid][0] = st_t0;
+            g_fill_stats[sid][1] = __builtin_amdgcn_s_memrealtime();
+            g_fill_stats[sid][2] = (unsigned long long)st_hwid | ((unsigned long long)st_xcc << 32);
         }
 #endif
         if constexpr (SOMAX) {

@@ -86,6 +86,9 @@ struct FillParams {
     uint32_t epoch;
     unsigned long long* band_part;
     uint32_t part_bands;
+    // score-only SW: per slot and (band, chunk) the wave's maximum of the chunk maxima (snap_m), so
+    // the end-cell replay reads the lane maxima of the chunks that reach its threshold only
+    int32_t* snap_c;
 };
 
 // SPLIT fills: per-pair fold of the per-band partials into sa_result (split_reduce_kernel).
@@ -128,6 +131,8 @@ struct EndcellParams {
     uint32_t pair_base, count;
     int32_t gap, gap_open, gap_extend;
     int hshift;                // SW: snapshots / chunk maxima / top rows hold H << hshift (2 tagged, 0 SO)
+    const int32_t* snap_c;     // score-only SW: per (band, chunk) maxima (FillParams::snap_c, snap_nch per band)
+    uint64_t snap_c_slot;
     const uint8_t* dirs;       // score-only: the fill's edge stream (TbParams::dirs, band_stride)
     uint64_t dir_slot, band_stride;
 };

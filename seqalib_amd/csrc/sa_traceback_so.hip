@@ -364,10 +364,11 @@ __global__ __launch_bounds__(64) void traceback_so_kernel(TbParams P) {
 // A lone wave's serial recompute per block drops from 32 columns x R rows of dependent cells to
 // (32 + 3) sub-steps x R/4 rows, and the wave's registers (R/4 rows of state) stay few, so the
 // traceback beside the next call's fill displaces fewer of its waves.
-// Lanes per pair by default: 8 at R = 32 (headline, 10,000 x 4096^2: traceback 6.50 -> 6.30 ms,
-// pipelined step 19.50 -> 19.35 ms), 4 below (R = 16, 10,000 x 1024^2: 1.80 ms at 4, 1.84 at 8);
-// profiles/tb_lp_ab_r04.txt.  $SEQALIB_TB_LP overrides.
-constexpr int so4_default_lp(int R) { return R >= 32 ? 8 : 4; }
+// Lanes per pair: 4 (16 pairs per wave).  Round 4 ran 8 at R = 32 (traceback 6.50 -> 6.30 ms,
+// profiles/tb_lp_ab_r04.txt); with round 5's lane walker and branch-free sub-steps, 4 lanes per pair
+// run half the waves beside the next call's fill and the pipelined headline step drops 18.4 ->
+// 17.9 ms (profiles/tb_lp_ab_r05.txt).  $SEQALIB_TB_LP=8 overrides.
+constexpr int kSo4DefaultLp = 4;
 #ifdef SA_TB_STATS
 // Debug build only (-DSA_TB_STATS, tools/so4_stats.py), per wave summed: [rounds, walk-loop
 // iterations, moves, wave cycles, recompute: load-wait cycles, sub-step cycles, sub-steps, waves]
@@ -650,9 +651,6 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
     int i = res.end_i, j = res.end_j, V = res.score;
     if (!NWK && (m == 0 || n == 0)) { i = 0; j = 0; }
     bool fin = !live, parked = true;
-    auto half = [](uint64_t x, uint32_t b) __attribute__((always_inline)) -> uint32_t {
-        return ((b < 32 ? (uint32_t)x : (uint32_t)(x >> 32)) >> (b & 31u)) & 3u;
-    };
     // the tag of block cell (r, q): word [q][quad * LP + r / RS], bits 2 (r % RS)
     const uint32_t tag_base = (uint32_t)(quad * LP);
     auto tag_at = [&](int r, int q) __attribute__((always_inline)) -> uint32_t {
@@ -681,29 +679,31 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         }
         if (sub != 0 || fin || parked) continue;
         // (cr, cq): the walk's cell in the block (recompute located it); a move that takes either
-        // below 0 leaves the block
-        uint32_t f = (cr >= 0 && cq >= 0) ? tag_at(cr, cq) : 0u;
+        // below 0 leaves the block.  One exit test per move, no branch inside (sublane 0 only runs here).
+        uint32_t f = tag_at(max(cr, 0), max(cq, 0));
         for (;;) {
 #ifdef SA_TB_STATS
             ++st_iters;
 #endif
             // SASmithWaterman.h: an edge or H == 0; NW: the walk leaves the interior (border moves below)
-            if (!(i > 0 && j > 0) || (!NWK && V == 0)) { fin = true; break; }
-            if (cr < 0 || cq < 0) { parked = true; break; }
+            if (!((i > 0) & (j > 0) & (NWK | (V != 0)) & (cr >= 0) & (cq >= 0))) break;
             // the three cells the next move may reach (clamped into the block: a move out of it parks)
-            const int ru = cr > 0 ? cr - 1 : 0, ql = cq > 0 ? cq - 1 : 0;
+            const int ru = max(cr - 1, 0), ql = max(cq - 1, 0);
             const uint32_t fu = tag_at(ru, cq), fl = tag_at(cr, ql), fd = tag_at(ru, ql);
             const bool dg = f == 3u, up = f == 2u;
-            const bool v = dg & (((mt >> (half(rowc, 2u * (uint32_t)cr) * 4 + half(colc, 2u * (uint32_t)cq))) & 1u) != 0);
-            emit(dg ? (v ? 'M' : (allow ? 'S' : 'X')) : (up ? 'U' : 'L'));
+            const uint32_t ca = (uint32_t)(rowc >> (2 * cr)) & 3u, cb2 = (uint32_t)(colc >> (2 * cq)) & 3u;
+            const bool v = dg & (((mt >> (ca * 4 + cb2)) & 1u) != 0);
+            ops[k++] = dg ? (v ? 'M' : (allow ? 'S' : 'X')) : (up ? 'U' : 'L');
             V -= dg ? (v ? MA : MI) : G;
-            const int di = (dg || up) ? 1 : 0, dj = up ? 0 : 1;
+            const int di = (dg | up) ? 1 : 0, dj = up ? 0 : 1;
             i -= di;
             j -= dj;
             cr -= di;
             cq -= dj;
             f = dg ? fd : up ? fu : fl;
         }
+        if (!((i > 0) & (j > 0) & (NWK | (V != 0)))) fin = true;
+        else parked = true;
     }
 #ifdef SA_TB_STATS
     if (lane == __builtin_amdgcn_readfirstlane(lane)) {
@@ -1080,10 +1080,10 @@ hipError_t launch_traceback_so(int algo, int R, const TbParams& p, hipStream_t s
         }
         return hipGetLastError();
     }
-    // lanes per pair: $SEQALIB_TB_LP (4 or 8), else so4_default_lp (16 lanes per pair, round 5:
+    // lanes per pair: $SEQALIB_TB_LP (4 or 8), else kSo4DefaultLp (16 lanes per pair, round 5:
     // 5 % fewer cycles per walk but twice the waves, traceback 6.01 -> 6.29 ms and pipelined step
     // 18.9 -> 20.4 ms)
-    int lp = so4_default_lp(R);
+    int lp = kSo4DefaultLp;
     if (const char* l = getenv("SEQALIB_TB_LP")) lp = (atoi(l) == 8 && R >= 8) ? 8 : 4;
     const uint32_t ppw = (uint32_t)(kWave / lp);
     const dim3 grid((p.count + ppw - 1) / ppw);

@@ -92,15 +92,16 @@ class Runner:
         t = lambda x: self.torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(self.dev)
         n = len(o1) - 1
         outs = [(self.torch.zeros(n * 32, dtype=self.torch.uint8, device=self.dev),
-                 self.torch.zeros(len(s1) + len(s2) + n, dtype=self.torch.uint8, device=self.dev)) for _ in range(2)]
+                 self.torch.zeros(len(s1) + len(s2) + n, dtype=self.torch.uint8, device=self.dev))
+                for _ in range(self.sa.SA_PIPELINE_DEPTH)]
         return [t(x) for x in (s1, o1, s2, o2)], outs, n
 
     def time_calls(self, algo, sc, dev_in, outs, n, m_max, n_max, steps, pipeline):
         d = dev_in
         self.eng.set_pipeline(pipeline)
         call = lambda k: self.eng.align_device(algo, sc, d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(),
-                                               d[3].data_ptr(), n, m_max, n_max, outs[k % 2][0].data_ptr(),
-                                               outs[k % 2][1].data_ptr(), self.stream.cuda_stream)
+                                               d[3].data_ptr(), n, m_max, n_max, outs[k % len(outs)][0].data_ptr(),
+                                               outs[k % len(outs)][1].data_ptr(), self.stream.cuda_stream)
         for k in range(2):
             call(k)
         self.eng.wait()
@@ -117,7 +118,7 @@ class Runner:
             self.fill_kernel_ms = self.eng.last_kernel_timings()[0]   # the fill kernel(s) alone
         except Exception:   # (SEQALIB_KERNEL_TIMING unset)
             self.fill_kernel_ms = None
-        return dt, (steps - 1) % 2, fill_ms, tb_ms
+        return dt, (steps - 1) % len(outs), fill_ms, tb_ms
 
     def fk(self):
         return {"fill_kernel_ms": round(self.fill_kernel_ms, 3) if self.fill_kernel_ms is not None else None}

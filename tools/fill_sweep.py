@@ -20,8 +20,8 @@ def batch(torch, dev, P, L, seed=10 ** 10, L1=None):
     s1, o1, s2, o2 = sa.synth_dna_batch(seed, P, L1 or L, L, threads=16)
     t = lambda x: torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)
     d = [t(x) for x in (s1, o1, s2, o2)]
-    res = [torch.zeros(P * 32, dtype=torch.uint8, device=dev) for _ in range(2)]
-    ops = [torch.zeros(len(s1) + len(s2) + P, dtype=torch.uint8, device=dev) for _ in range(2)]
+    res = [torch.zeros(P * 32, dtype=torch.uint8, device=dev) for _ in range(sa.SA_PIPELINE_DEPTH)]
+    ops = [torch.zeros(len(s1) + len(s2) + P, dtype=torch.uint8, device=dev) for _ in range(sa.SA_PIPELINE_DEPTH)]
     return d, res, ops
 
 
@@ -68,12 +68,12 @@ def main():
                     k, x = kv.split("=")
                     os.environ[k] = x
             for k in range(2):
-                eng.align_device(0, sc, *[x.data_ptr() for x in d], P, L, L, res[k % 2].data_ptr(), ops[k % 2].data_ptr(), st)
+                eng.align_device(0, sc, *[x.data_ptr() for x in d], P, L, L, res[k % len(res)].data_ptr(), ops[k % len(ops)].data_ptr(), st)
             eng.wait()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for k in range(a.steps):
-                eng.align_device(0, sc, *[x.data_ptr() for x in d], P, L, L, res[k % 2].data_ptr(), ops[k % 2].data_ptr(), st)
+                eng.align_device(0, sc, *[x.data_ptr() for x in d], P, L, L, res[k % len(res)].data_ptr(), ops[k % len(ops)].data_ptr(), st)
             eng.wait()
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / a.steps * 1e3
@@ -83,7 +83,7 @@ def main():
     for k in keys:
         os.environ.pop(k, None)
     # parity of the last variant's output against a plain call
-    r0 = np.frombuffer(res[(a.steps - 1) % 2].cpu().numpy().tobytes(), dtype=sa.RESULT_DTYPE).copy()
+    r0 = np.frombuffer(res[(a.steps - 1) % len(res)].cpu().numpy().tobytes(), dtype=sa.RESULT_DTYPE).copy()
     eng.align_device(0, sc, *[x.data_ptr() for x in d], P, L, L, res[0].data_ptr(), ops[0].data_ptr(), st)
     torch.cuda.synchronize()
     r1 = np.frombuffer(res[0].cpu().numpy().tobytes(), dtype=sa.RESULT_DTYPE)

@@ -41,7 +41,11 @@ def main():
             eng.align_device(0, sc, *[x.data_ptr() for x in d], P, a.len, a.len, res.data_ptr(), ops.data_ptr(), st)
             torch.cuda.synchronize()
         L.sa_debug_fill_stats_sw(buf.ctypes.data, 0)
-        b = buf[:P].astype(np.int64)
+        # band units (score-only fills): one entry per (band, pair) unit, band-major
+        _, _, W = eng.last_plan()
+        units = min(32768, P * max(1, -(-a.len // (64 * eng.last_plan()[1]))))
+        b = buf[:units].astype(np.int64)
+        P = units
         t0, t1, hw = b[:, 0], b[:, 1], b[:, 2]
         ok = (t0 > 0) & (t1 >= t0)
         base = t0[ok].min()
