@@ -39,7 +39,7 @@ SEED_BASE = 10 ** 10          # workload "T" seed base (config id x 1e9 conventi
 SCORING = (-1, 1, -1)         # SmithWatermanSA::getDefaultScoring (SASmithWaterman.h:352)
 # The fill kernel is VALU-issue bound.  Its VALU instructions per cell come from an ISA count of
 # the steady chunk loop (tools/issue_model.py -> ISSUE_MODEL).
-ISSUE_MODEL = os.path.join(ROOT, "profiles", "issue_model_r04.json")
+ISSUE_MODEL = os.path.join(ROOT, "profiles", "issue_model_r05.json")
 HBM_PEAK_GBPS = 8000.0
 # VALU peak of the guide (/opt/skills/guides/MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 VALU
 # instruction issues over 2 cycles, 2400 MHz max clock): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz.

@@ -28,22 +28,18 @@ ALIAS = {"v_mov_b32_dpp": "v_mov_b32_dpp_shr", "v_readlane_b32": "readlane", "v_
          "v_lshl_add_u64": "v_lshl_add_u32", "v_max3_i32": "v_max3_i32", "v_add_co_u32": "add_co_e64"}
 
 KERNELS = {  # label -> (TU, mangled name, cells per lane in one steady block = SPP * R)
-    "sw_t16_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELi0ELb1ELb1ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 64),
-    "sw_t16c_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELi0ELb1ELb1ELb1ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
+    # round 5: the score-only fills (fill_so_kernel<ALG, R>): SW / NW band units, LG / GG affine
+    "sw_so_r32": ("sa_fill_sw.hip", "_ZN2sa14fill_so_kernelILi0ELi32EEEvNS_10FillParamsE", 256),   # 8 steps x 32 rows
+    "sw_so_r16": ("sa_fill_sw.hip", "_ZN2sa14fill_so_kernelILi0ELi16EEEvNS_10FillParamsE", 128),
+    "nw_so_r16": ("sa_fill_nw.hip", "_ZN2sa14fill_so_kernelILi1ELi16EEEvNS_10FillParamsE", 128),
+    "lg_so_r16": ("sa_fill_lg.hip", "_ZN2sa14fill_so_kernelILi2ELi16EEEvNS_10FillParamsE", 64),    # 4 steps x 16 rows
+    "gg_so_r16": ("sa_fill_gg.hip", "_ZN2sa14fill_so_kernelILi3ELi16EEEvNS_10FillParamsE", 64),
+    # the tagged T16 and int32 fills (records for the traceback)
     "sw_t16c_r32": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi32ELi0ELb1ELb1ELb1ELb1ELb0ELb0EEEvNS_10FillParamsE", 64),
-    "sw_so_r32": ("sa_fill_sw.hip", "_ZN2sa14fill_so_kernelILi32EEEvNS_10FillParamsE", 256),   # 8 steps x 32 rows
-    "sw_so_r16": ("sa_fill_sw.hip", "_ZN2sa14fill_so_kernelILi16EEEvNS_10FillParamsE", 128),
-    "sw_t16_r32": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi32ELi0ELb1ELb1ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 64),
-    "nw_t16_r32": ("sa_fill_nw.hip", "_ZN2sa11fill_kernelILi1ELi32ELi0ELb1ELb0ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 64),
-    "sw_int32_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELi0ELb1ELb1ELb0ELb0ELb0ELb0EEEvNS_10FillParamsE", 64),
     "nw_t16_r16": ("sa_fill_nw.hip", "_ZN2sa11fill_kernelILi1ELi16ELi0ELb1ELb0ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 64),
-    "sw_x2_r16": ("sa_fill_x2.hip", "_ZN2sa14fill_x2_kernelILi16EEEvNS_10FillParamsE", 32),   # one step (exec-masked body): 16 rows x 2 pairs
-    "lg_int32_r16": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi16ELi0ELb1ELb1ELb0ELb0ELb0ELb0EEEvNS_10FillParamsE", 32),
-    "lg_t16_r16": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi16ELi0ELb1ELb1ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 16),
     "lg_t16c_r16": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi16ELi0ELb1ELb1ELb1ELb1ELb0ELb0EEEvNS_10FillParamsE", 16),
-    "lg_t16_r8": ("sa_fill_lg.hip", "_ZN2sa11fill_kernelILi2ELi8ELi0ELb1ELb1ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 16),
     "gg_t16_r16": ("sa_fill_gg.hip", "_ZN2sa11fill_kernelILi3ELi16ELi0ELb1ELb0ELb1ELb0ELb0ELb0EEEvNS_10FillParamsE", 16),
-    "gg_int32_r16": ("sa_fill_gg.hip", "_ZN2sa11fill_kernelILi3ELi16ELi0ELb1ELb0ELb0ELb0ELb0ELb0EEEvNS_10FillParamsE", 32),
+    "sw_int32_r16": ("sa_fill_sw.hip", "_ZN2sa11fill_kernelILi0ELi16ELi0ELb1ELb1ELb0ELb0ELb0ELb0EEEvNS_10FillParamsE", 64),
 }
 
 
