@@ -387,8 +387,10 @@ extern "C" int sa_debug_so4_stats(unsigned long long* out, int reset) {
 template <int R, int LP>
 struct So4Lds {
     static constexpr int kPairs = kWave / LP;                 // pairs per wave
-    static constexpr int kTags = 0;                           // [column q][lane] words
-    static constexpr int kEdge = kTags + 32 * 64 * 4;         // [lane] 16 B: packet (sub) of the quad
+    // [quad][column q][row r] bytes (1 KiB per quad, the cell's tag in bits 0-1); 64 B of pad in
+    // front: the walk reads the three cells up-left of its cell, also from a block's first row
+    static constexpr int kTags = 64;
+    static constexpr int kEdge = kTags + kPairs * 1024;       // [lane] 16 B: packet (sub) of the quad
     static constexpr int kEdge2 = kEdge + 64 * 16;            // LP = 4: [lane] 16 B: packet 4 (sublane 0)
     static constexpr int kRowC = kEdge2 + (LP < 5 ? 64 * 16 : 0);   // [quad][32] row codes (8 x code)
     static constexpr int kColC = kRowC + kPairs * 32;         // [quad][32] column codes
@@ -409,6 +411,7 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
     typedef volatile uint8_t __attribute__((address_space(3))) lds_u8;
     typedef volatile uint32_t __attribute__((address_space(3))) lds_u32;
     typedef volatile uint16_t __attribute__((address_space(3))) lds_u16;
+    typedef volatile uint64_t __attribute__((address_space(3))) lds_u64;
     lds_u8* const vb = (lds_u8*)s_so;
     lds_u32* const vw = (lds_u32*)s_so;
     const int lane = threadIdx.x, quad = lane / LP, sub = lane % LP;
@@ -615,10 +618,16 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
             if (on) {
                 uint32_t dcur;
                 asm("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(dcur) : "v"(tab[0]), "v"(sym), "v"(prev_up));
-                uint32_t hu = (uint32_t)up_h, rec = 0;
+                uint32_t hu = (uint32_t)up_h;
+                uint32_t rec[(RS + 3) / 4];   // row r's tagged value, low byte, at byte r % 4 of word r / 4
+#pragma unroll
+                for (int w = 0; w < (RS + 3) / 4; ++w) rec[w] = 0;
 #pragma unroll
                 for (int r = 0; r < RS; ++r) {
                     uint32_t a0, a1, adn;
+                    // v_perm_b32 selector: byte r % 4 from a0's byte 0, the others kept
+                    const uint32_t kSel = (r % 4 == 0) ? 0x03020104u : (r % 4 == 1) ? 0x03020400u
+                                            : (r % 4 == 2) ? 0x03040100u : 0x04020100u;
 #define SO4_CELL(UP)                                                                               \
     asm("v_add_u16 %[a0], %[cl], %[hp]\n\t"                                                         \
         "v_bfe_i32 %[adn], %[tabn], %[sym], 8\n\t"                                                  \
@@ -626,17 +635,26 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
         "v_max_i16 %[a0], %[dr], %[a0]\n\t"                                                         \
         "v_max_i16 %[a0], %[a1], %[a0]\n\t"                                                         \
         "v_and_b32 %[hp], -4, %[a0]\n\t"                                                            \
-        "v_alignbit_b32 %[rec], %[a0], %[rec], 2"                                                  \
-        : [a0] "=&v"(a0), [a1] "=&v"(a1), [adn] "=&v"(adn), [hp] "+v"(Hp[r]), [rec] "+v"(rec)       \
+        "v_perm_b32 %[rec], %[a0], %[rec], %[sel]"                                                 \
+        : [a0] "=&v"(a0), [a1] "=&v"(a1), [adn] "=&v"(adn), [hp] "+v"(Hp[r]), [rec] "+v"(rec[r / 4]) \
         : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU), [cl] "s"(CL),                                 \
-          [tabn] "v"(tab[r + 1 < RS ? r + 1 : r]), [sym] "v"(sym))
+          [tabn] "v"(tab[r + 1 < RS ? r + 1 : r]), [sym] "v"(sym), [sel] "s"(kSel))
                     if constexpr (NWK) SO4_CELL("v_add_u16 %[a1], %[cu], %[hu]\n\t");
                     else SO4_CELL("v_sub_u16_e64 %[a1], %[hu], %[cu] clamp\n\t");
 #undef SO4_CELL
                     dcur = adn;
                     hu = (uint32_t)Hp[r];
                 }
-                vw[q * 64 + lane] = RS == 16 ? rec : rec >> (32 - 2 * RS);   // row r at bits 2r
+                // the sublane's RS rows of column q: contiguous bytes of the quad's column
+                const uint32_t tpo = (uint32_t)(L::kTags + quad * 1024 + q * 32 + sub * RS);
+                if constexpr (RS == 1) vb[tpo] = (uint8_t)rec[0];
+                else if constexpr (RS == 2) *(lds_u16*)(s_so + tpo) = (uint16_t)rec[0];
+                else if constexpr (RS == 4) *(lds_u32*)(s_so + tpo) = rec[0];
+                else if constexpr (RS == 8) *(lds_u64*)(s_so + tpo) = (uint64_t)rec[1] << 32 | rec[0];
+                else {
+#pragma unroll
+                    for (int w = 0; w < RS / 4; ++w) ((lds_u32*)(s_so + tpo))[w] = rec[w];
+                }
                 prev_up = up_h;
                 hl = Hp[RS - 1];
             }
@@ -651,11 +669,10 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
     int i = res.end_i, j = res.end_j, V = res.score;
     if (!NWK && (m == 0 || n == 0)) { i = 0; j = 0; }
     bool fin = !live, parked = true;
-    // the tag of block cell (r, q): word [q][quad * LP + r / RS], bits 2 (r % RS)
-    const uint32_t tag_base = (uint32_t)(quad * LP);
+    // the tag of block cell (r, q): byte [quad][q][r] of the tags (bits 0-1)
+    const uint32_t tag_base = (uint32_t)(L::kTags + quad * 1024);
     auto tag_at = [&](int r, int q) __attribute__((always_inline)) -> uint32_t {
-        const uint32_t w = vw[(uint32_t)q * 64u + tag_base + (uint32_t)r / RS];
-        return (w >> (2u * ((uint32_t)r % RS))) & 3u;
+        return (uint32_t)vb[tag_base + (uint32_t)q * 32u + (uint32_t)r] & 3u;
     };
     // Rounds: recompute the block of every unfinished walk (all lanes: the sub-steps use DPP across
     // the quad), then each quad's sublane 0 walks its block alone, one move per iteration from the
@@ -687,9 +704,11 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
 #endif
             // SASmithWaterman.h: an edge or H == 0; NW: the walk leaves the interior (border moves below)
             if (!((i > 0) & (j > 0) & (NWK | (V != 0)) & (cr >= 0) & (cq >= 0))) break;
-            // the three cells the next move may reach (clamped into the block: a move out of it parks)
-            const int ru = max(cr - 1, 0), ql = max(cq - 1, 0);
-            const uint32_t fu = tag_at(ru, cq), fl = tag_at(cr, ql), fd = tag_at(ru, ql);
+            // the three cells the next move may reach, from one address: diagonal (r - 1, q - 1) at
+            // +0, left (r, q - 1) at +1, up (r - 1, q) at +32 (a move out of the block parks; the pad
+            // in front of the tags keeps those reads inside the LDS allocation)
+            const uint32_t a3 = tag_base + (uint32_t)(cq * 32 + cr) - 33u;
+            const uint32_t fd = (uint32_t)vb[a3] & 3u, fl = (uint32_t)vb[a3 + 1] & 3u, fu = (uint32_t)vb[a3 + 32] & 3u;
             const bool dg = f == 3u, up = f == 2u;
             const uint32_t ca = (uint32_t)(rowc >> (2 * cr)) & 3u, cb2 = (uint32_t)(colc >> (2 * cq)) & 3u;
             const bool v = dg & (((mt >> (ca * 4 + cb2)) & 1u) != 0);

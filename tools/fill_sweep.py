@@ -15,6 +15,17 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 
+
+def env_items(v):
+    """'A=1,B=2,3' -> ['A=1', 'B=2,3']: a comma starts a new assignment only before KEY=."""
+    out = []
+    for part in v.split(","):
+        if "=" in part or not out:
+            out.append(part)
+        else:
+            out[-1] += "," + part
+    return out
+
 def batch(torch, dev, P, L, seed=10 ** 10, L1=None):
     import seqalib_amd as sa
     s1, o1, s2, o2 = sa.synth_dna_batch(seed, P, L1 or L, L, threads=16)
@@ -57,15 +68,15 @@ def main():
     P = 10000
     d, res, ops = batch(torch, dev, P, L)
     variants = [v for v in a.variants.split(";") if v]
-    keys = sorted({kv.split("=")[0] for v in variants if v != "base" for kv in v.split(",")})
+    keys = sorted({kv.split("=")[0] for v in variants if v != "base" for kv in env_items(v)})
     eng.set_pipeline(True)
     for rnd in range(a.rounds):
         for v in variants:
             for k in keys:
                 os.environ.pop(k, None)
             if v != "base":
-                for kv in v.split(","):
-                    k, x = kv.split("=")
+                for kv in env_items(v):
+                    k, x = kv.split("=", 1)
                     os.environ[k] = x
             for k in range(2):
                 eng.align_device(0, sc, *[x.data_ptr() for x in d], P, L, L, res[k % len(res)].data_ptr(), ops[k % len(ops)].data_ptr(), st)
