@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
@@ -267,6 +268,40 @@ __global__ void lut_to_bits(const uint8_t* lut, uint32_t* bits) {
     uint32_t v = 0;
     for (int k = 0; k < 32; ++k) v |= (lut[a * 256 + b0 + k] != 0 ? 1u : 0u) << k;
     bits[w] = v;
+}
+
+// Host API downloads of a one-chunk call: the op streams packed back to back (pair q's nops bytes at
+// cpos[q], the exclusive prefix sum of nops; cpos[cnt] = the total), so the D2H moves the ops the
+// walks wrote instead of the m + n + 1 bytes reserved per pair (the headline batch: 48 of 92 MB).
+// ops_scan: one workgroup; ops_pack: one workgroup per pair.
+__global__ __launch_bounds__(1024) void ops_scan(const sa_result* res, uint32_t cnt, uint64_t* cpos) {
+    __shared__ uint64_t s_part[1024];
+    const uint32_t t = threadIdx.x, per = (cnt + 1023) / 1024;
+    const uint32_t a = min(t * per, cnt), b = min(a + per, cnt);
+    uint64_t sum = 0;
+    for (uint32_t q = a; q < b; ++q) sum += res[q].nops;
+    s_part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {   // inclusive scan (Hillis-Steele)
+        const uint64_t v = t >= off ? s_part[t - off] : 0;
+        __syncthreads();
+        s_part[t] += v;
+        __syncthreads();
+    }
+    uint64_t base = s_part[t] - sum;
+    for (uint32_t q = a; q < b; ++q) {
+        cpos[q] = base;
+        base += res[q].nops;
+    }
+    if (t == 1023) cpos[cnt] = s_part[1023];
+}
+__global__ __launch_bounds__(256) void ops_pack(const uint64_t* o1, const uint64_t* o2, const sa_result* res,
+                                                const uint64_t* cpos, const uint8_t* ops, uint8_t* packed) {
+    const uint32_t q = blockIdx.x;
+    const uint8_t* src = ops + o1[q] + o2[q] + q;
+    uint8_t* dst = packed + cpos[q];
+    const uint32_t n = res[q].nops;
+    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) dst[k] = src[k];
 }
 
 // Traceback flavour per launch: one wave per pair (sa_traceback_wave.hip) for few pairs, one lane
@@ -853,6 +888,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             tp.prof = fps[k].prof;
             tp.t16_delta = fps[k].t16_delta;
             tp.t16_sent = fps[k].t16_sent;
+            tp.so_lp = pipe ? 4 : 8;   // (sa_traceback_so.hip kSo4DefaultLp)
             return tp;
         };
         // Pipelined calls: the int32 variant of a T16 batch (it re-runs only the pairs the T16 fill
@@ -1058,6 +1094,8 @@ struct CopyPool {
         uint8_t* dst;
         const uint8_t* src;
         uint64_t n;
+        uint64_t grain = kSlice;                   // items per slice
+        std::function<void(uint64_t, uint64_t)> fn;   // set: items [a, b) of an index-range job
         std::atomic<uint64_t> next{0}, done{0};
     };
     static constexpr uint64_t kSlice = 1ull << 20;
@@ -1079,10 +1117,11 @@ struct CopyPool {
     }
     // one slice of job j; false when it has none left
     bool slice(Job& j) {
-        const uint64_t a = j.next.fetch_add(kSlice);
+        const uint64_t a = j.next.fetch_add(j.grain);
         if (a >= j.n) return false;
-        const uint64_t k = std::min(kSlice, j.n - a);
-        memcpy(j.dst + a, j.src + a, k);
+        const uint64_t k = std::min(j.grain, j.n - a);
+        if (j.fn) j.fn(a, a + k);
+        else memcpy(j.dst + a, j.src + a, k);
         if (j.done.fetch_add(k) + k == j.n) {
             std::lock_guard<std::mutex> g(mu);
             done_cv.notify_all();
@@ -1105,13 +1144,16 @@ struct CopyPool {
         }
     }
     std::atomic<int> in_flight{0}, max_in_flight{0};   // copy jobs posted and not yet done
-    void copy(void* d, const void* s, uint64_t bytes) {
+    void copy(void* d, const void* s, uint64_t bytes, uint64_t grain = kSlice,
+              std::function<void(uint64_t, uint64_t)> fn = nullptr) {
         const int f = in_flight.fetch_add(1) + 1;
         for (int m = max_in_flight.load(); f > m && !max_in_flight.compare_exchange_weak(m, f);) {}
         auto j = std::make_shared<Job>();
         j->dst = (uint8_t*)d;
         j->src = (const uint8_t*)s;
         j->n = bytes;
+        j->grain = grain;
+        j->fn = std::move(fn);
         {
             std::lock_guard<std::mutex> g(mu);
             jobs.push_back(j);
@@ -1126,16 +1168,29 @@ struct CopyPool {
 };
 CopyPool* g_copy_pool = nullptr;
 
+CopyPool* copy_pool() {
+    static CopyPool* pool = [] {   // never destroyed: exit-safe
+        const unsigned cpus = usable_cpus();
+        return g_copy_pool = new CopyPool(std::min(31u, cpus > 1 ? cpus - 1 : 1u));
+    }();
+    return pool;
+}
+
 void par_copy(void* dst, const void* src, uint64_t n) {
     if (n < (4ull << 20)) {
         if (n) memcpy(dst, src, n);
         return;
     }
-    static CopyPool* pool = [] {   // never destroyed: exit-safe
-        const unsigned cpus = usable_cpus();
-        return g_copy_pool = new CopyPool(std::min(31u, cpus > 1 ? cpus - 1 : 1u));
-    }();
-    pool->copy(dst, src, n);
+    copy_pool()->copy(dst, src, n);
+}
+
+// fn(a, b) over items [0, n) in slices of `grain` items, on the copy pool's workers and this thread
+void par_for(uint64_t n, uint64_t grain, std::function<void(uint64_t, uint64_t)> fn) {
+    if (n <= grain) {
+        if (n) fn(0, n);
+        return;
+    }
+    copy_pool()->copy(nullptr, nullptr, n, grain, std::move(fn));
 }
 
 // Host API batches may be cut into contiguous pair ranges ("chunks") of near-equal cells run
@@ -1315,7 +1370,15 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     // small calls: the host-decided T16 profile (HostSeqs::hhdr); chunked calls: one 32-byte
     // profile slot per chunk (HostSeqs::hprof)
     const uint64_t b_hdr = al(std::max<uint64_t>(256, 32ull * G));
-    const uint64_t io_need = b_hdr + b_s1 + b_s2 + 2 * b_o + b_res + b_ops + b_lut + b_bits;
+    // small call (one chunk, sequences the host scans, <= kSmallCall bytes each way): one upload
+    // (header + inputs, issued by run_device after it wrote the header) and one download
+    constexpr uint64_t kSmallCall = 1ull << 20;
+    const bool small = G == 1 && t1 + t2 <= kHostScanBytes && b_s1 + b_s2 + 2 * b_o <= kSmallCall &&
+                       b_res + ops_total <= kSmallCall;
+    // other one-chunk calls download their op streams packed (ops_scan / ops_pack): [cpos][packed]
+    const bool packed = G == 1 && !small && !dc;
+    const uint64_t b_cpos = packed ? al(8ull * (npairs + 1)) : 0, b_pack = packed ? b_ops : 0;
+    const uint64_t io_need = b_hdr + b_s1 + b_s2 + 2 * b_o + b_res + b_ops + b_lut + b_bits + b_cpos + b_pack;
     if (int rc = ensure_io(c, io_need)) return rc;
     uint8_t* p = c->io;
     uint32_t* const dhdr = reinterpret_cast<uint32_t*>(p); p += b_hdr;
@@ -1326,23 +1389,21 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     sa_result* dres = reinterpret_cast<sa_result*>(p); p += b_res;
     uint8_t* dops = p; p += b_ops;
     uint8_t* dlut = p; p += b_lut;
-    uint32_t* dbits = reinterpret_cast<uint32_t*>(p);
+    uint32_t* dbits = reinterpret_cast<uint32_t*>(p); p += b_bits;
+    uint64_t* const dcpos = reinterpret_cast<uint64_t*>(p); p += b_cpos;
+    uint8_t* const dpack = p;
     // pinned staging (pageable copies were measured to stall 10-25 ms per call next to PyTorch),
     // laid out as the device I/O: in = [seq1][seq2][off1'][off2'], out = [results][ops], so that a
     // small call moves its inputs in one copy and its outputs in one copy
     SA_HIP(c, c->stage.alloc(b_hdr + b_s1 + b_s2 + 2 * b_o));
-    SA_HIP(c, c->ostage.alloc(b_res + ops_total));
+    SA_HIP(c, c->ostage.alloc(b_res + al(ops_total) + 8ull * (npairs + 1)));
     uint32_t* const shdr = reinterpret_cast<uint32_t*>(c->stage.data());
     uint8_t* const si = c->stage.data() + b_hdr;
     uint64_t* const so1 = reinterpret_cast<uint64_t*>(si + b_s1 + b_s2);
     uint64_t* const so2 = reinterpret_cast<uint64_t*>(si + b_s1 + b_s2 + b_o);
     sa_result* const sres = reinterpret_cast<sa_result*>(c->ostage.data());
-    uint8_t* const sops = c->ostage.data() + b_res;
-    // small call (one chunk, sequences the host scans, <= kSmallCall bytes each way): one upload
-    // (header + inputs, issued by run_device after it wrote the header) and one download
-    constexpr uint64_t kSmallCall = 1ull << 20;
-    const bool small = G == 1 && t1 + t2 <= kHostScanBytes && b_s1 + b_s2 + 2 * b_o <= kSmallCall &&
-                       b_res + ops_total <= kSmallCall;
+    uint8_t* const sops = c->ostage.data() + b_res;   // (packed: the packed op bytes)
+    uint64_t* const scpos = reinterpret_cast<uint64_t*>(c->ostage.data() + b_res + al(ops_total));
     const bool pipe = G > 1;
     if (!c->s_out) SA_HIP(c, hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking));
     if (pipe && !c->s_fill) {
@@ -1362,7 +1423,7 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         const uint64_t ob = off1[p0] + off2[p0] + p0, on = off1[p1] + off2[p1] + p1 - ob;
         for (uint64_t x = 0; x < on || x == 0; x += kHostPiece) outp.push_back({g, ob + x, std::min(kHostPiece, on - x)});
     }
-    while (c->host_ev.size() < (size_t)G + outp.size()) {
+    while (c->host_ev.size() < (size_t)G + outp.size() + 1) {
         hipEvent_t ev;
         SA_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         c->host_ev.push_back(ev);
@@ -1441,8 +1502,19 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
             if (pipe) done = c->s_tb;   // the chunk's last kernel (its traceback) ran there
         }
         (void)on;
+        if (packed) {   // (one chunk: p0 = 0, g = 0)
+            hipLaunchKernelGGL(ops_scan, dim3(1), dim3(1024), 0, done, dres, cnt, dcpos);
+            hipLaunchKernelGGL(ops_pack, dim3(cnt), dim3(256), 0, done, do1, do2, dres, dcpos, dops, dpack);
+            SA_HIP(c, hipGetLastError());
+        }
         SA_HIP(c, hipEventRecord(c->host_ev[g], done));
         SA_HIP(c, hipStreamWaitEvent(c->s_out, c->host_ev[g], 0));
+        if (packed) {   // the results and the packed positions now; the packed bytes once their size is known
+            SA_HIP(c, hipMemcpyAsync(sres, dres, sizeof(sa_result) * cnt, hipMemcpyDeviceToHost, c->s_out));
+            SA_HIP(c, hipMemcpyAsync(scpos, dcpos, 8ull * (cnt + 1), hipMemcpyDeviceToHost, c->s_out));
+            SA_HIP(c, hipEventRecord(c->host_ev[G], c->s_out));
+            continue;
+        }
         if (small) {   // results and op bytes are contiguous in both layouts
             SA_HIP(c, hipMemcpyAsync(sres, dres, b_res + ops_total, hipMemcpyDeviceToHost, c->s_out));
             SA_HIP(c, hipEventRecord(c->host_ev[G + next_out], c->s_out));
@@ -1456,8 +1528,41 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
             SA_HIP(c, hipEventRecord(c->host_ev[G + next_out], c->s_out));
         }
     }
+    if (packed) {
+        const auto t_w = std::chrono::steady_clock::now();
+        SA_HIP(c, hipEventSynchronize(c->host_ev[G]));
+        ms_wait += since(t_w);
+        memcpy(results, sres, sizeof(sa_result) * npairs);
+        const uint64_t total = scpos[npairs];
+        if (total > ops_total) return fail(c, SA_ERR_HIP, "internal: packed op streams exceed their buffer");
+        // pieces of the packed bytes; the pairs whose bytes have all landed go to the caller's
+        // layout (pair q at off1[q] + off2[q] + q) while later pieces are in flight
+        const size_t np = (size_t)((total + kHostPiece - 1) / kHostPiece);
+        for (size_t k = 0; k < np; ++k) {
+            const uint64_t x = k * kHostPiece, n = std::min(kHostPiece, total - x);
+            SA_HIP(c, hipMemcpyAsync(sops + x, dpack + x, n, hipMemcpyDeviceToHost, c->s_out));
+            SA_HIP(c, hipEventRecord(c->host_ev[G + 1 + k], c->s_out));
+        }
+        uint32_t q0 = 0;
+        for (size_t k = 0; k <= np; ++k) {
+            const auto t_w2 = std::chrono::steady_clock::now();
+            if (k < np) SA_HIP(c, hipEventSynchronize(c->host_ev[G + 1 + k]));
+            ms_wait += since(t_w2);
+            const uint64_t landed = k < np ? (uint64_t)(k + 1) * kHostPiece : total;
+            uint32_t q1 = q0;
+            while (q1 < npairs && scpos[q1 + 1] <= landed) ++q1;
+            const auto t_o = std::chrono::steady_clock::now();
+            par_for(q1 - q0, 256, [&, q0](uint64_t a, uint64_t b) {
+                for (uint64_t q = q0 + a; q < q0 + b; ++q)
+                    memcpy(ops + off1[q] + off2[q] + q, sops + scpos[q], results[q].nops);
+            });
+            ms_out += since(t_o);
+            q0 = q1;
+        }
+        if (cb) cb(cb_user, 0, npairs);
+    }
     // each piece reaches the caller's buffers while later pieces and chunks still run
-    for (size_t k = 0; k < outp.size(); ++k) {
+    for (size_t k = 0; !packed && k < outp.size(); ++k) {
         const OutPiece& o = outp[k];
         const auto t_w = std::chrono::steady_clock::now();
         SA_HIP(c, hipEventSynchronize(c->host_ev[G + k]));

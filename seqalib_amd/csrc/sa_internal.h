@@ -178,6 +178,7 @@ struct TbParams {
     const uint32_t* prof;
     int32_t t16_delta;         // score-only NW: the fill's values are H - t16_delta (the borders)
     int32_t t16_sent;          // score-only Gotoh: the tagged Ix / Iy border (FillParams::t16_sent)
+    int so_lp;                 // score-only SW / NW: lanes per pair (0: kSo4DefaultLp)
 };
 // SA_FLAG_TIMEOUT: a SPLIT band's bounded wait for its producer expired (results invalid)
 

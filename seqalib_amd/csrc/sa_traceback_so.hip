@@ -364,10 +364,11 @@ __global__ __launch_bounds__(64) void traceback_so_kernel(TbParams P) {
 // A lone wave's serial recompute per block drops from 32 columns x R rows of dependent cells to
 // (32 + 3) sub-steps x R/4 rows, and the wave's registers (R/4 rows of state) stay few, so the
 // traceback beside the next call's fill displaces fewer of its waves.
-// Lanes per pair: 4 (16 pairs per wave).  Round 4 ran 8 at R = 32 (traceback 6.50 -> 6.30 ms,
-// profiles/tb_lp_ab_r04.txt); with round 5's lane walker and branch-free sub-steps, 4 lanes per pair
-// run half the waves beside the next call's fill and the pipelined headline step drops 18.4 ->
-// 17.9 ms (profiles/tb_lp_ab_r05.txt).  $SEQALIB_TB_LP=8 overrides.
+// Lanes per pair: 4 (16 pairs per wave) for pipelined calls, whose traceback runs beside the next
+// call's fill: half the waves of 8 lanes per pair, pipelined headline step 18.4 -> 17.9 ms (round 5,
+// profiles/tb_lp_ab_r05.txt); 8 for a call nothing else overlaps, where the traceback alone sets the
+// time (4.53 vs 4.74 ms on the headline batch, tools/so4_stats.py).  Round 4 ran 8 at R = 32
+// (profiles/tb_lp_ab_r04.txt).  TbParams::so_lp chooses (run_device); $SEQALIB_TB_LP overrides.
 constexpr int kSo4DefaultLp = 4;
 #ifdef SA_TB_STATS
 // Debug build only (-DSA_TB_STATS, tools/so4_stats.py), per wave summed: [rounds, walk-loop
@@ -1102,7 +1103,7 @@ hipError_t launch_traceback_so(int algo, int R, const TbParams& p, hipStream_t s
     // lanes per pair: $SEQALIB_TB_LP (4 or 8), else kSo4DefaultLp (16 lanes per pair, round 5:
     // 5 % fewer cycles per walk but twice the waves, traceback 6.01 -> 6.29 ms and pipelined step
     // 18.9 -> 20.4 ms)
-    int lp = kSo4DefaultLp;
+    int lp = p.so_lp == 8 && R >= 8 ? 8 : kSo4DefaultLp;
     if (const char* l = getenv("SEQALIB_TB_LP")) lp = (atoi(l) == 8 && R >= 8) ? 8 : 4;
     const uint32_t ppw = (uint32_t)(kWave / lp);
     const dim3 grid((p.count + ppw - 1) / ppw);
