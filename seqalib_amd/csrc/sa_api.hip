@@ -896,8 +896,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         // right after its fill.  On the traceback stream, behind the score-only traceback, its
         // workgroups waited for the next call's fill to be dispatched (up to 9.6 ms, round 4 rocprof)
         // and delayed the slot's release to the call after it.
-        const char* e_sk = getenv("SEQALIB_SKIPTB_STB");   // A/B (round 5), removed after measuring
-        const bool tb_on_fill = pipe && nv == 2 && !vars[1].t16 && !vars[1].pl.split && !(e_sk && e_sk[0] == '1');
+        const bool tb_on_fill = pipe && nv == 2 && !vars[1].t16 && !vars[1].pl.split;
         for (int k = 0; k < nv; ++k) {
             const Variant& v = vars[k];
             const Plan& pl = v.pl;

@@ -390,8 +390,11 @@ struct So4Lds {
     static constexpr int kPairs = kWave / LP;                 // pairs per wave
     // [quad][column q][row r] bytes (1 KiB per quad, the cell's tag in bits 0-1); 64 B of pad in
     // front: the walk reads the three cells up-left of its cell, also from a block's first row
+    // quads are 1 KiB + 32 B apart so the quads' tag stores land on different banks (at 1 KiB the
+    // same column's stores of every quad of the wave hit the same 8 banks)
     static constexpr int kTags = 64;
-    static constexpr int kEdge = kTags + kPairs * 1024;       // [lane] 16 B: packet (sub) of the quad
+    static constexpr int kQuad = 1024 + 32;
+    static constexpr int kEdge = kTags + kPairs * kQuad;       // [lane] 16 B: packet (sub) of the quad
     static constexpr int kEdge2 = kEdge + 64 * 16;            // LP = 4: [lane] 16 B: packet 4 (sublane 0)
     static constexpr int kRowC = kEdge2 + (LP < 5 ? 64 * 16 : 0);   // [quad][32] row codes (8 x code)
     static constexpr int kColC = kRowC + kPairs * 32;         // [quad][32] column codes
@@ -647,7 +650,7 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
                     hu = (uint32_t)Hp[r];
                 }
                 // the sublane's RS rows of column q: contiguous bytes of the quad's column
-                const uint32_t tpo = (uint32_t)(L::kTags + quad * 1024 + q * 32 + sub * RS);
+                const uint32_t tpo = (uint32_t)(L::kTags + quad * L::kQuad + q * 32 + sub * RS);
                 if constexpr (RS == 1) vb[tpo] = (uint8_t)rec[0];
                 else if constexpr (RS == 2) *(lds_u16*)(s_so + tpo) = (uint16_t)rec[0];
                 else if constexpr (RS == 4) *(lds_u32*)(s_so + tpo) = rec[0];
@@ -671,7 +674,7 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
     if (!NWK && (m == 0 || n == 0)) { i = 0; j = 0; }
     bool fin = !live, parked = true;
     // the tag of block cell (r, q): byte [quad][q][r] of the tags (bits 0-1)
-    const uint32_t tag_base = (uint32_t)(L::kTags + quad * 1024);
+    const uint32_t tag_base = (uint32_t)(L::kTags + quad * L::kQuad);
     auto tag_at = [&](int r, int q) __attribute__((always_inline)) -> uint32_t {
         return (uint32_t)vb[tag_base + (uint32_t)q * 32u + (uint32_t)r] & 3u;
     };

@@ -10,6 +10,7 @@
 //   SG   shipped round-4 shared-gap cell: max(U, L), bfe + add (next diag), sub clamp, max      (5)
 //   SD   shared-gap cell with the substitution by v_dot4_i32_i8 (profile bytes . one-hot column
 //        code + Hp = next diag in one op): max, dot4, sub clamp, max                          (4)
+//   SG2 / SG4  SG with 2 / 4 cells per inline-asm statement (no s_nop 0 between the cells)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -46,6 +47,39 @@ __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, i
                              : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU1), [tabn] "v"(tabn), [sym] "v"(sym));
                 (void)t0;
                 if (r % 8 == 7 && (s & 3) == 3) asm volatile("v_max3_u32 %0, %0, %1, %2" : "+v"(cml) : "v"(Hp[r - 4]), "v"(Hp[r]));
+            } else if constexpr (V == 7 || V == 8) {
+                // SG with K = 2 (V7) or 4 (V8) cells per asm statement: the compiler pads an
+                // s_nop 0 between consecutive asm statements, one per cell in SG
+                constexpr int K = V == 7 ? 2 : 4;
+                if (r % K == 0) {
+#define SG_C(HU, HP, DR, DN, TB)                                                                    \
+    "v_max_i16 %[t1], " HU ", " HP "\n\t"                                                           \
+    "v_bfe_i32 " DN ", " TB ", %[sym], 8\n\t"                                                       \
+    "v_add_u16 " DN ", " HP ", " DN "\n\t"                                                          \
+    "v_sub_u16_e64 %[t1], %[t1], %[cu] clamp\n\t"                                                   \
+    "v_max_i16 " HP ", " DR ", %[t1]\n\t"
+                    uint32_t d0, d1;
+                    const uint32_t t1_ = tab[r + 1 < R ? r + 1 : R - 1], t2_ = tab[r + 2 < R ? r + 2 : R - 1];
+                    if constexpr (K == 2) {
+                        asm volatile(SG_C("%[hu]", "%[h0]", "%[dr]", "%[d0]", "%[ta]") SG_C("%[h0]", "%[h1]", "%[d0]", "%[d1]", "%[tb]")
+                                     : [t1] "=&v"(t1), [d0] "=&v"(d0), [d1] "=&v"(d1), [h0] "+v"(Hp[r]), [h1] "+v"(Hp[r + 1 < R ? r + 1 : r])
+                                     : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU1), [ta] "v"(t1_), [tb] "v"(t2_), [sym] "v"(sym));
+                        dn = d1;
+                    } else {
+                        const uint32_t t3_ = tab[r + 3 < R ? r + 3 : R - 1], t4_ = tab[r + 4 < R ? r + 4 : R - 1];
+                        asm volatile(SG_C("%[hu]", "%[h0]", "%[dr]", "%[d0]", "%[ta]") SG_C("%[h0]", "%[h1]", "%[d0]", "%[d1]", "%[tb]")
+                                     SG_C("%[h1]", "%[h2]", "%[d1]", "%[d0]", "%[tc]") SG_C("%[h2]", "%[h3]", "%[d0]", "%[d1]", "%[td]")
+                                     : [t1] "=&v"(t1), [d0] "=&v"(d0), [d1] "=&v"(d1), [h0] "+v"(Hp[r]), [h1] "+v"(Hp[(r + 1) % R]),
+                                       [h2] "+v"(Hp[(r + 2) % R]), [h3] "+v"(Hp[(r + 3) % R])
+                                     : [dr] "v"(dcur), [hu] "v"(hu), [cu] "s"(CU1), [ta] "v"(t1_), [tb] "v"(t2_), [tc] "v"(t3_), [td] "v"(t4_), [sym] "v"(sym));
+                        dn = d1;
+                    }
+#undef SG_C
+                    if ((r + K) % 8 == 0 && (s & 3) == 3) asm volatile("v_max3_u32 %0, %0, %1, %2" : "+v"(cml) : "v"(Hp[r + K - 5]), "v"(Hp[r + K - 1]));
+                    dcur = dn;
+                    hu = Hp[r + K - 1];
+                }
+                continue;
             } else if constexpr (V == 6) {
                 asm volatile("v_max_i16 %[t1], %[hu], %[hp]\n\t"
                              "v_dot4_i32_i8 %[dn], %[tabn], %[oh], %[hp]\n\t"
@@ -112,6 +146,8 @@ int main(int argc, char** argv) {
         {"SOB SO + bottom-row stream R32", cells<4, 32>, 32},
         {"SG shared-gap shipped R32 (5)", cells<5, 32>, 32},
         {"SD shared-gap dot4 R32 (4)", cells<6, 32>, 32},
+        {"SG2 SG, 2 cells per asm R32 (5)", cells<7, 32>, 32},
+        {"SG4 SG, 4 cells per asm R32 (5)", cells<8, 32>, 32},
         {"SD shared-gap dot4 R16 (4)", cells<6, 16>, 16},
         {"SO score-only R16 (6.5)", cells<1, 16>, 16},
         {"SO score-only R64 (6.5)", cells<1, 64>, 64},
