@@ -217,7 +217,9 @@ struct Variant {
     bool so = false;   // score-only fill + block-recompute traceback (sa_traceback_so.hip)
     uint32_t snap_nch = 0;
     uint64_t snap_h_slot = 0, snap_p_slot = 0;   // 32-bit words per pair
-    uint64_t part_slot = 0;   // score-only band units: 64-bit per-band maxima per pair
+    uint64_t part_slot = 0;   // score-only band units: 64-bit per-unit maxima per pair
+    uint32_t segs = 1;        // score-only SW / NW: column segments per band (FillParams::part_segs)
+    uint64_t seg_slot = 0;    // their hand-off words per pair (FillParams::seg_hand)
     uint64_t snap_c_slot = 0; // score-only SW: 32-bit (band, chunk) maxima per pair (FillParams::snap_c)
     uint64_t slot_bytes = 0;
     int kernel = SA_KERNEL_INT32;
@@ -251,13 +253,21 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
     }
     if (v.so) {
         v.pl.g = make_geom(algo, v.pl.R, max_m, max_n, kGeomEdge);
-        v.part_slot = v.pl.g.bands;
+        if (!is_affine(algo)) {
+            // column segments: a band's chunks in kSoSegs units of at least 2 chunks each, so the
+            // launch tail is half a band (sa_fill_impl.h BU); $SEQALIB_SO_SEGS sets the count
+            uint32_t sg = kSoSegs;
+            if (const char* e = getenv("SEQALIB_SO_SEGS")) sg = (uint32_t)std::max(1, atoi(e));
+            v.segs = std::max(1u, std::min(sg, v.snap_nch / 2));
+            v.seg_slot = v.segs > 1 ? (uint64_t)v.pl.g.bands * v.segs * (v.pl.R + 1) * kWave : 0;
+        }
+        v.part_slot = (uint64_t)v.pl.g.bands * v.segs;
         if (algo == SA_SW) v.snap_c_slot = (uint64_t)v.pl.g.bands * v.snap_nch;
     }
     if (v.pl.split) v.pl.rowbuf_elems = 0;   // hand-off granules live in c->split
     v.kernel = v.cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
     v.slot_bytes = v.pl.g.dir_slot + v.pl.rowbuf_elems * 4 + (v.snap_h_slot + 2 * v.snap_p_slot) * 4 + v.part_slot * 8 +
-                   v.snap_c_slot * 4;
+                   v.snap_c_slot * 4 + v.seg_slot * 4;
     return v;
 }
 
@@ -852,8 +862,10 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             if (v.so) {   // band units: launch epoch, per-band maxima (after the chunk maxima); ticket below
                 fp.epoch = ++c->fill_epoch;
                 fp.band_part = reinterpret_cast<unsigned long long*>(fp.snap_m + per_launch * v.snap_p_slot);
-                fp.part_bands = (uint32_t)v.part_slot;
+                fp.part_bands = (uint32_t)v.pl.g.bands;
                 fp.snap_c = reinterpret_cast<int32_t*>(fp.band_part + per_launch * v.part_slot);
+                fp.seg_hand = reinterpret_cast<uint32_t*>(fp.snap_c + per_launch * v.snap_c_slot);
+                fp.seg_slot = v.seg_slot;
             }
             fp.snap_h_slot = v.snap_h_slot; fp.snap_p_slot = v.snap_p_slot; fp.snap_nch = v.snap_nch;
             fp.split_bands = (uint32_t)sp_bands;
@@ -862,6 +874,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fp.hand_x_off = pl.split ? hand_x_off : 0;
             fp.part = pl.split ? reinterpret_cast<int32_t*>(spbase + sp_part) : nullptr;
             fp.wait_ticks = wait_ticks;
+            fp.part_segs = std::max<uint32_t>(1, v.segs);
             FillVariant fv{pl.R, lut, allow || v.t16, keyed, v.t16, v.cmax, pl.split, bits};
             fv.so = v.so;
             return fv;
@@ -908,7 +921,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             // grid: SPLIT one workgroup per (pair, band) slot; score-only SW / NW one per (pair,
             // band) unit (band units, sa_fill_impl.h BU); otherwise one per pair
             const bool units = v.so && !is_affine(algo);
-            const uint32_t grid = pl.split ? (uint32_t)(cnt * sp_bands) : units ? cnt * pl.g.bands : cnt;
+            const uint32_t grid = pl.split ? (uint32_t)(cnt * sp_bands) : units ? cnt * pl.g.bands * v.segs : cnt;
             hipError_t e = launch_fill(algo, fv, fp, grid, sf);
             if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
             if (kev) SA_HIP(c, hipEventRecord(kev[2 * k + 1], sf));

@@ -279,13 +279,17 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     // SPLIT (few pairs): one single-wave workgroup per (pair, band).  Bands are handed out by a
     // ticket counter in the order workgroups actually start, so band b's producer (ticket - 1)
     // is always already running or done: no wait can deadlock whatever the residency.
-    uint32_t slot, band0 = 0;
+    uint32_t slot, band0 = 0, seg = 0;
     if constexpr (BU) {
+        // tickets band-major, then segment-major: (band, segment, pair)
         uint32_t t = 0;
         if (lane == 0) t = atomicAdd(P.ticket, 1u);
         t = __builtin_amdgcn_readlane(t, 0);
-        band0 = t / P.count;
-        slot = t - band0 * P.count;
+        const uint32_t row = P.count * P.part_segs;
+        band0 = t / row;
+        const uint32_t rem = t - band0 * row;
+        seg = rem / P.count;
+        slot = rem - seg * P.count;
     } else if constexpr (SPLIT) {
         if (threadIdx.x == 0) {
             s_ticket = atomicAdd(P.ticket, 1u);
@@ -404,7 +408,15 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
         for (int k = threadIdx.x; k < 2048; k += blockDim.x) s_lut[k] = P.lutbits[k];
     }
     if (P.stage_seq2) {
-        for (int k = threadIdx.x; k < n; k += blockDim.x)
+        // (BU: the columns of this unit's chunks and the 64 before them)
+        int k0 = 0, k1 = n;
+        if constexpr (BU) {
+            const uint32_t nc = chunks_per_band((uint32_t)n);
+            const uint32_t sp = max(1u, min(P.part_segs, nc / 2)), cp = (nc + sp - 1) / sp;
+            k0 = max(0, (int)(seg * cp * kChunk) - kWave);
+            k1 = min(n, (int)((seg + 1) * cp * kChunk));
+        }
+        for (int k = k0 + (int)threadIdx.x; k < k1; k += blockDim.x)
             s_seq2[k] = T16 ? (uint8_t)t16_code8(symp, s2[k]) : s2[k];
     }
     if constexpr (SPLIT) {   // tag 0 = no column yet (LDS holds a previous workgroup's data)
@@ -437,7 +449,17 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     if (BU && (int)band0 >= (B > 0 ? B : 1)) return;   // (an empty pair: unit 0 reports it)
     const uint32_t nch = chunks_per_band((uint32_t)n);
     const uint32_t period = sched_period(nch, W);
-    const uint32_t total = SPLIT ? nch : BU ? (B > 0 ? nch : 0u) : total_phases((uint32_t)B, (uint32_t)n, W);
+    // BU column segments: this unit runs chunks [c0, c1) of its band (a segment past the pair's
+    // chunks is empty and leaves at once); every boundary c0 >= 2 lies where all 64 lanes have
+    // reached their first column, so the unit starts from the state the previous segment handed on
+    const uint32_t SEGS = BU ? P.part_segs : 1u;
+    const uint32_t segs_p = max(1u, min(SEGS, nch / 2));   // this pair's (at least 2 chunks each)
+    const uint32_t cps = (nch + segs_p - 1) / segs_p;
+    const uint32_t c0 = BU ? seg * cps : 0u;
+    const uint32_t c1 = BU ? min(nch, c0 + cps) : nch;
+    const uint32_t last_seg = BU && nch > 0 ? (nch - 1) / cps : 0u;
+    if (BU && seg > (B > 0 ? last_seg : 0u)) return;   // (uniform) an empty segment (an empty pair: unit 0 reports)
+    const uint32_t total = SPLIT ? nch : BU ? (B > 0 ? c1 : 0u) : total_phases((uint32_t)B, (uint32_t)n, W);
     const uint32_t epoch16 = ((P.epoch % 65535u) + 1u) << 16;   // BU: this launch's granule tag
     // SPLIT hand-off: band b's last row as 8-byte {tag = 1, value} granules written
     // write-through (sc1) per column, polled by band b+1 with sc1 loads; the data is its own flag
@@ -445,6 +467,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     typedef unsigned long long __attribute__((address_space(1))) gu64;
     gu64* const hand_pair = SPLIT ? (gu64*)(P.hand + (uint64_t)slot * P.split_bands * P.max_n) : nullptr;
     uint32_t tmo = 0;   // SPLIT: a bounded wait expired
+    uint32_t seg_lost = 0;   // BU: the wait for the previous segment's hand-off expired (the pair is re-run)
 #ifdef SA_TB_STATS
     unsigned long long ev[12] = {};
 #endif
@@ -1196,7 +1219,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
         }
     };
 
-    for (uint32_t ph = 0; ph < total; ++ph) {
+    for (uint32_t ph = BU ? c0 : 0u; ph < total; ++ph) {
         const int rel = (int)ph - w * kLagPhases;
         if (SPLIT || BU || rel >= 0) {
             const uint32_t k = (SPLIT || BU) ? 0u : (uint32_t)rel / period;
@@ -1204,7 +1227,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
             const int band = (SPLIT || BU) ? (int)band0 : w + (int)k * W;
             if (chunk < nch && band < B) {
                 // ---------------------------------------------------------------- band start
-                if (chunk == 0) {
+                if (chunk == (BU ? c0 : 0u)) {
                     row0 = band * BAND + lane * R;
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
@@ -1233,6 +1256,42 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                     if constexpr (ALG == SA_NW) prev_up = SC * (row0 * G - P.t16_delta);
                     else if constexpr (ALG == SA_GLOBAL_GOTOH) prev_up = SC * ((row0 == 0 ? 0 : GO + row0 * GE) - P.t16_delta);
                     else prev_up = 0;
+                    if constexpr (BU) {
+                        if (c0 > 0) {
+                            // a later segment: this lane's R values and diagonal input at column
+                            // 32 c0 - 1 - lane from the previous segment's unit (epoch-tagged, polled
+                            // as the band granules are), its last-row value for the lane below and
+                            // the column symbol the DPP shift hands it at the first step
+                            const uint32_t* hs = P.seg_hand + (uint64_t)slot * P.seg_slot +
+                                                 ((uint64_t)band * SEGS + seg - 1) * (R + 1) * kWave + lane;
+                            uint32_t hv[R + 1];
+                            auto rd = [&]() __attribute__((always_inline)) {
+#pragma unroll
+                                for (int r = 0; r <= R; ++r)
+                                    hv[r] = __hip_atomic_load(hs + r * kWave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            };
+                            auto stale = [&]() __attribute__((always_inline)) -> bool {
+                                bool st = false;
+#pragma unroll
+                                for (int r = 0; r <= R; ++r) st |= (hv[r] & 0xffff0000u) != epoch16;
+                                return st;
+                            };
+                            rd();
+                            // (bounded: a producer that never comes leaves the unit after ~2^20
+                            // polls with the pair flagged for the int32 re-run)
+                            for (uint32_t it = 0; __builtin_amdgcn_ballot_w64(stale()) != 0; ++it) {
+                                if (it >= (1u << 20)) { seg_lost = 1; break; }
+                                __builtin_amdgcn_s_sleep(2);
+                                rd();
+                            }
+#pragma unroll
+                            for (int r = 0; r < R; ++r) Hp[r] = (int)(hv[r] & 0xffffu);
+                            prev_up = (int)(hv[R] & 0xffffu);
+                            hl = Hp[R - 1];
+                            const int cs = (int)(c0 * kChunk) - 1 - lane;
+                            sym = cs >= 0 && cs < n ? (P.stage_seq2 ? (int)s_seq2[cs] : (int)t16_code8(symp, s2[cs])) : 0;
+                        }
+                    }
                 }
                 // ---------------------------------------------------------------- one chunk
                 const int kC = (int)chunk * kChunk;
@@ -1359,6 +1418,18 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                         P.snap_p[(uint64_t)slot * P.snap_p_slot + e * kWave + lane] = prev_up;
                     }
                 }
+                if constexpr (BU) {
+                    if (chunk + 1 == c1 && c1 < nch) {   // hand this lane's state on to the next segment
+                        uint32_t* hs = P.seg_hand + (uint64_t)slot * P.seg_slot +
+                                       ((uint64_t)band * SEGS + seg) * (R + 1) * kWave + lane;
+#pragma unroll
+                        for (int r = 0; r < R; ++r)
+                            __hip_atomic_store(hs + r * kWave, epoch16 | ((uint32_t)Hp[r] & 0xffffu), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(hs + R * kWave, epoch16 | ((uint32_t)prev_up & 0xffffu), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
                 // ---------------------------------------------------------------- band end
                 if (chunk == nch - 1) {
                     if constexpr (CMAX) {
@@ -1434,13 +1505,15 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, off));
             typedef unsigned long long __attribute__((address_space(1))) gu64p;
-            gu64p* const part = (gu64p*)(P.band_part + (uint64_t)slot * P.part_bands);
-            if (B > 1 && (int)band0 < B - 1) {
+            gu64p* const part = (gu64p*)(P.band_part + (uint64_t)slot * P.part_bands * SEGS);
+            // the pair's final unit (last band, last segment) folds the other units' partials
+            const uint32_t me = band0 * SEGS + seg, nparts = B > 0 ? (uint32_t)(B - 1) * SEGS + last_seg : 0u;
+            if (me != nparts) {
                 if (lane == 0)
-                    __hip_atomic_store(part + band0, (unsigned long long)P.epoch << 32 | smax, __ATOMIC_RELAXED,
+                    __hip_atomic_store(part + me, (unsigned long long)P.epoch << 32 | smax | seg_lost << 31, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
 #ifdef SA_TB_STATS
-                const uint64_t sid = (uint64_t)band0 * P.count + slot;
+                const uint64_t sid = ((uint64_t)band0 * SEGS + seg) * P.count + slot;
                 if (threadIdx.x == 0 && sid < 32768) {
                     g_fill_stats[sid][0] = st_t0;
                     g_fill_stats[sid][1] = __builtin_amdgcn_s_memrealtime();
@@ -1451,15 +1524,18 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
             }
             // (the last band: every earlier band finished its last chunk before this one's last
             // chunk could read it, so its partial is at most a few instructions away)
-            for (int b = lane; b < B - 1; b += kWave) {
+            for (uint32_t b = lane; b < nparts; b += kWave) {
+                if (b % SEGS > last_seg) continue;   // (empty segments store nothing)
                 unsigned long long x;
                 while (((x = __hip_atomic_load(part + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != P.epoch)
                     __builtin_amdgcn_s_sleep(2);
-                smax = max(smax, (uint32_t)x);
+                seg_lost |= (uint32_t)(x >> 31) & 1u;
+                smax = max(smax, (uint32_t)x & 0x7fffffffu);
             }
+            seg_lost = __builtin_amdgcn_ballot_w64(seg_lost != 0) != 0 ? 1u : 0u;
         }
 #ifdef SA_TB_STATS
-        const uint64_t sid = BU ? (uint64_t)band0 * P.count + slot : slot;   // (BU: one entry per unit)
+        const uint64_t sid = BU ? ((uint64_t)band0 * SEGS + seg) * P.count + slot : slot;   // (BU: one entry per unit)
         if (threadIdx.x == 0 && sid < 32768) {
             g_fill_stats[sid][0] = st_t0;
             g_fill_stats[sid][1] = __builtin_amdgcn_s_memrealtime();
@@ -1505,12 +1581,13 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                 r.score = h; r.end_i = bi; r.end_j = bjj;
             }
             if (T16 && B != 0 && h > P.retry_above) r.flags |= kFlagRetry;
+            if (BU && seg_lost) r.flags |= kFlagRetry;
             if (redo) r.flags |= kFlagRedo;
             if (P.rerun) r.flags |= kFlagRerun;
             P.res[pidx] = r;
         }
     } else {
-        if (BU && B > 0 && (int)band0 != (m - 1) / BAND) return;   // (uniform) the unit holding row m reports
+        if (BU && B > 0 && ((int)band0 != (m - 1) / BAND || seg != last_seg)) return;   // (uniform) the unit holding (m, n) reports
         if (threadIdx.x == 0) {   // the phase loop's last barrier orders the owner's s_score store
             sa_result r = {};
             r.end_i = m;

@@ -86,6 +86,13 @@ struct FillParams {
     uint32_t epoch;
     unsigned long long* band_part;
     uint32_t part_bands;
+    // column segments of the band units (score-only SW / NW): every (pair, band) is cut into
+    // part_segs units of consecutive chunks; a unit hands its lanes' state at its last column to
+    // the next segment's unit through seg_hand (per slot: bands x segs x (R + 1) x 64 epoch-tagged
+    // 16-bit values, seg_slot words).  part_segs = 1: one unit per band.
+    uint32_t part_segs;
+    uint32_t* seg_hand;
+    uint64_t seg_slot;
     // score-only SW: per slot and (band, chunk) the wave's maximum of the chunk maxima (snap_m), so
     // the end-cell replay reads the lane maxima of the chunks that reach its threshold only
     int32_t* snap_c;
@@ -204,6 +211,11 @@ constexpr int kAuxTicket = 32;   // the score-only fill's unit ticket (zeroed be
 // Score-only SW fill: steady chunks track the lane maximum at rows and steps 3 mod 4 only, so a
 // cell is at most its tracked cell - kSoSlack * gap (3 rows + 3 columns of gap moves)
 constexpr int kSoSlack = 6;
+// Score-only SW / NW band units: column segments per band (FillParams::part_segs).  A band of a
+// 4096-column pair is ~3 ms of one wave; cut into 2 units the launch tail (the last generation of
+// units draining) is half of that.  Pipelined headline step (profiles/fill_segs_ab_r05.txt):
+// 1 segment 17.95 / 18.07 ms, 2: 17.51 / 17.53, 3: 17.66 / 17.64, 4: 17.75 / 17.75.
+constexpr uint32_t kSoSegs = 2;
 hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uint8_t* d2,
                                 const uint64_t* o2, uint32_t npairs, uint32_t* aux, hipStream_t s);
 // decide_t16: from the bitmap, aux[kAuxSel] = 1 if the batch has <= 4 distinct symbols (then the

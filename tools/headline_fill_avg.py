@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Average duration of the headline fill dispatches in a rocprofv3 --kernel-trace run of bench.py:
 the score-only SW fill (fill_so_kernel<0, 32>) launched on the headline batch's grid (10,000 pairs
-x 2 bands = 20,000 single-wave workgroups = 1,280,000 threads), so the configs legs' launches of
+x 2 bands x 2 column segments = 40,000 single-wave workgroups = 2,560,000 threads), so the configs legs' launches of
 the same kernel on other grids are not mixed in.  Prints one JSON line.
     python3 tools/headline_fill_avg.py gpurun_out/prof_bench [--grid 1280000]"""
 import argparse
@@ -12,7 +12,7 @@ import os
 
 ap = argparse.ArgumentParser()
 ap.add_argument("dir")
-ap.add_argument("--grid", type=int, default=10000 * 2 * 64)
+ap.add_argument("--grid", type=int, default=10000 * 2 * 2 * 64)   # pairs x bands x column segments x 64
 ap.add_argument("--kernel", default="fill_so_kernel<0, 32>")
 a = ap.parse_args()
 durs = []

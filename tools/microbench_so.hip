@@ -28,6 +28,11 @@ __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, i
     for (int r = 0; r < R; ++r) { tab[r] = in[(lane * 7 + r) & 1023]; Hp[r] = 0; }
     uint32_t hl = 0, sym = (lane & 3) * 8, prev_up = 0, rec = 0, acc = 0, cml = 0, bot = 0, oh = 1u << ((lane & 3) * 8);
     const uint32_t CU = 2, CL = 0xfffd, CU1 = 1, CL1 = 0xffff;
+    if constexpr (V == 9 || V == 10) {
+        // SGS: the SG cell with the waves of a SIMD started out of phase (the same work)
+        const int ph = (int)(blockIdx.x / 1024) % 4;   // (workgroups are spread over the SIMDs in launch order)
+        for (int k = 0; k < ph * (V == 9 ? 8 : 40); ++k) __builtin_amdgcn_s_sleep(127);
+    }
     for (int s = 0; s < steps; ++s) {
         const uint32_t up_h = shr1(in[s & 1023], hl);
         if constexpr (V == 6) oh = shr1(1u << (((s * 7) & 3) * 8), oh);
@@ -38,7 +43,7 @@ __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, i
         for (int r = 0; r < R; ++r) {
             uint32_t t0, t1, dn = 0;
             const uint32_t tabn = tab[r + 1 < R ? r + 1 : r];
-            if constexpr (V == 5) {
+            if constexpr (V == 5 || V == 9 || V == 10) {
                 asm volatile("v_max_i16 %[t1], %[hu], %[hp]\n\t"
                              "v_bfe_i32 %[dn], %[tabn], %[sym], 8\n\tv_add_u16 %[dn], %[hp], %[dn]\n\t"
                              "v_sub_u16_e64 %[t1], %[t1], %[cu] clamp\n\t"
@@ -146,6 +151,8 @@ int main(int argc, char** argv) {
         {"SOB SO + bottom-row stream R32", cells<4, 32>, 32},
         {"SG shared-gap shipped R32 (5)", cells<5, 32>, 32},
         {"SD shared-gap dot4 R32 (4)", cells<6, 32>, 32},
+        {"SGS SG, waves out of phase (8 x 8K cyc)", cells<9, 32>, 32},
+        {"SGT SG, waves out of phase (40 x 8K cyc)", cells<10, 32>, 32},
         {"SG2 SG, 2 cells per asm R32 (5)", cells<7, 32>, 32},
         {"SG4 SG, 4 cells per asm R32 (5)", cells<8, 32>, 32},
         {"SD shared-gap dot4 R16 (4)", cells<6, 16>, 16},
