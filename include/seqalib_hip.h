@@ -244,6 +244,15 @@ int sa_plan_query_ex(int algo, const sa_scoring* scoring, uint32_t max_m, uint32
                      uint32_t npairs, int nsym, int* kernel, int* rows_per_lane, int* waves,
                      uint64_t* workspace_bytes_per_pair);
 
+/* Tests only (tests/test_gpu_robust.py).  SA_HOOK_HAND_TAG: the band-unit hand-off tag of the
+ * context's last launch becomes `value` (0..65535; the next launch takes value + 1, and at 65535 the
+ * hand-off buffer is zeroed and the tags restart at 1).  SA_HOOK_POISON_WS: every 32-bit word of the
+ * context's cached workspace becomes `value` (after its pending work; synchronous), as stale words
+ * of earlier calls of other shapes would be.  Returns SA_OK or SA_ERR_ARG. */
+#define SA_HOOK_HAND_TAG 1
+#define SA_HOOK_POISON_WS 2
+int sa_test_hook(sa_ctx* ctx, int hook, uint64_t value);
+
 /* Synthetic DNA: std::mt19937_64(seed), symbol = "ACGT"[g() & 3]. */
 int sa_synth_dna(uint64_t seed, uint32_t len, uint8_t* out);
 /* "Related" copy of src: per position r = g() % 100: r < 10 substitute "ACGT"[g()&3];

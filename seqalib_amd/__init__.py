@@ -40,6 +40,7 @@ SA_FLAG_DIVERGED, SA_FLAG_BAD_SHAPE, SA_FLAG_SIZE_HACK, SA_FLAG_TIMEOUT = 1, 2, 
 SA_KERNEL_INT32, SA_KERNEL_T16, SA_KERNEL_T16_ENDCELL, SA_KERNEL_TINY = 0, 1, 2, 3
 SA_PIPELINE_DEPTH = 2   # pipelined device calls that may run at once (distinct output buffers)
 SA_RECORDS_FLAGS, SA_RECORDS_TAGS, SA_RECORDS_SCORE_ONLY = 0, 1, 2
+SA_HOOK_HAND_TAG, SA_HOOK_POISON_WS = 1, 2   # sa_test_hook (tests only)
 INT32_MIN = -(2 ** 31)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -134,13 +135,14 @@ def load_library():
     L.sa_last_plan_ex.argtypes = [vp, i32p, i32p, i32p, i32p]
     L.sa_set_pipeline.argtypes = [vp, C.c_int]
     L.sa_wait.argtypes = [vp]
+    L.sa_test_hook.argtypes = [vp, C.c_int, C.c_uint64]
     L.sa_synth_dna.argtypes = [C.c_uint64, C.c_uint32, vp]
     L.sa_synth_mutate.argtypes = [vp, C.c_uint32, C.c_uint64, vp, C.c_uint32, C.POINTER(C.c_uint32)]
     L.sa_synth_dna_batch.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_int]
     for fn in ("sa_set_workspace_limit", "sa_trim", "sa_align_batch", "sa_align_batch_bits", "sa_align_batch_device",
                "sa_multi_create", "sa_multi_align_batch",
                "sa_last_timings", "sa_last_kernel_timings", "sa_last_plan", "sa_last_plan_ex", "sa_plan_query", "sa_plan_query_ex", "sa_synth_dna", "sa_synth_mutate", "sa_synth_dna_batch",
-               "sa_create", "sa_device_count", "sa_set_pipeline", "sa_wait"):
+               "sa_create", "sa_device_count", "sa_set_pipeline", "sa_wait", "sa_test_hook"):
         getattr(L, fn).restype = C.c_int
     if L.sa_version() != 1:
         raise SeqalibError("libseqalib_hip ABI version mismatch")
@@ -478,6 +480,10 @@ class Engine:
     def set_pipeline(self, enable: bool):
         """Overlap consecutive align_device calls (sa_set_pipeline); results need wait()."""
         self._check(self.L.sa_set_pipeline(self.h, 1 if enable else 0), "sa_set_pipeline")
+
+    def test_hook(self, hook: int, value: int):
+        """Tests only (sa_test_hook): SA_HOOK_HAND_TAG / SA_HOOK_POISON_WS."""
+        self._check(self.L.sa_test_hook(self.h, hook, value), "sa_test_hook")
 
     def wait(self):
         """Wait for all pipelined align_device work (sa_wait)."""

@@ -62,7 +62,16 @@ struct sa_ctx {
     // cross-call pipeline of the device API (sa_set_pipeline): fills on s_fill, tracebacks on
     // s_tb, kPipeSlots workspace slots; ev_slot[k] = traceback of the last call that used slot k done
     int pipeline = 0;
-    uint32_t fill_epoch = 0;   // score-only fills: per-launch tag of their hand-off granules
+    // Band-unit hand-off buffer (score-only SW / NW fills, sa_fill_impl.h BU): the row granules, the
+    // column-segment state and the per-unit maxima, all {tag, value} words polled by their consumers.
+    // Only those fills write it (every kernel that touches it runs on the fill stream, so one copy
+    // serves both pipeline slots), and it is zeroed when allocated and whenever hand_tag wraps: a word
+    // there carries the tag of the launch that wrote it or 0, so a consumer can never take an earlier
+    // launch's word -- of any shape -- for its producer's.  hand_tag: the last launch's tag, 1..65535.
+    uint8_t* hand = nullptr;
+    uint64_t hand_bytes = 0;
+    uint32_t hand_tag = 0;
+    bool hand_dirty = false;   // (tests: sa_test_hook poisoned it) zero before the next launch
     hipStream_t s_fill = nullptr, s_tb = nullptr;
     hipEvent_t ev_in = nullptr, ev_slot[kPipeSlots] = {};
     uint64_t pipe_k = 0;
@@ -335,6 +344,39 @@ int tb_seg_mode() {
         if (!strcmp(e, "wave") || !strcmp(e, "lane")) return 0;
     }
     return 1;
+}
+
+int zero_hand(sa_ctx* c, uint64_t need, hipStream_t st, bool grow);
+// Before a band-unit launch: the hand-off buffer (sa_ctx::hand, grow-only) holds need bytes, and
+// a fresh one -- or one whose tag is about to wrap -- is zeroed on the fill stream st, where every
+// kernel that reads or writes it runs.  Then the launch takes the next tag (c->hand_tag).
+int next_hand_tag(sa_ctx* c, uint64_t need, hipStream_t st) {
+    const bool grow = c->hand_bytes < need;
+    if (grow || c->hand_dirty || c->hand_tag >= 65535) {
+        if (int rc = zero_hand(c, need, st, grow)) return rc;
+    }
+    ++c->hand_tag;
+    return SA_OK;
+}
+
+int zero_hand(sa_ctx* c, uint64_t need, hipStream_t st, bool grow) {
+    if (grow) {
+        if (c->hand) {
+            if (int rc = drain(c)) return rc;
+            (void)hipFree(c->hand);
+            c->hand = nullptr;
+            c->hand_bytes = 0;
+        }
+        if (hipMalloc(&c->hand, need) != hipSuccess) {
+            c->hand = nullptr;
+            return fail(c, SA_ERR_NOMEM, "hipMalloc of the band hand-off buffer (" + std::to_string(need) + " bytes) failed");
+        }
+        c->hand_bytes = need;
+    }
+    SA_HIP(c, hipMemsetAsync(c->hand, 0, c->hand_bytes, st));
+    c->hand_tag = 0;
+    c->hand_dirty = false;
+    return SA_OK;
 }
 
 int ensure_ws(sa_ctx* c, uint64_t need) {
@@ -689,8 +731,12 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         hp[5] = (uint32_t)ha->sel;
         if (in_hdr) prof = hs->dhdr;
         else SA_HIP(c, hipMemcpyAsync(aux + kAuxProf, hp, 24, hipMemcpyHostToDevice, stream));
+        // (band units that hand state between workgroups keep the int32 variant: a unit whose wait
+        // for its producer expired flags its pair for that re-run, sa_fill_impl.h BU)
+        const Variant vt = make_variant(algo, max_m, max_n, npairs, true, true);
+        const bool bu_hand = vt.so && !is_affine(algo) && (vt.pl.g.bands > 1 || vt.segs > 1);
         if (ha->sel == 0) only = 2;
-        else if (tm.retry_above == INT_MAX) only = 1;
+        else if (tm.retry_above == INT_MAX && !bu_hand) only = 1;
         else sel = prof + 5;
     }
     if (hs && hs->up_bytes)
@@ -735,6 +781,21 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                                          " bytes of workspace, above the limit");
     int rc = ensure_ws(c, std::max<uint64_t>(pipe ? nslots * need : need, 4096));
     if (rc) return rc;
+    // band units' hand-off words (score-only SW / NW), per launch: [row granules][per-unit words]
+    // [segment state], each part 256-byte aligned; one copy for both pipeline slots (sa_ctx::hand)
+    auto al256 = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
+    uint64_t hand_rb = 0, hand_part = 0, hand_seg = 0;
+    for (int k = 0; k < nv; ++k)
+        if (vars[k].so && !is_affine(algo)) {
+            hand_rb = std::max(hand_rb, al256(per_launch * vars[k].pl.rowbuf_elems * 4));
+            hand_part = std::max(hand_part, al256(per_launch * vars[k].part_slot * 8));
+            hand_seg = std::max(hand_seg, al256(per_launch * vars[k].seg_slot * 4));
+        }
+    const uint64_t hand_need = hand_rb + hand_part + hand_seg;
+    const uint32_t so_wait_polls = [] {
+        const char* e = getenv("SEQALIB_SO_WAIT_POLLS");   // tests only: force the lost-producer path
+        return e ? (uint32_t)std::max(1L, atol(e)) : kSoWaitPollsDefault;
+    }();
     // SPLIT scratch, per variant: [ticket][hand-off granules] (zeroed before its fill; the
     // segmented traceback reads the granules after both variants' fills), then the per-band
     // partials and the segmented traceback's exit records.  Pipelined calls alternate two copies
@@ -859,13 +920,25 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fp.retry_above = v.t16 ? tm.retry_above : INT_MAX;
             fp.t16_sent = v.t16 ? tm.sent : -10000;
             fp.snap_h = snap_h; fp.snap_p = snap_p; fp.snap_m = snap_p + per_launch * v.snap_p_slot;
-            if (v.so) {   // band units: launch epoch, per-band maxima (after the chunk maxima); ticket below
-                fp.epoch = ++c->fill_epoch;
-                fp.band_part = reinterpret_cast<unsigned long long*>(fp.snap_m + per_launch * v.snap_p_slot);
+            if (v.so) {   // (after the chunk maxima) per-(band, chunk) maxima; ticket below
                 fp.part_bands = (uint32_t)v.pl.g.bands;
-                fp.snap_c = reinterpret_cast<int32_t*>(fp.band_part + per_launch * v.part_slot);
-                fp.seg_hand = reinterpret_cast<uint32_t*>(fp.snap_c + per_launch * v.snap_c_slot);
+                fp.snap_c = reinterpret_cast<int32_t*>(snap_p + 2 * per_launch * v.snap_p_slot);
                 fp.seg_slot = v.seg_slot;
+            }
+            if (v.so && !is_affine(algo)) {   // band units: this launch's tag, the hand-off buffer
+                fp.epoch = c->hand_tag;   // (set by the launch loop below)
+#ifndef SA_R5_CONTROL
+                fp.rowbuf = reinterpret_cast<int32_t*>(c->hand);
+                fp.band_part = reinterpret_cast<unsigned long long*>(c->hand + hand_rb);
+                fp.seg_hand = reinterpret_cast<uint32_t*>(c->hand + hand_rb + hand_part);
+#else
+                // control build of tests/test_gpu_handoff.py (make variant V=r5ctl DEFS=-DSA_R5_CONTROL):
+                // round 5's layout, the hand-off words in the shared workspace after the chunk maxima
+                const uintptr_t bp = (reinterpret_cast<uintptr_t>(fp.snap_c + per_launch * v.snap_c_slot) + 7) & ~(uintptr_t)7;
+                fp.band_part = reinterpret_cast<unsigned long long*>(bp);
+                fp.seg_hand = reinterpret_cast<uint32_t*>(fp.band_part + per_launch * v.part_slot);
+#endif
+                fp.wait_polls = so_wait_polls;
             }
             fp.snap_h_slot = v.snap_h_slot; fp.snap_p_slot = v.snap_p_slot; fp.snap_nch = v.snap_nch;
             fp.split_bands = (uint32_t)sp_bands;
@@ -879,6 +952,13 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fv.so = v.so;
             return fv;
         };
+        // Pipelined calls: the int32 variant of a T16 batch (it re-runs only the pairs the T16 fill
+        // flagged, or every pair when the device chose int32) walks its traceback on the fill stream
+        // right after its fill.  On the traceback stream, behind the score-only traceback, its
+        // workgroups waited for the next call's fill to be dispatched (up to 9.6 ms, round 4 rocprof)
+        // and delayed the slot's release to the call after it.  It then walks before the T16 variant,
+        // so the pairs it re-ran are handed over by flags (TbParams::keep_redo / clear_redo).
+        const bool tb_on_fill = pipe && nv == 2 && !vars[1].t16 && !vars[1].pl.split;
         auto make_tp = [&](int k) {
             const Variant& v = vars[k];
             TbParams tp{};
@@ -902,17 +982,19 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             tp.t16_delta = fps[k].t16_delta;
             tp.t16_sent = fps[k].t16_sent;
             tp.so_lp = pipe ? 4 : 8;   // (sa_traceback_so.hip kSo4DefaultLp)
+            // the int32 re-run walked first (tb_on_fill): it leaves kFlagRedo, the T16 walk clears it
+            tp.keep_redo = tb_on_fill && k == 1 ? 1 : 0;
+            tp.clear_redo = tb_on_fill && k == 0 ? 1 : 0;
+#ifdef SA_R5_CONTROL
+            tp.keep_redo = tp.clear_redo = 0;   // (round 5: the int32 walk cleared kFlagRedo)
+#endif
             return tp;
         };
-        // Pipelined calls: the int32 variant of a T16 batch (it re-runs only the pairs the T16 fill
-        // flagged, or every pair when the device chose int32) walks its traceback on the fill stream
-        // right after its fill.  On the traceback stream, behind the score-only traceback, its
-        // workgroups waited for the next call's fill to be dispatched (up to 9.6 ms, round 4 rocprof)
-        // and delayed the slot's release to the call after it.
-        const bool tb_on_fill = pipe && nv == 2 && !vars[1].t16 && !vars[1].pl.split;
         for (int k = 0; k < nv; ++k) {
             const Variant& v = vars[k];
             const Plan& pl = v.pl;
+            if (v.so && !is_affine(algo))
+                if (int rc = next_hand_tag(c, hand_need, sf)) return rc;
             const FillVariant fv = make_fp(k);
             const FillParams& fp = fps[k];
             if (pl.split) SA_HIP(c, hipMemsetAsync(fp.ticket, 0, 256 + hand_x_off * 8 * aff2, sf));
@@ -1723,11 +1805,30 @@ void sa_destroy(sa_ctx* c) {
     if (c->h_sel) (void)hipHostFree(c->h_sel);
     if (c->tiny_io) (void)hipHostFree(c->tiny_io);
     if (c->split) (void)hipFree(c->split);
+    if (c->hand) (void)hipFree(c->hand);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
 const char* sa_last_error(const sa_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
+
+int sa_test_hook(sa_ctx* c, int hook, uint64_t value) {
+    if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
+    SA_HIP(c, hipSetDevice(c->device));
+    if (hook == SA_HOOK_HAND_TAG) {
+        if (value > 65535) return fail(c, SA_ERR_ARG, "hand-off tag must be <= 65535");
+        if (int rc = drain(c)) return rc;
+        c->hand_tag = (uint32_t)value;
+        return SA_OK;
+    }
+    if (hook == SA_HOOK_POISON_WS) {
+        if (int rc = drain(c)) return rc;
+        if (c->ws) SA_HIP(c, hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(c->ws), (int)(uint32_t)value, c->ws_bytes / 4));
+        SA_HIP(c, hipDeviceSynchronize());
+        return SA_OK;
+    }
+    return fail(c, SA_ERR_ARG, "unknown test hook");
+}
 
 int sa_set_workspace_limit(sa_ctx* c, uint64_t bytes) {
     if (!c) return fail(nullptr, SA_ERR_ARG, "ctx is NULL");
@@ -1742,6 +1843,8 @@ int sa_trim(sa_ctx* c) {
     if (c->ws) (void)hipFree(c->ws);
     if (c->io) (void)hipFree(c->io);
     if (c->split) (void)hipFree(c->split);
+    if (c->hand) (void)hipFree(c->hand);
+    c->hand = nullptr; c->hand_bytes = 0; c->hand_tag = 0;
     c->ws = nullptr; c->ws_bytes = 0;
     c->io = nullptr; c->io_bytes = 0;
     c->split = nullptr; c->split_bytes = 0;

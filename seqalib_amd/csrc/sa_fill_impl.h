@@ -195,6 +195,29 @@ static __device__ unsigned long long g_fill_stats[32768][3];
 #define SA_EV_FLUSH() do {} while (0)
 #endif
 
+// Band units (BU): the pair's final unit folds the per-unit words {tag << 32 | lost << 31 | maximum}
+// of units [0, nparts) (segments past last_seg store none).  Each wait is bounded by wait_polls; an
+// expired one counts as lost.  Returns this lane's maximum of the maxima it read (the caller reduces
+// over the wave); lost (every lane) is set when any unit, or a wait here, lost its producer.
+__device__ __forceinline__ uint32_t bu_fold_parts(const unsigned long long __attribute__((address_space(1)))* part,
+                                                  uint32_t nparts, uint32_t last_seg, uint32_t segs, uint32_t tag,
+                                                  uint32_t wait_polls, int lane, uint32_t& lost) {
+    uint32_t mx = 0, ls = lost;
+    for (uint32_t b = (uint32_t)lane; b < nparts; b += kWave) {
+        if (b % segs > last_seg) continue;
+        unsigned long long x = __hip_atomic_load(part + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t it = 0; (uint32_t)(x >> 32) != tag; ++it) {
+            if (it >= wait_polls) { x = 1ull << 31; break; }
+            __builtin_amdgcn_s_sleep(2);
+            x = __hip_atomic_load(part + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        ls |= (uint32_t)(x >> 31) & 1u;
+        mx = max(mx, (uint32_t)x & 0x7fffffffu);
+    }
+    lost = __builtin_amdgcn_ballot_w64(ls != 0) != 0 ? 1u : 0u;
+    return mx;
+}
+
 // MM: how a cell learns whether its two symbols match -- kMatchEq (byte equality), kMatchLut (the
 // 256 x 256 table of the user's match fn, LDS) or kMatchBits (a per-pair m x n match bitmap, the
 // generic-Ty path: any symbol type and count, the reference's cacheAllMatches packed to bits).
@@ -460,14 +483,14 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
     const uint32_t last_seg = BU && nch > 0 ? (nch - 1) / cps : 0u;
     if (BU && seg > (B > 0 ? last_seg : 0u)) return;   // (uniform) an empty segment (an empty pair: unit 0 reports)
     const uint32_t total = SPLIT ? nch : BU ? (B > 0 ? c1 : 0u) : total_phases((uint32_t)B, (uint32_t)n, W);
-    const uint32_t epoch16 = ((P.epoch % 65535u) + 1u) << 16;   // BU: this launch's granule tag
+    const uint32_t epoch16 = P.epoch << 16;   // BU: this launch's hand-off tag (P.epoch in [1, 65535])
     // SPLIT hand-off: band b's last row as 8-byte {tag = 1, value} granules written
     // write-through (sc1) per column, polled by band b+1 with sc1 loads; the data is its own flag
     // (cdna_hip_programming.md Guideline 16, R2).  The host zeroes them before every launch.
     typedef unsigned long long __attribute__((address_space(1))) gu64;
     gu64* const hand_pair = SPLIT ? (gu64*)(P.hand + (uint64_t)slot * P.split_bands * P.max_n) : nullptr;
     uint32_t tmo = 0;   // SPLIT: a bounded wait expired
-    uint32_t seg_lost = 0;   // BU: the wait for the previous segment's hand-off expired (the pair is re-run)
+    uint32_t seg_lost = 0;   // BU: a wait for a producer's hand-off expired (the pair is re-run in int32)
 #ifdef SA_TB_STATS
     unsigned long long ev[12] = {};
 #endif
@@ -1207,8 +1230,11 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
         // (split_sub); the values written to s_step here are placeholders
         if constexpr (BU) {
             if (band > 0) {   // (uniform) the producer band's granules of this chunk, this launch's
+                // (bounded, as the segment wait: after a lost producer the unit runs on without
+                // waiting and the pair is flagged for the int32 re-run)
                 const bool want = lane < kChunk && c < n;
-                while (__builtin_amdgcn_ballot_w64(want && ((uint32_t)vh & 0xffff0000u) != epoch16) != 0) {
+                for (uint32_t it = 0; !seg_lost && __builtin_amdgcn_ballot_w64(want && ((uint32_t)vh & 0xffff0000u) != epoch16) != 0; ++it) {
+                    if (it >= P.wait_polls) { seg_lost = 1; break; }
                     __builtin_amdgcn_s_sleep(2);
                     if (want)
                         vh = (int)__hip_atomic_load(rb_g + (uint64_t)(band - 1) * rbs + c, __ATOMIC_RELAXED,
@@ -1277,10 +1303,10 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
                                 return st;
                             };
                             rd();
-                            // (bounded: a producer that never comes leaves the unit after ~2^20
-                            // polls with the pair flagged for the int32 re-run)
-                            for (uint32_t it = 0; __builtin_amdgcn_ballot_w64(stale()) != 0; ++it) {
-                                if (it >= (1u << 20)) { seg_lost = 1; break; }
+                            // (bounded: a producer that never comes leaves the unit after
+                            // wait_polls polls with the pair flagged for the int32 re-run)
+                            for (uint32_t it = 0; !seg_lost && __builtin_amdgcn_ballot_w64(stale()) != 0; ++it) {
+                                if (it >= P.wait_polls) { seg_lost = 1; break; }
                                 __builtin_amdgcn_s_sleep(2);
                                 rd();
                             }
@@ -1510,7 +1536,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
             const uint32_t me = band0 * SEGS + seg, nparts = B > 0 ? (uint32_t)(B - 1) * SEGS + last_seg : 0u;
             if (me != nparts) {
                 if (lane == 0)
-                    __hip_atomic_store(part + me, (unsigned long long)P.epoch << 32 | smax | seg_lost << 31, __ATOMIC_RELAXED,
+                    __hip_atomic_store(part + me, (unsigned long long)epoch16 << 32 | smax | seg_lost << 31, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
 #ifdef SA_TB_STATS
                 const uint64_t sid = ((uint64_t)band0 * SEGS + seg) * P.count + slot;
@@ -1524,15 +1550,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
             }
             // (the last band: every earlier band finished its last chunk before this one's last
             // chunk could read it, so its partial is at most a few instructions away)
-            for (uint32_t b = lane; b < nparts; b += kWave) {
-                if (b % SEGS > last_seg) continue;   // (empty segments store nothing)
-                unsigned long long x;
-                while (((x = __hip_atomic_load(part + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != P.epoch)
-                    __builtin_amdgcn_s_sleep(2);
-                seg_lost |= (uint32_t)(x >> 31) & 1u;
-                smax = max(smax, (uint32_t)x & 0x7fffffffu);
-            }
-            seg_lost = __builtin_amdgcn_ballot_w64(seg_lost != 0) != 0 ? 1u : 0u;
+            smax = max(smax, bu_fold_parts(part, nparts, last_seg, SEGS, epoch16, P.wait_polls, lane, seg_lost));
         }
 #ifdef SA_TB_STATS
         const uint64_t sid = BU ? ((uint64_t)band0 * SEGS + seg) * P.count + slot : slot;   // (BU: one entry per unit)
@@ -1587,7 +1605,21 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
             P.res[pidx] = r;
         }
     } else {
-        if (BU && B > 0 && ((int)band0 != (m - 1) / BAND || seg != last_seg)) return;   // (uniform) the unit holding (m, n) reports
+        if constexpr (BU) {
+            // every unit's lost flag meets in the per-unit words (no maxima: NW reports H[m][n]), so
+            // a lost hand-off anywhere in the pair reaches the unit holding (m, n), which flags the
+            // pair for the int32 re-run
+            typedef unsigned long long __attribute__((address_space(1))) gu64p;
+            gu64p* const part = (gu64p*)(P.band_part + (uint64_t)slot * P.part_bands * SEGS);
+            const uint32_t me = band0 * SEGS + seg, nparts = B > 0 ? (uint32_t)(B - 1) * SEGS + last_seg : 0u;
+            if (me != nparts) {   // (uniform; B > 0 here: an empty pair has one unit, me == 0 == nparts)
+                if (lane == 0)
+                    __hip_atomic_store(part + me, (unsigned long long)epoch16 << 32 | seg_lost << 31, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
+            (void)bu_fold_parts(part, nparts, last_seg, SEGS, epoch16, P.wait_polls, lane, seg_lost);
+        }
         if (threadIdx.x == 0) {   // the phase loop's last barrier orders the owner's s_score store
             sa_result r = {};
             r.end_i = m;
@@ -1599,6 +1631,7 @@ __device__ __forceinline__ void fill_body(const FillParams& P) {
             } else {
                 r.score = s_score;
             }
+            if (BU && seg_lost) r.flags |= kFlagRetry;
             if (redo) r.flags |= kFlagRedo;
             if (P.rerun) r.flags |= kFlagRerun;
             P.res[pidx] = r;

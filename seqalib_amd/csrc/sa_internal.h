@@ -21,6 +21,10 @@ constexpr uint32_t kFlagRetry = 1u << 30, kFlagRedo = 1u << 31;
 constexpr uint32_t kFlagRerun = 1u << 29;
 // Bounded wait of a SPLIT band for its producer, in s_memrealtime ticks (100 MHz): 0.2 s.
 constexpr uint64_t kSplitWaitTicksDefault = 20000000ull;
+// Polls of a band unit's hand-off word before it gives up on the producer (FillParams::wait_polls):
+// a poll is one agent-scope load plus s_sleep 2, so about a second -- its producer holds a smaller
+// ticket and is always running, so only a lost wave gets there.  $SEQALIB_SO_WAIT_POLLS (tests).
+constexpr uint32_t kSoWaitPollsDefault = 1u << 20;
 
 struct FillParams {
     const uint8_t* seq1;
@@ -81,8 +85,11 @@ struct FillParams {
     // the fallback launch: re-runs only the pairs a SPLIT fill flagged SA_FLAG_TIMEOUT
     int rerun;
     // score-only fills (band units, sa_fill_impl.h BU): ticket = the unit counter (zeroed before
-    // the launch), epoch = this launch's tag of the row-buffer granules and of the per-band maxima
-    // band_part (part_bands 64-bit words per slot: epoch << 32 | the band's maximum)
+    // the launch), epoch = this launch's tag in [1, 65535] (sa_ctx::hand_tag) of the row-buffer
+    // granules, the segment state and the per-unit maxima band_part (part_bands 64-bit words per
+    // slot: epoch << 48 | lost << 31 | the unit's maximum).  All three live in the context's hand-off
+    // buffer, which only these fills write and which is zeroed when allocated and whenever the tag
+    // wraps, so any word there carries the tag of the launch that wrote it, or none (0).
     uint32_t epoch;
     unsigned long long* band_part;
     uint32_t part_bands;
@@ -96,6 +103,9 @@ struct FillParams {
     // score-only SW: per slot and (band, chunk) the wave's maximum of the chunk maxima (snap_m), so
     // the end-cell replay reads the lane maxima of the chunks that reach its threshold only
     int32_t* snap_c;
+    // band units: polls of a hand-off word (row granules, segment state, per-unit maxima) before the
+    // unit gives up on its producer and flags the pair for the int32 re-run (kFlagRetry)
+    uint32_t wait_polls;
 };
 
 // SPLIT fills: per-pair fold of the per-band partials into sa_result (split_reduce_kernel).
@@ -186,6 +196,10 @@ struct TbParams {
     int32_t t16_delta;         // score-only NW: the fill's values are H - t16_delta (the borders)
     int32_t t16_sent;          // score-only Gotoh: the tagged Ix / Iy border (FillParams::t16_sent)
     int so_lp;                 // score-only SW / NW: lanes per pair (0: kSo4DefaultLp)
+    // The int32 re-run of a T16 batch walked before the T16 variant (pipelined calls walk it on the
+    // fill stream, sa_api.hip tb_on_fill): keep_redo (the int32 walk) leaves kFlagRedo on the pairs
+    // it walked, clear_redo (the T16 walk) skips those pairs and clears the bit (tb_release).
+    int keep_redo, clear_redo;
 };
 // SA_FLAG_TIMEOUT: a SPLIT band's bounded wait for its producer expired (results invalid)
 
@@ -238,6 +252,19 @@ __device__ __forceinline__ bool tb_mine(const TP& P, uint32_t flags) {
     if (!P.sel) return true;
     const bool redone = (flags & kFlagRedo) != 0;
     return *P.sel == P.sel_want ? !redone : redone;
+}
+// The internal flags a walk clears on a pair it walked (the results it returns carry none): all of
+// them, except kFlagRedo when the T16 walk still follows (TbParams::keep_redo).
+template <typename TP>
+__device__ __forceinline__ uint32_t tb_clear_mask(const TP& P) {
+    return ~(kFlagRetry | kFlagRerun | (P.keep_redo ? 0u : kFlagRedo));
+}
+// A pair tb_mine() refused: when the int32 walk ran first (TbParams::clear_redo) and re-ran this
+// pair, the T16 walk leaves it to that walk's result and clears the kFlagRedo it left.  So the
+// pair is walked exactly once, by the variant that filled it, whichever walk is enqueued first.
+template <typename TP>
+__device__ __forceinline__ void tb_release(const TP& P, sa_result* r, uint32_t flags) {
+    if (P.clear_redo && (flags & kFlagRedo) && P.sel && *P.sel == P.sel_want) r->flags = flags & ~kFlagRedo;
 }
 // Does a pair take the segmented traceback?  The seg kernels and the wave walker evaluate it on
 // the same (unchanged) sa_result, so they agree.  *b_e: the band of the walk's first cell.  Long

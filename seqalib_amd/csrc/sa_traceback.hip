@@ -79,8 +79,11 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbParams P) {   // tb_min
     const uint32_t pidx = P.pair_base + slot;
     sa_result res = P.res[pidx];
     if (res.flags & SA_FLAG_BAD_SHAPE) return;
-    if (!tb_mine(P, res.flags)) return;
-    res.flags &= ~(kFlagRetry | kFlagRedo | kFlagRerun);
+    if (!tb_mine(P, res.flags)) {
+        tb_release(P, &P.res[pidx], res.flags);
+        return;
+    }
+    res.flags &= tb_clear_mask(P);
     const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
     const int m = (int)(P.off1[pidx + 1] - o1);
     const int n = (int)(P.off2[pidx + 1] - o2);

@@ -64,8 +64,11 @@ __global__ __launch_bounds__(64) void traceback_so_kernel(TbParams P) {
     const uint32_t pidx = P.pair_base + slot;
     sa_result res = P.res[pidx];
     if (res.flags & SA_FLAG_BAD_SHAPE) return;
-    if (!tb_mine(P, res.flags)) return;
-    res.flags &= ~(kFlagRetry | kFlagRedo | kFlagRerun);
+    if (!tb_mine(P, res.flags)) {
+        tb_release(P, &P.res[pidx], res.flags);
+        return;
+    }
+    res.flags &= tb_clear_mask(P);
     const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
     const int m = (int)(P.off1[pidx + 1] - o1);
     const int n = (int)(P.off2[pidx + 1] - o2);
@@ -424,9 +427,13 @@ __global__ __launch_bounds__(64) void traceback_so4_kernel(TbParams P) {
     bool live = slot < P.count;
     const uint32_t pidx = P.pair_base + (live ? slot : 0);
     sa_result res = P.res[pidx];
-    live = live && !(res.flags & SA_FLAG_BAD_SHAPE) && tb_mine(P, res.flags);
+    if (live && !(res.flags & SA_FLAG_BAD_SHAPE) && !tb_mine(P, res.flags)) {
+        if (sub == 0) tb_release(P, &P.res[pidx], res.flags);
+        live = false;
+    }
+    live = live && !(res.flags & SA_FLAG_BAD_SHAPE);
     if (__builtin_amdgcn_ballot_w64(live) == 0) return;
-    res.flags &= ~(kFlagRetry | kFlagRedo | kFlagRerun);
+    res.flags &= tb_clear_mask(P);
     const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
     const int m = (int)(P.off1[pidx + 1] - o1);
     const int n = (int)(P.off2[pidx + 1] - o2);
@@ -789,9 +796,13 @@ __global__ __launch_bounds__(64) void traceback_soa_kernel(TbParams P) {
     bool live = slot < P.count;
     const uint32_t pidx = P.pair_base + (live ? slot : 0);
     sa_result res = P.res[pidx];
-    live = live && !(res.flags & SA_FLAG_BAD_SHAPE) && tb_mine(P, res.flags);
+    if (live && !(res.flags & SA_FLAG_BAD_SHAPE) && !tb_mine(P, res.flags)) {
+        if (sub == 0) tb_release(P, &P.res[pidx], res.flags);
+        live = false;
+    }
+    live = live && !(res.flags & SA_FLAG_BAD_SHAPE);
     if (__builtin_amdgcn_ballot_w64(live) == 0) return;
-    res.flags &= ~(kFlagRetry | kFlagRedo | kFlagRerun);
+    res.flags &= tb_clear_mask(P);
     uint32_t flags = res.flags;
     const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
     const int m = (int)(P.off1[pidx + 1] - o1);

@@ -130,7 +130,10 @@ __global__ __launch_bounds__(64) void traceback_wave_kernel(TbParams P) {
     const uint32_t pidx = P.pair_base + slot;
     sa_result res = P.res[pidx];
     if (res.flags & SA_FLAG_BAD_SHAPE) return;
-    if (!tb_mine(P, res.flags)) return;
+    if (!tb_mine(P, res.flags)) {
+        if (lane == 0) tb_release(P, &P.res[pidx], res.flags);
+        return;
+    }
     const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
     const int m = (int)(P.off1[pidx + 1] - o1);
     const int n = (int)(P.off2[pidx + 1] - o2);
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(64) void traceback_wave_kernel(TbParams P) {
         const int4 f = P.seg_fin[slot];   // preset to -1 by the host
         if (f.z >= 0 && !(f.w & 16)) {
             if (lane == 0) {
-                res.flags &= ~(kFlagRetry | kFlagRedo | kFlagRerun);
+                res.flags &= tb_clear_mask(P);
                 res.start_i = f.x;
                 res.start_j = f.y;
                 res.nops = (uint32_t)f.z;
@@ -155,7 +158,7 @@ __global__ __launch_bounds__(64) void traceback_wave_kernel(TbParams P) {
         }
         recovered = true;
     }
-    res.flags &= ~(kFlagRetry | kFlagRedo | kFlagRerun);
+    res.flags &= tb_clear_mask(P);
     const uint8_t* s1 = P.seq1 + o1;
     const uint8_t* s2 = P.seq2 + o2;
     const int tagged = P.tagged;   // record layout (sa_layout.h Geom::tagged)
