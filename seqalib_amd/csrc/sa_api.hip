@@ -230,6 +230,7 @@ struct Variant {
     uint32_t segs = 1;        // score-only SW / NW: column segments per band (FillParams::part_segs)
     uint64_t seg_slot = 0;    // their hand-off words per pair (FillParams::seg_hand)
     uint64_t snap_c_slot = 0; // score-only SW: 32-bit (band, chunk) maxima per pair (FillParams::snap_c)
+    bool so2 = false;         // score-only SW with two pairs per wave (sa_fill_so2.hip)
     uint64_t slot_bytes = 0;
     int kernel = SA_KERNEL_INT32;
 };
@@ -272,6 +273,10 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
         }
         v.part_slot = (uint64_t)v.pl.g.bands * v.segs;
         if (algo == SA_SW) v.snap_c_slot = (uint64_t)v.pl.g.bands * v.snap_nch;
+        // two pairs per wave (sa_fill_so2.hip): the packed cell, for the SW band units at R = 16 / 32;
+        // $SEQALIB_SO2=0 runs one pair per wave (A/B, tests)
+        v.so2 = algo == SA_SW && (v.pl.R == 16 || v.pl.R == 32);
+        if (const char* e = getenv("SEQALIB_SO2")) if (e[0] == '0') v.so2 = false;
     }
     if (v.pl.split) v.pl.rowbuf_elems = 0;   // hand-off granules live in c->split
     v.kernel = v.cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;
@@ -948,8 +953,19 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             fp.part = pl.split ? reinterpret_cast<int32_t*>(spbase + sp_part) : nullptr;
             fp.wait_ticks = wait_ticks;
             fp.part_segs = std::max<uint32_t>(1, v.segs);
+            if (v.so2) {
+                // LDS for the unit's Seq2 codes, per pair: the widest column range a unit may run
+                // (ceil(chunks / segments) chunks + the 64 columns before them; one segment below 4
+                // chunks), when both pairs' fit 8 KiB (16 units per CU at 4 waves per SIMD)
+                const uint32_t nch = chunks_per_band(max_n);
+                const uint32_t sg = std::max(1u, std::min(fp.part_segs, nch / 2));
+                const uint32_t range = std::max((nch + sg - 1) / sg, 3u) * kChunk + kWave;
+                const uint32_t cap = (range + 15) & ~15u;
+                fp.so2_stage = (2 * cap <= 8192 && !no_stage) ? cap : 0;
+            }
             FillVariant fv{pl.R, lut, allow || v.t16, keyed, v.t16, v.cmax, pl.split, bits};
             fv.so = v.so;
+            fv.so2 = v.so2;
             return fv;
         };
         // Pipelined calls: the int32 variant of a T16 batch (it re-runs only the pairs the T16 fill
@@ -1003,8 +1019,9 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             // grid: SPLIT one workgroup per (pair, band) slot; score-only SW / NW one per (pair,
             // band) unit (band units, sa_fill_impl.h BU); otherwise one per pair
             const bool units = v.so && !is_affine(algo);
-            const uint32_t grid = pl.split ? (uint32_t)(cnt * sp_bands) : units ? cnt * pl.g.bands * v.segs : cnt;
-            hipError_t e = launch_fill(algo, fv, fp, grid, sf);
+            const uint32_t grid = pl.split ? (uint32_t)(cnt * sp_bands)
+                                : units ? (v.so2 ? (cnt + 1) / 2 : cnt) * pl.g.bands * v.segs : cnt;
+            hipError_t e = v.so2 ? launch_fill_so2(pl.R, fp, grid, sf) : launch_fill(algo, fv, fp, grid, sf);
             if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
             if (kev) SA_HIP(c, hipEventRecord(kev[2 * k + 1], sf));
             if (pl.split) {

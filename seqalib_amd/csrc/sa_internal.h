@@ -106,6 +106,9 @@ struct FillParams {
     // band units: polls of a hand-off word (row granules, segment state, per-unit maxima) before the
     // unit gives up on its producer and flags the pair for the int32 re-run (kFlagRetry)
     uint32_t wait_polls;
+    // the two-pairs-per-wave SW fill (sa_fill_so2.hip): bytes of LDS per pair for its unit's Seq2
+    // symbol codes (0: read from global memory per chunk)
+    uint32_t so2_stage;
 };
 
 // SPLIT fills: per-pair fold of the per-band partials into sa_result (split_reduce_kernel).
@@ -212,12 +215,16 @@ struct FillVariant {
     bool lut, allow, keyed, t16, cmax, split;
     bool bits = false;   // kMatchBits (then lut is ignored)
     bool so = false;     // score-only T16 SW chunk-max fill (edge stream instead of records)
+    bool so2 = false;    // score-only SW with two pairs per wave (sa_fill_so2.hip)
 };
 hipError_t launch_fill(int algo, const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t stream);
 hipError_t launch_fill_sw(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_fill_nw(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_fill_lg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
 hipError_t launch_fill_gg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
+// Score-only SW band units with two pairs per wave (sa_fill_so2.hip), R in {16, 32}: grid =
+// ceil(count / 2) x bands x part_segs units.
+hipError_t launch_fill_so2(int R, const FillParams& p, uint32_t grid, hipStream_t s);
 // Batch alphabet scan (presence bitmap of every byte of both sequence sets, 8 words) and the
 // device-side T16 decision.  aux layout (kAux* below): [bitmap 8][profile 4][sym_pack][sel].
 constexpr int kAuxProf = 8, kAuxSel = 13, kAuxWords = 64;

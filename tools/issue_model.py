@@ -25,9 +25,14 @@ ALIAS = {"v_mov_b32_dpp": "v_mov_b32_dpp_shr", "v_readlane_b32": "readlane", "v_
          "v_bfe_i32": "v_bfe_u32", "v_addc_co_u32": "addc_only", "v_cndmask_b32": "cndmask_e64_sgpr",
          "v_add_u16_sdwa": "add_u16_sdwa_byte1_sext", "v_sub_u16": "sub_u16_e64_clamp",
          "v_cmp_eq_u32": "cmp_only", "v_cmp_gt_u32": "cmp_only", "v_cmp_le_u32": "cmp_only",
-         "v_lshl_add_u64": "v_lshl_add_u32", "v_max3_i32": "v_max3_i32", "v_add_co_u32": "add_co_e64"}
+         "v_lshl_add_u64": "v_lshl_add_u32", "v_max3_i32": "v_max3_i32", "v_add_co_u32": "add_co_e64",
+         # packed 16-bit forms measured at one rate (profiles/microbench_valu_issue_r01.txt)
+         "v_pk_sub_u16": "v_pk_add_u16", "v_pk_max_u16": "v_pk_max_i16"}
 
-KERNELS = {  # label -> (TU, mangled name, cells per lane in one steady block = SPP * R)
+KERNELS = {  # label -> (TU, mangled name, cells per lane in one steady block = SPP * R [* pairs per lane])
+    # round 6: the score-only SW fill with two pairs per wave (fill_so2_kernel<R>, sa_fill_so2.hip)
+    "sw_so2_r32": ("sa_fill_so2.hip", "_ZN2sa15fill_so2_kernelILi32EEEvNS_10FillParamsE", 512),   # 8 steps x 32 rows x 2 pairs
+    "sw_so2_r16": ("sa_fill_so2.hip", "_ZN2sa15fill_so2_kernelILi16EEEvNS_10FillParamsE", 256),
     # round 5: the score-only fills (fill_so_kernel<ALG, R>): SW / NW band units, LG / GG affine
     "sw_so_r32": ("sa_fill_sw.hip", "_ZN2sa14fill_so_kernelILi0ELi32EEEvNS_10FillParamsE", 256),   # 8 steps x 32 rows
     "sw_so_r16": ("sa_fill_sw.hip", "_ZN2sa14fill_so_kernelILi0ELi16EEEvNS_10FillParamsE", 128),
@@ -98,11 +103,13 @@ def main():
                 cache[tu] = open(os.path.join(td, s)).read()
             blk = steady_block(cache[tu], name)
             cnt = collections.Counter(blk)
-            cyc, valu, unknown = 0.0, 0, {}
+            cyc, valu, elem, unknown = 0.0, 0, 0, {}
+            two = "so2" in label   # two pairs per lane: packed ops and v_perm carry two cells' work
             for op, c in cnt.items():
                 if not op.startswith("v_"):
                     continue
                 valu += c
+                elem += c * (2 if (op.startswith("v_pk_") or (two and op.startswith("v_perm"))) else 1)
                 r = rate_of(op, R)
                 if r is None:
                     unknown[op] = c
@@ -111,6 +118,9 @@ def main():
             cpc = cyc / cells
             out["kernels"][label] = {
                 "kernel": name, "cells_per_lane_in_block": cells, "valu_per_cell": round(valu / cells, 3),
+                # lane-element ops: a packed 16-bit op (and, two pairs per lane, a v_perm) does two
+                # lanes' work, issuing at half the wave rate -- the quantity the VALU peak counts
+                "valu_elem_per_cell": round(elem / cells, 3),
                 "cycles_per_lane_cell": round(cpc, 3),
                 "peak_gcups": round(SIMDS * CLOCK * 64 / cpc / 1e9, 1),
                 "mix": dict(sorted(((k, v) for k, v in cnt.items() if k.startswith("v_")), key=lambda x: -x[1])),

@@ -16,7 +16,7 @@ CELLS = 10000 * 4096 * 4096
 
 
 def fill_like(name):
-    return "fill_so_kernel" in name or "fill_kernel" in name
+    return "fill_so_kernel" in name or "fill_so2_kernel" in name or "fill_kernel" in name
 
 
 out = {"counters": {}, "durations_ms": {}}

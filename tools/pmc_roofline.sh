@@ -9,7 +9,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/roofline
+OUT=${OUT:-gpurun_out/roofline}
 rm -rf $OUT && mkdir -p $OUT
 RUN="python3 tools/headline_once.py --calls 2"
 echo "[roofline] stats $(date +%T)"
