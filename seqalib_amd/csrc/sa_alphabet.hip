@@ -4,6 +4,8 @@
 // from a per-row byte profile, so it applies when the whole batch uses at most four distinct
 // byte values (DNA).  The host learns that from a 256-bit presence bitmap of every byte of both
 // sequence sets (one streaming pass, ~HBM speed) before it plans the launch.
+#include <stdlib.h>
+
 #include "sa_internal.h"
 
 namespace sa {
@@ -19,7 +21,8 @@ __device__ __forceinline__ void mark4(uint32_t (&bm)[8], uint32_t v) {
     mark(bm, v & 255u); mark(bm, (v >> 8) & 255u); mark(bm, (v >> 16) & 255u); mark(bm, v >> 24);
 }
 
-__global__ __launch_bounds__(256) void alphabet_scan(const uint8_t* d1, const uint64_t* o1,
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void alphabet_scan(const uint8_t* d1, const uint64_t* o1,
                                                      const uint8_t* d2, const uint64_t* o2,
                                                      uint32_t npairs, uint32_t* bitmap) {
     __shared__ uint32_t sb[8];
@@ -99,7 +102,13 @@ hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uin
                                 const uint64_t* o2, uint32_t npairs, uint32_t* bitmap, hipStream_t s) {
     hipError_t e = hipMemsetAsync(bitmap, 0, 32, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(alphabet_scan, dim3(2048), dim3(256), 0, s, d1, o1, d2, o2, npairs, bitmap);
+    // One-wave workgroups: queued behind a running fill (the pipelined calls' case), a workgroup
+    // starts as soon as ONE fill unit's slot frees, where a 4-wave workgroup waited for four in one
+    // CU (bench rocprofv3 r05: scans of up to 15.7 ms, 14 % of the summed kernel time).
+    // $SEQALIB_SCAN_WG=256 restores the round-5 launch (A/B).
+    static const bool wide = [] { const char* e = getenv("SEQALIB_SCAN_WG"); return e && atoi(e) == 256; }();
+    if (wide) hipLaunchKernelGGL(alphabet_scan<256>, dim3(2048), dim3(256), 0, s, d1, o1, d2, o2, npairs, bitmap);
+    else hipLaunchKernelGGL(alphabet_scan<64>, dim3(2048), dim3(64), 0, s, d1, o1, d2, o2, npairs, bitmap);
     return hipGetLastError();
 }
 

@@ -370,10 +370,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
                 smA[ln] = (int32_t)lo16(cml);
                 if (lane == kWave - 1) P.snap_c[(uint64_t)sA * P.part_bands * P.snap_nch + e] = (int32_t)lo16(wm);
                 if (chunk + 1 < nchA) {
-                    uint32_t* const sh = P.snap_h + (uint64_t)sA * P.snap_h_slot + e * (R / 2) * kWave;
+                    uint32_t* const sh = P.snap_h + (uint64_t)sA * P.snap_h_slot + e * (R / 2) * kWave + ln;
 #pragma unroll
-                    for (int q = 0; q < R / 2; ++q)
-                        sh[(uint32_t)(q * kWave) + ln] = __builtin_amdgcn_perm(Hp[2 * q + 1], Hp[2 * q], 0x05040100u);
+                    for (int q = 0; q < R / 2; ++q)   // (one address, immediate offsets)
+                        sh[q * kWave] = __builtin_amdgcn_perm(Hp[2 * q + 1], Hp[2 * q], 0x05040100u);
                     int32_t* const spA = P.snap_p + (uint64_t)sA * P.snap_p_slot + e * kWave;
                     spA[ln] = (int32_t)lo16(prev_up);
                 }
@@ -383,10 +383,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
                 smB[ln] = (int32_t)hi16(cml);
                 if (lane == kWave - 1) P.snap_c[(uint64_t)sB * P.part_bands * P.snap_nch + e] = (int32_t)hi16(wm);
                 if (chunk + 1 < nchB) {
-                    uint32_t* const sh = P.snap_h + (uint64_t)sB * P.snap_h_slot + e * (R / 2) * kWave;
+                    uint32_t* const sh = P.snap_h + (uint64_t)sB * P.snap_h_slot + e * (R / 2) * kWave + ln;
 #pragma unroll
-                    for (int q = 0; q < R / 2; ++q)
-                        sh[(uint32_t)(q * kWave) + ln] = __builtin_amdgcn_perm(Hp[2 * q + 1], Hp[2 * q], 0x07060302u);
+                    for (int q = 0; q < R / 2; ++q)   // (one address, immediate offsets)
+                        sh[q * kWave] = __builtin_amdgcn_perm(Hp[2 * q + 1], Hp[2 * q], 0x07060302u);
                     int32_t* const spB = P.snap_p + (uint64_t)sB * P.snap_p_slot + e * kWave;
                     spB[ln] = (int32_t)hi16(prev_up);
                 }
@@ -397,18 +397,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         if (chunk + 1 == c1 && c1 < nch2) {
             const uint64_t hoff = ((uint64_t)band0 * SEGS + seg) * (R + 1) * kWave;
             if (liveA) {
-                uint32_t* const hs = P.seg_hand + (uint64_t)sA * P.seg_slot + hoff;
+                uint32_t* const hs = P.seg_hand + (uint64_t)sA * P.seg_slot + hoff + ln;
 #pragma unroll
                 for (int r = 0; r < R; ++r)
-                    __hip_atomic_store(hs + (uint32_t)(r * kWave) + ln, epoch16 | lo16(Hp[r]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(hs + (uint32_t)(R * kWave) + ln, epoch16 | lo16(prev_up), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(hs + r * kWave, epoch16 | lo16(Hp[r]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(hs + R * kWave, epoch16 | lo16(prev_up), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             if (liveB) {
-                uint32_t* const hs = P.seg_hand + (uint64_t)sB * P.seg_slot + hoff;
+                uint32_t* const hs = P.seg_hand + (uint64_t)sB * P.seg_slot + hoff + ln;
 #pragma unroll
                 for (int r = 0; r < R; ++r)
-                    __hip_atomic_store(hs + (uint32_t)(r * kWave) + ln, epoch16 | hi16(Hp[r]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(hs + (uint32_t)(R * kWave) + ln, epoch16 | hi16(prev_up), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(hs + r * kWave, epoch16 | hi16(Hp[r]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(hs + R * kWave, epoch16 | hi16(prev_up), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         __syncthreads();   // (the step buffer of the next chunk)
