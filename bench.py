@@ -39,7 +39,7 @@ SEED_BASE = 10 ** 10          # workload "T" seed base (config id x 1e9 conventi
 SCORING = (-1, 1, -1)         # SmithWatermanSA::getDefaultScoring (SASmithWaterman.h:352)
 # The fill kernel is VALU-issue bound.  Its VALU instructions per cell come from an ISA count of
 # the steady chunk loop (tools/issue_model.py -> ISSUE_MODEL).
-ISSUE_MODEL = os.path.join(ROOT, "profiles", "issue_model_r05.json")
+ISSUE_MODEL = os.path.join(ROOT, "profiles", "issue_model_r06.json")
 HBM_PEAK_GBPS = 8000.0
 # VALU peak of the guide (/opt/skills/guides/MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 VALU
 # instruction issues over 2 cycles, 2400 MHz max clock): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz.
@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pairs", type=int, default=10000, help="pairs per GPU")
+    ap.add_argument("--total-pairs", type=int, default=0,
+                    help="strong scaling: a fixed global batch of this many pairs split over the ranks "
+                         "(BASELINE config 5: --total-pairs 100000 --len 2048); 0 = --pairs per GPU (weak)")
     ap.add_argument("--len", type=int, default=4096, help="length of both sequences")
     ap.add_argument("--cpu-pairs", type=int, default=0,
                     help="CPU baseline sample, all-core leg (pairs; 0 = 64 per thread, ~10 s)")
@@ -167,6 +170,19 @@ def shard_seed_base(rank: int, world: int, pairs_per_gpu: int) -> int:
     from seqalib_amd.multi import shard_range
     start, _ = shard_range(rank, world, world * pairs_per_gpu)
     return SEED_BASE + 2 * start
+
+
+def rank_shard(rank: int, world: int, pairs_per_gpu: int, total_pairs: int, L: int):
+    """(pairs, seed base, workload name) of this rank.  Weak scaling (total_pairs 0): every rank
+    aligns pairs_per_gpu pairs of a world x pairs_per_gpu batch.  Strong scaling (BASELINE config 5,
+    --total-pairs): the global batch is fixed and rank r aligns its contiguous slice
+    (seqalib_amd.multi.shard_range).  Either way pair p of the global batch is seeded
+    SEED_BASE + 2p + 1 / + 2, so the union of the shards is one batch whatever the rank count."""
+    if total_pairs > 0:
+        from seqalib_amd.multi import shard_range
+        start, stop = shard_range(rank, world, total_pairs)
+        return stop - start, SEED_BASE + 2 * start, f"sw_batch_{total_pairs}x{L}x{L}_strong"
+    return pairs_per_gpu, shard_seed_base(rank, world, pairs_per_gpu), f"sw_batch_{pairs_per_gpu}x{L}x{L}"
 
 
 def host_cores():
@@ -308,6 +324,26 @@ def load_pmc(workload: str, label: str):
         return None
 
 
+def fill_streams(pairs: int, m: int, n: int, R: int, segs: int = 2):
+    """Bytes the score-only SW fill writes per launch of `pairs` m x n pairs, stream by stream
+    (sa_fill_impl.h BU / sa_fill_so2.hip; geometry of sa_layout.h)."""
+    bands = -(-m // (64 * R))
+    nch = (n + 63 + 31) // 32                       # chunks_per_band
+    sg = max(1, min(segs, nch // 2))
+    per = {
+        "edge_stream": bands * nch * 32 * 64 * 2,          # 16 bits per lane-step, every step run
+        "snapshots": bands * (nch - 1) * 64 * (R // 2 + 1) * 4,   # R/2 value words + the diagonal input
+        "chunk_maxima": bands * nch * 64 * 4 + bands * nch * 4,  # per lane, and the wave's (snap_c)
+        "band_rows": (bands - 1) * n * 4,                  # {tag, H} granules to the next band
+        "segment_state": bands * (sg - 1) * (R + 1) * 64 * 4,
+        "unit_words": bands * sg * 8,
+        "result": 32,
+    }
+    out = {k: v * pairs for k, v in per.items()}
+    out["total"] = sum(out.values())
+    return out
+
+
 def issue_model(label: str):
     try:
         return json.load(open(ISSUE_MODEL))["kernels"][label]
@@ -342,10 +378,10 @@ def main():
     gpu = gpu_index(local)
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    P, Lq = args.pairs, args.len
-    workload = f"sw_batch_{P}x{Lq}x{Lq}"
+    Lq = args.len
+    P, seed_base, workload = rank_shard(rank, world, args.pairs, args.total_pairs, Lq)
 
-    s1, o1, s2, o2 = sa.synth_dna_batch(shard_seed_base(rank, world, P), P, Lq, Lq, threads=16)
+    s1, o1, s2, o2 = sa.synth_dna_batch(seed_base, P, Lq, Lq, threads=16)
     as_t = lambda x: torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)
     d1, do1, d2, do2 = as_t(s1), as_t(o1), as_t(s2), as_t(o2)
     # SA_PIPELINE_DEPTH output sets: with the cross-call pipeline, step k's traceback still writes
@@ -407,7 +443,8 @@ def main():
         e2e_ms = max_over_ranks(time.perf_counter() - te, world) / args.e2e_steps * 1e3
 
     cells_rank = float(P) * Lq * Lq
-    value = world * cells_rank * args.steps / elapsed / 1e9
+    cells_job = float(args.total_pairs) * Lq * Lq if args.total_pairs > 0 else world * cells_rank
+    value = cells_job * args.steps / elapsed / 1e9
     ms_per_step = elapsed / args.steps * 1e3
     kernel, plan_R, plan_W, records = eng.last_plan_ex()
 
@@ -430,7 +467,7 @@ def main():
     if args.rank_out:
         os.makedirs(args.rank_out, exist_ok=True)
         with open(os.path.join(args.rank_out, f"rank{rank}.json"), "w") as f:
-            json.dump({"rank": rank, "world": world, "own_s": own, "max_s": elapsed, "seed_base": shard_seed_base(rank, world, P),
+            json.dump({"rank": rank, "world": world, "own_s": own, "max_s": elapsed, "seed_base": seed_base, "pairs": P,
                        "parity": par, "flags": int(np.count_nonzero(res["flags"])), "plan": list(eng.last_plan())}, f)
     if rank != 0:
         return
@@ -439,7 +476,9 @@ def main():
     t16 = kernel in (sa.SA_KERNEL_T16, sa.SA_KERNEL_T16_ENDCELL)
     endcell = kernel == sa.SA_KERNEL_T16_ENDCELL
     so = records == sa.SA_RECORDS_SCORE_ONLY
-    label = f"sw_{'so' if so else 't16c' if endcell else 't16' if t16 else 'int32'}_r{plan_R}"
+    # two pairs per wave (sa_fill_so2.hip) on the score-only SW plans at R = 16 / 32 unless SEQALIB_SO2=0
+    so2 = so and plan_R in (16, 32) and os.environ.get("SEQALIB_SO2", "1") != "0"
+    label = f"sw_{'so2' if so2 else 'so' if so else 't16c' if endcell else 't16' if t16 else 'int32'}_r{plan_R}"
     model = issue_model(label)
     fill_gcups = per_launch_cells / fill_s / 1e9
     # algorithmic HBM bytes per cell: score-only fill -- the edge stream (16 bits per lane-step =
@@ -447,6 +486,12 @@ def main():
     # chunk maxima (1 word per lane-chunk); tagged fill -- 2 record bits per cell + the snapshots
     snap = (plan_R // 2 + 1) * 4 / (32 * plan_R) if endcell else 0.0
     bytes_per_cell = (2.0 / plan_R + snap + 4 / (32 * plan_R)) if so else (SW_FLAG_BYTES_PER_CELL + snap)
+    # every stream the score-only fill writes, per launch, from its geometry:
+    # the streams above over the steps and chunks it really runs (n + 63 steps per band, snapshots
+    # of all chunks but the last) plus the band rows, segment state, per-unit words and results
+    streams = fill_streams(P, Lq, Lq, plan_R) if so else None
+    if streams:
+        bytes_per_cell = streams["total"] / per_launch_cells
     hbm_gbps = per_launch_cells * bytes_per_cell / fill_s / 1e9
     pmc = load_pmc(workload, label)
     kname = ("fill_so_kernel<R=%d> (score-only T16, chunk-max end cell, 4 waves/SIMD)" % plan_R if so else
@@ -455,7 +500,10 @@ def main():
     # achieved = fill cells/s x ISA-counted VALU instructions per cell of the steady loop (each lane
     # computes its own cells, so lane-instructions); peak = the guide's VALU issue peak at 2.4 GHz
     vpc = model["valu_per_cell"] if model else None
-    achieved = fill_gcups * vpc / 1e3 if vpc else None
+    # lane-element ops per cell: a packed 16-bit op (and the two-pair v_perm lookup) does two lanes'
+    # work in a half-rate issue slot, so the VALU peak counts it twice (tools/issue_model.py)
+    epc = model.get("valu_elem_per_cell", vpc) if model else None
+    achieved = fill_gcups * epc / 1e3 if epc else None
     roof = {"bound": "valu", "achieved": round(achieved, 2) if achieved else None, "peak": round(VALU_PEAK_TLANE, 2),
             "unit": "T lane-instr/s", "frac": round(achieved / VALU_PEAK_TLANE, 4) if achieved else None,
             "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None}
@@ -463,7 +511,7 @@ def main():
     roof.update({"kernel": kname, "avg_launch_ms": round(fill_s * 1e3, 3),
                  "avg_launch_basis": "HIP events around the fill kernel on its stream, last timed step "
                                      "(sa_last_kernel_timings)",
-                 "fill_gcups": round(fill_gcups, 1), "valu_per_cell": vpc,
+                 "fill_gcups": round(fill_gcups, 1), "valu_per_cell": vpc, "valu_elem_per_cell": epc,
                  "valu_per_cell_basis": f"ISA count of the steady chunk loop (tools/issue_model.py, {os.path.relpath(ISSUE_MODEL, ROOT)})",
                  "peak_basis": "MI355X_MICROARCH.md: 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz (wave64 VALU op = 2 cycles)",
                  "clock_ghz_measured": clk,
@@ -472,13 +520,15 @@ def main():
                  "valu_per_cell_pmc": pmc.get("valu_wave_instr_per_cell") if pmc else None,
                  "pmc_kernel_ms": pmc.get("kernel_ms_per_pass") if pmc else None,
                  "bytes_per_cell": round(bytes_per_cell, 4), "hbm_achieved_GBps": round(hbm_gbps, 1),
+                 "fill_streams_bytes_per_launch": streams,
                  "hbm_peak_GBps": HBM_PEAK_GBPS, "hbm_frac": round(hbm_gbps / HBM_PEAK_GBPS, 4)})
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GCUPS", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "int16" if t16 else "int32",
+        "scaling": "strong" if args.total_pairs > 0 else "weak", "vs_baseline": None, "dtype": "int16" if t16 else "int32",
         "data": "synthetic DNA, std::mt19937_64 'ACGT'[g()&3], seeds base+2p+1/base+2p+2, resident in HBM",
-        "config": {"workload": workload, "pairs_per_gpu": P, "m": Lq, "n": Lq, "algo": "SmithWatermanSA",
+        "config": {"workload": workload, "pairs_per_gpu": P, "total_pairs": args.total_pairs or world * P,
+                   "m": Lq, "n": Lq, "algo": "SmithWatermanSA",
                    "scoring": list(SCORING), "match": "equal<char>", "parallelism": f"pair-shard x{world}"},
         "roofline": roof,
         "fill_ms": round(fill_ms, 2), "fill_kernel_ms": round(fill_kernel_ms, 2),
@@ -487,7 +537,7 @@ def main():
                          "replay), traceback_ms = traceback stream after the fill stream",
         "records": "score-only fill + block-recompute traceback" if so else ("tagged" if t16 else "flags"),
         "e2e_ms_per_step": round(e2e_ms, 2) if e2e_ms else None,
-        "e2e_gcups": round(world * cells_rank / (e2e_ms / 1e3) / 1e9, 1) if e2e_ms else None,
+        "e2e_gcups": round(cells_job / (e2e_ms / 1e3) / 1e9, 1) if e2e_ms else None,
         "e2e_basis": "host API sa_align_batch from pageable host buffers, one call at a time, one chunk: pinned "
                      "upload of sequences + offsets in 16 MiB pieces (host copy of piece k+1 beside the H2D of "
                      "piece k), fill, end cell, traceback, download of results and op streams into the caller's "

@@ -171,7 +171,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // and loads take the SGPR-base form and no 64-bit address pair stays live across the chunks)
     const int row0 = (int)band0 * BAND + lane * R;
     uint32_t Hp[R], sel[R];
-    uint32_t prev_up = 0, hl = 0, colA = 0, colB = 0, cml = 0, smax = 0;
+    uint32_t prev_up = 0, colA = 0, colB = 0, cml = 0, smax = 0;   // (the lane's last row: Hp[R - 1])
 #pragma unroll
     for (int r = 0; r < R; ++r) Hp[r] = 0;
     if (c0 > 0) {
@@ -206,7 +206,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 #pragma unroll
         for (int r = 0; r < R; ++r) Hp[r] = lo16(Hp[r]) | sel[r] << 16;
         prev_up = lo16(pa_) | pb_ << 16;
-        hl = Hp[R - 1];
         col_pair((int)(c0 * kChunk) - 1 - lane, colA, colB);
     }
 #pragma unroll
@@ -219,12 +218,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 
     // One step of the chunk at kC: lane t computes column j = kC + q - t of its R rows of both
     // pairs (RAMP: a lane left of its first column keeps its border state).
-    auto step = [&](auto ramp, auto phase, int kC, int q, uint32_t& recA, uint32_t& recB) {
+    // (sq = s_step + q0, sc = s_step + 32 + 2 q0, g the step in its packet: one LDS address per
+    // packet and array, immediate offsets)
+    auto step = [&](auto ramp, auto gc, int kC, int q0, const uint32_t* sq, const uint32_t* sc, uint32_t* sp,
+                    uint32_t& recA, uint32_t& recB) {
         constexpr bool RAMP = decltype(ramp)::value;
-        constexpr int PH = decltype(phase)::value;
-        const uint32_t vh = s_step[q];
-        const uint32_t va = s_step[32 + 2 * q], vb = s_step[33 + 2 * q];
-        const uint32_t up = (uint32_t)shr1((int)vh, (int)hl);
+        constexpr int g = decltype(gc)::value;
+        constexpr int PH = g & 3;
+        const int q = q0 + g;
+        const uint32_t vh = sq[g];
+        const uint32_t va = sc[2 * g], vb = sc[2 * g + 1];
+        const uint32_t up = (uint32_t)shr1((int)vh, (int)Hp[R - 1]);
         colA = (uint32_t)shr1((int)va, (int)colA);
         colB = (uint32_t)shr1((int)vb, (int)colB);
         if (!RAMP || kC + q - lane >= 0) {
@@ -267,12 +271,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
                 hu = Hp[r];
             }
             prev_up = up;
-            hl = Hp[R - 1];
         }
         // the lane's last row of each pair, pushed into its packet word (two steps per word)
-        recA = __builtin_amdgcn_alignbit(hl, recA, 16u);
-        recB = __builtin_amdgcn_perm(hl, recB, 0x07060302u);
-        s_park[q] = hl;
+        recA = __builtin_amdgcn_alignbit(Hp[R - 1], recA, 16u);
+        recB = __builtin_amdgcn_perm(Hp[R - 1], recB, 0x07060302u);
+        sp[g] = Hp[R - 1];
     };
 
     uint8_t* const dA = P.dirs + (uint64_t)sA * P.dir_slot + (uint64_t)band0 * P.band_stride;
@@ -318,9 +321,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         // lane's rows stay in fixed registers)
         auto packet = [&](auto rmp, int q0) __attribute__((always_inline)) {
             uint32_t pa[SPP / 2] = {0, 0, 0, 0}, pb[SPP / 2] = {0, 0, 0, 0};
+            const uint32_t* const sq = s_step + q0;
+            const uint32_t* const sc = s_step + 32 + 2 * q0;
+            uint32_t* const sp = s_park + q0;
             auto st = [&](auto gc) __attribute__((always_inline)) {
                 constexpr int g = decltype(gc)::value;
-                step(rmp, std::integral_constant<int, g & 3>{}, kC, q0 + g, pa[g / 2], pb[g / 2]);
+                step(rmp, gc, kC, q0, sq, sc, sp, pa[g / 2], pb[g / 2]);
             };
             st(std::integral_constant<int, 0>{});
             st(std::integral_constant<int, 1>{});

@@ -70,6 +70,27 @@ def test_two_rank_shards_reassemble_the_global_batch():
         assert flat[p] == (o["score"], o["end_i"], o["end_j"], o["ops"])
 
 
+def test_strong_scaling_shards_tile_the_fixed_batch():
+    """bench.py --total-pairs (BASELINE config 5, strong scaling): the ranks' slices of the fixed
+    global batch are contiguous, cover it exactly, and regenerate its pairs byte for byte."""
+    import seqalib_amd as sa
+    import bench
+    T, L = 7, 40
+    s1, o1, s2, o2 = sa.synth_dna_batch(bench.SEED_BASE, T, L, L, threads=2)
+    for world in (1, 2, 3, 8):
+        got = []
+        for rank in range(world):
+            P, base, name = bench.rank_shard(rank, world, 10000, T, L)
+            assert name == f"sw_batch_{T}x{L}x{L}_strong"
+            if P == 0:
+                continue
+            a1, b1, a2, b2 = sa.synth_dna_batch(base, P, L, L, threads=2)
+            got += [(a1[b1[p]:b1[p + 1]].tobytes(), a2[b2[p]:b2[p + 1]].tobytes()) for p in range(P)]
+        assert got == [(s1[o1[p]:o1[p + 1]].tobytes(), s2[o2[p]:o2[p + 1]].tobytes()) for p in range(T)], world
+    P, base, name = bench.rank_shard(1, 2, 6, 0, L)   # weak scaling: per-GPU pairs, as shard_seed_base
+    assert (P, base, name) == (6, bench.shard_seed_base(1, 2, 6), f"sw_batch_6x{L}x{L}")
+
+
 def test_static_and_balanced_splits():
     assert static_split(10, 4) == [(0, 2), (2, 5), (5, 7), (7, 10)]
     assert shard_range(1, 2, 20000) == (10000, 20000)
