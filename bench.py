@@ -252,11 +252,39 @@ def dropin_e2e(args):
     if args.dropin_pairs <= 0 or not os.path.exists(exe):
         return None
     try:
-        out = subprocess.run([exe, str(args.dropin_pairs), str(args.len), str(args.dropin_reps)],
-                             capture_output=True, text=True, timeout=300, check=True).stdout
-        return json.loads(out.strip().splitlines()[-1])
+        # SEQALIB_HOST_TIMING: the host phases of every getAlignments call on stderr (a few lines
+        # per call), split per timed rep below
+        env = dict(os.environ, SEQALIB_HOST_TIMING="1")
+        r = subprocess.run([exe, str(args.dropin_pairs), str(args.len), str(args.dropin_reps)],
+                           capture_output=True, text=True, timeout=300, check=True, env=env)
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        d["phases_ms_each"] = dropin_phases(r.stderr)[1:]   # (the first call is the untimed warm-up)
+        return d
     except Exception as e:   # reported, never fatal for the bench line
         return {"error": str(e)[:200]}
+
+
+def dropin_phases(stderr: str):
+    """Per getAlignments call, the host phases its SEQALIB_HOST_TIMING lines report (ms): symbol
+    coding, match table + buffers, the GPU call (upload staging, waits, downloads, with the lists
+    of landed ranges built beside it) and the lists left after it."""
+    import re
+    calls = []
+    for line in stderr.splitlines():
+        m = re.match(r"\[seqalib host\] (.+?)\s+([\d.]+) ms$", line)
+        if m:
+            name = m.group(1).strip()
+            if name == "symbol coding":
+                calls.append({})
+            if calls:
+                calls[-1][name] = float(m.group(2))
+            continue
+        m = re.search(r"\[seqalib host api\] \d+ pairs, \d+ chunks: ([\d.]+) ms = staging in ([\d.]+) \+ "
+                      r"waiting ([\d.]+) \+ copies out ([\d.]+)", line)
+        if m and calls:
+            calls[-1].update({"api_total": float(m.group(1)), "api_staging_in": float(m.group(2)),
+                              "api_waiting": float(m.group(3)), "api_copies_out": float(m.group(4))})
+    return calls
 
 
 def small_call_phases(stderr: str):

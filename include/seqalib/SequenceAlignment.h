@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cassert>
 #include <climits>
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <exception>
@@ -200,8 +201,14 @@ std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std
                 self.forceGlobal(*pairs[p].first, *pairs[p].second, out[p], r.start_i, r.start_j, r.end_i, r.end_j);
         }
     };
+    // while the chunked GPU call is still landing ranges, its copy workers use half of the CPU share
+    // (copies of the next ranges' results and op streams): the lists take the other half, so the
+    // process stays inside its cgroup quota (over it, the whole process is throttled for the rest
+    // of the CFS period -- the drop-in's run-to-run spread of round 5)
+    std::atomic<bool> landing{true};
     auto build_range = [&](size_t p0, size_t p1) {
-        parallel_pairs(p1 - p0, host_threads(p1 - p0), [&](size_t, size_t q0, size_t q1) { build(p0 + q0, p0 + q1); });
+        parallel_pairs(p1 - p0, host_threads(p1 - p0, landing.load() ? 2 : 1),
+                       [&](size_t, size_t q0, size_t q1) { build(p0 + q0, p0 + q1); });
     };
     PhaseTimer tm;
     const size_t G = P >= 2 * kChunkPairs ? (P + kChunkPairs - 1) / kChunkPairs : 1;
@@ -258,6 +265,7 @@ std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std
         throw;
     }
     tm.lap("GPU call (lists overlapped)");
+    landing = false;
     close();
     if (lq.err) std::rethrow_exception(lq.err);
     tm.lap("AlignedSequence lists (tail)");

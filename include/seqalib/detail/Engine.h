@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <array>
+#include <sched.h>
 #include <chrono>
 #include <climits>
 #include <cstdint>
@@ -107,11 +108,32 @@ struct DefaultInitAlloc : std::allocator<T> {
 template <typename T>
 using raw_vector = std::vector<T, DefaultInitAlloc<T>>;
 
-// Host threads for per-pair work of a batch of P pairs (symbol coding, list construction): at most
-// 16 (the GPU box's CPU share), at least 32 pairs each.
-inline size_t host_threads(size_t P) {
-    const size_t hw = std::max(1u, std::thread::hardware_concurrency());
-    return std::max<size_t>(1, std::min<size_t>(std::min<size_t>(hw, 16), P / 32));
+// CPUs this process may use: hardware threads, capped by its affinity mask and its cgroup CPU
+// quota (a GPU box shows every core of the machine but grants a share; threads beyond the quota
+// get the whole process throttled for the rest of the CFS period).
+inline size_t host_cpu_share() {
+    static const size_t share = [] {
+        size_t n = std::max(1u, std::thread::hardware_concurrency());
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::min<size_t>(n, (size_t)std::max(1, CPU_COUNT(&set)));
+        if (std::FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {   // "<quota> <period>" or "max <period>"
+            char q[32] = {0};
+            unsigned long long per = 0;
+            if (std::fscanf(f, "%31s %llu", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0)
+                n = std::min<size_t>(n, (size_t)std::max<unsigned long long>(1, std::strtoull(q, nullptr, 10) / per));
+            std::fclose(f);
+        }
+        return n;
+    }();
+    return share;
+}
+
+// Host threads for per-pair work of a batch of P pairs (symbol coding, list construction): the
+// CPU share (at most 16), at least 32 pairs each.  share_div: the work runs beside the library's
+// copy workers (a chunked GPU call still landing), which take the other part of the share.
+inline size_t host_threads(size_t P, size_t share_div = 1) {
+    const size_t cpus = std::max<size_t>(1, std::min<size_t>(host_cpu_share(), 16) / share_div);
+    return std::max<size_t>(1, std::min<size_t>(cpus, P / 32));
 }
 
 // Runs body(t, p0, p1) over nth contiguous pair ranges [P*t/nth, P*(t+1)/nth), one host thread

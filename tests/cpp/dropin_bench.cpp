@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -14,6 +15,20 @@
 
 template <typename T>
 bool equal(T V1, T V2) { return V1 == V2; }
+
+// cgroup v2 CPU throttling counters of this process's cgroup (nr_throttled, throttled_usec)
+static void cpu_stat(unsigned long long& nr, unsigned long long& us) {
+    nr = us = 0;
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.stat", "r")) {
+        char k[64];
+        unsigned long long v;
+        while (fscanf(f, "%63s %llu", k, &v) == 2) {
+            if (!strcmp(k, "nr_throttled")) nr = v;
+            if (!strcmp(k, "throttled_usec")) us = v;
+        }
+        fclose(f);
+    }
+}
 
 int main(int argc, char** argv) {
     const uint32_t P = argc > 1 ? (uint32_t)atoi(argv[1]) : 1000;
@@ -32,11 +47,17 @@ int main(int argc, char** argv) {
         auto warm = sw.getAlignments(pairs);   // first call: context + workspace allocation
     }
     double best = 1e30, sum = 0;
-    std::string each;
+    std::string each, thr;
     for (int r = 0; r < reps; ++r) {
+        unsigned long long n0, u0, n1, u1;
+        cpu_stat(n0, u0);
         const auto t0 = std::chrono::steady_clock::now();
         auto out = sw.getAlignments(pairs);
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        cpu_stat(n1, u1);
+        char tb[96];
+        snprintf(tb, sizeof tb, "%s{\"nr_throttled\": %llu, \"throttled_ms\": %.2f}", r ? ", " : "", n1 - n0, (u1 - u0) / 1e3);
+        thr += tb;
         best = std::min(best, s);
         sum += s;
         entries = 0;
@@ -48,7 +69,9 @@ int main(int argc, char** argv) {
     const double cells = (double)P * L * L;
     printf("{\"what\": \"C++ drop-in SmithWatermanSA<std::string,char,'-'>::getAlignments, end-to-end incl. "
            "std::list construction\", \"pairs\": %u, \"len\": %u, \"reps\": %d, \"ms_best\": %.2f, "
-           "\"ms_mean\": %.2f, \"ms_each\": [%s], \"gcups_best\": %.1f, \"gcups_mean\": %.1f, \"entries\": %zu}\n",
-           P, L, reps, best * 1e3, sum / reps * 1e3, each.c_str(), cells / best / 1e9, cells / (sum / reps) / 1e9, entries);
+           "\"ms_mean\": %.2f, \"ms_each\": [%s], \"gcups_best\": %.1f, \"gcups_mean\": %.1f, \"entries\": %zu, "
+           "\"cgroup_throttle_each\": [%s]}\n",
+           P, L, reps, best * 1e3, sum / reps * 1e3, each.c_str(), cells / best / 1e9, cells / (sum / reps) / 1e9, entries,
+           thr.c_str());
     return 0;
 }
