@@ -16,7 +16,6 @@
 #include <algorithm>
 #include <cassert>
 #include <climits>
-#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <exception>
@@ -187,7 +186,7 @@ std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std
     const sa_scoring sc = self.getScoring().toC();
     const size_t P = pairs.size();
     std::vector<AlignedSequence<Ty, Blank>> out(P);
-    raw_vector<uint8_t> ops;
+    raw_vector<uint8_t>& ops = host_buffer(kHostOps);
     std::vector<uint64_t> off;
     auto build = [&](size_t p0, size_t p1) {
         for (size_t p = p0; p < p1; ++p) {
@@ -201,17 +200,13 @@ std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std
                 self.forceGlobal(*pairs[p].first, *pairs[p].second, out[p], r.start_i, r.start_j, r.end_i, r.end_j);
         }
     };
-    // while the chunked GPU call is still landing ranges, its copy workers use half of the CPU share
-    // (copies of the next ranges' results and op streams): the lists take the other half, so the
-    // process stays inside its cgroup quota (over it, the whole process is throttled for the rest
-    // of the CFS period -- the drop-in's run-to-run spread of round 5)
-    std::atomic<bool> landing{true};
     auto build_range = [&](size_t p0, size_t p1) {
-        parallel_pairs(p1 - p0, host_threads(p1 - p0, landing.load() ? 2 : 1),
-                       [&](size_t, size_t q0, size_t q1) { build(p0 + q0, p0 + q1); });
+        parallel_pairs(p1 - p0, host_threads(p1 - p0), [&](size_t, size_t q0, size_t q1) { build(p0 + q0, p0 + q1); });
     };
     PhaseTimer tm;
-    const size_t G = P >= 2 * kChunkPairs ? (P + kChunkPairs - 1) / kChunkPairs : 1;
+    size_t cp = kChunkPairs;
+    if (const char* e = std::getenv("SEQALIB_LIST_CHUNK_PAIRS")) cp = std::max<size_t>(1, std::strtoull(e, nullptr, 10));   // (A/B)
+    const size_t G = P >= 2 * cp ? (P + cp - 1) / cp : 1;
     if (G == 1) {
         align<Ty>(ALGO, sc, fn, has_fn, pairs, res, ops, off);
         build_range(0, P);
@@ -265,7 +260,6 @@ std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std
         throw;
     }
     tm.lap("GPU call (lists overlapped)");
-    landing = false;
     close();
     if (lq.err) std::rethrow_exception(lq.err);
     tm.lap("AlignedSequence lists (tail)");

@@ -108,6 +108,16 @@ struct DefaultInitAlloc : std::allocator<T> {
 template <typename T>
 using raw_vector = std::vector<T, DefaultInitAlloc<T>>;
 
+// The batch's large host buffers (coded Seq1 / Seq2 and the op streams: ~2 x 82 MB for the
+// 10,000 x 4096^2 batch) are kept per host thread across calls (grow-only): allocated per call they
+// came from fresh mmap'd pages, ~40 K first-touch page faults per call (round 6, tests/cpp/
+// dropin_bench per-rep counters), on the threads that build the lists at the same time.
+enum HostBuf { kHostSeq1, kHostSeq2, kHostOps, kHostBufs };
+inline raw_vector<uint8_t>& host_buffer(int which) {
+    thread_local raw_vector<uint8_t> bufs[kHostBufs];
+    return bufs[which];
+}
+
 // CPUs this process may use: hardware threads, capped by its affinity mask and its cgroup CPU
 // quota (a GPU box shows every core of the machine but grants a share; threads beyond the quota
 // get the whole process throttled for the rest of the CFS period).
@@ -129,10 +139,9 @@ inline size_t host_cpu_share() {
 }
 
 // Host threads for per-pair work of a batch of P pairs (symbol coding, list construction): the
-// CPU share (at most 16), at least 32 pairs each.  share_div: the work runs beside the library's
-// copy workers (a chunked GPU call still landing), which take the other part of the share.
-inline size_t host_threads(size_t P, size_t share_div = 1) {
-    const size_t cpus = std::max<size_t>(1, std::min<size_t>(host_cpu_share(), 16) / share_div);
+// CPU share (at most 16), at least 32 pairs each.
+inline size_t host_threads(size_t P) {
+    const size_t cpus = std::max<size_t>(1, std::min<size_t>(host_cpu_share(), 16));
     return std::max<size_t>(1, std::min<size_t>(cpus, P / 32));
 }
 
@@ -351,7 +360,10 @@ void align(int algo, const sa_scoring& sc, MatchFnTy& fn, bool has_fn,
         o1.push_back(o1.back() + (uint64_t)p.first->size());
         o2.push_back(o2.back() + (uint64_t)p.second->size());
     }
-    raw_vector<uint8_t> s1(o1.back() + 1), s2(o2.back() + 1);   // +1: never a NULL pointer
+    raw_vector<uint8_t>& s1 = host_buffer(kHostSeq1);   // (+1 below: never a NULL pointer)
+    raw_vector<uint8_t>& s2 = host_buffer(kHostSeq2);
+    s1.resize(o1.back() + 1);
+    s2.resize(o2.back() + 1);
     constexpr bool kDirect = std::is_integral<Ty>::value && sizeof(Ty) == 1;
     code_symbols(std::integral_constant<bool, kDirect>{}, coder, pairs, o1, o2, s1, s2);
     tm.lap("symbol coding");
