@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cassert>
 #include <climits>
+#include <cstdint>
 #include <condition_variable>
 #include <deque>
 #include <exception>
@@ -169,10 +170,14 @@ void build_from_ops(ContainerType& Seq1, ContainerType& Seq2, const sa_result& r
     }
 }
 
-// Pairs per chunk when a large batch is aligned in chunks (run below).  The GPU call is one
-// sa_align_batch_cb over the whole batch, pipelined chunk by chunk on the device; the lists of a
-// chunk are built while the GPU works on the chunks after it.
-constexpr size_t kChunkPairs = 2048;
+// Pairs per chunk when a large batch is aligned in chunks (run below): the GPU call is one
+// sa_align_batch_cb over the whole batch, pipelined chunk by chunk on the device, and the lists of a
+// chunk are built while the GPU works on the chunks after it.  Off by default since round 6: the
+// lists built beside the landing chunks faulted in fresh heap pages in bursts (0.3 K - 59 K minor
+// faults per call against a steady 24 K), and those reps ran 2-3x slower; one GPU call followed by
+// the lists is 103-106 ms per 10,000 x 4096^2 call, 3 % spread (profiles/dropin_spread_r06.txt).
+// $SEQALIB_LIST_CHUNK_PAIRS=N turns chunking on (N pairs per chunk).
+constexpr size_t kChunkPairs = SIZE_MAX;
 
 // Shared getAlignment()/getAlignments() body of the four aligners.  Building the std::list of
 // every pair (one allocation per Entry, as the reference's buildResult) dominates a large batch
@@ -205,8 +210,8 @@ std::vector<AlignedSequence<Ty, Blank>> run(Aligner& self, const std::vector<std
     };
     PhaseTimer tm;
     size_t cp = kChunkPairs;
-    if (const char* e = std::getenv("SEQALIB_LIST_CHUNK_PAIRS")) cp = std::max<size_t>(1, std::strtoull(e, nullptr, 10));   // (A/B)
-    const size_t G = P >= 2 * cp ? (P + cp - 1) / cp : 1;
+    if (const char* e = std::getenv("SEQALIB_LIST_CHUNK_PAIRS")) cp = std::max<size_t>(1, std::strtoull(e, nullptr, 10));
+    const size_t G = cp <= P / 2 ? (P + cp - 1) / cp : 1;
     if (G == 1) {
         align<Ty>(ALGO, sc, fn, has_fn, pairs, res, ops, off);
         build_range(0, P);

@@ -106,8 +106,9 @@ def test_chunked_batch_lists_match_oracle(binaries, engine, algo, code, args):
     import seqalib_amd as sa
     from util import oracle_batch, pack_bytes
     P = 4500
+    env = dict(os.environ, SEQALIB_LIST_CHUNK_PAIRS="2048")   # (chunking is opt-in since round 6)
     out = subprocess.run([os.path.join(CPP, "dropin_chunks"), str(P), algo], capture_output=True, text=True,
-                         timeout=240, check=True).stdout.split()
+                         timeout=240, check=True, env=env).stdout.split()
     assert len(out) == P
     pairs = []
     for p in range(P):
