@@ -16,6 +16,7 @@
 // fill's work at 4096 x 4096.
 #include <limits.h>
 
+#include "sa_endcell_so.h"
 #include "sa_internal.h"
 
 namespace sa {
@@ -28,10 +29,6 @@ __device__ __forceinline__ int32_t ec_top(const int32_t* p) {
     return __hip_atomic_load((cgi32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ uint32_t ec_code8(uint32_t sp, uint32_t b) {
-    return (b == ((sp >> 8) & 255u) ? 8u : 0u) | (b == ((sp >> 16) & 255u) ? 16u : 0u) |
-           (b == (sp >> 24) ? 24u : 0u);
-}
 
 template <int R>
 __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
@@ -169,10 +166,6 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
 // than kSoCand candidate blocks (an all-zero or low-scoring matrix: smax = 0 lists every block)
 // replays whole chunks instead (64 lanes, from the snapshots), as endcell_kernel does.
 constexpr int kSoCand = 1024;
-#ifndef SA_EC_SCAN
-#define SA_EC_SCAN 16
-#endif
-constexpr int kEcScan = SA_EC_SCAN;
 #ifdef SA_TB_STATS
 // Debug build only (-DSA_TB_STATS, tools/so4_stats.py): [pairs, candidate lane blocks, dense
 // fallbacks, wave cycles, scan cycles]
@@ -201,6 +194,25 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
     const uint32_t pidx = P.pair_base + slot;
     sa_result res = P.res[pidx];
     if (res.reserved == 0 || (res.flags & (SA_FLAG_BAD_SHAPE | kFlagRetry))) return;   // uniform over the wave
+    if constexpr (!DENSE) {
+        __shared__ uint32_t s_cand[kSoCand], s_hit[kSoCand];
+        __shared__ uint32_t s_pk[kWave / R][kChunk + 1];
+#ifdef SA_TB_STATS
+        const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
+        int cnt = 0;
+        const bool done = endcell_so_lanes<R, kSoCand>(P, slot, res.score, s_cand, s_hit, s_pk, &cnt);
+        if (lane == 0) {
+            atomicAdd(&g_ecso_stats[0], 1ull);
+            atomicAdd(&g_ecso_stats[1], (unsigned long long)cnt);
+            atomicAdd(&g_ecso_stats[2], done ? 0ull : 1ull);
+            atomicAdd(&g_ecso_stats[3], __builtin_amdgcn_s_memtime() - st_t0);
+        }
+#else
+        (void)endcell_so_lanes<R, kSoCand>(P, slot, res.score, s_cand, s_hit, s_pk);
+#endif
+        (void)symp;
+        return;
+    }
     const uint64_t o1 = P.off1[pidx], o2 = P.off2[pidx];
     const int m = (int)(P.off1[pidx + 1] - o1);
     const int n = (int)(P.off2[pidx + 1] - o2);
@@ -219,169 +231,7 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
     auto take = [&](int H, int row, int col) __attribute__((always_inline)) {
         if (H > bv || (H == bv && (row > bi || (row == bi && col > bj)))) { bv = H; bi = row; bj = col; }
     };
-
-#ifdef SA_TB_STATS
-    const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
-#endif
-    // ---- the candidate lane blocks, in [band][chunk][lane] order.  First level: the fill's
-    // (band, chunk) maxima of the lane maxima (FillParams::snap_c), kEcScan x 64 entries per round of
-    // loads issued together; second level: the 64 lane maxima of each (band, chunk) that reaches thr
-    __shared__ uint32_t s_cand[DENSE ? 1 : kSoCand];   // band << 22 | chunk << 6 | lane
-    __shared__ uint32_t s_hit[DENSE ? 1 : kSoCand];    // (band, chunk) entries whose maximum reaches thr
-    const uint32_t total = DENSE ? 0u : (uint32_t)B * snch;
-    const int32_t* const sc = P.snap_c + (uint64_t)slot * P.snap_c_slot;
-    int nhit = 0;
-    for (uint32_t e0 = 0; e0 < total; e0 += kWave * kEcScan) {
-        int v[kEcScan];
-#pragma unroll
-        for (int k = 0; k < kEcScan; ++k) {
-            const uint32_t e = e0 + (uint32_t)(k * kWave + lane);
-            v[k] = e < total && (int)(e % snch) < nch ? sc[e] : INT_MIN;
-        }
-#pragma unroll
-        for (int k = 0; k < kEcScan; ++k) {
-            const bool hit = v[k] >= thr;
-            const uint64_t hits = __builtin_amdgcn_ballot_w64(hit);
-            if (hit) {
-                const int pos = nhit + (int)__builtin_popcountll(hits & ((1ull << lane) - 1));
-                if (pos < kSoCand) s_hit[pos] = e0 + (uint32_t)(k * kWave + lane);
-            }
-            nhit += (int)__builtin_popcountll(hits);
-        }
-    }
-    const bool over = nhit > kSoCand;   // (uniform) more chunks than the list holds: the DENSE launch
-    nhit = min(nhit, kSoCand);
-    __syncthreads();
-    int cnt = over ? kSoCand + 1 : 0;
-    for (int h0 = 0; h0 < (over ? 0 : nhit); h0 += kEcScan) {
-        int v[kEcScan];
-        uint32_t ee[kEcScan];
-#pragma unroll
-        for (int k = 0; k < kEcScan; ++k) {   // (wave-uniform)
-            ee[k] = h0 + k < nhit ? s_hit[h0 + k] : 0u;
-            v[k] = h0 + k < nhit ? cm[(uint64_t)ee[k] * kWave + lane] : INT_MIN;
-        }
-#pragma unroll
-        for (int k = 0; k < kEcScan; ++k) {
-            const bool hit = v[k] >= thr;
-            const uint64_t hits = __builtin_amdgcn_ballot_w64(hit);
-            if (hit) {
-                const int pos = cnt + (int)__builtin_popcountll(hits & ((1ull << lane) - 1));
-                const uint32_t bb = ee[k] / snch, cc = ee[k] - bb * snch;
-                if (pos < kSoCand) s_cand[pos] = bb << 22 | cc << 6 | (uint32_t)lane;
-            }
-            cnt += (int)__builtin_popcountll(hits);
-        }
-    }
-    __syncthreads();
-#ifdef SA_TB_STATS
-    if (!DENSE && lane == 0) {
-        atomicAdd(&g_ecso_stats[0], 1ull);
-        atomicAdd(&g_ecso_stats[1], (unsigned long long)cnt);
-        atomicAdd(&g_ecso_stats[2], cnt > kSoCand ? 1ull : 0ull);
-        atomicAdd(&g_ecso_stats[4], __builtin_amdgcn_s_memtime() - st_t0);
-    }
-#endif
-
-    if (!DENSE && cnt > kSoCand) return;   // (uniform) pending: the DENSE launch takes the pair
-    if constexpr (!DENSE) {
-        // ---- lane blocks: 64 / R per round, lane = block g's row r
-        constexpr int NB = kWave / R;
-        const int g = lane / R, r = lane % R;
-        __shared__ uint32_t s_pk[NB][kChunk + 1];   // per block, q = -1 .. 31: top H | column code << 16
-        const uint8_t* const dir = P.dirs + (uint64_t)slot * P.dir_slot;
-        const uint64_t bst = P.band_stride;
-        // Round k+1's loads (left word, top values, Seq2 / Seq1 bytes) are issued before round k's
-        // steps and consumed after them, so a round's dependent global reads do not stall it; the
-        // profile words are registers (no load behind the Seq1 byte).
-        constexpr int QN = (kChunk + R) / R;   // q = r - 1 + R k < kChunk: at most QN per lane
-        const uint32_t pf0 = P.prof[0], pf1 = P.prof[1], pf2 = P.prof[2], pf3 = P.prof[3];
-        struct Pre {
-            uint32_t w, s1c;
-            uint32_t top[QN], s2c[QN];
-        };
-        auto fetch = [&](int c0, Pre& x) __attribute__((always_inline)) {
-            const int ci = c0 + g;
-            const bool act = ci < cnt;
-            const uint32_t cd = act ? s_cand[ci] : 0u;
-            const int b = (int)(cd >> 22), c = (int)((cd >> 6) & 0xffffu), t = (int)(cd & 63u);
-            const int i = b * BAND + t * R + r;
-            const int j0 = kChunk * c - t;
-            x.w = 0;
-            if (act && j0 >= 1 && i < m) x.w = sh_base[(((uint64_t)b * snch + (c - 1)) * (R / 2) + (r >> 1)) * kWave + t];
-            // the top row (row i0 - 1, the last row of lane t - 1, or of lane 63 of band b - 1) and the
-            // column codes: lane tp computed column jj at step jj + tp of its band's edge stream
-            const bool has_top = !(b == 0 && t == 0);
-            const int bp = t > 0 ? b : b - 1, tp = t > 0 ? t - 1 : kWave - 1;
-#pragma unroll
-            for (int k = 0; k < QN; ++k) {
-                const int q = r - 1 + R * k, jj = j0 + q;
-                x.top[k] = 0;
-                x.s2c[k] = 0;
-                if (q < kChunk && act && jj >= 0 && jj < n) {
-                    if (has_top) {
-                        if (q < 0 && j0 >= 1) {
-                            x.top[k] = (uint32_t)sp_base[((uint64_t)b * snch + (c - 1)) * kWave + t] & 0xffffu;
-                        } else {
-                            const int st = jj + tp;
-                            x.top[k] = *reinterpret_cast<const uint16_t*>(dir + (uint64_t)bp * bst +
-                                                                        ((uint64_t)(st >> 3) * kWave + tp) * 16 + (st & 7) * 2);
-                        }
-                    }
-                    x.s2c[k] = s2[jj];
-                }
-            }
-            x.s1c = act && i < m ? s1[i] : 0u;
-        };
-        Pre cur, nxt;
-        fetch(0, cur);
-        for (int c0 = 0; c0 < cnt; c0 += NB) {
-            const int ci = c0 + g;
-            const bool act = ci < cnt;
-            const uint32_t cd = act ? s_cand[ci] : 0u;
-            const int b = (int)(cd >> 22), c = (int)((cd >> 6) & 0xffffu), t = (int)(cd & 63u);
-            const int i = b * BAND + t * R + r;   // this lane's row (0-based)
-            const int j0 = kChunk * c - t;        // the block's first column
-            // H at column j0 - 1 (left of the block)
-            int h = (int)((r & 1) ? (cur.w >> 16) : (cur.w & 0xffffu));
-#pragma unroll
-            for (int k = 0; k < QN; ++k) {
-                const int q = r - 1 + R * k, jj = j0 + q;
-                const uint32_t code = (act && jj >= 0 && jj < n) ? ec_code8(symp, cur.s2c[k]) : 0u;
-                if (q < kChunk) s_pk[g][q + 1] = cur.top[k] | code << 16;
-            }
-            const uint32_t c8 = ec_code8(symp, cur.s1c);
-            const uint32_t tab = act && i < m ? (c8 == 0 ? pf0 : c8 == 8 ? pf1 : c8 == 16 ? pf2 : pf3) : 0u;
-            if (c0 + NB < cnt) fetch(c0 + NB, nxt);
-            __syncthreads();
-            uint32_t pk = 0;            // (top H | column code << 16) of this lane's current column
-            int up_prev = (int)(s_pk[g][0] & 0xffffu);   // row 0: the corner; other rows: set below
-            for (int u = 0; u < kChunk + R - 1; ++u) {
-                // row r at column q = u - r: up = row r - 1's H at q (its previous step), diagonal =
-                // row r - 1's H at q - 1 (the up of this lane's previous step)
-                int up = __builtin_amdgcn_update_dpp(0, h, 0x138, 0xf, 0xf, false);   // wave_shr:1
-                pk = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pk, 0x138, 0xf, 0xf, false);
-                if (r == 0) {
-                    pk = u < kChunk ? s_pk[g][u + 1] : 0u;
-                    up = (int)(pk & 0xffffu);
-                }
-                const int diag = up_prev;
-                up_prev = up;
-                const int q = u - r, j = j0 + q;
-                if (act && q >= 0 && q < kChunk && j >= 0 && j < n && i < m) {
-                    const int sub = ((int)__builtin_amdgcn_sbfe(tab, pk >> 16, 8) - 3) >> 2;
-                    int H = (j == 0 ? 0 : diag) + sub;
-                    H = max(H, up + G);
-                    H = max(H, (j == 0 ? 0 : h) + G);
-                    H = max(H, 0);
-                    h = H;
-                    take(H, i, j);
-                }
-            }
-            __syncthreads();   // (s_pk and s_cand reads of this round)
-            cur = nxt;
-        }
-    } else {
+    {
         // ---- dense: whole chunks holding a candidate lane, all 64 lanes from the snapshots
         __shared__ uint8_t s_sym[kWave + kChunk];
         __shared__ int s_top[kChunk];
@@ -460,9 +310,6 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
         const int ov = __shfl_xor(bv, off), oi = __shfl_xor(bi, off), oj = __shfl_xor(bj, off);
         if (ov > bv || (ov == bv && (oi > bi || (oi == bi && oj > bj)))) { bv = ov; bi = oi; bj = oj; }
     }
-#ifdef SA_TB_STATS
-    if (!DENSE && lane == 0) atomicAdd(&g_ecso_stats[3], __builtin_amdgcn_s_memtime() - st_t0);
-#endif
     if (lane == 0) {   // (the other fields stay as the fill wrote them)
         sa_result* const o = P.res + pidx;
         o->score = bv;
@@ -471,6 +318,7 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
         o->reserved = 0;
     }
 }
+
 
 // LocalGotoh (T16 affine CMAX fill): the same replay on the three-state recurrence
 // (SALocalGotoh.h:108-130).  The fill's snapshot of a lane holds its R values of M (8M), then its
