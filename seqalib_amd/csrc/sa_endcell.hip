@@ -168,7 +168,8 @@ __global__ __launch_bounds__(64) void endcell_kernel(EndcellParams P) {
 constexpr int kSoCand = 1024;
 #ifdef SA_TB_STATS
 // Debug build only (-DSA_TB_STATS, tools/so4_stats.py): [pairs, candidate lane blocks, dense
-// fallbacks, wave cycles, scan cycles]
+// fallbacks, wave cycles, cycles to the scan's first load (parameters, result, offsets), first-level
+// scan cycles, second-level cycles, summed over waves; [7]: the wave lifetime's maximum]
 __device__ unsigned long long g_ecso_stats[8];
 extern "C" int sa_debug_ecso_stats(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ecso_stats), sizeof(g_ecso_stats)) != hipSuccess) return 1;
@@ -196,16 +197,22 @@ __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
     if (res.reserved == 0 || (res.flags & (SA_FLAG_BAD_SHAPE | kFlagRetry))) return;   // uniform over the wave
     if constexpr (!DENSE) {
         __shared__ uint32_t s_cand[kSoCand], s_hit[kSoCand];
-        __shared__ uint32_t s_pk[kWave / R][kChunk + 1];
+        __shared__ __attribute__((aligned(16))) uint32_t s_pk[kWave / R][kEcPk<R>];
 #ifdef SA_TB_STATS
         const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
         int cnt = 0;
-        const bool done = endcell_so_lanes<R, kSoCand>(P, slot, res.score, s_cand, s_hit, s_pk, &cnt);
+        unsigned long long ph[3] = {st_t0, st_t0, st_t0};
+        const bool done = endcell_so_lanes<R, kSoCand>(P, slot, res.score, s_cand, s_hit, s_pk, &cnt, ph);
         if (lane == 0) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memtime();
             atomicAdd(&g_ecso_stats[0], 1ull);
             atomicAdd(&g_ecso_stats[1], (unsigned long long)cnt);
             atomicAdd(&g_ecso_stats[2], done ? 0ull : 1ull);
-            atomicAdd(&g_ecso_stats[3], __builtin_amdgcn_s_memtime() - st_t0);
+            atomicAdd(&g_ecso_stats[3], t1 - st_t0);
+            atomicAdd(&g_ecso_stats[4], ph[0] - st_t0);
+            atomicAdd(&g_ecso_stats[5], ph[1] - ph[0]);
+            atomicAdd(&g_ecso_stats[6], ph[2] - ph[1]);
+            atomicMax(&g_ecso_stats[7], t1 - st_t0);
         }
 #else
         (void)endcell_so_lanes<R, kSoCand>(P, slot, res.score, s_cand, s_hit, s_pk);

@@ -19,6 +19,10 @@ __device__ __forceinline__ uint32_t ec_code8(uint32_t sp, uint32_t b) {
 #define SA_EC_SCAN 16
 #endif
 constexpr int kEcScan = SA_EC_SCAN;
+// words per block row of the replay's LDS staging (endcell_so_lanes): one per step, rounded to
+// whole 16-byte groups, and the corner
+template <int R>
+constexpr int kEcPk = ((kChunk + R - 1 + 3) & ~3) + 4;
 
 // The score-only fill tracked the rows 3 mod 4 at the steps 3 mod 4 and stored, per (band, chunk,
 // lane), the lane's maximum of its tracked cells; every cell is at most a tracked cell of the same
@@ -28,14 +32,15 @@ constexpr int kEcScan = SA_EC_SCAN;
 // per round of loads; second level: the 64 lane maxima of each hit) into s_cand (CAND entries;
 // s_hit: CAND) and recomputes each block alone -- its left column from the snapshot of the chunk
 // before, its top row from the edge stream, one row per lane in a 32 + R - 1 step wavefront,
-// 64 / R blocks per round (s_pk: 64 / R x (kChunk + 1) words) -- keeping per lane the
+// 64 / R blocks per round (s_pk: 64 / R x kEcPk<R> words, 16-byte aligned) -- keeping per lane the
 // lexicographically largest (H, i, j): the reference's last row-major maximum,
 // SASmithWaterman.h:110.  Writes (score, end_i, end_j, reserved = 0) of pair `slot` and returns
 // true; with more than CAND candidate blocks it writes nothing and returns false (the pair stays
 // pending for endcell_so_kernel<R, DENSE = true>).  *ncand (if given): the candidate count.  One wave.
 template <int R, int CAND>
 __device__ __forceinline__ bool endcell_so_lanes(const EndcellParams& P, uint32_t slot, int score, uint32_t* s_cand,
-                                                 uint32_t* s_hit, uint32_t (*s_pk)[kChunk + 1], int* ncand = nullptr) {
+                                                 uint32_t* s_hit, uint32_t (*s_pk)[kEcPk<R>], int* ncand = nullptr,
+                                                 unsigned long long* ph = nullptr) {
     const int lane = threadIdx.x;
     const uint32_t symp = P.prof[4];
     const uint32_t pidx = P.pair_base + slot;
@@ -64,6 +69,7 @@ __device__ __forceinline__ bool endcell_so_lanes(const EndcellParams& P, uint32_
     const uint32_t total = (uint32_t)B * snch;
     const int32_t* const sc = P.snap_c + (uint64_t)slot * P.snap_c_slot;
     int nhit = 0;
+    if (ph) ph[0] = __builtin_amdgcn_s_memtime();
     for (uint32_t e0 = 0; e0 < total; e0 += kWave * kEcScan) {
         int v[kEcScan];
 #pragma unroll
@@ -85,6 +91,7 @@ __device__ __forceinline__ bool endcell_so_lanes(const EndcellParams& P, uint32_
     const bool over = nhit > CAND;   // (uniform) more chunks than the list holds: the DENSE launch
     nhit = min(nhit, CAND);
     __syncthreads();
+    if (ph) ph[1] = __builtin_amdgcn_s_memtime();
     int cnt = over ? CAND + 1 : 0;
     for (int h0 = 0; h0 < (over ? 0 : nhit); h0 += kEcScan) {
         int v[kEcScan];
@@ -107,6 +114,7 @@ __device__ __forceinline__ bool endcell_so_lanes(const EndcellParams& P, uint32_
         }
     }
     __syncthreads();
+    if (ph) ph[2] = __builtin_amdgcn_s_memtime();
     if (ncand) *ncand = cnt;
 
     if (cnt > CAND) return false;   // (uniform) pending: the DENSE launch takes the pair
@@ -114,7 +122,8 @@ __device__ __forceinline__ bool endcell_so_lanes(const EndcellParams& P, uint32_
         // ---- lane blocks: 64 / R per round, lane = block g's row r
         constexpr int NB = kWave / R;
         const int g = lane / R, r = lane % R;
-        // s_pk[NB][kChunk + 1]: per block, q = -1 .. 31: top H | column code << 16
+        // s_pk[NB][kEcPk<R>]: per block, entry q = 0 .. 31 = column code | top H << 16 (the value row
+        // 0 reads at step q), the corner (top H at q = -1) in the row's last word
         const uint8_t* const dir = P.dirs + (uint64_t)slot * P.dir_slot;
         const uint64_t bst = P.band_stride;
         // Round k+1's loads (left word, top values, Seq2 / Seq1 bytes) are issued before round k's
@@ -159,6 +168,10 @@ __device__ __forceinline__ bool endcell_so_lanes(const EndcellParams& P, uint32_
             }
             x.s1c = act && i < m ? s1[i] : 0u;
         };
+        // steps of a round, rounded up to whole ds_read_b128 groups: the extra steps only touch
+        // columns q >= kChunk, which no lane takes and no lane below reads inside its block
+        constexpr int kSteps = (kChunk + R - 1 + 3) & ~3;
+        static_assert(kSteps <= kEcPk<R> - 1, "s_pk row holds every step's word and the corner");
         Pre cur, nxt;
         fetch(0, cur);
         for (int c0 = 0; c0 < cnt; c0 += NB) {
@@ -168,42 +181,57 @@ __device__ __forceinline__ bool endcell_so_lanes(const EndcellParams& P, uint32_
             const int b = (int)(cd >> 22), c = (int)((cd >> 6) & 0xffffu), t = (int)(cd & 63u);
             const int i = b * BAND + t * R + r;   // this lane's row (0-based)
             const int j0 = kChunk * c - t;        // the block's first column
-            // H at column j0 - 1 (left of the block)
+            // H at column j0 - 1 (left of the block; 0 where j0 <= 0: the left border)
             int h = (int)((r & 1) ? (cur.w >> 16) : (cur.w & 0xffffu));
 #pragma unroll
             for (int k = 0; k < QN; ++k) {
                 const int q = r - 1 + R * k, jj = j0 + q;
                 const uint32_t code = (act && jj >= 0 && jj < n) ? ec_code8(symp, cur.s2c[k]) : 0u;
-                if (q < kChunk) s_pk[g][q + 1] = cur.top[k] | code << 16;
+                if (q < 0) s_pk[g][kEcPk<R> - 1] = cur.top[k] << 16;
+                else if (q < kChunk) s_pk[g][q] = code | cur.top[k] << 16;
             }
+            // this lane's substitution scores by column code (bytes 0, 8, 16, 24), the profile's
+            // (s * 4 + 3) bytes decoded once per round
             const uint32_t c8 = ec_code8(symp, cur.s1c);
-            const uint32_t tab = act && i < m ? (c8 == 0 ? pf0 : c8 == 8 ? pf1 : c8 == 16 ? pf2 : pf3) : 0u;
+            const uint32_t tab = c8 == 0 ? pf0 : c8 == 8 ? pf1 : c8 == 16 ? pf2 : pf3;
+            uint32_t sub4 = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                sub4 |= ((uint32_t)(((int)__builtin_amdgcn_sbfe(tab, 8u * k, 8u) - 3) >> 2) & 0xffu) << (8 * k);
+            // the cells this lane takes: steps u = q + r with 0 <= q < kChunk and 0 <= j = j0 + q < n;
+            // h advances from the first step with q >= 0 and j >= 0 (cells left of column 0 keep 0)
+            const int ustart = r + max(0, -j0);
+            const int uend = min(r + kChunk, r - j0 + n);
+            const uint32_t span = act && i < m && uend > ustart ? (uint32_t)(uend - ustart) : 0u;
             if (c0 + NB < cnt) fetch(c0 + NB, nxt);
             __syncthreads();
-            uint32_t pk = 0;            // (top H | column code << 16) of this lane's current column
-            int up_prev = (int)(s_pk[g][0] & 0xffffu);   // row 0: the corner; other rows: set below
-            for (int u = 0; u < kChunk + R - 1; ++u) {
-                // row r at column q = u - r: up = row r - 1's H at q (its previous step), diagonal =
-                // row r - 1's H at q - 1 (the up of this lane's previous step)
-                int up = __builtin_amdgcn_update_dpp(0, h, 0x138, 0xf, 0xf, false);   // wave_shr:1
-                pk = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pk, 0x138, 0xf, 0xf, false);
-                if (r == 0) {
-                    pk = u < kChunk ? s_pk[g][u + 1] : 0u;
-                    up = (int)(pk & 0xffffu);
-                }
-                const int diag = up_prev;
-                up_prev = up;
-                const int q = u - r, j = j0 + q;
-                if (act && q >= 0 && q < kChunk && j >= 0 && j < n && i < m) {
-                    const int sub = ((int)__builtin_amdgcn_sbfe(tab, pk >> 16, 8) - 3) >> 2;
-                    int H = (j == 0 ? 0 : diag) + sub;
-                    H = max(H, up + G);
-                    H = max(H, (j == 0 ? 0 : h) + G);
-                    H = max(H, 0);
-                    h = H;
-                    take(H, i, j);
+            const bool row0 = r == 0;
+            uint32_t pk = 0;   // (column code | top H << 16) of this lane's current column
+            int up_prev = (int)(s_pk[g][kEcPk<R> - 1] >> 16);   // row 0: the corner; other rows: set below
+            int rbv = -1, ru = 0;   // this round's best H and its step (ties: the later column)
+            for (int u0 = 0; u0 < kSteps; u0 += 4) {
+                const uint4 w4 = *reinterpret_cast<const uint4*>(&s_pk[g][u0]);
+                const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int u = u0 + k;
+                    // row r at column q = u - r: up = row r - 1's H at q (its previous step), diagonal =
+                    // row r - 1's H at q - 1 (the up of this lane's previous step)
+                    const int up_d = __builtin_amdgcn_update_dpp(0, h, 0x138, 0xf, 0xf, true);   // wave_shr:1
+                    const uint32_t pk_d = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pk, 0x138, 0xf, 0xf, true);
+                    pk = row0 ? wv[k] : pk_d;
+                    const int up = row0 ? (int)(wv[k] >> 16) : up_d;
+                    const int diag = up_prev;
+                    up_prev = up;
+                    const int sub = (int)__builtin_amdgcn_sbfe(sub4, pk, 8);
+                    const int H = max(max(diag + sub, max(up, h) + G), 0);
+                    h = u >= ustart ? H : h;
+                    const bool tk = (uint32_t)(u - ustart) < span && H >= rbv;
+                    rbv = tk ? H : rbv;
+                    ru = tk ? u : ru;
                 }
             }
+            if (rbv >= 0) take(rbv, i, j0 + ru - r);
             __syncthreads();   // (s_pk and s_cand reads of this round)
             cur = nxt;
         }

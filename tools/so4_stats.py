@@ -31,7 +31,8 @@ for it in range(2):
     ep = max(ec[0], 1)
     kf, ks = eng.last_kernel_timings()
     print(f"end cell: {ks - kf:.3f} ms, {ec[0]} pairs, {ec[1] / ep:.1f} candidate lane blocks per pair, {ec[2]} dense fallbacks, "
-          f"{ec[3] / ep:.0f} cycles per wave of which scan {ec[4] / ep:.0f}")
+          f"{ec[3] / ep:.0f} cycles per wave = to first scan load {ec[4] / ep:.0f} + first level {ec[5] / ep:.0f} + "
+          f"second level {ec[6] / ep:.0f} + replay {(ec[3] - ec[4] - ec[5] - ec[6]) / ep:.0f}; longest wave {ec[7]}")
     rounds, iters, moves, cyc, wait, sub, nsub, waves = list(out)
     w = max(waves, 1)
     print(f"pairs {P} fill {f:.2f} ms tb {tb:.2f} ms | per wave: rounds {rounds / w:.0f} iters {iters / w:.0f} "
