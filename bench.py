@@ -522,7 +522,9 @@ def main():
         bytes_per_cell = streams["total"] / per_launch_cells
     hbm_gbps = per_launch_cells * bytes_per_cell / fill_s / 1e9
     pmc = load_pmc(workload, label)
-    kname = ("fill_so_kernel<R=%d> (score-only T16, chunk-max end cell, 4 waves/SIMD)" % plan_R if so else
+    kname = ("fill_so2_kernel<R=%d> (score-only T16, two pairs per wave in packed 16-bit halves, band units, "
+             "4 waves/SIMD)" % plan_R if so2 else
+             "fill_so_kernel<R=%d> (score-only T16, chunk-max end cell, 4 waves/SIMD)" % plan_R if so else
              f"fill_kernel<SW,R={plan_R},W={plan_W}," + ("T16 tagged int16 profile" if t16 else "int32 flags")
              + (",chunk-max end cell>" if endcell else ",KEYED>"))
     # achieved = fill cells/s x ISA-counted VALU instructions per cell of the steady loop (each lane
@@ -533,7 +535,7 @@ def main():
     epc = model.get("valu_elem_per_cell", vpc) if model else None
     achieved = fill_gcups * epc / 1e3 if epc else None
     roof = {"bound": "valu", "achieved": round(achieved, 2) if achieved else None, "peak": round(VALU_PEAK_TLANE, 2),
-            "unit": "T lane-instr/s", "frac": round(achieved / VALU_PEAK_TLANE, 4) if achieved else None,
+            "unit": "T lane-ops/s", "frac": round(achieved / VALU_PEAK_TLANE, 4) if achieved else None,
             "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None}
     clk = pmc.get("clock_ghz") if pmc else None
     roof.update({"kernel": kname, "avg_launch_ms": round(fill_s * 1e3, 3),

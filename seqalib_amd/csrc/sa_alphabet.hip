@@ -106,7 +106,8 @@ hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uin
     // starts as soon as ONE fill unit's slot frees, where a 4-wave workgroup waited for four in one
     // CU (bench rocprofv3 r05: scans of up to 15.7 ms, 14 % of the summed kernel time).
     // $SEQALIB_SCAN_WG=256 restores the round-5 launch (A/B).
-    static const bool wide = [] { const char* e = getenv("SEQALIB_SCAN_WG"); return e && atoi(e) == 256; }();
+    const char* ev = getenv("SEQALIB_SCAN_WG");   // (read per launch: tests switch it in-process)
+    const bool wide = ev && atoi(ev) == 256;
     if (wide) hipLaunchKernelGGL(alphabet_scan<256>, dim3(2048), dim3(256), 0, s, d1, o1, d2, o2, npairs, bitmap);
     else hipLaunchKernelGGL(alphabet_scan<64>, dim3(2048), dim3(64), 0, s, d1, o1, d2, o2, npairs, bitmap);
     return hipGetLastError();

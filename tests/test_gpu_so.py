@@ -120,6 +120,32 @@ def test_so_ragged_matches_tagged_and_oracle(engine, maxlen, R, tb):
         assert so[1][off:off + int(so[0]["nops"][p])].tobytes() == oops[ooff:ooff + int(ores["nops"][q])].tobytes(), int(p)
 
 
+@pytest.mark.parametrize("maxlen,R,npairs", [(1000, 16, 1101), (3000, 32, 1100)])
+def test_so2_matches_one_pair_per_wave(engine, monkeypatch, maxlen, R, npairs):
+    """Two pairs per wave (fill_so2_kernel, the default on the score-only SW plans at R = 16 / 32)
+    against one pair per wave (SEQALIB_SO2=0) and against round 5's alphabet-scan launch
+    (SEQALIB_SCAN_WG=256): identical results and op streams on ragged batches (an odd pair count
+    leaves the last couple's second half empty); every end cell against the linear-space oracle."""
+    batch = ragged_batch(90 + maxlen, npairs, maxlen)
+    s1, o1, s2, o2 = batch
+    a = run(engine, True, *batch)
+    monkeypatch.setenv("SEQALIB_SO2", "0")
+    b = run(engine, True, *batch)
+    monkeypatch.delenv("SEQALIB_SO2")
+    monkeypatch.setenv("SEQALIB_SCAN_WG", "256")
+    c = run(engine, True, *batch)
+    monkeypatch.delenv("SEQALIB_SCAN_WG")
+    assert a[2] == (sa.SA_KERNEL_T16_ENDCELL, R, 1) and b[2] == a[2] and c[2] == a[2]
+    assert (a[0]["flags"] == 0).all()
+    assert_same(a, b, o1, o2)
+    assert_same(a, c, o1, o2)
+    exp = oracle_sw_scores(SW, s1, o1, s2, o2, threads=THREADS)
+    got = np.stack([a[0]["score"], a[0]["end_i"], a[0]["end_j"]], axis=1)
+    nonempty = (np.diff(o1) > 0) & (np.diff(o2) > 0)
+    bad = np.nonzero((got != exp).any(axis=1) & nonempty)[0]
+    assert len(bad) == 0, [(int(p), got[p].tolist(), exp[p].tolist()) for p in bad[:5]]
+
+
 def test_so_scorings_and_lut(engine):
     """Other scorings (match 2, mismatch -3, gap -2; !AllowMismatch) and a non-identity match table
     on a 4-symbol alphabet (A~G, C~T): identical to the tagged path; a sample against the oracle."""
