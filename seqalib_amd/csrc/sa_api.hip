@@ -263,20 +263,21 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
     }
     if (v.so) {
         v.pl.g = make_geom(algo, v.pl.R, max_m, max_n, kGeomEdge);
+        // two pairs per wave (sa_fill_so2.hip): the packed cell, for the SW band units at R = 16 / 32;
+        // $SEQALIB_SO2=0 runs one pair per wave (A/B, tests)
+        v.so2 = algo == SA_SW && (v.pl.R == 16 || v.pl.R == 32);
+        if (const char* e = getenv("SEQALIB_SO2")) if (e[0] == '0') v.so2 = false;
         if (!is_affine(algo)) {
-            // column segments: a band's chunks in kSoSegs units of at least 2 chunks each, so the
-            // launch tail is half a band (sa_fill_impl.h BU); $SEQALIB_SO_SEGS sets the count
-            uint32_t sg = kSoSegs;
+            // column segments: a band's chunks in kSoSegs (two pairs per wave: kSo2Segs) units of at
+            // least 2 chunks each, so the launch tail is a fraction of a band (sa_fill_impl.h BU);
+            // $SEQALIB_SO_SEGS sets the count
+            uint32_t sg = v.so2 ? kSo2Segs : kSoSegs;
             if (const char* e = getenv("SEQALIB_SO_SEGS")) sg = (uint32_t)std::max(1, atoi(e));
             v.segs = std::max(1u, std::min(sg, v.snap_nch / 2));
             v.seg_slot = v.segs > 1 ? (uint64_t)v.pl.g.bands * v.segs * (v.pl.R + 1) * kWave : 0;
         }
         v.part_slot = (uint64_t)v.pl.g.bands * v.segs;
         if (algo == SA_SW) v.snap_c_slot = (uint64_t)v.pl.g.bands * v.snap_nch;
-        // two pairs per wave (sa_fill_so2.hip): the packed cell, for the SW band units at R = 16 / 32;
-        // $SEQALIB_SO2=0 runs one pair per wave (A/B, tests)
-        v.so2 = algo == SA_SW && (v.pl.R == 16 || v.pl.R == 32);
-        if (const char* e = getenv("SEQALIB_SO2")) if (e[0] == '0') v.so2 = false;
     }
     if (v.pl.split) v.pl.rowbuf_elems = 0;   // hand-off granules live in c->split
     v.kernel = v.cmax ? SA_KERNEL_T16_ENDCELL : t16 ? SA_KERNEL_T16 : SA_KERNEL_INT32;

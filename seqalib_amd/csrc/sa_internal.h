@@ -237,6 +237,12 @@ constexpr int kSoSlack = 6;
 // units draining) is half of that.  Pipelined headline step (profiles/fill_segs_ab_r05.txt):
 // 1 segment 17.95 / 18.07 ms, 2: 17.51 / 17.53, 3: 17.66 / 17.64, 4: 17.75 / 17.75.
 constexpr uint32_t kSoSegs = 2;
+// Two pairs per wave (sa_fill_so2.hip): a unit carries two pairs' work, so the tail is twice as
+// long at the same count; pipelined 10,000-pair steps by segments (profiles/so2_segs_r06.jsonl):
+// 4096^2 2: 16.85-16.88 ms, 3: 16.56-16.59, 4: 16.46-16.55, 5: 16.51-16.55, 6: 16.55-16.57,
+// 8: 16.45-16.49, 12: 16.58-16.62; 2048^2 2: 5.00-5.09, 4: 4.88-4.89, 8: 4.80; 1024^2 (33 chunks)
+// 2: 1.66-1.70, 6: 1.63, 8: 1.64-1.65.
+constexpr uint32_t kSo2Segs = 8;
 hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uint8_t* d2,
                                 const uint64_t* o2, uint32_t npairs, uint32_t* aux, hipStream_t s);
 // decide_t16: from the bitmap, aux[kAuxSel] = 1 if the batch has <= 4 distinct symbols (then the

@@ -366,15 +366,16 @@ def test_so_retry_pair_leaves_neighbours_intact(engine):
 
 @pytest.mark.parametrize("algo,scoring", [(0, SW), (1, (-1, 2, -1))])
 def test_so_column_segments_any_count(engine, monkeypatch, algo, scoring):
-    """Column segments of the band units (SEQALIB_SO_SEGS, default kSoSegs = 2): the same ragged
-    batch with 1, 2, 3 and 5 segments per band (pairs with fewer chunks than 2 per segment use
-    fewer) gives identical results and op streams, equal to the tagged path."""
+    """Column segments of the band units (SEQALIB_SO_SEGS; default kSoSegs = 2, two pairs per wave
+    kSo2Segs = 8): the same ragged batch with 1, 2, 3, 5 and 8 segments per band (pairs with fewer
+    chunks than 2 per segment use fewer) gives identical results and op streams, equal to the
+    tagged path."""
     batch = ragged_batch(123 + algo, 1100, 3000)
     s1, o1, s2, o2 = batch
     monkeypatch.delenv("SEQALIB_SO_SEGS", raising=False)
     base = run(engine, True, *batch, scoring=scoring, algo=algo)
     assert engine.last_plan_ex()[3] == sa.SA_RECORDS_SCORE_ONLY
-    for segs in ("1", "3", "5"):
+    for segs in ("1", "2", "3", "5", "8"):
         monkeypatch.setenv("SEQALIB_SO_SEGS", segs)
         assert_same(run(engine, True, *batch, scoring=scoring, algo=algo), base, o1, o2)
     monkeypatch.delenv("SEQALIB_SO_SEGS")
