@@ -241,7 +241,9 @@ constexpr uint32_t kSoSegs = 2;
 // long at the same count; pipelined 10,000-pair steps by segments (profiles/so2_segs_r06.jsonl):
 // 4096^2 2: 16.85-16.88 ms, 3: 16.56-16.59, 4: 16.46-16.55, 5: 16.51-16.55, 6: 16.55-16.57,
 // 8: 16.45-16.49, 12: 16.58-16.62; 2048^2 2: 5.00-5.09, 4: 4.88-4.89, 8: 4.80; 1024^2 (33 chunks)
-// 2: 1.66-1.70, 6: 1.63, 8: 1.64-1.65.
+// 2: 1.66-1.70, 6: 1.63, 8: 1.64-1.65.  The one-pair-per-wave NW units keep 2
+// (profiles/nw_segs_r06.jsonl: 1024^2 2: 1.68 ms, 4: 1.68-1.71, 8: 1.81; 4096^2 2: 17.1-17.3,
+// 4: 17.2-17.3, 8: 17.9).
 constexpr uint32_t kSo2Segs = 8;
 hipError_t launch_alphabet_scan(const uint8_t* d1, const uint64_t* o1, const uint8_t* d2,
                                 const uint64_t* o2, uint32_t npairs, uint32_t* aux, hipStream_t s);

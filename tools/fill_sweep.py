@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--variants", default="base")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--algo", type=int, default=0, help="0 SW (-1,1,-1), 1 NW (-1,2,-1)")
     a = ap.parse_args()
     os.environ["SEQALIB_KERNEL_TIMING"] = "1"
     import torch
@@ -50,14 +51,14 @@ def main():
     dev = torch.device("cuda", 0)
     eng = sa.Engine(0)
     st = torch.cuda.current_stream(dev).cuda_stream
-    sc = sa.ScoringSystem(-1, 1, -1)
+    sc = sa.ScoringSystem(-1, 1, -1) if a.algo == 0 else sa.ScoringSystem(-1, 2, -1)
     L = a.len
     for spec in [x for x in a.sizes.split(",") if x]:
         P, m = (int(spec.split(":")[0]), int(spec.split(":")[1])) if ":" in spec else (int(spec), L)
         d, res, ops = batch(torch, dev, P, L, L1=m)
         best = 1e9
         for _ in range(3):
-            eng.align_device(0, sc, *[x.data_ptr() for x in d], P, m, L, res[0].data_ptr(), ops[0].data_ptr(), st)
+            eng.align_device(a.algo, sc, *[x.data_ptr() for x in d], P, m, L, res[0].data_ptr(), ops[0].data_ptr(), st)
             torch.cuda.synchronize()
             best = min(best, eng.last_kernel_timings()[0])
         print(json.dumps({"sweep": "fill_vs_pairs", "pairs": P, "m": m, "n": L, "fill_kernel_ms": round(best, 3),
@@ -79,12 +80,12 @@ def main():
                     k, x = kv.split("=", 1)
                     os.environ[k] = x
             for k in range(2):
-                eng.align_device(0, sc, *[x.data_ptr() for x in d], P, L, L, res[k % len(res)].data_ptr(), ops[k % len(ops)].data_ptr(), st)
+                eng.align_device(a.algo, sc, *[x.data_ptr() for x in d], P, L, L, res[k % len(res)].data_ptr(), ops[k % len(ops)].data_ptr(), st)
             eng.wait()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for k in range(a.steps):
-                eng.align_device(0, sc, *[x.data_ptr() for x in d], P, L, L, res[k % len(res)].data_ptr(), ops[k % len(ops)].data_ptr(), st)
+                eng.align_device(a.algo, sc, *[x.data_ptr() for x in d], P, L, L, res[k % len(res)].data_ptr(), ops[k % len(ops)].data_ptr(), st)
             eng.wait()
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / a.steps * 1e3
@@ -95,7 +96,7 @@ def main():
         os.environ.pop(k, None)
     # parity of the last variant's output against a plain call
     r0 = np.frombuffer(res[(a.steps - 1) % len(res)].cpu().numpy().tobytes(), dtype=sa.RESULT_DTYPE).copy()
-    eng.align_device(0, sc, *[x.data_ptr() for x in d], P, L, L, res[0].data_ptr(), ops[0].data_ptr(), st)
+    eng.align_device(a.algo, sc, *[x.data_ptr() for x in d], P, L, L, res[0].data_ptr(), ops[0].data_ptr(), st)
     torch.cuda.synchronize()
     r1 = np.frombuffer(res[0].cpu().numpy().tobytes(), dtype=sa.RESULT_DTYPE)
     print(json.dumps({"check": "last pipelined variant == plain call", "equal": bool((r0 == r1).all())}), flush=True)
