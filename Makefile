@@ -15,7 +15,7 @@ LIB       = seqalib_amd/lib/libseqalib_hip.so
 HIP_SRCS  = $(CSRC)/sa_fill_sw.hip $(CSRC)/sa_fill_so2.hip $(CSRC)/sa_fill_nw.hip $(CSRC)/sa_fill_lg.hip $(CSRC)/sa_fill_gg.hip \
             $(CSRC)/sa_traceback.hip $(CSRC)/sa_traceback_so.hip $(CSRC)/sa_traceback_wave.hip $(CSRC)/sa_traceback_seg.hip $(CSRC)/sa_alphabet.hip $(CSRC)/sa_endcell.hip $(CSRC)/sa_hirschberg.hip $(CSRC)/sa_dc.hip \
             $(CSRC)/sa_myersmiller.hip $(CSRC)/sa_tiny.hip $(CSRC)/sa_api.hip
-CPP_SRCS  = $(CSRC)/sa_synth.cpp $(CSRC)/sa_multi.cpp
+CPP_SRCS  = $(CSRC)/sa_synth.cpp $(CSRC)/sa_multi.cpp $(CSRC)/sa_codec.cpp
 HDRS      = $(CSRC)/sa_internal.h $(CSRC)/sa_layout.h $(CSRC)/sa_fill_impl.h $(CSRC)/sa_dc.h include/seqalib_hip.h
 OBJS      = $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(CPP_SRCS))
 

@@ -23,6 +23,11 @@
 
 using namespace sa;
 
+namespace sa {   // sa_codec.cpp: 2-bit transfer codecs of the host API
+bool dna2_pack(uint8_t* dst, const uint8_t* src, uint64_t n);
+void ops2_unpack(uint8_t* dst, const uint8_t* src, uint32_t n, const uint32_t* lut);
+}  // namespace sa
+
 constexpr int kKEv = 6;   // SEQALIB_KERNEL_TIMING events per fill launch (two per variant, <= 3)
 // Cross-call pipeline: workspace slots (call k's fill waits for call k-2's traceback).  Three slots
 // with the fills alternating between two streams (call k+1's fill starting in call k's fill tail)
@@ -299,34 +304,98 @@ __global__ void lut_to_bits(const uint8_t* lut, uint32_t* bits) {
 // cpos[q], the exclusive prefix sum of nops; cpos[cnt] = the total), so the D2H moves the ops the
 // walks wrote instead of the m + n + 1 bytes reserved per pair (the headline batch: 48 of 92 MB).
 // ops_scan: one workgroup; ops_pack: one workgroup per pair.
-__global__ __launch_bounds__(1024) void ops_scan(const sa_result* res, uint32_t cnt, uint64_t* cpos) {
-    __shared__ uint64_t s_part[1024];
+// cpos2: the same over ceil(nops / 4) (the 2-bit streams, ops_pack).
+__global__ __launch_bounds__(1024) void ops_scan(const sa_result* res, uint32_t cnt, uint64_t* cpos, uint64_t* cpos2) {
+    __shared__ uint64_t s_part[1024], s_part2[1024];
     const uint32_t t = threadIdx.x, per = (cnt + 1023) / 1024;
     const uint32_t a = min(t * per, cnt), b = min(a + per, cnt);
-    uint64_t sum = 0;
-    for (uint32_t q = a; q < b; ++q) sum += res[q].nops;
+    uint64_t sum = 0, sum2 = 0;
+    for (uint32_t q = a; q < b; ++q) {
+        sum += res[q].nops;
+        sum2 += (res[q].nops + 3) / 4;
+    }
     s_part[t] = sum;
+    s_part2[t] = sum2;
     __syncthreads();
     for (uint32_t off = 1; off < 1024; off <<= 1) {   // inclusive scan (Hillis-Steele)
-        const uint64_t v = t >= off ? s_part[t - off] : 0;
+        const uint64_t v = t >= off ? s_part[t - off] : 0, v2 = t >= off ? s_part2[t - off] : 0;
         __syncthreads();
         s_part[t] += v;
+        s_part2[t] += v2;
         __syncthreads();
     }
-    uint64_t base = s_part[t] - sum;
+    uint64_t base = s_part[t] - sum, base2 = s_part2[t] - sum2;
     for (uint32_t q = a; q < b; ++q) {
         cpos[q] = base;
+        if (cpos2) cpos2[q] = base2;
         base += res[q].nops;
+        base2 += (res[q].nops + 3) / 4;
     }
-    if (t == 1023) cpos[cnt] = s_part[1023];
+    if (t == 1023) {
+        cpos[cnt] = s_part[1023];
+        if (cpos2) cpos2[cnt] = s_part2[1023];
+    }
 }
 __global__ __launch_bounds__(256) void ops_pack(const uint64_t* o1, const uint64_t* o2, const sa_result* res,
-                                                const uint64_t* cpos, const uint8_t* ops, uint8_t* packed) {
+                                                const uint64_t* cpos, const uint8_t* ops, uint8_t* packed,
+                                                const uint64_t* cpos2, uint8_t* packed2, uint8_t* letters) {
     const uint32_t q = blockIdx.x;
     const uint8_t* src = ops + o1[q] + o2[q] + q;
     uint8_t* dst = packed + cpos[q];
     const uint32_t n = res[q].nops;
-    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) dst[k] = src[k];
+    uint8_t* dst2 = packed2 ? packed2 + cpos2[q] : nullptr;
+    // the same ops at 2 bits (sa_codec.cpp): M 0, S / X 1, U 2, L 3, one letter per lane, four lanes'
+    // codes to one byte by DPP; seen: bit 0 S, bit 1 X, bit 2 another letter (the host then
+    // downloads the bytes)
+    uint32_t seen = 0;
+    for (uint32_t k0 = 0; k0 < n; k0 += blockDim.x) {   // (uniform trip count: the DPP below)
+        const uint32_t k = k0 + threadIdx.x;
+        const uint32_t ch = k < n ? src[k] : 'M';
+        if (k < n) dst[k] = (uint8_t)ch;
+        if (!dst2) continue;
+        const uint32_t code = ch == 'M' ? 0u : (ch == 'S' || ch == 'X') ? 1u : ch == 'U' ? 2u : 3u;
+        seen |= ch == 'S' ? 1u : ch == 'X' ? 2u : (ch == 'M' || ch == 'U' || ch == 'L') ? 0u : 4u;
+        // lane 4i + t holds code t of byte i: or in lanes +1, +2, +3 (row_shr within rows of 16)
+        uint32_t v = code << (2 * (threadIdx.x & 3));
+        v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xf, 0xf, false);   // row_shl:1
+        v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x102, 0xf, 0xf, false);   // row_shl:2
+        if ((threadIdx.x & 3) == 0 && k < n) dst2[k / 4] = (uint8_t)v;
+    }
+    if (dst2) {
+        // one byte per pair, or-ed on the host: 40,000 waves or-ing one word serialise on it (0.48 ms)
+        __shared__ uint32_t s_seen;
+        if (threadIdx.x == 0) s_seen = 0;
+        __syncthreads();
+        for (int off = 32; off >= 1; off >>= 1) seen |= (uint32_t)__shfl_xor((int)seen, off);
+        if ((threadIdx.x & 63) == 0 && seen) atomicOr(&s_seen, seen);
+        __syncthreads();
+        if (threadIdx.x == 0) letters[q] = (uint8_t)s_seen;
+    }
+}
+
+// 2-bit sequence pieces (sa_codec.cpp dna2_pack) back to bytes: codes 0 A, 1 C, 2 T, 3 G; one
+// thread per 4 packed bytes (16 symbols).  n: symbols.
+__global__ __launch_bounds__(256) void dna2_unpack(const uint8_t* pk, uint8_t* dst, uint64_t n) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (16 * t >= n) return;
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(pk + 4 * t);   // (the landing zone is padded)
+    uint32_t o[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t c = (w >> (2 * (4 * d + k))) & 3u;
+            x |= (0x47544341u >> (8 * c) & 0xffu) << (8 * k);   // "ACTG"
+        }
+        o[d] = x;
+    }
+    if (16 * t + 16 <= n) {
+        *reinterpret_cast<uint4*>(dst + 16 * t) = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {
+        const uint8_t* ob = reinterpret_cast<const uint8_t*>(o);
+        for (uint64_t k = 16 * t; k < n; ++k) dst[k] = ob[k - 16 * t];
+    }
 }
 
 // Traceback flavour per launch: one wave per pair (sa_traceback_wave.hip) for few pairs, one lane
@@ -1490,7 +1559,14 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     // other one-chunk calls download their op streams packed (ops_scan / ops_pack): [cpos][packed]
     const bool packed = G == 1 && !small && !dc;
     const uint64_t b_cpos = packed ? al(8ull * (npairs + 1)) : 0, b_pack = packed ? b_ops : 0;
-    const uint64_t io_need = b_hdr + b_s1 + b_s2 + 2 * b_o + b_res + b_ops + b_lut + b_bits + b_cpos + b_pack;
+    // 2-bit transfers (sa_codec.cpp; $SEQALIB_XFER2=0 sends bytes): sequence pieces land in the
+    // packed-ops region (free until the traceback has run) and are unpacked into d1 / d2; op streams
+    // come down 2-bit from their own region ([cpos2][a letters byte per pair][packed2])
+    const char* x2e = getenv("SEQALIB_XFER2");
+    const bool xfer2 = packed && !(x2e && x2e[0] == '0');
+    const uint64_t b_pk1 = al(t1 / 4 + 64);   // (seq2's landing zone follows seq1's)
+    const uint64_t b_cpos2 = xfer2 ? al(8ull * (npairs + 1)) + al(npairs) : 0, b_pack2 = xfer2 ? al(ops_total / 4 + npairs + 64) : 0;
+    const uint64_t io_need = b_hdr + b_s1 + b_s2 + 2 * b_o + b_res + b_ops + b_lut + b_bits + b_cpos + b_pack + b_cpos2 + b_pack2;
     if (int rc = ensure_io(c, io_need)) return rc;
     uint8_t* p = c->io;
     uint32_t* const dhdr = reinterpret_cast<uint32_t*>(p); p += b_hdr;
@@ -1503,12 +1579,16 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     uint8_t* dlut = p; p += b_lut;
     uint32_t* dbits = reinterpret_cast<uint32_t*>(p); p += b_bits;
     uint64_t* const dcpos = reinterpret_cast<uint64_t*>(p); p += b_cpos;
-    uint8_t* const dpack = p;
+    uint8_t* const dpack = p; p += b_pack;
+    uint64_t* const dcpos2 = reinterpret_cast<uint64_t*>(p); p += b_cpos2;
+    uint8_t* const dletters = reinterpret_cast<uint8_t*>(dcpos2 + (npairs + 1));   // per pair (ops_pack)
+    uint8_t* const dpack2 = p;
+    if (xfer2 && b_pk1 + al((t2 + 3) / 4 + 64) > b_pack) return fail(c, SA_ERR_HIP, "internal: 2-bit landing zone");
     // pinned staging (pageable copies were measured to stall 10-25 ms per call next to PyTorch),
     // laid out as the device I/O: in = [seq1][seq2][off1'][off2'], out = [results][ops], so that a
     // small call moves its inputs in one copy and its outputs in one copy
     SA_HIP(c, c->stage.alloc(b_hdr + b_s1 + b_s2 + 2 * b_o));
-    SA_HIP(c, c->ostage.alloc(b_res + al(ops_total) + 8ull * (npairs + 1)));
+    SA_HIP(c, c->ostage.alloc(b_res + al(ops_total) + 8ull * (npairs + 1) + (xfer2 ? 8ull * (npairs + 1) + npairs : 0)));
     uint32_t* const shdr = reinterpret_cast<uint32_t*>(c->stage.data());
     uint8_t* const si = c->stage.data() + b_hdr;
     uint64_t* const so1 = reinterpret_cast<uint64_t*>(si + b_s1 + b_s2);
@@ -1516,6 +1596,7 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
     sa_result* const sres = reinterpret_cast<sa_result*>(c->ostage.data());
     uint8_t* const sops = c->ostage.data() + b_res;   // (packed: the packed op bytes)
     uint64_t* const scpos = reinterpret_cast<uint64_t*>(c->ostage.data() + b_res + al(ops_total));
+    uint64_t* const scpos2 = scpos + (npairs + 1);   // (xfer2) [cpos2][letters seen, a byte per pair]
     const bool pipe = G > 1;
     if (!c->s_out) SA_HIP(c, hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking));
     if (pipe && !c->s_fill) {
@@ -1568,15 +1649,33 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
             memcpy(si + b_s1, seq2, n2);
             if (dc) SA_HIP(c, hipMemcpyAsync(dhdr, shdr, small_up, hipMemcpyHostToDevice, st));
         }
+        // one piece of a sequence buffer: 2-bit when every byte is A / C / G / T (packed into the
+        // piece's own staging bytes, unpacked on the device), else the bytes
+        auto put_piece = [&](uint8_t* dst, uint8_t* stg, const uint8_t* src, uint64_t k, uint8_t* land) -> int {
+            if (xfer2) {
+                std::atomic<bool> ok{true};
+                par_for(k, CopyPool::kSlice, [&](uint64_t a, uint64_t b) {   // (slices: multiples of 4 bytes)
+                    if (!dna2_pack(stg + a / 4, src + a, b - a)) ok.store(false, std::memory_order_relaxed);
+                });
+                if (ok.load()) {
+                    SA_HIP(c, hipMemcpyAsync(land, stg, (k + 3) / 4, hipMemcpyHostToDevice, st));
+                    const uint64_t thr = (k + 15) / 16;
+                    hipLaunchKernelGGL(dna2_unpack, dim3((uint32_t)((thr + 255) / 256)), dim3(256), 0, st, land, dst, k);
+                    SA_HIP(c, hipGetLastError());
+                    return SA_OK;
+                }
+            }
+            par_copy(stg, src, k);
+            SA_HIP(c, hipMemcpyAsync(dst, stg, k, hipMemcpyHostToDevice, st));
+            return SA_OK;
+        };
         for (uint64_t x = 0; !small && x < n1; x += kHostPiece) {
             const uint64_t k = std::min(kHostPiece, n1 - x);
-            par_copy(si + a1 + x, seq1 + a1 + x, k);
-            SA_HIP(c, hipMemcpyAsync(d1 + a1 + x, si + a1 + x, k, hipMemcpyHostToDevice, st));
+            if (int rc = put_piece(d1 + a1 + x, si + a1 + x, seq1 + a1 + x, k, dpack + x / 4)) return rc;
         }
         for (uint64_t x = 0; !small && x < n2; x += kHostPiece) {
             const uint64_t k = std::min(kHostPiece, n2 - x);
-            par_copy(si + b_s1 + a2 + x, seq2 + a2 + x, k);
-            SA_HIP(c, hipMemcpyAsync(d2 + a2 + x, si + b_s1 + a2 + x, k, hipMemcpyHostToDevice, st));
+            if (int rc = put_piece(d2 + a2 + x, si + b_s1 + a2 + x, seq2 + a2 + x, k, dpack + b_pk1 + x / 4)) return rc;
         }
         if (!small) {
             SA_HIP(c, hipMemcpyAsync(do1 + p0 + g, so1 + p0 + g, 8ull * (cnt + 1), hipMemcpyHostToDevice, st));
@@ -1615,8 +1714,14 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         }
         (void)on;
         if (packed) {   // (one chunk: p0 = 0, g = 0)
-            hipLaunchKernelGGL(ops_scan, dim3(1), dim3(1024), 0, done, dres, cnt, dcpos);
-            hipLaunchKernelGGL(ops_pack, dim3(cnt), dim3(256), 0, done, do1, do2, dres, dcpos, dops, dpack);
+            uint64_t* const c2 = dcpos2;
+            hipLaunchKernelGGL(ops_scan, dim3(1), dim3(1024), 0, done, dres, cnt, dcpos, xfer2 ? dcpos2 : nullptr);
+            if (xfer2)
+                hipLaunchKernelGGL(ops_pack, dim3(cnt), dim3(256), 0, done, do1, do2, dres, dcpos, dops, dpack, c2, dpack2,
+                                   dletters);
+            else
+                hipLaunchKernelGGL(ops_pack, dim3(cnt), dim3(256), 0, done, do1, do2, dres, dcpos, dops, dpack,
+                                   (const uint64_t*)nullptr, (uint8_t*)nullptr, (uint8_t*)nullptr);
             SA_HIP(c, hipGetLastError());
         }
         SA_HIP(c, hipEventRecord(c->host_ev[g], done));
@@ -1624,6 +1729,7 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         if (packed) {   // the results and the packed positions now; the packed bytes once their size is known
             SA_HIP(c, hipMemcpyAsync(sres, dres, sizeof(sa_result) * cnt, hipMemcpyDeviceToHost, c->s_out));
             SA_HIP(c, hipMemcpyAsync(scpos, dcpos, 8ull * (cnt + 1), hipMemcpyDeviceToHost, c->s_out));
+            if (xfer2) SA_HIP(c, hipMemcpyAsync(scpos2, dcpos2, 8ull * (cnt + 1) + cnt, hipMemcpyDeviceToHost, c->s_out));
             SA_HIP(c, hipEventRecord(c->host_ev[G], c->s_out));
             continue;
         }
@@ -1645,14 +1751,29 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         SA_HIP(c, hipEventSynchronize(c->host_ev[G]));
         ms_wait += since(t_w);
         memcpy(results, sres, sizeof(sa_result) * npairs);
-        const uint64_t total = scpos[npairs];
+        // 2-bit op streams unless a letter has no code (another letter, or S and X in one call)
+        uint32_t letters = xfer2 ? 0u : 4u;
+        if (xfer2) {
+            const uint8_t* const seen = reinterpret_cast<const uint8_t*>(scpos2 + (npairs + 1));
+            for (uint32_t q = 0; q < npairs; ++q) letters |= seen[q];
+        }
+        const bool ops2 = xfer2 && !(letters & 4u) && letters != 3u;
+        const uint64_t* const cp = ops2 ? scpos2 : scpos;
+        uint32_t lut4[256];
+        if (ops2) {
+            const uint8_t lt[4] = {'M', (uint8_t)(letters & 2u ? 'X' : 'S'), 'U', 'L'};
+            for (uint32_t b = 0; b < 256; ++b)
+                lut4[b] = lt[b & 3] | (uint32_t)lt[(b >> 2) & 3] << 8 | (uint32_t)lt[(b >> 4) & 3] << 16 |
+                          (uint32_t)lt[b >> 6] << 24;
+        }
+        const uint64_t total = cp[npairs];
         if (total > ops_total) return fail(c, SA_ERR_HIP, "internal: packed op streams exceed their buffer");
         // pieces of the packed bytes; the pairs whose bytes have all landed go to the caller's
         // layout (pair q at off1[q] + off2[q] + q) while later pieces are in flight
         const size_t np = (size_t)((total + kHostPiece - 1) / kHostPiece);
         for (size_t k = 0; k < np; ++k) {
             const uint64_t x = k * kHostPiece, n = std::min(kHostPiece, total - x);
-            SA_HIP(c, hipMemcpyAsync(sops + x, dpack + x, n, hipMemcpyDeviceToHost, c->s_out));
+            SA_HIP(c, hipMemcpyAsync(sops + x, (ops2 ? dpack2 : dpack) + x, n, hipMemcpyDeviceToHost, c->s_out));
             SA_HIP(c, hipEventRecord(c->host_ev[G + 1 + k], c->s_out));
         }
         uint32_t q0 = 0;
@@ -1662,11 +1783,13 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
             ms_wait += since(t_w2);
             const uint64_t landed = k < np ? (uint64_t)(k + 1) * kHostPiece : total;
             uint32_t q1 = q0;
-            while (q1 < npairs && scpos[q1 + 1] <= landed) ++q1;
+            while (q1 < npairs && cp[q1 + 1] <= landed) ++q1;
             const auto t_o = std::chrono::steady_clock::now();
             par_for(q1 - q0, 256, [&, q0](uint64_t a, uint64_t b) {
-                for (uint64_t q = q0 + a; q < q0 + b; ++q)
-                    memcpy(ops + off1[q] + off2[q] + q, sops + scpos[q], results[q].nops);
+                for (uint64_t q = q0 + a; q < q0 + b; ++q) {
+                    if (ops2) ops2_unpack(ops + off1[q] + off2[q] + q, sops + cp[q], results[q].nops, lut4);
+                    else memcpy(ops + off1[q] + off2[q] + q, sops + cp[q], results[q].nops);
+                }
             });
             ms_out += since(t_o);
             q0 = q1;

@@ -215,3 +215,17 @@ def test_expand_ops_matches_oracle_strings():
         r = sa.PairResult(o["score"], o["end_i"], o["end_j"], o["start_i"], o["start_j"], 0, o["ops"])
         got = sa.expand_ops(algo, a.decode(), b.decode(), r).rows()
         assert got == o["rows"]
+
+
+def test_transfer_codec_round_trips(tmp_path):
+    """The host API's 2-bit transfer codecs (seqalib_amd/csrc/sa_codec.cpp), both packing paths
+    (scalar and AVX2), against a byte-by-byte restatement (tests/cpp/codec_test.cpp): every length
+    0..300 and large ones, every byte value at every position (only A / C / G / T pack), and the
+    op-letter expansion."""
+    import subprocess
+    exe = str(tmp_path / "codec_test")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-DSA_CODEC_TEST", "-o", exe,
+                    os.path.join(ROOT, "tests", "cpp", "codec_test.cpp"),
+                    os.path.join(ROOT, "seqalib_amd", "csrc", "sa_codec.cpp")], check=True)
+    out = subprocess.run([exe], check=True, capture_output=True, text=True)
+    assert out.stdout.strip() == "ok"
