@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--dropin-pairs", type=int, default=10000,
                     help="C++ drop-in end-to-end leg (tests/cpp/dropin_bench): pairs (0 = skip)")
     ap.add_argument("--dropin-reps", type=int, default=3)
-    ap.add_argument("--e2e-steps", type=int, default=2,
+    ap.add_argument("--e2e-steps", type=int, default=5,
                     help="host-API steps (H2D + fill + traceback + D2H of results and ops) timed after the run")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
@@ -353,8 +353,9 @@ def load_pmc(workload: str, label: str):
 
 
 def fill_streams(pairs: int, m: int, n: int, R: int, segs: int = 2):
-    """Bytes the score-only SW fill writes per launch of `pairs` m x n pairs, stream by stream
-    (sa_fill_impl.h BU / sa_fill_so2.hip; geometry of sa_layout.h)."""
+    """Bytes the score-only SW fill moves per launch of `pairs` m x n pairs, stream by stream: every
+    stream it writes and what it reads back or stages (sa_fill_impl.h BU / sa_fill_so2.hip; geometry
+    of sa_layout.h)."""
     bands = -(-m // (64 * R))
     nch = (n + 63 + 31) // 32                       # chunks_per_band
     sg = max(1, min(segs, nch // 2))
@@ -366,6 +367,11 @@ def fill_streams(pairs: int, m: int, n: int, R: int, segs: int = 2):
         "segment_state": bands * (sg - 1) * (R + 1) * 64 * 4,
         "unit_words": bands * sg * 8,
         "result": 32,
+        # reads: the hand-off words back (segment state, band rows) and the sequences each unit
+        # stages (its band's Seq1 rows, its column range of Seq2 and the 64 columns before it)
+        "read_segment_state": bands * (sg - 1) * (R + 1) * 64 * 4,
+        "read_band_rows": (bands - 1) * n * 4,
+        "read_sequences": sg * min(m, bands * 64 * R) + bands * (n + 64 * sg),
     }
     out = {k: v * pairs for k, v in per.items()}
     out["total"] = sum(out.values())
@@ -460,14 +466,17 @@ def main():
     fill_kernel_ms = max_over_ranks(fill_kernel_ms, world)
     # end to end through the host API (what the C++ drop-in does): sequences H2D, fill, end cell,
     # traceback, results + op streams D2H; outside the timed region
-    e2e_ms = None
+    e2e_ms, e2e_each = None, None
     if args.e2e_steps > 0:
         eng.set_pipeline(False)
         sc_ = sa.ScoringSystem(*SCORING)
         out = eng.align_packed(sa.SA_SW, sc_, s1, o1, s2, o2)   # warm the host-API buffers
         te = time.perf_counter()
+        e2e_each = []
         for _ in range(args.e2e_steps):
+            tc = time.perf_counter()
             out = eng.align_packed(sa.SA_SW, sc_, s1, o1, s2, o2, out=out)   # caller keeps its buffers
+            e2e_each.append(round((time.perf_counter() - tc) * 1e3, 2))
         e2e_ms = max_over_ranks(time.perf_counter() - te, world) / args.e2e_steps * 1e3
 
     cells_rank = float(P) * Lq * Lq
@@ -517,7 +526,10 @@ def main():
     # every stream the score-only fill writes, per launch, from its geometry:
     # the streams above over the steps and chunks it really runs (n + 63 steps per band, snapshots
     # of all chunks but the last) plus the band rows, segment state, per-unit words and results
-    streams = fill_streams(P, Lq, Lq, plan_R) if so else None
+    # column segments per band unit as the engine picks them (sa_api.hip make_variant: kSo2Segs = 8
+    # for two pairs per wave, kSoSegs = 2 otherwise; $SEQALIB_SO_SEGS overrides)
+    segs = int(os.environ.get("SEQALIB_SO_SEGS", "0") or 0) or (8 if so2 else 2)
+    streams = fill_streams(P, Lq, Lq, plan_R, segs) if so else None
     if streams:
         bytes_per_cell = streams["total"] / per_launch_cells
     hbm_gbps = per_launch_cells * bytes_per_cell / fill_s / 1e9
@@ -567,11 +579,13 @@ def main():
                          "replay), traceback_ms = traceback stream after the fill stream",
         "records": "score-only fill + block-recompute traceback" if so else ("tagged" if t16 else "flags"),
         "e2e_ms_per_step": round(e2e_ms, 2) if e2e_ms else None,
+        "e2e_ms_each": e2e_each if e2e_ms else None,
         "e2e_gcups": round(cells_job / (e2e_ms / 1e3) / 1e9, 1) if e2e_ms else None,
-        "e2e_basis": "host API sa_align_batch from pageable host buffers, one call at a time, one chunk: pinned "
-                     "upload of sequences + offsets in 16 MiB pieces (host copy of piece k+1 beside the H2D of "
-                     "piece k), fill, end cell, traceback, download of results and op streams into the caller's "
-                     "(reused) buffers piece by piece",
+        "e2e_basis": "host API sa_align_batch from pageable host buffers, one call at a time (mean of e2e_steps "
+                     "calls after one warm call), one chunk: upload of sequences + offsets in 16 MiB pieces, "
+                     "A/C/G/T pieces packed to 2 bits on the host and unpacked on the device (host pass over "
+                     "piece k+1 beside the H2D of piece k), fill, end cell, traceback, download of results and "
+                     "2-bit op streams, expanded into the caller's (reused) buffers as pieces land",
         "pipelined": pipelined, "serial_ms_per_step": round(serial_ms, 2) if serial_ms else None,
         "parity": "; ".join(
             (f"rank {r}: " if world > 1 else "")
