@@ -526,9 +526,10 @@ def main():
     # every stream the score-only fill writes, per launch, from its geometry:
     # the streams above over the steps and chunks it really runs (n + 63 steps per band, snapshots
     # of all chunks but the last) plus the band rows, segment state, per-unit words and results
-    # column segments per band unit as the engine picks them (sa_api.hip make_variant: kSo2Segs = 8
-    # for two pairs per wave, kSoSegs = 2 otherwise; $SEQALIB_SO_SEGS overrides)
-    segs = int(os.environ.get("SEQALIB_SO_SEGS", "0") or 0) or (8 if so2 else 2)
+    # column segments per band unit as the engine picks them (sa_api.hip make_variant: two pairs per
+    # wave up to kSo2Segs = 8 with at least 8 chunks each, kSoSegs = 2 otherwise; $SEQALIB_SO_SEGS overrides)
+    nch_ = (Lq + 63 + 31) // 32
+    segs = int(os.environ.get("SEQALIB_SO_SEGS", "0") or 0) or (max(2, min(8, nch_ // 8)) if so2 else 2)
     streams = fill_streams(P, Lq, Lq, plan_R, segs) if so else None
     if streams:
         bytes_per_cell = streams["total"] / per_launch_cells

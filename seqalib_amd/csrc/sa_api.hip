@@ -268,15 +268,16 @@ Variant make_variant(int algo, uint32_t max_m, uint32_t max_n, uint32_t npairs, 
     }
     if (v.so) {
         v.pl.g = make_geom(algo, v.pl.R, max_m, max_n, kGeomEdge);
-        // two pairs per wave (sa_fill_so2.hip): the packed cell, for the SW band units at R = 16 / 32;
+        // two pairs per wave (sa_fill_so2.hip): the packed cell, for the SW / NW band units at R = 16 / 32;
         // $SEQALIB_SO2=0 runs one pair per wave (A/B, tests)
-        v.so2 = algo == SA_SW && (v.pl.R == 16 || v.pl.R == 32);
+        v.so2 = (algo == SA_SW || algo == SA_NW) && (v.pl.R == 16 || v.pl.R == 32);
         if (const char* e = getenv("SEQALIB_SO2")) if (e[0] == '0') v.so2 = false;
         if (!is_affine(algo)) {
             // column segments: a band's chunks in kSoSegs (two pairs per wave: kSo2Segs) units of at
             // least 2 chunks each, so the launch tail is a fraction of a band (sa_fill_impl.h BU);
             // $SEQALIB_SO_SEGS sets the count
-            uint32_t sg = v.so2 ? kSo2Segs : kSoSegs;
+            // (two pairs per wave: at least 8 chunks per segment -- 1024^2 batches take 4)
+            uint32_t sg = v.so2 ? std::max(2u, std::min(kSo2Segs, v.snap_nch / 8)) : kSoSegs;
             if (const char* e = getenv("SEQALIB_SO_SEGS")) sg = (uint32_t)std::max(1, atoi(e));
             v.segs = std::max(1u, std::min(sg, v.snap_nch / 2));
             v.seg_slot = v.segs > 1 ? (uint64_t)v.pl.g.bands * v.segs * (v.pl.R + 1) * kWave : 0;
@@ -1091,7 +1092,7 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             const bool units = v.so && !is_affine(algo);
             const uint32_t grid = pl.split ? (uint32_t)(cnt * sp_bands)
                                 : units ? (v.so2 ? (cnt + 1) / 2 : cnt) * pl.g.bands * v.segs : cnt;
-            hipError_t e = v.so2 ? launch_fill_so2(pl.R, fp, grid, sf) : launch_fill(algo, fv, fp, grid, sf);
+            hipError_t e = v.so2 ? launch_fill_so2(algo, pl.R, fp, grid, sf) : launch_fill(algo, fv, fp, grid, sf);
             if (e != hipSuccess) return hip_fail(c, e, "fill kernel launch");
             if (kev) SA_HIP(c, hipEventRecord(kev[2 * k + 1], sf));
             if (pl.split) {
@@ -1769,10 +1770,17 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
         const uint64_t total = cp[npairs];
         if (total > ops_total) return fail(c, SA_ERR_HIP, "internal: packed op streams exceed their buffer");
         // pieces of the packed bytes; the pairs whose bytes have all landed go to the caller's
-        // layout (pair q at off1[q] + off2[q] + q) while later pieces are in flight
-        const size_t np = (size_t)((total + kHostPiece - 1) / kHostPiece);
+        // layout (pair q at off1[q] + off2[q] + q) while later pieces are in flight (2-bit: 2 MiB
+        // pieces, whose expansion to 8 MiB of letters takes longer than the next piece's D2H)
+        const uint64_t piece = ops2 ? (2ull << 20) : kHostPiece;
+        const size_t np = (size_t)((total + piece - 1) / piece);
+        while (c->host_ev.size() < (size_t)G + 1 + np) {
+            hipEvent_t ev;
+            SA_HIP(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            c->host_ev.push_back(ev);
+        }
         for (size_t k = 0; k < np; ++k) {
-            const uint64_t x = k * kHostPiece, n = std::min(kHostPiece, total - x);
+            const uint64_t x = k * piece, n = std::min(piece, total - x);
             SA_HIP(c, hipMemcpyAsync(sops + x, (ops2 ? dpack2 : dpack) + x, n, hipMemcpyDeviceToHost, c->s_out));
             SA_HIP(c, hipEventRecord(c->host_ev[G + 1 + k], c->s_out));
         }
@@ -1781,7 +1789,7 @@ int align_host(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* seq1, c
             const auto t_w2 = std::chrono::steady_clock::now();
             if (k < np) SA_HIP(c, hipEventSynchronize(c->host_ev[G + 1 + k]));
             ms_wait += since(t_w2);
-            const uint64_t landed = k < np ? (uint64_t)(k + 1) * kHostPiece : total;
+            const uint64_t landed = k < np ? (uint64_t)(k + 1) * piece : total;
             uint32_t q1 = q0;
             while (q1 < npairs && cp[q1 + 1] <= landed) ++q1;
             const auto t_o = std::chrono::steady_clock::now();

@@ -28,6 +28,12 @@
 //
 // Work units, tickets, column segments, {tag, value} hand-off words, bounded waits and the per-unit
 // maxima are those of the one-pair band units (sa_fill_impl.h BU), per pair.
+//
+// ALG = SA_NW (round 6): the same cell without the clamp (SANeedlemanWunsch.h:69-86; registers hold
+// H - delta, the T16 window of t16_mode), the borders i Gap - delta / j Gap - delta in the left
+// column, the corner and band 0's top row, no chunk maxima.  H[m][n] of each pair is taken at the
+// one step where its lane computes column n - 1 of row m - 1 (columns past n run on, as in SW), and
+// reaches the couple's final unit through the per-unit words.
 #include "sa_fill_impl.h"
 
 namespace sa {
@@ -63,8 +69,9 @@ __device__ __forceinline__ uint32_t wave_pk_max(uint32_t v) {
 
 }  // namespace
 
-template <int R>
+template <int ALG, int R>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void fill_so2_kernel(FillParams P) {
+    constexpr bool NWK = ALG == SA_NW;
     if (sa_skip(P.sel, P.sel_want)) return;   // (the score-only variant has no redo launch)
     static_assert(R >= 8 && R % 2 == 0, "the sampled chunk maximum needs 8 rows per lane");
     constexpr int BAND = kWave * R;
@@ -112,6 +119,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     const uint32_t epoch16 = P.epoch << 16;
     const uint32_t symp = P.prof[4];
     const int G = P.gap;
+    const int D0 = P.t16_delta;
+    // NW border H(i, 0) = H(0, i) = i Gap as H - delta in both halves (SW: 0)
+    auto border2 = [&](int i) __attribute__((always_inline)) -> uint32_t {
+        return NWK ? ((uint32_t)(i * G - D0) & 0xffffu) * 0x10001u : 0u;
+    };
     uint32_t seg_lost = 0;
 
     // the column table words: byte x of cw[c] = s(x, c) + 128 (x: row symbol code, c: column code)
@@ -171,9 +183,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // and loads take the SGPR-base form and no 64-bit address pair stays live across the chunks)
     const int row0 = (int)band0 * BAND + lane * R;
     uint32_t Hp[R], sel[R];
-    uint32_t prev_up = 0, colA = 0, colB = 0, cml = 0, smax = 0;   // (the lane's last row: Hp[R - 1])
+    uint32_t prev_up = border2(row0), colA = 0, colB = 0, cml = 0, smax = 0;   // (the lane's last row: Hp[R - 1])
 #pragma unroll
-    for (int r = 0; r < R; ++r) Hp[r] = 0;
+    for (int r = 0; r < R; ++r) Hp[r] = border2(row0 + r + 1);
+    // NW: H[m][n] of each pair is Hp[rr] of lane L after wavefront step n - 1 + L of the band holding
+    // row m - 1 (-1: not this unit's band); cap*: the value, in lane L, took*: this unit's segment
+    // holds that step
+    // (capI = (m - 1) mod BAND = L R + rr: one scalar per pair besides the step)
+    int capSA = -1, capSB = -1, capIA = 0, capIB = 0;
+    uint32_t capA = 0, capB = 0;
+    bool tookA = false, tookB = false;   // (uniform) this unit ran the step
+    if constexpr (NWK) {
+        if (liveA && mA > 0 && nA > 0 && (int)band0 == (mA - 1) / BAND) {
+            capIA = (mA - 1) % BAND;
+            capSA = nA - 1 + capIA / R;
+        }
+        if (liveB && mB > 0 && nB > 0 && (int)band0 == (mB - 1) / BAND) {
+            capIB = (mB - 1) % BAND;
+            capSB = nB - 1 + capIB / R;
+        }
+    }
     if (c0 > 0) {
         // a later segment: this lane's R values and diagonal input of each pair at column
         // 32 c0 - 1 - lane, handed on by the previous segment's unit (tagged, bounded wait).  Pair
@@ -236,41 +265,64 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             asm("v_perm_b32 %1, %2, %3, %4\n\tv_pk_add_u16 %0, %5, %1"
                 : "=&v"(dcur), "=&v"(pt) : "v"(colB), "v"(colA), "v"(sel[0]), "v"(prev_up));
             uint32_t hu = up;
+            // the bias off again: SW with the zero clamp (unsigned saturation), NW without
+#define SO2_CELL_N(LAST)                                                                          \
+    asm("v_perm_b32 %[dn], %[cb], %[ca], %[sn]\n\t"                                                \
+        "v_pk_add_u16 %[dn], %[hp], %[dn]\n\t"                                                     \
+        "v_pk_max_i16 %[t1], %[hu], %[hp]\n\t"                                                     \
+        "v_pk_add_u16 %[t1], %[t1], %[g]\n\t"                                                      \
+        "v_pk_max_i16 %[t1], %[t1], %[dr]\n\t" LAST                                                \
+        : [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r])                                         \
+        : [dr] "v"(dcur), [hu] "v"(hu), [g] "s"(G128), [c] "s"(C128),                              \
+          [sn] "v"(sel[r + 1 < R ? r + 1 : r]), [ca] "v"(colA), [cb] "v"(colB))
+#define SO2_CELL_L(LAST)                                                                          \
+    asm("v_pk_max_i16 %[t1], %[hu], %[hp]\n\t"                                                     \
+        "v_pk_add_u16 %[t1], %[t1], %[g]\n\t"                                                      \
+        "v_pk_max_i16 %[t1], %[t1], %[dr]\n\t" LAST                                                \
+        : [t1] "=&v"(t1), [hp] "+v"(Hp[r])                                                         \
+        : [dr] "v"(dcur), [hu] "v"(hu), [g] "s"(G128), [c] "s"(C128))
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 uint32_t t1;
                 if (r + 1 < R) {
                     uint32_t dn;
-                    asm("v_perm_b32 %[dn], %[cb], %[ca], %[sn]\n\t"
-                        "v_pk_add_u16 %[dn], %[hp], %[dn]\n\t"
-                        "v_pk_max_i16 %[t1], %[hu], %[hp]\n\t"
-                        "v_pk_add_u16 %[t1], %[t1], %[g]\n\t"
-                        "v_pk_max_i16 %[t1], %[t1], %[dr]\n\t"
-                        "v_pk_sub_u16 %[hp], %[t1], %[c] clamp"
-                        : [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r])
-                        : [dr] "v"(dcur), [hu] "v"(hu), [g] "s"(G128), [c] "s"(C128),
-                          [sn] "v"(sel[r + 1 < R ? r + 1 : r]), [ca] "v"(colA), [cb] "v"(colB));
+                    if constexpr (NWK) SO2_CELL_N("v_pk_sub_u16 %[hp], %[t1], %[c]");
+                    else SO2_CELL_N("v_pk_sub_u16 %[hp], %[t1], %[c] clamp");
                     dcur = dn;
                 } else {
-                    asm("v_pk_max_i16 %[t1], %[hu], %[hp]\n\t"
-                        "v_pk_add_u16 %[t1], %[t1], %[g]\n\t"
-                        "v_pk_max_i16 %[t1], %[t1], %[dr]\n\t"
-                        "v_pk_sub_u16 %[hp], %[t1], %[c] clamp"
-                        : [t1] "=&v"(t1), [hp] "+v"(Hp[r])
-                        : [dr] "v"(dcur), [hu] "v"(hu), [g] "s"(G128), [c] "s"(C128));
+                    if constexpr (NWK) SO2_CELL_L("v_pk_sub_u16 %[hp], %[t1], %[c]");
+                    else SO2_CELL_L("v_pk_sub_u16 %[hp], %[t1], %[c] clamp");
                 }
                 // the lane's chunk maximum of the rows 3 mod 4 at the steps 3 mod 4: every cell of
                 // the chunk has such a cell of the same lane at most 3 rows below and 3 steps later,
                 // and a cell is at most its lower / right neighbour - Gap (kSoSlack, as
                 // fill_so_kernel).  Valid in ramp chunks too: the cells right of the matrix edge
                 // follow the recurrence (substitution -128), so the bound holds through them.
-                if (PH == 3 && (r & 7) == 7) {
+                if (!NWK && PH == 3 && (r & 7) == 7) {
                     cml = pk_max_u16(cml, Hp[r - 4]);
                     cml = pk_max_u16(cml, Hp[r]);
                 }
                 hu = Hp[r];
             }
+#undef SO2_CELL_N
+#undef SO2_CELL_L
             prev_up = up;
+        }
+        if constexpr (NWK) {   // (uniform) H[m][n] of a pair: lane L's row rr after column n - 1
+            if (kC + q == capSA) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) v = r == capIA % R ? Hp[r] : v;
+                capA = lane == capIA / R ? lo16(v) : capA;
+                tookA = true;
+            }
+            if (kC + q == capSB) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) v = r == capIB % R ? Hp[r] : v;
+                capB = lane == capIB / R ? hi16(v) : capB;
+                tookB = true;
+            }
         }
         // the lane's last row of each pair, pushed into its packet word (two steps per word)
         recA = __builtin_amdgcn_alignbit(Hp[R - 1], recA, 16u);
@@ -296,7 +348,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             const bool wantA = in && band0 > 0 && liveA && c < nA, wantB = in && band0 > 0 && liveB && c < nB;
             gu32* const ga = gA + (uint32_t)c;
             gu32* const gb = gB + (uint32_t)c;
-            uint32_t ha = 0, hb = 0;   // band 0: the SW top border
+            // band 0: the top border (SW 0, NW H(0, c + 1) = (c + 1) Gap)
+            uint32_t ha = lo16(border2(c + 1)), hb = ha;
             if (wantA) ha = __hip_atomic_load(ga, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (wantB) hb = __hip_atomic_load(gb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (band0 > 0) {   // (uniform) the producer band's granules of this chunk, this launch's
@@ -370,11 +423,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             const uint64_t e = (uint64_t)band0 * P.snap_nch + chunk;
             if (kC + kChunk - 1 < lane) cml = 0;   // (a lane that has not reached its first column)
             smax = pk_max_u16(smax, cml);
-            const uint32_t wm = wave_pk_max(cml);
+            const uint32_t wm = NWK ? 0u : wave_pk_max(cml);
             if (liveA && chunk < nchA) {
-                int32_t* const smA = P.snap_m + (uint64_t)sA * P.snap_p_slot + e * kWave;
-                smA[ln] = (int32_t)lo16(cml);
-                if (lane == kWave - 1) P.snap_c[(uint64_t)sA * P.part_bands * P.snap_nch + e] = (int32_t)lo16(wm);
+                if constexpr (!NWK) {
+                    int32_t* const smA = P.snap_m + (uint64_t)sA * P.snap_p_slot + e * kWave;
+                    smA[ln] = (int32_t)lo16(cml);
+                    if (lane == kWave - 1) P.snap_c[(uint64_t)sA * P.part_bands * P.snap_nch + e] = (int32_t)lo16(wm);
+                }
                 if (chunk + 1 < nchA) {
                     uint32_t* const sh = P.snap_h + (uint64_t)sA * P.snap_h_slot + e * (R / 2) * kWave + ln;
 #pragma unroll
@@ -385,9 +440,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
                 }
             }
             if (liveB && chunk < nchB) {
-                int32_t* const smB = P.snap_m + (uint64_t)sB * P.snap_p_slot + e * kWave;
-                smB[ln] = (int32_t)hi16(cml);
-                if (lane == kWave - 1) P.snap_c[(uint64_t)sB * P.part_bands * P.snap_nch + e] = (int32_t)hi16(wm);
+                if constexpr (!NWK) {
+                    int32_t* const smB = P.snap_m + (uint64_t)sB * P.snap_p_slot + e * kWave;
+                    smB[ln] = (int32_t)hi16(cml);
+                    if (lane == kWave - 1) P.snap_c[(uint64_t)sB * P.part_bands * P.snap_nch + e] = (int32_t)hi16(wm);
+                }
                 if (chunk + 1 < nchB) {
                     uint32_t* const sh = P.snap_h + (uint64_t)sB * P.snap_h_slot + e * (R / 2) * kWave + ln;
 #pragma unroll
@@ -424,18 +481,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // every unit of the couple stores one word per pair {tag, lost, the unit's maximum of the pair};
     // the couple's final unit (last band, last segment) folds them and reports both pairs
     seg_lost = __builtin_amdgcn_ballot_w64(seg_lost != 0) != 0 ? 1u : 0u;
+    // the unit's word of each pair: SW its maximum of the tracked cells; NW H[m][n] - delta as
+    // 1 << 16 | (v ^ 0x8000) (order-preserving, above every word of a unit without it) or 0
+    uint32_t wA = 0, wB = 0;
+    if constexpr (NWK) {
+        if (tookA) wA = 1u << 16 | (((uint32_t)__builtin_amdgcn_readlane((int)capA, capIA / R) & 0xffffu) ^ 0x8000u);
+        if (tookB) wB = 1u << 16 | (((uint32_t)__builtin_amdgcn_readlane((int)capB, capIB / R) & 0xffffu) ^ 0x8000u);
+    } else {
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) smax = pk_max_u16(smax, (uint32_t)__shfl_xor((int)smax, off));
+        for (int off = 32; off >= 1; off >>= 1) smax = pk_max_u16(smax, (uint32_t)__shfl_xor((int)smax, off));
+        wA = liveA ? lo16(smax) : 0u;
+        wB = liveB ? hi16(smax) : 0u;
+    }
     typedef unsigned long long __attribute__((address_space(1))) gu64p;
     gu64p* const partA = (gu64p*)(P.band_part + (uint64_t)sA * P.part_bands * SEGS);
     gu64p* const partB = (gu64p*)(P.band_part + (uint64_t)sB * P.part_bands * SEGS);
     const uint32_t me = band0 * SEGS + seg, nparts = B2 > 0 ? (uint32_t)(B2 - 1) * SEGS + last_seg : 0u;
     if (me != nparts) {
         if (lane == 0) {
-            __hip_atomic_store(partA + me, (unsigned long long)epoch16 << 32 | (liveA ? lo16(smax) : 0u) | seg_lost << 31,
+            __hip_atomic_store(partA + me, (unsigned long long)epoch16 << 32 | wA | seg_lost << 31,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (hasB)
-                __hip_atomic_store(partB + me, (unsigned long long)epoch16 << 32 | (liveB ? hi16(smax) : 0u) | seg_lost << 31,
+                __hip_atomic_store(partB + me, (unsigned long long)epoch16 << 32 | wB | seg_lost << 31,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         return;
@@ -443,18 +510,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     uint32_t lostA = seg_lost, lostB = seg_lost;
     uint32_t mxA = bu_fold_parts(partA, nparts, last_seg, SEGS, epoch16, P.wait_polls, lane, lostA);
     uint32_t mxB = hasB ? bu_fold_parts(partB, nparts, last_seg, SEGS, epoch16, P.wait_polls, lane, lostB) : 0u;
-    mxA = max(mxA, liveA ? lo16(smax) : 0u);
-    mxB = max(mxB, liveB ? hi16(smax) : 0u);
+    mxA = max(mxA, wA);
+    mxB = max(mxB, wB);
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         mxA = max(mxA, (uint32_t)__shfl_xor((int)mxA, off));
         mxB = max(mxB, (uint32_t)__shfl_xor((int)mxB, off));
     }
     if (lane == 0) {
-        auto report = [&](uint32_t pidx, bool bad, int Bx, uint32_t mx, uint32_t lost) {
+        auto report = [&](uint32_t pidx, bool bad, int Bx, int mx_, int nx_, uint32_t mx, uint32_t lost) {
             sa_result r = {};
             if (bad) {
                 r.flags = SA_FLAG_BAD_SHAPE;
+            } else if constexpr (NWK) {
+                // SANeedlemanWunsch.h: H[m][n], the walk starts at (m, n); an empty input is the
+                // border's max(m, n) Gap
+                r.end_i = mx_;
+                r.end_j = nx_;
+                if (Bx == 0) {
+                    r.score = (mx_ > nx_ ? mx_ : nx_) * G;
+                } else {
+                    r.score = (int)(int16_t)(uint16_t)((mx & 0xffffu) ^ 0x8000u) + D0;
+                    if (!((mx >> 16) & 1u) || lost) r.flags |= kFlagRetry;   // (no unit took it: re-run)
+                }
             } else if (Bx == 0) {
                 r.score = INT_MIN;   // empty input: SW keeps MaxScore = INT_MIN, (MaxRow, MaxCol) = (0, 0)
             } else {
@@ -467,21 +545,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             }
             P.res[pidx] = r;
         };
-        report(pA, badA, BA, mxA, lostA);
-        if (hasB) report(pB, badB, BB, mxB, lostB);
+        report(pA, badA, BA, mA, nA, mxA, lostA);
+        if (hasB) report(pB, badB, BB, mB, nB, mxB, lostB);
     }
 }
 
-hipError_t launch_fill_so2(int R, const FillParams& p, uint32_t grid, hipStream_t stream) {
+hipError_t launch_fill_so2(int algo, int R, const FillParams& p, uint32_t grid, hipStream_t stream) {
     const size_t lds = (size_t)kStepBufWords * 4 + 2 * (size_t)p.so2_stage;
-    if (R == 32) {
-        hipLaunchKernelGGL((fill_so2_kernel<32>), dim3(grid), dim3(kWave), lds, stream, p);
-        return hipGetLastError();
+#define SO2_LAUNCH(A, RR)                                                                           \
+    if (algo == (A) && R == (RR)) {                                                                 \
+        hipLaunchKernelGGL((fill_so2_kernel<A, RR>), dim3(grid), dim3(kWave), lds, stream, p);     \
+        return hipGetLastError();                                                                  \
     }
-    if (R == 16) {
-        hipLaunchKernelGGL((fill_so2_kernel<16>), dim3(grid), dim3(kWave), lds, stream, p);
-        return hipGetLastError();
-    }
+    SO2_LAUNCH(SA_SW, 32)
+    SO2_LAUNCH(SA_SW, 16)
+    SO2_LAUNCH(SA_NW, 32)
+    SO2_LAUNCH(SA_NW, 16)
+#undef SO2_LAUNCH
     return hipErrorInvalidValue;
 }
 

@@ -224,7 +224,7 @@ hipError_t launch_fill_lg(const FillVariant& v, const FillParams& p, uint32_t gr
 hipError_t launch_fill_gg(const FillVariant& v, const FillParams& p, uint32_t grid, hipStream_t s);
 // Score-only SW band units with two pairs per wave (sa_fill_so2.hip), R in {16, 32}: grid =
 // ceil(count / 2) x bands x part_segs units.
-hipError_t launch_fill_so2(int R, const FillParams& p, uint32_t grid, hipStream_t s);
+hipError_t launch_fill_so2(int algo, int R, const FillParams& p, uint32_t grid, hipStream_t s);
 // Batch alphabet scan (presence bitmap of every byte of both sequence sets, 8 words) and the
 // device-side T16 decision.  aux layout (kAux* below): [bitmap 8][profile 4][sym_pack][sel].
 constexpr int kAuxProf = 8, kAuxSel = 13, kAuxWords = 64;
@@ -241,7 +241,9 @@ constexpr uint32_t kSoSegs = 2;
 // long at the same count; pipelined 10,000-pair steps by segments (profiles/so2_segs_r06.jsonl):
 // 4096^2 2: 16.85-16.88 ms, 3: 16.56-16.59, 4: 16.46-16.55, 5: 16.51-16.55, 6: 16.55-16.57,
 // 8: 16.45-16.49, 12: 16.58-16.62; 2048^2 2: 5.00-5.09, 4: 4.88-4.89, 8: 4.80; 1024^2 (33 chunks)
-// 2: 1.66-1.70, 6: 1.63, 8: 1.64-1.65.  The one-pair-per-wave NW units keep 2
+// 2: 1.66-1.70, 6: 1.63, 8: 1.64-1.65; NW 1024^2 (profiles/so2_r16_r06.jsonl) 4: 1.58, 8: 1.63-1.69,
+// one pair per wave at 2: 1.61 -- so at most 8, and at least 8 chunks per segment (sa_api.hip).
+// The one-pair-per-wave NW units keep 2
 // (profiles/nw_segs_r06.jsonl: 1024^2 2: 1.68 ms, 4: 1.68-1.71, 8: 1.81; 4096^2 2: 17.1-17.3,
 // 4: 17.2-17.3, 8: 17.9).
 constexpr uint32_t kSo2Segs = 8;

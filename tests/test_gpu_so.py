@@ -121,6 +121,23 @@ def test_so_ragged_matches_tagged_and_oracle(engine, maxlen, R, tb):
 
 
 @pytest.mark.parametrize("maxlen,R,npairs", [(1000, 16, 1101), (3000, 32, 1100)])
+def test_so2_nw_matches_one_pair_per_wave(engine, monkeypatch, maxlen, R, npairs):
+    """NeedlemanWunsch with two pairs per wave (fill_so2_kernel<SA_NW, R>) against one pair per wave
+    (SEQALIB_SO2=0): identical results (H[m][n] of both pairs of every couple, taken at its one
+    step) and op streams on ragged batches, an odd pair count; a sample against the oracle."""
+    batch = ragged_batch(190 + maxlen, npairs, maxlen)
+    s1, o1, s2, o2 = batch
+    a = run(engine, True, *batch, scoring=NW, algo=1)
+    monkeypatch.setenv("SEQALIB_SO2", "0")
+    b = run(engine, True, *batch, scoring=NW, algo=1)
+    monkeypatch.delenv("SEQALIB_SO2")
+    assert a[2] == b[2] and a[2][1] == R
+    assert (a[0]["flags"] == 0).all()
+    assert_same(a, b, o1, o2)
+    check_vs_oracle(1, NW, a, batch, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 500, npairs - 1])
+
+
+@pytest.mark.parametrize("maxlen,R,npairs", [(1000, 16, 1101), (3000, 32, 1100)])
 def test_so2_matches_one_pair_per_wave(engine, monkeypatch, maxlen, R, npairs):
     """Two pairs per wave (fill_so2_kernel, the default on the score-only SW plans at R = 16 / 32)
     against one pair per wave (SEQALIB_SO2=0) and against round 5's alphabet-scan launch
