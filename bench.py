@@ -378,6 +378,14 @@ def fill_streams(pairs: int, m: int, n: int, R: int, segs: int = 2):
     return out
 
 
+def f16_hi_exact(x: int) -> bool:
+    """An f16 whose low byte is 0 holds x exactly (sa_api.hip f16_hi_exact)."""
+    if not -2048 <= x <= 2048:
+        return False
+    h = np.array([x], np.float16)
+    return int(h[0]) == x and (int(h.view(np.uint16)[0]) & 0xff) == 0
+
+
 def issue_model(label: str):
     try:
         return json.load(open(ISSUE_MODEL))["kernels"][label]
@@ -515,7 +523,10 @@ def main():
     so = records == sa.SA_RECORDS_SCORE_ONLY
     # two pairs per wave (sa_fill_so2.hip) on the score-only SW plans at R = 16 / 32 unless SEQALIB_SO2=0
     so2 = so and plan_R in (16, 32) and os.environ.get("SEQALIB_SO2", "1") != "0"
-    label = f"sw_{'so2' if so2 else 'so' if so else 't16c' if endcell else 't16' if t16 else 'int32'}_r{plan_R}"
+    # the f16 cell (sa_fill_so2.hip FK) as the engine picks it (sa_api.hip so2_f16_scoring): SW at
+    # an f16-exact match / mismatch unless SEQALIB_SO2_F16=0 (random DNA never turns it off)
+    f16 = so2 and os.environ.get("SEQALIB_SO2_F16", "1") != "0" and all(f16_hi_exact(x) for x in (SCORING[1], SCORING[2]))
+    label = f"sw_{'so2f' if f16 else 'so2' if so2 else 'so' if so else 't16c' if endcell else 't16' if t16 else 'int32'}_r{plan_R}"
     model = issue_model(label)
     fill_gcups = per_launch_cells / fill_s / 1e9
     # algorithmic HBM bytes per cell: score-only fill -- the edge stream (16 bits per lane-step =
@@ -535,7 +546,9 @@ def main():
         bytes_per_cell = streams["total"] / per_launch_cells
     hbm_gbps = per_launch_cells * bytes_per_cell / fill_s / 1e9
     pmc = load_pmc(workload, label)
-    kname = ("fill_so2_kernel<R=%d> (score-only T16, two pairs per wave in packed 16-bit halves, band units, "
+    kname = ("fill_so2_kernel<SW,R=%d,f16> (score-only, two pairs per wave in packed f16 halves, exact below 2048, "
+             "band units, 4 waves/SIMD)" % plan_R if f16 else
+             "fill_so2_kernel<SW,R=%d> (score-only T16, two pairs per wave in packed 16-bit halves, band units, "
              "4 waves/SIMD)" % plan_R if so2 else
              "fill_so_kernel<R=%d> (score-only T16, chunk-max end cell, 4 waves/SIMD)" % plan_R if so else
              f"fill_kernel<SW,R={plan_R},W={plan_W}," + ("T16 tagged int16 profile" if t16 else "int32 flags")

@@ -248,9 +248,13 @@ int sa_plan_query_ex(int algo, const sa_scoring* scoring, uint32_t max_m, uint32
  * context's last launch becomes `value` (0..65535; the next launch takes value + 1, and at 65535 the
  * hand-off buffer is zeroed and the tags restart at 1).  SA_HOOK_POISON_WS: every 32-bit word of the
  * context's cached workspace becomes `value` (after its pending work; synchronous), as stale words
- * of earlier calls of other shapes would be.  Returns SA_OK or SA_ERR_ARG. */
+ * of earlier calls of other shapes would be.  SA_HOOK_F16: 0 / 1 allows / turns off the f16 cell of
+ * the two-pairs-per-wave SW fill for the context (after its pending work); 2 returns 1 when it is
+ * off (the context turned it off after a launch flagged more than 1/64 of its pairs), else 0.
+ * Returns SA_OK or SA_ERR_ARG (SA_HOOK_F16 with 2: 1 / 0). */
 #define SA_HOOK_HAND_TAG 1
 #define SA_HOOK_POISON_WS 2
+#define SA_HOOK_F16 3
 int sa_test_hook(sa_ctx* ctx, int hook, uint64_t value);
 
 /* Synthetic DNA: std::mt19937_64(seed), symbol = "ACGT"[g() & 3]. */

@@ -40,7 +40,7 @@ SA_FLAG_DIVERGED, SA_FLAG_BAD_SHAPE, SA_FLAG_SIZE_HACK, SA_FLAG_TIMEOUT = 1, 2, 
 SA_KERNEL_INT32, SA_KERNEL_T16, SA_KERNEL_T16_ENDCELL, SA_KERNEL_TINY = 0, 1, 2, 3
 SA_PIPELINE_DEPTH = 2   # pipelined device calls that may run at once (distinct output buffers)
 SA_RECORDS_FLAGS, SA_RECORDS_TAGS, SA_RECORDS_SCORE_ONLY = 0, 1, 2
-SA_HOOK_HAND_TAG, SA_HOOK_POISON_WS = 1, 2   # sa_test_hook (tests only)
+SA_HOOK_HAND_TAG, SA_HOOK_POISON_WS, SA_HOOK_F16 = 1, 2, 3   # sa_test_hook (tests only)
 INT32_MIN = -(2 ** 31)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -481,9 +481,14 @@ class Engine:
         """Overlap consecutive align_device calls (sa_set_pipeline); results need wait()."""
         self._check(self.L.sa_set_pipeline(self.h, 1 if enable else 0), "sa_set_pipeline")
 
-    def test_hook(self, hook: int, value: int):
-        """Tests only (sa_test_hook): SA_HOOK_HAND_TAG / SA_HOOK_POISON_WS."""
-        self._check(self.L.sa_test_hook(self.h, hook, value), "sa_test_hook")
+    def test_hook(self, hook: int, value: int) -> int:
+        """Tests only (sa_test_hook): SA_HOOK_HAND_TAG / SA_HOOK_POISON_WS / SA_HOOK_F16 (value 2:
+        returns 1 when the context turned the f16 cell off)."""
+        rc = self.L.sa_test_hook(self.h, hook, value)
+        if rc > 0:
+            return rc
+        self._check(rc, "sa_test_hook")
+        return 0
 
     def wait(self):
         """Wait for all pipelined align_device work (sa_wait)."""

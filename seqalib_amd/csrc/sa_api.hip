@@ -79,6 +79,15 @@ struct sa_ctx {
     bool hand_dirty = false;   // (tests: sa_test_hook poisoned it) zero before the next launch
     hipStream_t s_fill = nullptr, s_tb = nullptr;
     hipEvent_t ev_in = nullptr, ev_slot[kPipeSlots] = {};
+    // The f16 SW cell (sa_fill_so2.hip FK) re-runs in int32 every pair whose score may pass 2,000.
+    // Each of its launches has a number f16_seq; its end cell posts {seq, flagged pairs} to h_f16
+    // (coherent pinned, d_f16 on the device) and f16_cnt[seq % 4] keeps the launch's pair count.
+    // A launch that flagged more than 1/64 of its pairs turns the cell off for the context
+    // (f16_off): such batches run the 16-bit integer cell, exact to 8,191, instead of re-running.
+    unsigned long long* h_f16 = nullptr;
+    unsigned long long* d_f16 = nullptr;
+    uint32_t f16_seq = 0, f16_seen = 0, f16_cnt[4] = {};
+    bool f16_off = false;
     uint64_t pipe_k = 0;
     // SPLIT plans (few pairs, one workgroup per band): [ticket, pad to 256 B][granules][partials]
     uint8_t* split = nullptr;
@@ -656,6 +665,21 @@ int validate_scoring(sa_ctx* c, int algo, const sa_scoring* s) {
 }
 
 // T16 by scoring and shape (the batch alphabet is checked on the device, decide_t16).
+// The f16 cell of the two-pairs-per-wave SW fill (sa_fill_so2.hip FK): the substitutions the T16
+// fill runs with (match, tm.mismatch) must be f16 values whose low byte is 0 (+-1..8, 10, 12, 14,
+// 16, 20, ...), so that the perm's table byte is their high byte.  $SEQALIB_SO2_F16=0: the 16-bit
+// integer cell (A/B, tests).
+bool f16_hi_exact(int s) {
+    if (s < -2048 || s > 2048) return false;
+    const _Float16 h = (_Float16)(float)s;
+    return (int)(float)h == s && (__builtin_bit_cast(uint16_t, h) & 0xffu) == 0;
+}
+bool so2_f16_scoring(const sa_ctx* c, int algo, const sa_scoring* sc, const T16Mode& tm) {
+    if (algo != SA_SW || !tm.ok || c->f16_off) return false;
+    if (const char* e = getenv("SEQALIB_SO2_F16")) if (e[0] == '0') return false;
+    return f16_hi_exact(sc->match) && f16_hi_exact(tm.mismatch) && f16_hi_exact(-128);
+}
+
 T16Mode t16_candidate(int algo, const sa_scoring* sc, uint32_t max_m, uint32_t max_n, uint32_t npairs) {
     T16Mode t = t16_mode(algo, sc, max_m, max_n);
     if ((algo == SA_SW || algo == SA_LOCAL_GOTOH) && !keyed_ok(algo, sc, max_m, max_n)) t.ok = false;
@@ -787,6 +811,21 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
     const int slot = pipe ? (int)(c->pipe_k % (uint64_t)nslots) : 0;
     uint32_t* aux = c->aux + kAuxWords * slot;
     if (pipe && c->ev_slot[slot]) SA_HIP(c, hipStreamWaitEvent(stream, c->ev_slot[slot], 0));   // slot free
+    if (!c->h_f16) {
+        SA_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_f16), 8, hipHostMallocCoherent));
+        *c->h_f16 = 0;
+        void* dp = nullptr;
+        SA_HIP(c, hipHostGetDevicePointer(&dp, c->h_f16, 0));
+        c->d_f16 = static_cast<unsigned long long*>(dp);
+    }
+    {   // the f16 policy: the latest posted launch (one of the last 4) flagged > 1/64 of its pairs
+        const unsigned long long w = __atomic_load_n(c->h_f16, __ATOMIC_ACQUIRE);
+        const uint32_t s = (uint32_t)(w >> 32);
+        if (s != 0 && s != c->f16_seen) {
+            c->f16_seen = s;
+            if (c->f16_seq - s < 4 && (uint64_t)(uint32_t)w * 64 > c->f16_cnt[s & 3]) c->f16_off = true;
+        }
+    }
     const uint32_t* sel = nullptr;
     const uint32_t* prof = aux + kAuxProf;   // the T16 profile words (+5: the selection word)
     static_assert(kAuxSel == kAuxProf + 5, "profile and selection word: one upload");
@@ -811,8 +850,10 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
         // for its producer expired flags its pair for that re-run, sa_fill_impl.h BU)
         const Variant vt = make_variant(algo, max_m, max_n, npairs, true, true);
         const bool bu_hand = vt.so && !is_affine(algo) && (vt.pl.g.bands > 1 || vt.segs > 1);
+        // (the f16 cell may flag any pair: its int32 re-run stays)
+        const bool f16 = vt.so2 && so2_f16_scoring(c, algo, sc, tm);
         if (ha->sel == 0) only = 2;
-        else if (tm.retry_above == INT_MAX && !bu_hand) only = 1;
+        else if (tm.retry_above == INT_MAX && !bu_hand && !f16) only = 1;
         else sel = prof + 5;
     }
     if (hs && hs->up_bytes)
@@ -1033,6 +1074,10 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 const uint32_t range = std::max((nch + sg - 1) / sg, 3u) * kChunk + kWave;
                 const uint32_t cap = (range + 15) & ~15u;
                 fp.so2_stage = (2 * cap <= 8192 && !no_stage) ? cap : 0;
+                if (v.t16 && so2_f16_scoring(c, algo, sc, tm)) {
+                    fp.so2_f16 = 1;
+                    fp.retry_above = std::min(fp.retry_above, kSo2F16RetryAbove);
+                }
             }
             FillVariant fv{pl.R, lut, allow || v.t16, keyed, v.t16, v.cmax, pl.split, bits};
             fv.so = v.so;
@@ -1085,7 +1130,8 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
             const FillVariant fv = make_fp(k);
             const FillParams& fp = fps[k];
             if (pl.split) SA_HIP(c, hipMemsetAsync(fp.ticket, 0, 256 + hand_x_off * 8 * aff2, sf));
-            if (v.so && !is_affine(algo)) SA_HIP(c, hipMemsetAsync(fp.ticket, 0, 4, sf));
+            if (v.so && !is_affine(algo)) SA_HIP(c, hipMemsetAsync(fp.ticket, 0, 8, sf));   // (+ kAuxF16Flags)
+            static_assert(kAuxF16Flags == kAuxTicket + 1, "ticket and f16 count: one memset");
             if (kev) SA_HIP(c, hipEventRecord(kev[2 * k], sf));
             // grid: SPLIT one workgroup per (pair, band) slot; score-only SW / NW one per (pair,
             // band) unit (band units, sa_fill_impl.h BU); otherwise one per pair
@@ -1128,6 +1174,13 @@ int run_device(sa_ctx* c, int algo, const sa_scoring* sc, const uint8_t* d1, con
                 ep.hshift = v.so ? 0 : 2;
                 ep.snap_c = fp.snap_c; ep.snap_c_slot = v.snap_c_slot;
                 ep.dirs = fp.dirs; ep.dir_slot = fp.dir_slot; ep.band_stride = fp.band_stride;
+                if (fp.so2_f16) {
+                    const uint32_t seq = ++c->f16_seq ? c->f16_seq : ++c->f16_seq;   // (0: none posted)
+                    c->f16_cnt[seq & 3] = cnt;
+                    ep.f16_count = fp.ticket + (kAuxF16Flags - kAuxTicket);
+                    ep.f16_host = c->d_f16;
+                    ep.f16_seq = seq;
+                }
                 // on the fill stream, right after the fill: run beside the next call's fill (on the
                 // traceback stream) its 10,000 short waves slowed that fill by 4 % in round 4, and
                 // the whole pipelined step by 12 % in round 5 (21.4 vs 19.1 ms per step)
@@ -1952,6 +2005,7 @@ void sa_destroy(sa_ctx* c) {
     if (c->io) (void)hipFree(c->io);
     if (c->aux) (void)hipFree(c->aux);
     if (c->h_sel) (void)hipHostFree(c->h_sel);
+    if (c->h_f16) (void)hipHostFree(c->h_f16);
     if (c->tiny_io) (void)hipHostFree(c->tiny_io);
     if (c->split) (void)hipFree(c->split);
     if (c->hand) (void)hipFree(c->hand);
@@ -1974,6 +2028,14 @@ int sa_test_hook(sa_ctx* c, int hook, uint64_t value) {
         if (int rc = drain(c)) return rc;
         if (c->ws) SA_HIP(c, hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(c->ws), (int)(uint32_t)value, c->ws_bytes / 4));
         SA_HIP(c, hipDeviceSynchronize());
+        return SA_OK;
+    }
+    if (hook == SA_HOOK_F16) {
+        if (value == 2) return c->f16_off ? 1 : 0;
+        if (value > 1) return fail(c, SA_ERR_ARG, "SA_HOOK_F16 takes 0, 1 or 2");
+        if (int rc = drain(c)) return rc;
+        c->f16_off = value == 1;
+        c->f16_seen = c->h_f16 ? (uint32_t)(__atomic_load_n(c->h_f16, __ATOMIC_ACQUIRE) >> 32) : 0;
         return SA_OK;
     }
     return fail(c, SA_ERR_ARG, "unknown test hook");

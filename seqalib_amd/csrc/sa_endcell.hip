@@ -187,6 +187,11 @@ extern "C" int sa_debug_ecso_stats(unsigned long long* out, int reset) {
 // common kernel's occupancy (121 -> fewer VGPRs, more resident waves).
 template <int R, bool DENSE>
 __global__ __launch_bounds__(64) void endcell_so_kernel(EndcellParams P) {
+    if constexpr (DENSE) {   // (after the fill: its count is final) to the host's pinned word
+        if (P.f16_count && blockIdx.x == 0 && threadIdx.x == 0)
+            __hip_atomic_store(P.f16_host, (unsigned long long)P.f16_seq << 32 | *P.f16_count, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (sa_skip(P.sel, P.sel_want)) return;
     const int lane = threadIdx.x;
     const uint32_t slot = blockIdx.x;

@@ -29,6 +29,25 @@
 // Work units, tickets, column segments, {tag, value} hand-off words, bounded waits and the per-unit
 // maxima are those of the one-pair band units (sa_fill_impl.h BU), per pair.
 //
+// FK (round 6, SW): the cell in f16 arithmetic, 5 ops per 2 cells (tools/microbench_pk6.hip PK5F:
+// 12.11 vs 14.15 SIMD-cycles per 64 cells, profiles/microbench_pk5f_r06.txt):
+//   p  = v_perm_b32(colB, colA, sel_r)   s(a_r, c) as an f16 whose low byte is 0 (the table byte is
+//                                        its high byte; sel_r selects it into the high byte of each
+//                                        half and the constant 0 into the low byte)
+//   dn = v_pk_add_f16(hp, p)             Hd + s
+//   t  = v_pk_max_i16(hu, hp)            max(Hu, Hl) (H >= 0: f16 patterns order as integers)
+//   t  = v_pk_add_f16(t, Gap)
+//   hp = v_pk_maximum3_f16(t, dr, 0)     max(0, Hu + Gap, Hl + Gap, Hd + s)
+// Exact while every value stays below 2048 (f16 integers); the host takes it when match and mismatch
+// are such f16 values (sa_api.hip so2_f16_scoring) and flags for the int32 re-run every pair whose
+// sampled maximum says a value may have reached 2048 (retry_above <= kSo2F16RetryAbove: the first
+// such cell is computed >= 2048 and the sampled cell below it >= 2048 + kSoSlack Gap - kSoSlack).
+// Every word other kernels read (edge stream, snapshots, chunk maxima, band rows) is converted to
+// the integers of the 16-bit path on its way out (v_cvt_u16_f16, 2 ops per word), and band rows
+// back to f16 on their way in; the segment hand-off words stay f16 (only this kernel reads them).
+// Rows past a pair's m take s = 0 (the selector's constant byte), columns past its n s = -128:
+// s <= 0 keeps those cells at most the matrix maximum, all the bounds above need.
+//
 // ALG = SA_NW (round 6): the same cell without the clamp (SANeedlemanWunsch.h:69-86; registers hold
 // H - delta, the T16 window of t16_mode), the borders i Gap - delta / j Gap - delta in the left
 // column, the corner and band 0's top row, no chunk maxima.  H[m][n] of each pair is taken at the
@@ -66,12 +85,37 @@ __device__ __forceinline__ uint32_t wave_pk_max(uint32_t v) {
     v = pk_max_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
     return v;
 }
+__device__ __forceinline__ uint32_t pk_max_i16(uint32_t a, uint32_t b) {
+    uint32_t d;
+    asm("v_pk_max_i16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+// both halves: f16 integer -> u16 integer, and back
+__device__ __forceinline__ uint32_t f16x2_to_u16x2(uint32_t x) {
+    uint32_t d;
+    asm("v_cvt_u16_f16_sdwa %0, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0\n\t"
+        "v_cvt_u16_f16_sdwa %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1"
+        : "=&v"(d) : "v"(x));
+    return d;
+}
+__device__ __forceinline__ uint32_t u16x2_to_f16x2(uint32_t x) {
+    uint32_t d;
+    asm("v_cvt_f16_u16_sdwa %0, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0\n\t"
+        "v_cvt_f16_u16_sdwa %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1"
+        : "=&v"(d) : "v"(x));
+    return d;
+}
+__device__ __forceinline__ uint32_t f16_bits(int s) {
+    const _Float16 h = (_Float16)(float)s;
+    return (uint32_t)__builtin_bit_cast(uint16_t, h);
+}
 
 }  // namespace
 
-template <int ALG, int R>
+template <int ALG, int R, bool FK>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void fill_so2_kernel(FillParams P) {
     constexpr bool NWK = ALG == SA_NW;
+    static_assert(!(FK && NWK), "the f16 cell is SW's");
     if (sa_skip(P.sel, P.sel_want)) return;   // (the score-only variant has no redo launch)
     static_assert(R >= 8 && R % 2 == 0, "the sampled chunk maximum needs 8 rows per lane");
     constexpr int BAND = kWave * R;
@@ -134,7 +178,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 #pragma unroll
         for (int x = 0; x < 4; ++x) {
             const int s = (int)(int8_t)(so_profile(P.prof[x]) >> (8 * c));
-            w |= ((uint32_t)(s + 128) & 255u) << (8 * x);
+            if constexpr (FK) w |= (f16_bits(s) >> 8) << (8 * x);
+            else w |= ((uint32_t)(s + 128) & 255u) << (8 * x);
         }
         cw[c] = w;
     }
@@ -156,7 +201,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         }
         __syncthreads();
     }
-    // the column table word of column c of each pair (0 -- substitution -128 -- outside it)
+    // the column table word of column c of each pair (substitution -128 outside it: 0, FK 0xd8 = -128.0)
+    constexpr uint32_t kOut = FK ? 0xd8d8d8d8u : 0u;
     auto col_pair = [&](int c, uint32_t& wa, uint32_t& wb) {
         const bool ia = liveA && c >= 0 && c < nA, ib = liveB && c >= 0 && c < nB;
         uint32_t xa, xb;
@@ -167,10 +213,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             xa = ia ? (t16_code8(symp, s2A[(uint32_t)c]) >> 3) : 0u;
             xb = ib ? (t16_code8(symp, s2B[(uint32_t)c]) >> 3) : 0u;
         }
-        wa = ia ? (xa == 0 ? cw[0] : xa == 1 ? cw[1] : xa == 2 ? cw[2] : cw[3]) : 0u;
-        wb = ib ? (xb == 0 ? cw[0] : xb == 1 ? cw[1] : xb == 2 ? cw[2] : cw[3]) : 0u;
+        wa = ia ? (xa == 0 ? cw[0] : xa == 1 ? cw[1] : xa == 2 ? cw[2] : cw[3]) : kOut;
+        wb = ib ? (xb == 0 ? cw[0] : xb == 1 ? cw[1] : xb == 2 ? cw[2] : cw[3]) : kOut;
     };
-    const uint32_t G128 = ((uint32_t)(G + 128) & 0xffffu) * 0x10001u;
+    // (FK: the packed f16 Gap)
+    const uint32_t G128 = FK ? f16_bits(G) * 0x10001u : ((uint32_t)(G + 128) & 0xffffu) * 0x10001u;
     const uint32_t C128 = 0x00800080u;
 
     typedef uint32_t __attribute__((address_space(1))) gu32;
@@ -242,7 +289,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         const int row = row0 + r;
         const uint32_t ca = (liveA && row < mA) ? (t16_code8(symp, s1A[(uint32_t)row]) >> 3) : 12u;
         const uint32_t cb = (liveB && row < mB) ? (4u + (t16_code8(symp, s1B[(uint32_t)row]) >> 3)) : 12u;
-        sel[r] = ca | 0x0c00u | cb << 16 | 0x0c000000u;
+        sel[r] = FK ? 0x0cu | ca << 8 | 0x0c0000u | cb << 24 : ca | 0x0c00u | cb << 16 | 0x0c000000u;
     }
 
     // One step of the chunk at kC: lane t computes column j = kC + q - t of its R rows of both
@@ -262,8 +309,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         colB = (uint32_t)shr1((int)vb, (int)colB);
         if (!RAMP || kC + q - lane >= 0) {
             uint32_t dcur, pt;
-            asm("v_perm_b32 %1, %2, %3, %4\n\tv_pk_add_u16 %0, %5, %1"
-                : "=&v"(dcur), "=&v"(pt) : "v"(colB), "v"(colA), "v"(sel[0]), "v"(prev_up));
+            if constexpr (FK)
+                asm("v_perm_b32 %1, %2, %3, %4\n\tv_pk_add_f16 %0, %5, %1"
+                    : "=&v"(dcur), "=&v"(pt) : "v"(colB), "v"(colA), "v"(sel[0]), "v"(prev_up));
+            else
+                asm("v_perm_b32 %1, %2, %3, %4\n\tv_pk_add_u16 %0, %5, %1"
+                    : "=&v"(dcur), "=&v"(pt) : "v"(colB), "v"(colA), "v"(sel[0]), "v"(prev_up));
             uint32_t hu = up;
             // the bias off again: SW with the zero clamp (unsigned saturation), NW without
 #define SO2_CELL_N(LAST)                                                                          \
@@ -281,16 +332,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         "v_pk_max_i16 %[t1], %[t1], %[dr]\n\t" LAST                                                \
         : [t1] "=&v"(t1), [hp] "+v"(Hp[r])                                                         \
         : [dr] "v"(dcur), [hu] "v"(hu), [g] "s"(G128), [c] "s"(C128))
+#define SO2_CELL_FN                                                                               \
+    asm("v_perm_b32 %[dn], %[cb], %[ca], %[sn]\n\t"                                                \
+        "v_pk_add_f16 %[dn], %[hp], %[dn]\n\t"                                                     \
+        "v_pk_max_i16 %[t1], %[hu], %[hp]\n\t"                                                     \
+        "v_pk_add_f16 %[t1], %[t1], %[g]\n\t"                                                      \
+        "v_pk_maximum3_f16 %[hp], %[t1], %[dr], 0"                                                 \
+        : [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r])                                         \
+        : [dr] "v"(dcur), [hu] "v"(hu), [g] "s"(G128),                                             \
+          [sn] "v"(sel[r + 1 < R ? r + 1 : r]), [ca] "v"(colA), [cb] "v"(colB))
+#define SO2_CELL_FL                                                                               \
+    asm("v_pk_max_i16 %[t1], %[hu], %[hp]\n\t"                                                     \
+        "v_pk_add_f16 %[t1], %[t1], %[g]\n\t"                                                      \
+        "v_pk_maximum3_f16 %[hp], %[t1], %[dr], 0"                                                 \
+        : [t1] "=&v"(t1), [hp] "+v"(Hp[r])                                                         \
+        : [dr] "v"(dcur), [hu] "v"(hu), [g] "s"(G128))
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 uint32_t t1;
                 if (r + 1 < R) {
                     uint32_t dn;
-                    if constexpr (NWK) SO2_CELL_N("v_pk_sub_u16 %[hp], %[t1], %[c]");
+                    if constexpr (FK) SO2_CELL_FN;
+                    else if constexpr (NWK) SO2_CELL_N("v_pk_sub_u16 %[hp], %[t1], %[c]");
                     else SO2_CELL_N("v_pk_sub_u16 %[hp], %[t1], %[c] clamp");
                     dcur = dn;
                 } else {
-                    if constexpr (NWK) SO2_CELL_L("v_pk_sub_u16 %[hp], %[t1], %[c]");
+                    if constexpr (FK) SO2_CELL_FL;
+                    else if constexpr (NWK) SO2_CELL_L("v_pk_sub_u16 %[hp], %[t1], %[c]");
                     else SO2_CELL_L("v_pk_sub_u16 %[hp], %[t1], %[c] clamp");
                 }
                 // the lane's chunk maximum of the rows 3 mod 4 at the steps 3 mod 4: every cell of
@@ -299,13 +367,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
                 // fill_so_kernel).  Valid in ramp chunks too: the cells right of the matrix edge
                 // follow the recurrence (substitution -128), so the bound holds through them.
                 if (!NWK && PH == 3 && (r & 7) == 7) {
-                    cml = pk_max_u16(cml, Hp[r - 4]);
-                    cml = pk_max_u16(cml, Hp[r]);
+                    if constexpr (FK) {   // (f16 patterns of H >= 0; a -0.0 is the smallest i16)
+                        cml = pk_max_i16(cml, Hp[r - 4]);
+                        cml = pk_max_i16(cml, Hp[r]);
+                    } else {
+                        cml = pk_max_u16(cml, Hp[r - 4]);
+                        cml = pk_max_u16(cml, Hp[r]);
+                    }
                 }
                 hu = Hp[r];
             }
 #undef SO2_CELL_N
 #undef SO2_CELL_L
+#undef SO2_CELL_FN
+#undef SO2_CELL_FL
             prev_up = up;
         }
         if constexpr (NWK) {   // (uniform) H[m][n] of a pair: lane L's row rr after column n - 1
@@ -363,7 +438,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
                 }
             }
             if (in) {
-                s_step[ln] = lo16(ha) | hb << 16;
+                s_step[ln] = FK ? u16x2_to_f16x2(lo16(ha) | hb << 16) : lo16(ha) | hb << 16;
                 s_step[32 + 2 * ln] = wa;
                 s_step[33 + 2 * ln] = wb;
             }
@@ -390,6 +465,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             st(std::integral_constant<int, 6>{});
             st(std::integral_constant<int, 7>{});
             const uint32_t po = ((uint32_t)((kC + q0) / SPP) * kWave + (uint32_t)lane) * 16u;
+            if constexpr (FK) {
+#pragma unroll
+                for (int w = 0; w < SPP / 2; ++w) {
+                    pa[w] = f16x2_to_u16x2(pa[w]);
+                    pb[w] = f16x2_to_u16x2(pb[w]);
+                }
+            }
             if (liveA) {
                 const u32x4 v4 = {pa[0], pa[1], pa[2], pa[3]};
                 __builtin_nontemporal_store(v4, reinterpret_cast<u32x4*>(dA + po));
@@ -409,7 +491,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         // ------------------------------------------------ the band's last row to the next band
         const uint32_t ln = lane_here();
         {
-            const uint32_t acc = s_step[96 + (ln & 31)];   // lane q < 32: column kC + q - 63
+            uint32_t acc = s_step[96 + (ln & 31)];   // lane q < 32: column kC + q - 63
+            if constexpr (FK) acc = f16x2_to_u16x2(acc);
             const int cc = kC + (int)ln - (kWave - 1);
             if (lane < kChunk && cc >= 0) {
                 if ((int)band0 + 1 < BA && cc < nA)
@@ -422,8 +505,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         {
             const uint64_t e = (uint64_t)band0 * P.snap_nch + chunk;
             if (kC + kChunk - 1 < lane) cml = 0;   // (a lane that has not reached its first column)
+            if constexpr (FK) cml = f16x2_to_u16x2(cml);   // (integers from here on)
             smax = pk_max_u16(smax, cml);
             const uint32_t wm = NWK ? 0u : wave_pk_max(cml);
+            const uint32_t pup = FK ? f16x2_to_u16x2(prev_up) : prev_up;
             if (liveA && chunk < nchA) {
                 if constexpr (!NWK) {
                     int32_t* const smA = P.snap_m + (uint64_t)sA * P.snap_p_slot + e * kWave;
@@ -433,10 +518,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
                 if (chunk + 1 < nchA) {
                     uint32_t* const sh = P.snap_h + (uint64_t)sA * P.snap_h_slot + e * (R / 2) * kWave + ln;
 #pragma unroll
-                    for (int q = 0; q < R / 2; ++q)   // (one address, immediate offsets)
-                        sh[q * kWave] = __builtin_amdgcn_perm(Hp[2 * q + 1], Hp[2 * q], 0x05040100u);
+                    for (int q = 0; q < R / 2; ++q) {   // (one address, immediate offsets)
+                        const uint32_t w = __builtin_amdgcn_perm(Hp[2 * q + 1], Hp[2 * q], 0x05040100u);
+                        sh[q * kWave] = FK ? f16x2_to_u16x2(w) : w;
+                    }
                     int32_t* const spA = P.snap_p + (uint64_t)sA * P.snap_p_slot + e * kWave;
-                    spA[ln] = (int32_t)lo16(prev_up);
+                    spA[ln] = (int32_t)lo16(pup);
                 }
             }
             if (liveB && chunk < nchB) {
@@ -448,10 +535,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
                 if (chunk + 1 < nchB) {
                     uint32_t* const sh = P.snap_h + (uint64_t)sB * P.snap_h_slot + e * (R / 2) * kWave + ln;
 #pragma unroll
-                    for (int q = 0; q < R / 2; ++q)   // (one address, immediate offsets)
-                        sh[q * kWave] = __builtin_amdgcn_perm(Hp[2 * q + 1], Hp[2 * q], 0x07060302u);
+                    for (int q = 0; q < R / 2; ++q) {   // (one address, immediate offsets)
+                        const uint32_t w = __builtin_amdgcn_perm(Hp[2 * q + 1], Hp[2 * q], 0x07060302u);
+                        sh[q * kWave] = FK ? f16x2_to_u16x2(w) : w;
+                    }
                     int32_t* const spB = P.snap_p + (uint64_t)sB * P.snap_p_slot + e * kWave;
-                    spB[ln] = (int32_t)hi16(prev_up);
+                    spB[ln] = (int32_t)hi16(pup);
                 }
             }
             cml = 0;
@@ -540,7 +629,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
                 // row-major cell
                 r.score = (int)mx;
                 r.reserved = 1;
-                if ((int)mx - kSoSlack * G > P.retry_above) r.flags |= kFlagRetry;
+                if ((int)mx - kSoSlack * G > P.retry_above) {
+                    r.flags |= kFlagRetry;
+                    if constexpr (FK) atomicAdd(P.ticket + (kAuxF16Flags - kAuxTicket), 1u);   // (the host's f16 policy)
+                }
                 if (lost) r.flags |= kFlagRetry;
             }
             P.res[pidx] = r;
@@ -552,15 +644,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 
 hipError_t launch_fill_so2(int algo, int R, const FillParams& p, uint32_t grid, hipStream_t stream) {
     const size_t lds = (size_t)kStepBufWords * 4 + 2 * (size_t)p.so2_stage;
-#define SO2_LAUNCH(A, RR)                                                                           \
-    if (algo == (A) && R == (RR)) {                                                                 \
-        hipLaunchKernelGGL((fill_so2_kernel<A, RR>), dim3(grid), dim3(kWave), lds, stream, p);     \
+#define SO2_LAUNCH(A, RR, F)                                                                        \
+    if (algo == (A) && R == (RR) && (p.so2_f16 != 0) == (F)) {                                      \
+        hipLaunchKernelGGL((fill_so2_kernel<A, RR, F>), dim3(grid), dim3(kWave), lds, stream, p);  \
         return hipGetLastError();                                                                  \
     }
-    SO2_LAUNCH(SA_SW, 32)
-    SO2_LAUNCH(SA_SW, 16)
-    SO2_LAUNCH(SA_NW, 32)
-    SO2_LAUNCH(SA_NW, 16)
+    SO2_LAUNCH(SA_SW, 32, true)
+    SO2_LAUNCH(SA_SW, 16, true)
+    SO2_LAUNCH(SA_SW, 32, false)
+    SO2_LAUNCH(SA_SW, 16, false)
+    SO2_LAUNCH(SA_NW, 32, false)
+    SO2_LAUNCH(SA_NW, 16, false)
 #undef SO2_LAUNCH
     return hipErrorInvalidValue;
 }

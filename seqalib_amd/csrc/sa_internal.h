@@ -109,7 +109,12 @@ struct FillParams {
     // the two-pairs-per-wave SW fill (sa_fill_so2.hip): bytes of LDS per pair for its unit's Seq2
     // symbol codes (0: read from global memory per chunk)
     uint32_t so2_stage;
+    // 1: its f16 cell (SW; every value exact below 2048, pairs above kSo2F16RetryAbove re-run)
+    uint32_t so2_f16;
 };
+// the f16 cell's retry threshold on (sampled maximum - kSoSlack Gap): below it every value of the
+// pair stayed below 2048 (sa_fill_so2.hip)
+constexpr int32_t kSo2F16RetryAbove = 2000;
 
 // SPLIT fills: per-pair fold of the per-band partials into sa_result (split_reduce_kernel).
 struct SplitReduceParams {
@@ -155,6 +160,11 @@ struct EndcellParams {
     uint64_t snap_c_slot;
     const uint8_t* dirs;       // score-only: the fill's edge stream (TbParams::dirs, band_stride)
     uint64_t dir_slot, band_stride;
+    // the f16 SW fill's flagged-pair count of this launch (FillParams::ticket + 1; null: none) and
+    // where the dense kernel's first lane posts {f16_seq, count} for the host (sa_api.hip f16 policy)
+    const uint32_t* f16_count;
+    unsigned long long* f16_host;
+    uint32_t f16_seq;
 };
 
 struct TbParams {
@@ -229,6 +239,7 @@ hipError_t launch_fill_so2(int algo, int R, const FillParams& p, uint32_t grid, 
 // device-side T16 decision.  aux layout (kAux* below): [bitmap 8][profile 4][sym_pack][sel].
 constexpr int kAuxProf = 8, kAuxSel = 13, kAuxWords = 64;
 constexpr int kAuxTicket = 32;   // the score-only fill's unit ticket (zeroed before each launch)
+constexpr int kAuxF16Flags = 33;   // the f16 SW fill's flagged pairs (zeroed with the ticket)
 // Score-only SW fill: steady chunks track the lane maximum at rows and steps 3 mod 4 only, so a
 // cell is at most its tracked cell - kSoSlack * gap (3 rows + 3 columns of gap moves)
 constexpr int kSoSlack = 6;

@@ -397,3 +397,79 @@ def test_so_column_segments_any_count(engine, monkeypatch, algo, scoring):
         assert_same(run(engine, True, *batch, scoring=scoring, algo=algo), base, o1, o2)
     monkeypatch.delenv("SEQALIB_SO_SEGS")
     assert_same(base, run(engine, False, *batch, scoring=scoring, algo=algo), o1, o2)
+
+
+def identical_pairs_batch(seed, npairs, lengths, maxlen=2200):
+    """Random pairs of ragged lengths with, first, identical pairs of the given lengths (SW score =
+    length at (-1, 1, -1)): scores just below and above the f16 cell's retry threshold."""
+    rng = np.random.default_rng(seed)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    pairs = []
+    for p in range(npairs):
+        if p < len(lengths):
+            a = acgt[rng.integers(0, 4, lengths[p])]
+            pairs.append((a.tobytes(), a.tobytes()))
+        else:
+            m, n = int(rng.integers(1, maxlen + 1)), int(rng.integers(1, maxlen + 1))
+            pairs.append((acgt[rng.integers(0, 4, m)].tobytes(), acgt[rng.integers(0, 4, n)].tobytes()))
+    o1 = np.zeros(npairs + 1, np.uint64)
+    o2 = np.zeros(npairs + 1, np.uint64)
+    o1[1:] = np.cumsum([len(a) for a, _ in pairs])
+    o2[1:] = np.cumsum([len(b) for _, b in pairs])
+    s1 = np.frombuffer(b"".join(a for a, _ in pairs), np.uint8).copy()
+    s2 = np.frombuffer(b"".join(b for _, b in pairs), np.uint8).copy()
+    return s1, o1, s2, o2
+
+
+def test_so2_f16_threshold_pairs(engine, monkeypatch):
+    """The f16 cell (fill_so2_kernel FK, exact below 2048) at its threshold: identical pairs scoring
+    1,990 .. 3,000 among random ones -- the ones above the retry threshold re-run in int32 -- against
+    the 16-bit integer cell (SEQALIB_SO2_F16=0) and the oracle; 10 flagged pairs of 1,100 leave the
+    cell on (SA_HOOK_F16)."""
+    engine.test_hook(sa.SA_HOOK_F16, 0)
+    lengths = [1990, 1993, 1994, 1999, 2005, 2040, 2047, 2048, 2049, 2100, 2500, 3000]
+    batch = identical_pairs_batch(5, 1100, lengths)
+    s1, o1, s2, o2 = batch
+    a = run(engine, True, *batch)
+    monkeypatch.setenv("SEQALIB_SO2_F16", "0")
+    b = run(engine, True, *batch)
+    monkeypatch.delenv("SEQALIB_SO2_F16")
+    assert (a[0]["flags"] == 0).all()
+    assert [int(x) for x in a[0]["score"][:len(lengths)]] == lengths
+    assert_same(a, b, o1, o2)
+    check_vs_oracle(0, SW, a, batch, list(range(len(lengths))) + [500, 1099])
+    run(engine, True, *batch)
+    assert engine.test_hook(sa.SA_HOOK_F16, 2) == 0
+
+
+def test_so2_f16_policy_high_identity(engine, monkeypatch):
+    """A batch of near-identical 3,000-symbol pairs (scores ~2,800: every pair re-runs in int32 after
+    the f16 cell) is exact, and its launch turns the f16 cell off for the context: the next call runs
+    the 16-bit integer cell, with the same results."""
+    engine.test_hook(sa.SA_HOOK_F16, 0)
+    try:
+        rng = np.random.default_rng(11)
+        acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+        pairs = []
+        for p in range(1030):
+            a = acgt[rng.integers(0, 4, 3000)]
+            b = a.copy()
+            mut = rng.random(3000) < 0.02
+            b[mut] = acgt[rng.integers(0, 4, int(mut.sum()))]
+            pairs.append((a.tobytes(), b.tobytes()))
+        o1 = np.arange(1031, dtype=np.uint64) * 3000
+        o2 = o1.copy()
+        s1 = np.frombuffer(b"".join(x for x, _ in pairs), np.uint8).copy()
+        s2 = np.frombuffer(b"".join(y for _, y in pairs), np.uint8).copy()
+        a = run(engine, True, s1, o1, s2, o2)
+        assert (a[0]["flags"] == 0).all() and (a[0]["score"] > 2000).all()
+        monkeypatch.setenv("SEQALIB_SO2_F16", "0")
+        b = run(engine, True, s1, o1, s2, o2)
+        monkeypatch.delenv("SEQALIB_SO2_F16")
+        assert_same(a, b, o1, o2)
+        assert engine.test_hook(sa.SA_HOOK_F16, 2) == 1
+        c = run(engine, True, s1, o1, s2, o2)
+        assert_same(a, c, o1, o2)
+        check_vs_oracle(0, SW, a, (s1, o1, s2, o2), [0, 1, 515, 1029])
+    finally:
+        engine.test_hook(sa.SA_HOOK_F16, 0)

@@ -27,12 +27,20 @@ ALIAS = {"v_mov_b32_dpp": "v_mov_b32_dpp_shr", "v_readlane_b32": "readlane", "v_
          "v_cmp_eq_u32": "cmp_only", "v_cmp_gt_u32": "cmp_only", "v_cmp_le_u32": "cmp_only",
          "v_lshl_add_u64": "v_lshl_add_u32", "v_max3_i32": "v_max3_i32", "v_add_co_u32": "add_co_e64",
          # packed 16-bit forms measured at one rate (profiles/microbench_valu_issue_r01.txt)
-         "v_pk_sub_u16": "v_pk_add_u16", "v_pk_max_u16": "v_pk_max_i16"}
+         "v_pk_sub_u16": "v_pk_add_u16", "v_pk_max_u16": "v_pk_max_i16",
+         # the f16 cell's packed ops: the same cycles per cell as the integer forms
+         # (tools/microbench_pk6.hip PK5F vs PK5, profiles/microbench_pk5f_r06.txt)
+         "v_pk_add_f16": "v_pk_add_u16", "v_pk_maximum3_f16": "v_pk_max_i16",
+         # one-half SDWA conversions: the SDWA rate (profiles/microbench_sdwa_r01.txt)
+         "v_cvt_u16_f16_sdwa": "mov_b32_sdwa_preserve", "v_cvt_f16_u16_sdwa": "mov_b32_sdwa_preserve"}
 
 KERNELS = {  # label -> (TU, mangled name, cells per lane in one steady block = SPP * R [* pairs per lane])
     # round 6: the score-only SW fill with two pairs per wave (fill_so2_kernel<R>, sa_fill_so2.hip)
-    "sw_so2_r32": ("sa_fill_so2.hip", "_ZN2sa15fill_so2_kernelILi32EEEvNS_10FillParamsE", 512),   # 8 steps x 32 rows x 2 pairs
-    "sw_so2_r16": ("sa_fill_so2.hip", "_ZN2sa15fill_so2_kernelILi16EEEvNS_10FillParamsE", 256),
+    # (fill_so2_kernel<ALG, R, FK>; FK: the f16 cell, the default for SW at f16-exact scorings)
+    "sw_so2f_r32": ("sa_fill_so2.hip", "_ZN2sa15fill_so2_kernelILi0ELi32ELb1EEEvNS_10FillParamsE", 512),   # 8 steps x 32 rows x 2 pairs
+    "sw_so2f_r16": ("sa_fill_so2.hip", "_ZN2sa15fill_so2_kernelILi0ELi16ELb1EEEvNS_10FillParamsE", 256),
+    "sw_so2_r32": ("sa_fill_so2.hip", "_ZN2sa15fill_so2_kernelILi0ELi32ELb0EEEvNS_10FillParamsE", 512),
+    "sw_so2_r16": ("sa_fill_so2.hip", "_ZN2sa15fill_so2_kernelILi0ELi16ELb0EEEvNS_10FillParamsE", 256),
     # round 5: the score-only fills (fill_so_kernel<ALG, R>): SW / NW band units, LG / GG affine
     "sw_so_r32": ("sa_fill_sw.hip", "_ZN2sa14fill_so_kernelILi0ELi32EEEvNS_10FillParamsE", 256),   # 8 steps x 32 rows
     "sw_so_r16": ("sa_fill_sw.hip", "_ZN2sa14fill_so_kernelILi0ELi16EEEvNS_10FillParamsE", 128),

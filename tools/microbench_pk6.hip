@@ -8,6 +8,8 @@
 //   t  = v_pk_add_u16(t, G + 128)             max(U, L) + G, biased +128
 //   h  = v_pk_max_i16(t, dr)                  max(M + G, D + s) + 128
 //   hp = v_pk_sub_u16(h, 128) clamp           max(0, M + G, D + s)
+//   PK5F (V = 3): the same cell in f16 -- sub as an f16 whose low byte is 0 (the perm's high byte),
+//   one v_pk_maximum3_f16 takes max(D + s, M + G, 0): 5 ops per 2 cells
 // argv[1] = waves per SIMD (1024 * wps single-wave workgroups).  Cycles are SIMD-cycles per 64
 // lane-cells at 2.4 GHz (time-based, as tools/microbench_so.hip).
 #include <hip/hip_runtime.h>
@@ -27,12 +29,15 @@ __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, i
     uint32_t tab[R], Hp[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        tab[r] = V == 0 ? in[(lane * 7 + r) & 1023] : ((r + lane) & 3) | 0x0c00u | ((((r * 3 + lane) & 3) + 4) << 16) | 0x0c000000u;
+        tab[r] = V == 0 ? in[(lane * 7 + r) & 1023]
+                 : V == 3 ? 0x0cu | (((r + lane) & 3) << 8) | 0x0c0000u | ((((r * 3 + lane) & 3) + 4) << 24)
+                          : ((r + lane) & 3) | 0x0c00u | ((((r * 3 + lane) & 3) + 4) << 16) | 0x0c000000u;
         Hp[r] = 0;
     }
     uint32_t hl = 0, sym = (lane & 3) * 8, prev_up = 0, cml = 0, srcA = 0x7f7f7f81u, srcB = 0x7f817f7fu;
     const uint32_t CU1 = 1;
     const uint32_t G128 = 0x007f007fu, C128 = 0x00800080u;   // packed G + 128 (G = -1), 128
+    const uint32_t GF16 = 0xbc00bc00u;                        // packed f16 -1.0
     for (int s = 0; s < steps; ++s) {
         const uint32_t up_h = shr1(in[s & 1023], hl);
         uint32_t hu = up_h, dcur;
@@ -41,8 +46,13 @@ __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, i
             asm volatile("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(dcur) : "v"(tab[0]), "v"(sym), "v"(prev_up));
         } else {
             // the step's column tables of both pairs ride the DPP shift (lane 0: a new column)
-            srcA = shr1(0x7f7f7f7fu + (2u << (((s * 7) & 3) * 8)), srcA);
-            srcB = shr1(0x7f7f7f7fu + (2u << (((s * 5) & 3) * 8)), srcB);
+            if constexpr (V == 3) {   // f16 high bytes: -1.0 (0xbc) but +1.0 (0x3c) at the match
+                srcA = shr1(0xbcbcbcbcu ^ (0x80u << (((s * 7) & 3) * 8)), srcA);
+                srcB = shr1(0xbcbcbcbcu ^ (0x80u << (((s * 5) & 3) * 8)), srcB);
+            } else {
+                srcA = shr1(0x7f7f7f7fu + (2u << (((s * 7) & 3) * 8)), srcA);
+                srcB = shr1(0x7f7f7f7fu + (2u << (((s * 5) & 3) * 8)), srcB);
+            }
             uint32_t p;
             asm volatile("v_perm_b32 %0, %1, %2, %3\n\tv_pk_add_u16 %0, %4, %0" : "=&v"(dcur), "=&v"(p) : "v"(srcB), "v"(srcA), "v"(tab[0]), "v"(prev_up));
             (void)p;
@@ -69,6 +79,15 @@ __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, i
                              : [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r])
                              : [dr] "v"(dcur), [hu] "v"(hu), [g] "s"(G128), [c] "s"(C128), [tabn] "v"(tabn), [sa] "v"(srcA),
                                [sb] "v"(srcB));
+                if (r % 8 == 7 && (s & 3) == 3) asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(cml) : "v"(Hp[r]));
+            } else if constexpr (V == 3) {
+                asm volatile("v_perm_b32 %[dn], %[sb], %[sa], %[tabn]\n\t"
+                             "v_pk_add_f16 %[dn], %[hp], %[dn]\n\t"
+                             "v_pk_max_i16 %[t1], %[hu], %[hp]\n\t"
+                             "v_pk_add_f16 %[t1], %[t1], %[g]\n\t"
+                             "v_pk_maximum3_f16 %[hp], %[t1], %[dr], 0"
+                             : [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r])
+                             : [dr] "v"(dcur), [hu] "v"(hu), [g] "s"(GF16), [tabn] "v"(tabn), [sa] "v"(srcA), [sb] "v"(srcB));
                 if (r % 8 == 7 && (s & 3) == 3) asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(cml) : "v"(Hp[r]));
             } else {
                 asm volatile("v_perm_b32 %[dn], %[sb], %[sa], %[tabn]\n\t"
@@ -105,6 +124,7 @@ int main(int argc, char** argv) {
         {"PK6 2 pairs packed, R32 (6 / 2 cells)", cells<1, 32>, 64},
         {"PK6 2 pairs packed, R16 (6 / 2 cells)", cells<1, 16>, 32},
         {"PK5 packed without clamp, R32 (bound)", cells<2, 32>, 64},
+        {"PK5F f16 with maximum3 floor, R32", cells<3, 32>, 64},
     };
     const int steps = 4000;
     for (auto& k : ks) {
