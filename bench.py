@@ -581,7 +581,7 @@ def main():
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "GCUPS", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
-        "scaling": "strong" if args.total_pairs > 0 else "weak", "vs_baseline": None, "dtype": "int16" if t16 else "int32",
+        "scaling": "strong" if args.total_pairs > 0 else "weak", "vs_baseline": None, "dtype": ("f16 (integer-exact below 2048)" if f16 else "int16") if t16 else "int32",
         "data": "synthetic DNA, std::mt19937_64 'ACGT'[g()&3], seeds base+2p+1/base+2p+2, resident in HBM",
         "config": {"workload": workload, "pairs_per_gpu": P, "total_pairs": args.total_pairs or world * P,
                    "m": Lq, "n": Lq, "algo": "SmithWatermanSA",
