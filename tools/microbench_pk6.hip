@@ -8,6 +8,9 @@
 //   t  = v_pk_add_u16(t, G + 128)             max(U, L) + G, biased +128
 //   h  = v_pk_max_i16(t, dr)                  max(M + G, D + s) + 128
 //   hp = v_pk_sub_u16(h, 128) clamp           max(0, M + G, D + s)
+//   PK4F (V = 4): f16 scaled by 2^-11 so that the add's clamp is the zero floor, and F = max(H + Gap,
+//   0) kept per row beside H: dn = Hd + s, H = v_pk_maximum3_f16(dn, Fu, Fl), F = clamp(H + Gap) --
+//   4 ops per 2 cells, 2R registers of state
 //   PK5F (V = 3): the same cell in f16 -- sub as an f16 whose low byte is 0 (the perm's high byte),
 //   one v_pk_maximum3_f16 takes max(D + s, M + G, 0): 5 ops per 2 cells
 // argv[1] = waves per SIMD (1024 * wps single-wave workgroups).  Cycles are SIMD-cycles per 64
@@ -26,13 +29,14 @@ __device__ __forceinline__ uint32_t shr1(uint32_t old, uint32_t src) {
 template <int V, int R>
 __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, int steps) {
     const int lane = threadIdx.x;
-    uint32_t tab[R], Hp[R];
+    uint32_t tab[R], Hp[R], Fr[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         tab[r] = V == 0 ? in[(lane * 7 + r) & 1023]
-                 : V == 3 ? 0x0cu | (((r + lane) & 3) << 8) | 0x0c0000u | ((((r * 3 + lane) & 3) + 4) << 24)
+                 : V >= 3 ? 0x0cu | (((r + lane) & 3) << 8) | 0x0c0000u | ((((r * 3 + lane) & 3) + 4) << 24)
                           : ((r + lane) & 3) | 0x0c00u | ((((r * 3 + lane) & 3) + 4) << 16) | 0x0c000000u;
         Hp[r] = 0;
+        Fr[r] = 0;
     }
     uint32_t hl = 0, sym = (lane & 3) * 8, prev_up = 0, cml = 0, srcA = 0x7f7f7f81u, srcB = 0x7f817f7fu;
     const uint32_t CU1 = 1;
@@ -46,7 +50,7 @@ __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, i
             asm volatile("v_bfe_i32 %0, %1, %2, 8\n\tv_add_u16 %0, %3, %0" : "=&v"(dcur) : "v"(tab[0]), "v"(sym), "v"(prev_up));
         } else {
             // the step's column tables of both pairs ride the DPP shift (lane 0: a new column)
-            if constexpr (V == 3) {   // f16 high bytes: -1.0 (0xbc) but +1.0 (0x3c) at the match
+            if constexpr (V >= 3) {   // f16 high bytes: -1.0 (0xbc) but +1.0 (0x3c) at the match
                 srcA = shr1(0xbcbcbcbcu ^ (0x80u << (((s * 7) & 3) * 8)), srcA);
                 srcB = shr1(0xbcbcbcbcu ^ (0x80u << (((s * 5) & 3) * 8)), srcB);
             } else {
@@ -89,6 +93,19 @@ __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, i
                              : [t1] "=&v"(t1), [dn] "=&v"(dn), [hp] "+v"(Hp[r])
                              : [dr] "v"(dcur), [hu] "v"(hu), [g] "s"(GF16), [tabn] "v"(tabn), [sa] "v"(srcA), [sb] "v"(srcB));
                 if (r % 8 == 7 && (s & 3) == 3) asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(cml) : "v"(Hp[r]));
+            } else if constexpr (V == 4) {
+                // PK4F: scaled f16 (H / 2048, clamp = the zero floor), F = max(H + Gap, 0) kept per row:
+                // dn = Hd + s; H = max3(dn, Fu, Fl); F = clamp(H + Gap)
+                asm volatile("v_perm_b32 %[dn], %[sb], %[sa], %[tabn]\n\t"
+                             "v_pk_add_f16 %[dn], %[hp], %[dn]\n\t"
+                             "v_pk_maximum3_f16 %[hp], %[dr], %[fu], %[fl]\n\t"
+                             "v_pk_add_f16 %[fl], %[hp], %[g] clamp"
+                             : [dn] "=&v"(dn), [hp] "+v"(Hp[r]), [fl] "+v"(Fr[r])
+                             : [dr] "v"(dcur), [fu] "v"(hu), [g] "s"(GF16), [tabn] "v"(tabn), [sa] "v"(srcA), [sb] "v"(srcB));
+                if (r % 8 == 7 && (s & 3) == 3) asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(cml) : "v"(Hp[r]));
+                dcur = dn;
+                hu = Fr[r];
+                continue;
             } else {
                 asm volatile("v_perm_b32 %[dn], %[sb], %[sa], %[tabn]\n\t"
                              "v_pk_add_u16 %[dn], %[hp], %[dn]\n\t"
@@ -107,7 +124,7 @@ __global__ __launch_bounds__(64) void cells(const uint32_t* in, uint32_t* out, i
     }
     uint32_t x = hl ^ cml ^ srcA ^ srcB;
 #pragma unroll
-    for (int r = 0; r < R; ++r) x ^= Hp[r];
+    for (int r = 0; r < R; ++r) x ^= Hp[r] ^ Fr[r];
     out[blockIdx.x * 64 + lane] = x;
 }
 
@@ -125,6 +142,9 @@ int main(int argc, char** argv) {
         {"PK6 2 pairs packed, R16 (6 / 2 cells)", cells<1, 16>, 32},
         {"PK5 packed without clamp, R32 (bound)", cells<2, 32>, 64},
         {"PK5F f16 with maximum3 floor, R32", cells<3, 32>, 64},
+        {"PK5F f16 with maximum3 floor, R16", cells<3, 16>, 32},
+        {"PK4F scaled f16, F kept, R16", cells<4, 16>, 32},
+        {"PK4F scaled f16, F kept, R32", cells<4, 32>, 64},
     };
     const int steps = 4000;
     for (auto& k : ks) {
