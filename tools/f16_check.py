@@ -29,5 +29,10 @@ for plan in (None, "16,1"):
         os.environ.pop("SEQALIB_SO2_F16", None)
         bad = np.nonzero((r1["score"] != r2["score"]) | (r1["end_i"] != r2["end_i"]) | (r1["end_j"] != r2["end_j"]))[0]
         m = np.diff(b[1])
+        BAND = 64 * p1[1]
+        bands = (m + BAND - 1) // BAND
+        partner = np.where(np.arange(len(m)) % 2 == 1, np.roll(bands, 1), np.roll(bands, -1))
+        print("   bad pairs whose partner has fewer bands:", int((partner[bad] < bands[bad]).sum()), "of", len(bad),
+              "; such odd pairs in the batch:", int(((np.arange(len(m)) % 2 == 1) & (partner < bands)).sum()), flush=True)
         print(plan, maxlen, p1, "bad", len(bad), "odd", int((bad % 2).sum()), "m>2048", int((m[bad] > 2048).sum()),
               "m>1024", int((m[bad] > 1024).sum()), [(int(p), int(r1["score"][p]), int(r2["score"][p]), int(m[p])) for p in bad[:4]], flush=True)
